@@ -1,0 +1,245 @@
+"""butterfly_amd ops: hand-written HIP/CDNA4 kernels bound as torch.ops.bfly.*.
+
+GPU tensors always run the HIP kernels from the in-tree `butterfly_amd/_C.so`; if that
+library is missing or fails to load, every GPU call raises (no silent eager fallback).
+CPU tensors run `ops.reference` (the CPU/gloo plumbing path and the numerics oracle).
+
+Workspaces (split-K GEMM partials, split-KV decode partials, sampling partials) come from a
+per-device arena that the engine sizes before hipGraph capture (`reserve_workspace`), so
+captured steps never allocate.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import torch
+
+from . import reference as ref
+from .reference import SILU_INTERLEAVE, interleave_gate_up, rope_tables, split_gate_up  # noqa: F401
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "_C.so"
+_loaded = False
+_load_error: str | None = None
+
+EPILOGUES = {"none": 0, "bias": 1, "silu": 2}
+DECODE_PART_TOKENS = 256
+
+
+def load_library(path: str | os.PathLike | None = None) -> bool:
+    """Load the HIP kernel library (idempotent). Returns True on success."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    p = Path(path) if path else _LIB_PATH
+    if not p.exists():
+        _load_error = f"{p} not built (run `python -m butterfly_amd._build`)"
+        return False
+    try:
+        torch.ops.load_library(str(p))
+        _loaded = True
+        _load_error = None
+    except Exception as e:  # pragma: no cover - depends on the environment
+        _load_error = f"failed to load {p}: {e}"
+    return _loaded
+
+
+def native_available() -> bool:
+    return load_library()
+
+
+def library_path() -> str:
+    return str(_LIB_PATH)
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    if not t.is_cuda:
+        return False
+    if not load_library():
+        raise RuntimeError(f"butterfly_amd HIP kernels unavailable: {_load_error}")
+    return True
+
+
+# ---------------------------------------------------------------------------------------
+# Workspace arena
+# ---------------------------------------------------------------------------------------
+class _Arena:
+    def __init__(self):
+        self.bufs: dict[tuple, torch.Tensor] = {}
+        self.frozen = False
+
+    def get(self, device, name: str, numel: int, dtype) -> torch.Tensor:
+        key = (str(device), name, dtype)
+        buf = self.bufs.get(key)
+        if buf is None or buf.numel() < numel:
+            if self.frozen or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+                raise RuntimeError(
+                    f"workspace '{name}' needs {numel} elements but is frozen/capturing; "
+                    "call ops.reserve_workspace() before capture")
+            buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
+            self.bufs[key] = buf
+        return buf
+
+
+_arena = _Arena()
+
+
+def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch: int = 0,
+                      max_ctx: int = 0, num_kv_heads: int = 0, head_dim: int = 128) -> None:
+    """Pre-size every workspace for problems up to the given bounds (call before capture)."""
+    if not load_library():
+        return
+    ws = 0
+    for m in sorted({1, 16, 32, 48, 64, 128, 256, max_tokens}):
+        if m > max_tokens:
+            continue
+        ws = max(ws, torch.ops.bfly.gemm_workspace_size(m, max_n, max_k))
+    _arena.get(device, "gemm", ws // 4 + 1, torch.float32)
+    if max_batch and max_ctx:
+        ns = torch.ops.bfly.attn_decode_splits(max_ctx, DECODE_PART_TOKENS)
+        _arena.get(device, "attn_o", max_batch * num_kv_heads * ns * 16 * head_dim, torch.float32)
+        _arena.get(device, "attn_ml", max_batch * num_kv_heads * ns * 16 * 2, torch.float32)
+    _arena.get(device, "sample", max(max_batch, max_tokens, 1) * 64, torch.int64)
+
+
+# ---------------------------------------------------------------------------------------
+# Ops
+# ---------------------------------------------------------------------------------------
+def rms_norm(x, w, eps: float, out=None, residual=None):
+    """y = x * rsqrt(mean(x^2) + eps) * w; with `residual`: residual += x first (in place)
+    and y is the norm of the updated residual (the fused add+norm of every block)."""
+    if not _gpu(x):
+        return ref.rms_norm(x, w, eps, out, residual)
+    if out is None:
+        out = torch.empty_like(x)
+    torch.ops.bfly.rms_norm(x, w, eps, out, residual)
+    return out
+
+
+def layer_norm(x, w, b, eps: float, out=None, residual=None):
+    if not _gpu(x):
+        return ref.layer_norm(x, w, b, eps, out, residual)
+    if out is None:
+        out = torch.empty_like(x)
+    torch.ops.bfly.layer_norm(x, w, b, eps, out, residual)
+    return out
+
+
+def rope_kv(qkv, positions, cos, sin, n_q: int, n_kv: int, slots=None, k_cache=None,
+            v_cache=None):
+    """In-place RoPE on the Q/K heads of a fused QKV row; optional paged KV append."""
+    if not _gpu(qkv):
+        return ref.rope_kv(qkv, positions, cos, sin, n_q, n_kv, slots, k_cache, v_cache)
+    torch.ops.bfly.rope_kv(qkv, positions, cos, sin, n_q, n_kv, slots, k_cache, v_cache)
+    return qkv
+
+
+def kv_append(k, v, slots, k_cache, v_cache):
+    if not _gpu(k):
+        return ref.kv_append(k, v, slots, k_cache, v_cache)
+    torch.ops.bfly.kv_append(k, v, slots, k_cache, v_cache)
+
+
+def silu_mul(gu, out=None, interleave: int = 0):
+    if not _gpu(gu):
+        return ref.silu_mul(gu, out, interleave)
+    if out is None:
+        out = torch.empty(*gu.shape[:-1], gu.shape[-1] // 2, dtype=gu.dtype, device=gu.device)
+    torch.ops.bfly.silu_mul(gu, out, interleave)
+    return out
+
+
+def gelu(x, out=None):
+    if not _gpu(x):
+        return ref.gelu(x, out)
+    if out is None:
+        out = torch.empty_like(x)
+    torch.ops.bfly.gelu(x, out)
+    return out
+
+
+def add(a, b, out=None):
+    if not _gpu(a):
+        return ref.add(a, b, out)
+    if out is None:
+        out = torch.empty_like(a)
+    torch.ops.bfly.add(a, b, out)
+    return out
+
+
+def embed(ids, table, vstart: int = 0, out=None):
+    if not _gpu(ids):
+        return ref.embed(ids, table, vstart, out)
+    if out is None:
+        out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
+    torch.ops.bfly.embed(ids, table, out, vstart)
+    return out
+
+
+def sample(logits, temps=None, seeds=None, vstart: int = 0, out_ids=None, out_scores=None):
+    """Greedy / Gumbel-max sampling over a (vocab-shard of) logits -> (ids int32, scores f32)."""
+    if not _gpu(logits):
+        return ref.sample(logits, temps, seeds, vstart)
+    rows = logits.shape[0]
+    if out_ids is None:
+        out_ids = torch.empty(rows, dtype=torch.int32, device=logits.device)
+    if out_scores is None:
+        out_scores = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    ws = _arena.get(logits.device, "sample", rows * 64, torch.int64)
+    torch.ops.bfly.sample(logits, temps, seeds, vstart, out_ids, out_scores, ws)
+    return out_ids, out_scores
+
+
+def linear(x, w, bias=None, epilogue: str = "none", out=None):
+    """y = x @ w.T (+ bias) with optional fused SwiGLU epilogue ('silu': w rows gate/up
+    interleaved in 16-row groups, output width w.shape[0] // 2)."""
+    if not _gpu(x):
+        return ref.linear(x, w, bias, epilogue, out)
+    epi = EPILOGUES["bias"] if (bias is not None and epilogue == "none") else EPILOGUES[epilogue]
+    if epilogue == "silu" and bias is not None:
+        raise ValueError("bias + silu epilogue not supported")
+    M, N = x.shape[0], w.shape[0]
+    nout = N // 2 if epilogue == "silu" else N
+    if out is None:
+        out = torch.empty(M, nout, dtype=x.dtype, device=x.device)
+    need = torch.ops.bfly.gemm_workspace_size(M, N, x.shape[1])
+    ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32) if need else None
+    torch.ops.bfly.gemm(x, w, out, bias, epi, ws)
+    return out
+
+
+def gemm_plan(M: int, N: int, K: int) -> dict:
+    load_library()
+    k, mt, nt, bm, bn, sk = torch.ops.bfly.gemm_plan(M, N, K)
+    return {"kind": "skinny" if k == 0 else "tile", "mt": mt, "nt": nt, "bm": bm, "bn": bn, "splitk": sk}
+
+
+def attn_prefill(q, k, v, cu_seqlens, max_seqlen: int, scale: float, causal: bool = True,
+                 out=None):
+    if not _gpu(q):
+        return ref.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out)
+    if out is None:
+        out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+    torch.ops.bfly.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out)
+    return out
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_ctx: int,
+                part_tokens: int = DECODE_PART_TOKENS, out=None):
+    """One query token per sequence against the paged cache. `max_ctx` bounds ctx_lens (it
+    fixes the split-KV grid, so it is a static parameter under graph capture)."""
+    if not _gpu(q):
+        return ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx,
+                               part_tokens, out)
+    B, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    if out is None:
+        out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
+    ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
+    po = pml = None
+    if ns > 1:
+        po = _arena.get(q.device, "attn_o", B * Hkv * ns * 16 * D, torch.float32)
+        pml = _arena.get(q.device, "attn_ml", B * Hkv * ns * 16 * 2, torch.float32)
+    torch.ops.bfly.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx,
+                               part_tokens, out, po, pml)
+    return out

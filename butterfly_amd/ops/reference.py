@@ -1,0 +1,256 @@
+"""Plain-PyTorch reference implementations of every butterfly_amd op.
+
+Two roles:
+  * the numerics oracle for the HIP kernels (tests compare each kernel against the fp32
+    computation here), and
+  * the CPU execution path for the gloo plumbing configuration (SURVEY.md §7.3 item 8:
+    the GPU path is HIP-only; the CPU path exists for tests and the CPU/gloo config).
+
+Semantics match the kernels exactly, including in-place side effects and cache layouts:
+  k_cache [num_blocks, Hkv, BS, D], v_cache [num_blocks, Hkv, D, BS] (V transposed).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+SILU_INTERLEAVE = 16  # gate/up row-group size of the fused SwiGLU weight layout
+
+
+def rms_norm(x, w, eps, out=None, residual=None):
+    if residual is not None:
+        residual.copy_((x.float() + residual.float()).to(residual.dtype))
+        src = residual
+    else:
+        src = x
+    xf = src.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    y = y.to(x.dtype)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
+def layer_norm(x, w, b, eps, out=None, residual=None):
+    if residual is not None:
+        residual.copy_((x.float() + residual.float()).to(residual.dtype))
+        src = residual
+    else:
+        src = x
+    y = F.layer_norm(src.float(), (src.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
+def rope_tables(head_dim: int, max_pos: int, theta: float, scaling: dict | None = None,
+                device="cpu"):
+    """cos/sin tables [max_pos, head_dim/2] (f32) for the rotate-half convention.
+
+    `scaling` supports the Llama-3.1 "llama3" frequency remap
+    ({"type": "llama3", "factor", "low_freq_factor", "high_freq_factor",
+      "original_max_position_embeddings"}).
+    """
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling and scaling.get("type") == "llama3":
+        factor = scaling["factor"]
+        lo, hi = scaling["low_freq_factor"], scaling["high_freq_factor"]
+        orig = scaling["original_max_position_embeddings"]
+        lo_wl, hi_wl = orig / lo, orig / hi
+        wl = 2 * math.pi / inv
+        smooth = (orig / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        mid = (wl <= lo_wl) & (wl >= hi_wl)
+        scaled = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+        inv = scaled
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device), f.sin().float().to(device)
+
+
+def _rotate(x, cos, sin):
+    h = x.shape[-1] // 2
+    x0, x1 = x[..., :h].float(), x[..., h:].float()
+    return torch.cat([x0 * cos - x1 * sin, x1 * cos + x0 * sin], -1)
+
+
+def rope_kv(qkv, positions, cos, sin, n_q, n_kv, slots=None, k_cache=None, v_cache=None):
+    T = qkv.shape[0]
+    D = qkv.shape[1] // (n_q + 2 * n_kv)
+    v3 = qkv.view(T, n_q + 2 * n_kv, D)
+    c = cos[positions.long()].unsqueeze(1)
+    s = sin[positions.long()].unsqueeze(1)
+    rot = _rotate(v3[:, : n_q + n_kv], c, s).to(qkv.dtype)
+    v3[:, : n_q + n_kv] = rot
+    if slots is not None:
+        kv_append(v3[:, n_q: n_q + n_kv], v3[:, n_q + n_kv:], slots, k_cache, v_cache)
+    return qkv
+
+
+def kv_append(k, v, slots, k_cache, v_cache):
+    BS = k_cache.shape[2]
+    sl = slots.long()
+    keep = sl >= 0
+    sl = sl[keep]
+    blk, off = sl // BS, sl % BS
+    k_cache[blk, :, off, :] = k[keep].to(k_cache.dtype)
+    v_cache[blk, :, :, off] = v[keep].to(v_cache.dtype)
+
+
+def silu_mul(gu, out=None, interleave=0):
+    ffn = gu.shape[-1] // 2
+    g, u = split_gate_up(gu, interleave)
+    y = (F.silu(g.float()) * u.float()).to(gu.dtype)
+    if out is None:
+        return y
+    out.copy_(y.view(out.shape))
+    return out
+
+
+def split_gate_up(gu, interleave=0):
+    ffn = gu.shape[-1] // 2
+    if interleave == 0:
+        return gu[..., :ffn], gu[..., ffn:]
+    lead = gu.shape[:-1]
+    r = gu.reshape(*lead, ffn // interleave, 2, interleave)
+    return r[..., 0, :].reshape(*lead, ffn), r[..., 1, :].reshape(*lead, ffn)
+
+
+def interleave_gate_up(gate_w, up_w, group=SILU_INTERLEAVE):
+    """[ffn, K] gate and up weights -> [2*ffn, K] rows in alternating `group`-row blocks."""
+    ffn, K = gate_w.shape
+    g = gate_w.reshape(ffn // group, group, K)
+    u = up_w.reshape(ffn // group, group, K)
+    return torch.stack([g, u], 1).reshape(2 * ffn, K)
+
+
+def gelu(x, out=None):
+    y = F.gelu(x.float(), approximate="tanh").to(x.dtype)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
+def add(a, b, out=None):
+    y = (a.float() + b.float()).to(a.dtype)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
+def embed(ids, table, vstart=0, out=None):
+    local = ids.long() - vstart
+    ok = (local >= 0) & (local < table.shape[0])
+    y = table[local.clamp(0, table.shape[0] - 1)] * ok.unsqueeze(-1).to(table.dtype)
+    if out is None:
+        return y
+    out.copy_(y.view(out.shape))
+    return out
+
+
+def _mix64(z):
+    # splitmix64 finaliser on int64 tensors with wrap-around (matches sample.hip)
+    m = (1 << 64) - 1
+    z = z & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def gumbel_uniform(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    """Python-int exact replica of the kernel's counter-based uniform (slow; tests only)."""
+    m = (1 << 64) - 1
+    out = []
+    for i in idx.tolist():
+        h = _mix64((seed * 0x9E3779B97F4A7C15 + i + 1) & m)
+        out.append(((h >> 40) + 0.5) * (1.0 / 16777216.0))
+    return torch.tensor(out, dtype=torch.float32)
+
+
+def sample(logits, temps=None, seeds=None, vstart=0):
+    """Greedy (temp <= 0) or Gumbel-max temperature sampling; returns (ids int32, scores f32)."""
+    lf = logits.float()
+    rows, V = lf.shape
+    ids, scores = [], []
+    for r in range(rows):
+        t = float(temps[r]) if temps is not None else 0.0
+        s = lf[r]
+        if t > 0:
+            u = gumbel_uniform(int(seeds[r]), torch.arange(vstart, vstart + V))
+            s = s / t - torch.log(-torch.log(u))
+        i = int(torch.argmax(s))
+        ids.append(i + vstart)
+        scores.append(float(s[i]))
+    return (torch.tensor(ids, dtype=torch.int32, device=logits.device),
+            torch.tensor(scores, dtype=torch.float32, device=logits.device))
+
+
+def linear(x, w, bias=None, epilogue="none", out=None):
+    y = x.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if epilogue == "silu":
+        g, u = split_gate_up(y, SILU_INTERLEAVE)
+        y = F.silu(g) * u
+    y = y.to(x.dtype)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
+def attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal=True, out=None):
+    """q [T, Hq, D], k/v [T, Hkv, D]; varlen sequences given by cu_seqlens (int32)."""
+    T, Hq, D = q.shape
+    Hkv = k.shape[1]
+    G = Hq // Hkv
+    res = torch.empty(T, Hq, D, dtype=q.dtype, device=q.device)
+    cu = cu_seqlens.tolist()
+    for i in range(len(cu) - 1):
+        a, b = cu[i], cu[i + 1]
+        if b <= a:
+            continue
+        qs = q[a:b].float().transpose(0, 1)                       # [Hq, L, D]
+        ks = k[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
+        vs = v[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
+        s = (qs @ ks.transpose(1, 2)) * scale
+        if causal:
+            L = b - a
+            mask = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
+            s = s.masked_fill(mask, float("-inf"))
+        p = torch.softmax(s, -1)
+        res[a:b] = (p @ vs).transpose(0, 1).to(q.dtype)
+    if out is None:
+        return res
+    out.copy_(res)
+    return out
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx=None,
+                part_tokens=None, out=None, **_):
+    """q [B, Hq, D] (one token per sequence) against the paged cache."""
+    B, Hq, D = q.shape
+    Hkv, BS = k_cache.shape[1], k_cache.shape[2]
+    G = Hq // Hkv
+    res = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
+    for b in range(B):
+        n = int(ctx_lens[b])
+        nblk = (n + BS - 1) // BS
+        blocks = block_tables[b, :nblk].long()
+        ks = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nblk * BS, D)[:, :n].float()
+        vs = v_cache[blocks].permute(1, 0, 3, 2).reshape(Hkv, nblk * BS, D)[:, :n].float()
+        ks = ks.repeat_interleave(G, 0)
+        vs = vs.repeat_interleave(G, 0)
+        s = torch.einsum("hd,hnd->hn", q[b].float(), ks) * scale
+        p = torch.softmax(s, -1)
+        res[b] = torch.einsum("hn,hnd->hd", p, vs).to(q.dtype)
+    if out is None:
+        return res
+    out.copy_(res.view(out.shape))
+    return out

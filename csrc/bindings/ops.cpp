@@ -1,0 +1,328 @@
+// torch.ops.bfly.* registrations for the HIP kernels in csrc/kernels.
+//
+// Every op validates shapes/dtypes/strides on the host (a bad shape must never reach a
+// kernel: a GPU fault can reset every GPU of the host) and launches on the current HIP stream
+// without allocating or synchronising, so whole decode steps can be captured in a hipGraph
+// (torch.cuda.CUDAGraph on ROCm). Ops write into caller-provided outputs ("out" style): the
+// engine owns static buffers, which is what graph replay needs.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <torch/library.h>
+
+#include "bfly_kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+inline bfly::bf16* bf(const Tensor& t) { return reinterpret_cast<bfly::bf16*>(t.data_ptr()); }
+
+#define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_INNER(t) TORCH_CHECK((t).stride(-1) == 1, #t " must have unit inner stride")
+#define CHECK_ALIGN16(t) \
+  TORCH_CHECK(reinterpret_cast<uintptr_t>((t).data_ptr()) % 16 == 0, #t " must be 16-B aligned")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+
+void rms_norm(const Tensor& x, const Tensor& w, double eps, Tensor& out,
+              const c10::optional<Tensor>& residual) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "rms_norm expects 2-D x/out");
+  CHECK_INNER(x); CHECK_INNER(out); CHECK_ALIGN16(x); CHECK_ALIGN16(out);
+  const int rows = x.size(0), dim = x.size(1);
+  TORCH_CHECK(dim % 8 == 0 && dim <= 16384, "rms_norm: dim must be a multiple of 8, <= 16384");
+  TORCH_CHECK(w.numel() == dim && w.is_contiguous(), "rms_norm: weight shape");
+  TORCH_CHECK(out.size(0) == rows && out.size(1) == dim, "rms_norm: out shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "rms_norm: row strides % 8");
+  bfly::bf16* res = nullptr;
+  if (residual.has_value()) {
+    const Tensor& r = *residual;
+    CHECK_BF16(r);
+    TORCH_CHECK(r.is_contiguous() && r.size(0) == rows && r.size(1) == dim, "rms_norm: residual");
+    res = bf(r);
+  }
+  c10::hip::HIPGuard g(x.device());
+  bfly::launch_rmsnorm(bf(x), x.stride(0), res, bf(w), bf(out), out.stride(0), rows, dim,
+                       (float)eps, res != nullptr, cur_stream());
+}
+
+void layer_norm(const Tensor& x, const Tensor& w, const Tensor& b, double eps, Tensor& out,
+                const c10::optional<Tensor>& residual) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(b); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && out.is_contiguous(), "layer_norm: 2-D contiguous");
+  const int rows = x.size(0), dim = x.size(1);
+  TORCH_CHECK(dim % 8 == 0 && dim <= 16384, "layer_norm: dim");
+  TORCH_CHECK(w.numel() == dim && b.numel() == dim, "layer_norm: params");
+  bfly::bf16* res = nullptr;
+  if (residual.has_value()) {
+    TORCH_CHECK(residual->is_contiguous() && residual->sizes() == x.sizes(), "layer_norm: residual");
+    res = bf(*residual);
+  }
+  c10::hip::HIPGuard g(x.device());
+  bfly::launch_layernorm(bf(x), res, bf(w), bf(b), bf(out), rows, dim, (float)eps, res != nullptr,
+                         cur_stream());
+}
+
+void rope_kv(Tensor& qkv, const Tensor& positions, const Tensor& cos_t, const Tensor& sin_t,
+             int64_t num_q_heads, int64_t num_kv_heads, const c10::optional<Tensor>& slots,
+             const c10::optional<Tensor>& k_cache, const c10::optional<Tensor>& v_cache) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous(), "rope_kv: qkv must be 2-D contiguous");
+  const int T = qkv.size(0);
+  const int H = num_q_heads + 2 * num_kv_heads;
+  TORCH_CHECK(qkv.size(1) % H == 0, "rope_kv: row length not divisible by heads");
+  const int D = qkv.size(1) / H;
+  TORCH_CHECK(D == 128 || D == 64, "rope_kv: head_dim must be 64 or 128");
+  CHECK_I32(positions);
+  TORCH_CHECK(positions.numel() == T && positions.is_contiguous(), "rope_kv: positions");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat, "rope_kv: f32 tables");
+  TORCH_CHECK(cos_t.is_contiguous() && sin_t.is_contiguous() && cos_t.size(-1) == D / 2 &&
+                  sin_t.sizes() == cos_t.sizes(), "rope_kv: table shape [max_pos, D/2]");
+  const int* sl = nullptr;
+  bfly::bf16 *kc = nullptr, *vc = nullptr;
+  int BS = 1;
+  if (slots.has_value()) {
+    CHECK_I32(*slots);
+    TORCH_CHECK(slots->numel() == T, "rope_kv: slots");
+    TORCH_CHECK(k_cache.has_value() && v_cache.has_value(), "rope_kv: caches required with slots");
+    const Tensor& K = *k_cache;
+    const Tensor& V = *v_cache;
+    CHECK_BF16(K); CHECK_BF16(V);
+    TORCH_CHECK(K.dim() == 4 && K.is_contiguous() && K.size(1) == num_kv_heads && K.size(3) == D,
+                "rope_kv: k_cache must be [blocks, Hkv, BS, D]");
+    TORCH_CHECK(V.dim() == 4 && V.is_contiguous() && V.size(1) == num_kv_heads && V.size(2) == D &&
+                    V.size(3) == K.size(2) && V.size(0) == K.size(0),
+                "rope_kv: v_cache must be [blocks, Hkv, D, BS]");
+    sl = slots->data_ptr<int>();
+    kc = bf(K);
+    vc = bf(V);
+    BS = K.size(2);
+  }
+  c10::hip::HIPGuard g(qkv.device());
+  bfly::launch_rope_kv(bf(qkv), T, num_q_heads, num_kv_heads, D, positions.data_ptr<int>(),
+                       cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), sl, kc, vc, BS,
+                       cur_stream());
+}
+
+void kv_append(const Tensor& k, const Tensor& v, const Tensor& slots, Tensor& k_cache,
+               Tensor& v_cache) {
+  CHECK_GPU(k); CHECK_BF16(k); CHECK_BF16(v); CHECK_I32(slots);
+  TORCH_CHECK(k.dim() == 3 && v.dim() == 3 && k.sizes() == v.sizes(), "kv_append: [T, Hkv, D]");
+  TORCH_CHECK(k.stride(2) == 1 && k.stride(1) == k.size(2) && v.stride(2) == 1 &&
+                  v.stride(1) == v.size(2), "kv_append: rows must be dense over heads");
+  const int T = k.size(0), Hkv = k.size(1), D = k.size(2);
+  TORCH_CHECK(D == 128 || D == 64, "kv_append: head_dim");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "kv_append: k_cache");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == D, "kv_append: v_cache");
+  TORCH_CHECK(slots.numel() == T, "kv_append: slots");
+  c10::hip::HIPGuard g(k.device());
+  bfly::launch_kv_append(bf(k), k.stride(0), bf(v), v.stride(0), slots.data_ptr<int>(),
+                         bf(k_cache), bf(v_cache), T, Hkv, D, k_cache.size(2), cur_stream());
+}
+
+void silu_mul(const Tensor& gu, Tensor& out, int64_t interleave) {
+  CHECK_GPU(gu); CHECK_BF16(gu); CHECK_BF16(out);
+  TORCH_CHECK(gu.is_contiguous() && out.is_contiguous(), "silu_mul: contiguous");
+  const int ffn = out.size(-1);
+  TORCH_CHECK(gu.size(-1) == 2 * ffn && ffn % 8 == 0, "silu_mul: shapes");
+  TORCH_CHECK(interleave == 0 || (interleave % 8 == 0 && ffn % interleave == 0), "silu_mul: interleave");
+  const long rows = out.numel() / ffn;
+  TORCH_CHECK(gu.numel() == rows * 2 * ffn, "silu_mul: rows");
+  c10::hip::HIPGuard g(gu.device());
+  bfly::launch_silu_mul(bf(gu), bf(out), rows, ffn, interleave, cur_stream());
+}
+
+void gelu(const Tensor& x, Tensor& out) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(out);
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() == out.numel() &&
+                  x.numel() % 8 == 0, "gelu: shapes");
+  c10::hip::HIPGuard g(x.device());
+  bfly::launch_gelu(bf(x), bf(out), x.numel(), cur_stream());
+}
+
+void add(const Tensor& a, const Tensor& b, Tensor& out) {
+  CHECK_GPU(a); CHECK_BF16(a); CHECK_BF16(b); CHECK_BF16(out);
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && out.is_contiguous() &&
+                  a.numel() == b.numel() && a.numel() == out.numel() && a.numel() % 8 == 0,
+              "add: shapes");
+  c10::hip::HIPGuard g(a.device());
+  bfly::launch_add(bf(a), bf(b), bf(out), a.numel(), cur_stream());
+}
+
+void embed(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) {
+  CHECK_GPU(ids); CHECK_I32(ids); CHECK_BF16(table); CHECK_BF16(out);
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && out.is_contiguous(), "embed: layout");
+  const int T = ids.numel(), dim = table.size(1);
+  TORCH_CHECK(dim % 8 == 0 && out.numel() == (long)T * dim, "embed: shapes");
+  c10::hip::HIPGuard g(ids.device());
+  bfly::launch_embed(ids.data_ptr<int>(), bf(table), bf(out), T, dim, vstart, table.size(0),
+                     cur_stream());
+}
+
+void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
+            const c10::optional<Tensor>& seeds, int64_t vstart, Tensor& out_ids,
+            Tensor& out_scores, Tensor& workspace) {
+  CHECK_GPU(logits); CHECK_BF16(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0, "sample: logits");
+  CHECK_ALIGN16(logits);
+  const int rows = logits.size(0), V = logits.size(1);
+  CHECK_I32(out_ids);
+  TORCH_CHECK(out_ids.numel() == rows && out_scores.numel() == rows &&
+                  out_scores.scalar_type() == at::kFloat, "sample: outputs");
+  TORCH_CHECK(workspace.scalar_type() == at::kLong &&
+                  workspace.numel() >= (long)rows * bfly::kSampleMaxChunks, "sample: workspace");
+  const float* tp = nullptr;
+  const long* sp = nullptr;
+  if (temps.has_value()) {
+    TORCH_CHECK(temps->scalar_type() == at::kFloat && temps->numel() == rows, "sample: temps");
+    tp = temps->data_ptr<float>();
+  }
+  if (seeds.has_value()) {
+    TORCH_CHECK(seeds->scalar_type() == at::kLong && seeds->numel() == rows, "sample: seeds");
+    sp = seeds->data_ptr<int64_t>();
+  }
+  c10::hip::HIPGuard g(logits.device());
+  bfly::launch_sample(bf(logits), logits.stride(0), rows, V, vstart, tp, sp,
+                      reinterpret_cast<uint64_t*>(workspace.data_ptr()), out_ids.data_ptr<int>(),
+                      out_scores.data_ptr<float>(), cur_stream());
+}
+
+int64_t gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
+  return (int64_t)bfly::gemm_workspace_bytes(M, N, K);
+}
+
+std::vector<int64_t> gemm_plan(int64_t M, int64_t N, int64_t K) {
+  const bfly::GemmPlan p = bfly::plan_gemm(M, N, K);
+  return {p.kind, p.mt, p.nt, p.bm, p.bn, p.sk};
+}
+
+void gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& bias,
+          int64_t epilogue, const c10::optional<Tensor>& workspace) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm: 2-D operands");
+  CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm: K mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm: row strides % 8");
+  TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64, got ", K);
+  TORCH_CHECK(N % 32 == 0, "gemm: N must be a multiple of 32, got ", N);
+  const bfly::GemmPlan plan = bfly::plan_gemm(M, N, K);
+  if (plan.kind == 1) TORCH_CHECK(N % 128 == 0, "gemm: N must be a multiple of 128 for M > 64, got ", N);
+  const int nout = epilogue == bfly::EPI_SILU ? N / 2 : N;
+  TORCH_CHECK(out.size(0) == M && out.size(1) == nout, "gemm: out shape");
+  const bfly::bf16* bp = nullptr;
+  if (epilogue == bfly::EPI_BIAS) {
+    TORCH_CHECK(bias.has_value() && bias->numel() == N, "gemm: bias required");
+    CHECK_BF16(*bias);
+    bp = bf(*bias);
+  }
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  if (workspace.has_value()) {
+    ws = reinterpret_cast<float*>(workspace->data_ptr());
+    ws_bytes = workspace->numel() * workspace->element_size();
+  }
+  c10::hip::HIPGuard g(x.device());
+  const int rc = bfly::launch_gemm(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, epilogue, bp,
+                                   bf(out), out.stride(0), ws, ws_bytes, cur_stream());
+  TORCH_CHECK(rc == 0, "gemm: unsupported shape M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
+}
+
+int64_t attn_decode_splits(int64_t max_ctx, int64_t part_tokens) {
+  return bfly::attn_decode_splits(max_ctx, part_tokens);
+}
+
+void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
+                 const Tensor& block_tables, const Tensor& ctx_lens, double scale,
+                 int64_t max_ctx, int64_t part_tokens, Tensor& out,
+                 const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "attn_decode: q [B, Hq, D]");
+  const int B = q.size(0), Hq = q.size(1), D = q.size(2);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "attn_decode: caches");
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2);
+  TORCH_CHECK(k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS, "attn_decode: cache dims");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)B * Hq * D, "attn_decode: out");
+  CHECK_I32(block_tables); CHECK_I32(ctx_lens);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1,
+              "attn_decode: block_tables");
+  TORCH_CHECK(ctx_lens.numel() >= B, "attn_decode: ctx_lens");
+  TORCH_CHECK((long)block_tables.size(1) * BS >= max_ctx, "attn_decode: block table too narrow for max_ctx");
+  const int nsplit = bfly::attn_decode_splits(max_ctx, part_tokens);
+  float *po = nullptr, *pml = nullptr;
+  if (nsplit > 1) {
+    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "attn_decode: partial buffers required");
+    TORCH_CHECK(part_o->numel() >= (long)B * Hkv * nsplit * 16 * D, "attn_decode: part_o too small");
+    TORCH_CHECK(part_ml->numel() >= (long)B * Hkv * nsplit * 16 * 2, "attn_decode: part_ml too small");
+    po = part_o->data_ptr<float>();
+    pml = part_ml->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(q.device());
+  const int rc = bfly::launch_attn_decode(bf(q), q.stride(0), bf(k_cache), bf(v_cache),
+                                          block_tables.data_ptr<int>(), block_tables.stride(0),
+                                          ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale,
+                                          max_ctx, part_tokens, bf(out), po, pml, cur_stream());
+  TORCH_CHECK(rc == 0, "attn_decode: unsupported configuration (rc=", rc, ")");
+}
+
+void attn_prefill(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& cu_seqlens,
+                  int64_t max_seqlen, double scale, bool causal, Tensor& out) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_BF16(out);
+  for (const Tensor* t : {&q, &k, &v, (const Tensor*)&out})
+    TORCH_CHECK(t->dim() == 3 && t->stride(2) == 1 && t->stride(1) == t->size(2) && t->stride(0) % 8 == 0,
+                "attn_prefill: [T, H, D] with dense heads");
+  const int Hq = q.size(1), Hkv = k.size(1), D = q.size(2);
+  TORCH_CHECK(k.size(2) == D && v.size(2) == D && v.size(1) == Hkv, "attn_prefill: dims");
+  TORCH_CHECK(out.size(1) == Hq && out.size(2) == D && out.size(0) == q.size(0), "attn_prefill: out");
+  CHECK_I32(cu_seqlens);
+  const int nseq = cu_seqlens.numel() - 1;
+  c10::hip::HIPGuard g(q.device());
+  const int rc = bfly::launch_attn_prefill(bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0),
+                                           cu_seqlens.data_ptr<int>(), nseq, max_seqlen, Hq, Hkv, D,
+                                           (float)scale, causal, bf(out), out.stride(0), cur_stream());
+  TORCH_CHECK(rc == 0, "attn_prefill: unsupported configuration (rc=", rc, ")");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(bfly, m) {
+  m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out, Tensor(b!)? residual) -> ()");
+  m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor(a!) out, Tensor(b!)? residual) -> ()");
+  m.def("rope_kv(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, int num_q_heads, "
+        "int num_kv_heads, Tensor? slots, Tensor(b!)? k_cache, Tensor(c!)? v_cache) -> ()");
+  m.def("kv_append(Tensor k, Tensor v, Tensor slots, Tensor(a!) k_cache, Tensor(b!) v_cache) -> ()");
+  m.def("silu_mul(Tensor gu, Tensor(a!) out, int interleave) -> ()");
+  m.def("gelu(Tensor x, Tensor(a!) out) -> ()");
+  m.def("add(Tensor a, Tensor b, Tensor(a!) out) -> ()");
+  m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vstart) -> ()");
+  m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
+        "Tensor(b!) out_scores, Tensor(c!) workspace) -> ()");
+  m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
+  m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
+  m.def("gemm_plan(int M, int N, int K) -> int[]", &gemm_plan);
+  m.def("attn_decode_splits(int max_ctx, int part_tokens) -> int", &attn_decode_splits);
+  m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
+        "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
+        "Tensor(c!)? part_ml) -> ()");
+  m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
+        "bool causal, Tensor(a!) out) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
+  m.impl("rms_norm", &rms_norm);
+  m.impl("layer_norm", &layer_norm);
+  m.impl("rope_kv", &rope_kv);
+  m.impl("kv_append", &kv_append);
+  m.impl("silu_mul", &silu_mul);
+  m.impl("gelu", &gelu);
+  m.impl("add", &add);
+  m.impl("embed", &embed);
+  m.impl("sample", &sample);
+  m.impl("gemm", &gemm);
+  m.impl("attn_decode", &attn_decode);
+  m.impl("attn_prefill", &attn_prefill);
+}

@@ -1,0 +1,68 @@
+// Host-side launch API of the butterfly_amd HIP kernels. Every launcher is stream-ordered,
+// allocation-free and synchronisation-free, so it can be captured into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace bfly {
+
+typedef __bf16 bf16;
+
+enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_SILU = 2 };
+
+struct GemmPlan {
+  int kind;  // 0 = skinny (decode), 1 = LDS-tiled
+  int mt, nt;
+  int bm, bn;
+  int sk;    // split-K factor
+};
+
+// norm.hip
+void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y,
+                    long y_stride, int rows, int dim, float eps, bool add_residual,
+                    hipStream_t stream);
+void launch_layernorm(const bf16* x, bf16* residual, const bf16* w, const bf16* b, bf16* y,
+                      int rows, int dim, float eps, bool add_residual, hipStream_t stream);
+
+// rope.hip
+void launch_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* positions,
+                    const float* cos_t, const float* sin_t, const int* slots, bf16* k_cache,
+                    bf16* v_cache, int block_size, hipStream_t stream);
+void launch_kv_append(const bf16* k, long k_stride, const bf16* v, long v_stride,
+                      const int* slots, bf16* k_cache, bf16* v_cache, int T, int Hkv, int D,
+                      int block_size, hipStream_t stream);
+
+// elementwise.hip
+void launch_silu_mul(const bf16* gu, bf16* out, long rows, int ffn, int interleave,
+                     hipStream_t stream);
+void launch_gelu(const bf16* x, bf16* out, long n, hipStream_t stream);
+void launch_add(const bf16* a, const bf16* b, bf16* out, long n, hipStream_t stream);
+void launch_embed(const int* ids, const bf16* table, bf16* out, int T, int dim, int vstart,
+                  int vlocal, hipStream_t stream);
+
+// sample.hip
+constexpr int kSampleMaxChunks = 64;
+void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vstart,
+                   const float* temps, const long* seeds, uint64_t* workspace, int* out_ids,
+                   float* out_scores, hipStream_t stream);
+
+// gemm.hip
+GemmPlan plan_gemm(int M, int N, int K);
+size_t gemm_workspace_bytes(int M, int N, int K);
+int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
+                const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
+                hipStream_t stream);
+
+// attention.hip
+int attn_decode_splits(int max_ctx, int part_tokens);
+int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
+                       const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
+                       int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
+                       bf16* out, float* part_o, float* part_ml, hipStream_t stream);
+int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
+                        long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
+                        int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
+                        hipStream_t stream);
+
+}  // namespace bfly

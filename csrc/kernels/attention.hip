@@ -1,0 +1,419 @@
+// Attention kernels (K3 flash prefill, K4 paged decode, split-K combine) for GQA, head_dim 128.
+//
+// Decode (attn_decode_kernel): one workgroup per (context split, kv head, sequence), 4 waves
+// that walk the split's KV pages round-robin. The whole query group of a kv head (Hq/Hkv <= 16
+// rows, padded to 16) rides in ONE mfma_f32_16x16x32_bf16 B operand, so every K/V byte
+// streamed from HBM feeds all query heads that share it. K/V go straight to VGPRs (decode
+// row of cdna_hip_programming.md §5 table); no LDS round trip.
+//   S^T = K . Q^T  ("swapped", K is the A operand): lane column = query row, so the softmax
+//   state (m, l) is per lane and the P^T tile is already in the B-operand layout of the PV
+//   product O^T = V^T . P^T. The key order inside each 16x16 S tile is chosen by which K row
+//   each lane loads (sigma below) so that the 8 keys a lane holds for the PV step are 8
+//   CONSECUTIVE keys: with V^T pages ([D][BS], written transposed by rope_kv) the PV A
+//   operand is then one 16-B load.
+//   Split-K over the context (flash-decoding) with an f32 partial combine kernel.
+//
+// Prefill (attn_prefill_kernel): causal varlen flash attention. Workgroup = 128 query rows
+// of one head (4 waves x 32 rows), KV tiles of 64 keys register-staged into a double-buffered,
+// XOR-swizzled LDS image (cdna_hip_programming.md T10 image (b)): K is read by ds_read_b128
+// as the 32x32x16 A operand of S^T = K . Q^T, V by ds_read_b64_tr_b16 as the A operand of
+// O^T = V^T . P^T; the S^T accumulator is converted in registers into the P^T B operand
+// (§3 "An accumulator tile as the next MFMA's operand").
+#include "bfly_common.h"
+#include "bfly_kernels.h"
+
+namespace bfly {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4* lds_s4_ptr;
+
+constexpr int kAttnThreads = 256;
+constexpr float kNegInf = -INFINITY;
+
+// ---------------------------------------------------------------------------------------
+// Decode
+// ---------------------------------------------------------------------------------------
+template <int D, int BS>
+__global__ void __launch_bounds__(kAttnThreads)
+attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k_cache,
+                   const bf16* __restrict__ v_cache, const int* __restrict__ block_tables,
+                   int bt_stride, const int* __restrict__ ctx_lens, int Hq, int Hkv,
+                   float scale_log2, int part_tokens, bf16* __restrict__ out,
+                   float* __restrict__ part_o, float* __restrict__ part_ml) {
+  static_assert(D == 128 && BS == 32, "decode kernel is specialised for D=128, BS=32");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int nsplit = gridDim.x;
+  const int G = Hq / Hkv;
+  const int ctx = ctx_lens[b];
+  const int tok0 = s * part_tokens;
+  const int tok1 = min(ctx, tok0 + part_tokens);
+  const long part_base = ((long)(b * Hkv + h) * nsplit + s);
+
+  __shared__ float s_o[4][8][4][64];
+  __shared__ float s_m[4][16], s_l[4][16];
+
+  if (tok0 >= tok1) {  // empty split: mark it so the combine kernel skips it
+    if (nsplit > 1 && threadIdx.x < 16) {
+      part_ml[(part_base * 16 + threadIdx.x) * 2 + 0] = kNegInf;
+      part_ml[(part_base * 16 + threadIdx.x) * 2 + 1] = 0.f;
+    }
+    return;
+  }
+
+  const int g = lane >> 4, r = lane & 15;
+  // Q^T fragment (B operand): lane holds Q[row r][d = 32g + 8ds + j]; rows >= G are zero.
+  bf16x8 qf[4];
+  {
+    const int qr = r < G ? r : 0;
+    const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (long)b * q_stride + (long)(h * G + qr) * D + 32 * g);
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      qf[ds] = qp[ds];
+      if (r >= G) qf[ds] = bf16x8{};
+    }
+  }
+
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = kNegInf, l = 0.f;
+
+  const int p0 = tok0 / BS, p1 = (tok1 + BS - 1) / BS;
+  const int* bt = block_tables + (long)b * bt_stride;
+  for (int p = p0 + wid; p < p1; p += 4) {
+    const long blk = bt[p];
+    const bf16* kb = k_cache + ((blk * Hkv + h) * BS) * D;
+    const bf16* vb = v_cache + (blk * Hkv + h) * (long)D * BS;
+    // K rows: tile kt, lane row r -> key sigma(kt, r) = 8*(r>>2) + 4*kt + (r&3)
+    bf16x8 kf[2][4];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int key = 8 * (r >> 2) + 4 * kt + (r & 3);
+      const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + key * D + 32 * g);
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) kf[kt][ds] = ld_nt(kp + ds);
+    }
+    // V^T rows: d = 16dt + r, keys 8g .. 8g+7
+    bf16x8 vf[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vf[dt] = ld_nt(reinterpret_cast<const bf16x8*>(vb + (16 * dt + r) * BS + 8 * g));
+
+    f32x4 st[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      st[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) st[kt] = mfma16(kf[kt][ds], qf[ds], st[kt]);
+    }
+    // st[kt][i] = S[key = p*BS + 8g + 4kt + i][query r]
+    float x[8];
+    float tmax = kNegInf;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = p * BS + 8 * g + 4 * kt + i;
+        const float v = key < tok1 ? st[kt][i] * scale_log2 : kNegInf;
+        x[kt * 4 + i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float mb = mn == kNegInf ? 0.f : mn;
+    const float alpha = exp2f(m - mb);
+    bf16x8 pb;
+    float ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pv = exp2f(x[j] - mb);
+      ps += pv;
+      pb[j] = f2bf(pv);
+    }
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      o[dt] *= alpha;
+      o[dt] = mfma16(vf[dt], pb, o[dt]);
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+
+  // Merge the 4 waves: o[dt][i] = O[query r][d = 16dt + 4g + i]
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_o[wid][dt][i][lane] = o[dt][i];
+  if (g == 0) {
+    s_m[wid][r] = m;
+    s_l[wid][r] = l;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 16 * D; e += kAttnThreads) {
+    const int qr = e / D, d = e % D;
+    if (qr >= G) continue;
+    float M = kNegInf;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][qr]);
+    const float Mb = M == kNegInf ? 0.f : M;
+    float L = 0.f, O = 0.f;
+    const int dt = d >> 4, i = d & 3, ln = qr + 16 * ((d & 15) >> 2);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = exp2f(s_m[w][qr] - Mb);
+      L += f * s_l[w][qr];
+      O += f * s_o[w][dt][i][ln];
+    }
+    if (nsplit == 1) {
+      out[((long)b * Hq + h * G + qr) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+    } else {
+      part_o[(part_base * 16 + qr) * D + d] = O;
+      if (d == 0) {
+        part_ml[(part_base * 16 + qr) * 2 + 0] = M;
+        part_ml[(part_base * 16 + qr) * 2 + 1] = L;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(kAttnThreads)
+attn_decode_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
+                           int nsplit, int Hq, int Hkv, bf16* __restrict__ out) {
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int G = Hq / Hkv;
+  const long base = (long)(b * Hkv + h) * nsplit;
+  for (int e = threadIdx.x; e < G * D; e += kAttnThreads) {
+    const int qr = e / D, d = e % D;
+    float M = kNegInf;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[((base + s) * 16 + qr) * 2]);
+    const float Mb = M == kNegInf ? 0.f : M;
+    float L = 0.f, O = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const float ms = part_ml[((base + s) * 16 + qr) * 2];
+      if (ms == kNegInf) continue;
+      const float f = exp2f(ms - Mb);
+      L += f * part_ml[((base + s) * 16 + qr) * 2 + 1];
+      O += f * part_o[((base + s) * 16 + qr) * D + d];
+    }
+    out[((long)b * Hq + h * G + qr) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Prefill
+// ---------------------------------------------------------------------------------------
+constexpr int kPfBQ = 128, kPfBKV = 64;
+
+// Byte offset of 16-B chunk `ch` (0..15) of row `row` in a [rows][128 x bf16] LDS image
+// (T10 image (b): conflict-free for 32x32x16 row reads and for the transposed reads).
+__device__ __forceinline__ int pf_off(int row, int ch) {
+  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+template <int D>
+__global__ void __launch_bounds__(kAttnThreads)
+attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
+                    long k_stride, const bf16* __restrict__ v, long v_stride,
+                    const int* __restrict__ cu_seqlens, int Hq, int Hkv, float scale_log2,
+                    int causal, bf16* __restrict__ out, long o_stride) {
+  static_assert(D == 128, "prefill kernel is specialised for D=128");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE_BYTES = kPfBKV * D * 2;  // 16 KiB
+  // smem = [K0 | V0 | K1 | V1]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int seq = blockIdx.y, h = blockIdx.z;
+  const int s0 = cu_seqlens[seq];
+  const int L = cu_seqlens[seq + 1] - s0;
+  const int q0 = blockIdx.x * kPfBQ;
+  if (q0 >= L) return;
+  const int kh = h / (Hq / Hkv);
+  const int hi = lane >> 5, c = lane & 31;
+
+  // Q^T fragments (B operand of 32x32x16): lane holds Q[row c][d = 16ks + 8hi + j].
+  const int qrow = q0 + 32 * wid + c;
+  bf16x8 qf[8];
+  {
+    const int qr = qrow < L ? qrow : L - 1;
+    const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (long)(s0 + qr) * q_stride + (long)h * D + 8 * hi);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = qp[2 * ks];
+  }
+
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+  float m = kNegInf, lsum = 0.f;
+
+  const int kv_end = causal ? min(L, q0 + kPfBQ) : L;
+  const int ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
+  const int wave_qmax = q0 + 32 * wid + 31;
+
+  // Register staging: 64 rows x 16 chunks = 1024 chunks per tile; 4 per thread per operand.
+  bf16x8 rk[4], rv[4];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cl = i * kAttnThreads + threadIdx.x;
+      const int row = cl >> 4, ch = cl & 15;
+      int key = t * kPfBKV + row;
+      key = key < L ? key : L - 1;
+      rk[i] = *reinterpret_cast<const bf16x8*>(k + (long)(s0 + key) * k_stride + (long)kh * D + ch * 8);
+      rv[i] = *reinterpret_cast<const bf16x8*>(v + (long)(s0 + key) * v_stride + (long)kh * D + ch * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* kb = smem + buf * 2 * TILE_BYTES;
+    char* vb = kb + TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cl = i * kAttnThreads + threadIdx.x;
+      const int row = cl >> 4, ch = cl & 15;
+      *reinterpret_cast<bf16x8*>(kb + pf_off(row, ch)) = rk[i];
+      *reinterpret_cast<bf16x8*>(vb + pf_off(row, ch)) = rv[i];
+    }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load_tile(t + 1);
+    const int kv0 = t * kPfBKV;
+    const char* kb = smem + (t & 1) * 2 * TILE_BYTES;
+    const char* vb = kb + TILE_BYTES;
+    if (!(causal && kv0 > wave_qmax)) {
+      // S^T tiles: st[kt][r] = S[key = kv0 + 32kt + (r&3) + 8(r>>2) + 4hi][query c]
+      f32x16 st[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        st[kt] = f32x16{};
+        const int row = 32 * kt + c;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + pf_off(row, 2 * ks + hi));
+          st[kt] = mfma32(kf, qf[ks], st[kt]);
+        }
+      }
+      float tmax = kNegInf;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kv0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          const bool ok = key < L && (!causal || key <= qrow);
+          const float xv = ok ? st[kt][r] * scale_log2 : kNegInf;
+          st[kt][r] = xv;
+          tmax = fmaxf(tmax, xv);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m, tmax);
+      const float mb = mn == kNegInf ? 0.f : mn;
+      const float alpha = exp2f(m - mb);
+      m = mn;
+      bf16x8 pb[2][2];
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float pv = exp2f(st[kt][8 * s + j] - mb);
+            ps += pv;
+            pb[kt][s][j] = f2bf(pv);
+          }
+      lsum = lsum * alpha + ps;
+      // O^T[d][q] += V^T[d][key] P^T[key][q]; A operand via transposed LDS reads.
+      const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        o[dt] *= alpha;
+        const int ch = 4 * dt + 2 * tg + (tp >> 1);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const int krow = 32 * kt + 16 * s + 4 * hi + tq;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s4_ptr)(vb + pf_off(krow, ch) + 8 * (tp & 1)));
+            const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s4_ptr)(vb + pf_off(krow + 8, ch) + 8 * (tp & 1)));
+            bf16x8 vf;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              vf[j] = __builtin_bit_cast(bf16, lo[j]);
+              vf[4 + j] = __builtin_bit_cast(bf16, hi4[j]);
+            }
+            o[dt] = mfma32(vf, pb[kt][s], o[dt]);
+          }
+      }
+    }
+    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (qrow >= L) return;
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16* op = out + (long)(s0 + qrow) * o_stride + (long)h * D;
+  // o[dt][r] = O[query c][d = 32dt + (r&3) + 8(r>>2) + 4hi]
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      bf16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = f2bf(o[dt][4 * a + j] * inv);
+      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * a + 4 * hi) = w;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------------
+int attn_decode_splits(int max_ctx, int part_tokens) {
+  return (max_ctx + part_tokens - 1) / part_tokens;
+}
+
+int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
+                       const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
+                       int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
+                       bf16* out, float* part_o, float* part_ml, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (D != 128 || block_size != 32 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
+  if (part_tokens % block_size != 0) return -2;
+  const int nsplit = attn_decode_splits(max_ctx, part_tokens);
+  if (nsplit > 1 && (part_o == nullptr || part_ml == nullptr)) return -3;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(nsplit, Hkv, B);
+  attn_decode_kernel<128, 32><<<grid, kAttnThreads, 0, stream>>>(
+      q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, Hq, Hkv, scale_log2,
+      part_tokens, out, part_o, part_ml);
+  if (nsplit > 1) {
+    dim3 g2(Hkv, B);
+    attn_decode_combine_kernel<128><<<g2, kAttnThreads, 0, stream>>>(part_o, part_ml, nsplit, Hq,
+                                                                     Hkv, out);
+  }
+  return 0;
+}
+
+int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
+                        long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
+                        int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
+                        hipStream_t stream) {
+  if (nseq <= 0 || max_seqlen <= 0) return 0;
+  if (D != 128 || Hq % Hkv != 0) return -1;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid((max_seqlen + kPfBQ - 1) / kPfBQ, nseq, Hq);
+  const size_t lds = 4 * kPfBKV * D * 2;  // 64 KiB: K,V x 2 buffers
+  attn_prefill_kernel<128><<<grid, kAttnThreads, lds, stream>>>(
+      q, q_stride, k, k_stride, v, v_stride, cu_seqlens, Hq, Hkv, scale_log2, causal ? 1 : 0,
+      out, o_stride);
+  return 0;
+}
+
+}  // namespace bfly

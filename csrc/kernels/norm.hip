@@ -1,0 +1,162 @@
+// RMSNorm / fused residual-add + RMSNorm / LayerNorm kernels (K5, K15 in SURVEY.md §2.7-K).
+//
+// One workgroup per row; each lane moves 16 B (8 x bf16) per access (Guideline 13).
+// The row is held in registers between the sum-of-squares pass and the scale pass, so
+// each element is read from HBM exactly once and written once.
+//   rows x dim, dim % 8 == 0, dim <= 8 * 8 * blockDim (checked on the host).
+#include "bfly_common.h"
+#include "bfly_kernels.h"
+
+namespace bfly {
+
+constexpr int kNormThreads = 256;
+constexpr int kNormMaxVec = 8;  // up to 8 x 16 B per lane -> dim <= 16384 at 256 threads
+
+template <int NV>
+__global__ void __launch_bounds__(kNormThreads)
+rmsnorm_kernel(const bf16* __restrict__ x, long x_stride, bf16* __restrict__ residual,
+               const bf16* __restrict__ w, bf16* __restrict__ y, long y_stride, int dim,
+               float eps, int add_residual) {
+  __shared__ float red[16];
+  const long row = blockIdx.x;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + row * x_stride);
+  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + row * (long)dim);
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + row * y_stride);
+  const int nvec = dim >> 3;
+  float v[NV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+      bf16x8 a = xr[c];
+      if (add_residual) {
+        bf16x8 r = rr[c];
+        bf16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // Round the sum to bf16 first: the residual stream is stored in bf16 and the
+          // normalised value must be computed from exactly what is stored.
+          s[j] = f2bf(bf2f(a[j]) + bf2f(r[j]));
+          v[i][j] = bf2f(s[j]);
+        }
+        rr[c] = s;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(a[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)dim + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+      bf16x8 g = wr[c], o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
+      yr[c] = o;
+    }
+  }
+}
+
+template <int NV>
+__global__ void __launch_bounds__(kNormThreads)
+layernorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ residual,
+                 const bf16* __restrict__ w, const bf16* __restrict__ b,
+                 bf16* __restrict__ y, int dim, float eps, int add_residual) {
+  __shared__ float red[16];
+  const long row = blockIdx.x;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + row * (long)dim);
+  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + row * (long)dim);
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
+  const bf16x8* br = reinterpret_cast<const bf16x8*>(b);
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + row * (long)dim);
+  const int nvec = dim >> 3;
+  float v[NV][8];
+  float s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+      bf16x8 a = xr[c];
+      if (add_residual) {
+        bf16x8 r = rr[c], s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] = f2bf(bf2f(a[j]) + bf2f(r[j]));
+          v[i][j] = bf2f(s[j]);
+        }
+        rr[c] = s;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(a[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s1 += v[i][j];
+    }
+  }
+  const float mean = block_sum(s1, red) / (float)dim;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        s2 += d * d;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum(s2, red) / (float)dim + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * kNormThreads;
+    if (c < nvec) {
+      bf16x8 g = wr[c], bb = br[c], o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf((v[i][j] - mean) * inv * bf2f(g[j]) + bf2f(bb[j]));
+      yr[c] = o;
+    }
+  }
+}
+
+void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y,
+                    long y_stride, int rows, int dim, float eps, bool add_residual,
+                    hipStream_t stream) {
+  if (rows <= 0) return;
+  const int nvec = dim / 8;
+  const int nv = (nvec + kNormThreads - 1) / kNormThreads;
+  dim3 grid(rows), block(kNormThreads);
+  const int ar = add_residual ? 1 : 0;
+  switch (nv) {
+    case 1: rmsnorm_kernel<1><<<grid, block, 0, stream>>>(x, x_stride, residual, w, y, y_stride, dim, eps, ar); break;
+    case 2: rmsnorm_kernel<2><<<grid, block, 0, stream>>>(x, x_stride, residual, w, y, y_stride, dim, eps, ar); break;
+    case 3:
+    case 4: rmsnorm_kernel<4><<<grid, block, 0, stream>>>(x, x_stride, residual, w, y, y_stride, dim, eps, ar); break;
+    default: rmsnorm_kernel<kNormMaxVec><<<grid, block, 0, stream>>>(x, x_stride, residual, w, y, y_stride, dim, eps, ar); break;
+  }
+}
+
+void launch_layernorm(const bf16* x, bf16* residual, const bf16* w, const bf16* b, bf16* y,
+                      int rows, int dim, float eps, bool add_residual, hipStream_t stream) {
+  if (rows <= 0) return;
+  const int nvec = dim / 8;
+  const int nv = (nvec + kNormThreads - 1) / kNormThreads;
+  dim3 grid(rows), block(kNormThreads);
+  const int ar = add_residual ? 1 : 0;
+  switch (nv) {
+    case 1: layernorm_kernel<1><<<grid, block, 0, stream>>>(x, residual, w, b, y, dim, eps, ar); break;
+    case 2: layernorm_kernel<2><<<grid, block, 0, stream>>>(x, residual, w, b, y, dim, eps, ar); break;
+    case 3:
+    case 4: layernorm_kernel<4><<<grid, block, 0, stream>>>(x, residual, w, b, y, dim, eps, ar); break;
+    default: layernorm_kernel<kNormMaxVec><<<grid, block, 0, stream>>>(x, residual, w, b, y, dim, eps, ar); break;
+  }
+}
+
+}  // namespace bfly

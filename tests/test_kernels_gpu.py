@@ -1,0 +1,188 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference (ops/reference.py).
+
+Random normal (asymmetric) operands throughout: a symmetric or identity operand hides a
+transposed C-write (cdna_hip_programming.md §3, "Always A=I-check with ASYMMETRIC B").
+"""
+import math
+
+import pytest
+import torch
+
+from butterfly_amd import ops
+from butterfly_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+
+def _close(a, b, atol, rtol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad}/{a.numel()} mismatches, max err {err.max().item():.4g}"
+
+
+def test_native_library_loaded():
+    assert ops.native_available(), ops._load_error
+
+
+@pytest.mark.parametrize("rows,dim", [(1, 768), (7, 4096), (64, 8192), (3, 16384)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rms_norm(rows, dim, with_res):
+    x = _bf(rows, dim, seed=1)
+    w = _bf(dim, seed=2)
+    res = _bf(rows, dim, seed=3) if with_res else None
+    res_ref = res.clone() if with_res else None
+    y = ops.rms_norm(x, w, 1e-5, residual=res)
+    y_ref = ref.rms_norm(x, w, 1e-5, residual=res_ref)
+    _close(y, y_ref, 2e-2, 2e-2)
+    if with_res:
+        _close(res, res_ref, 0, 0)
+
+
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layer_norm(with_res):
+    x = _bf(9, 768, seed=4)
+    w, b = _bf(768, seed=5), _bf(768, seed=6)
+    res = _bf(9, 768, seed=7) if with_res else None
+    res_ref = res.clone() if with_res else None
+    _close(ops.layer_norm(x, w, b, 1e-5, residual=res), ref.layer_norm(x, w, b, 1e-5, residual=res_ref), 3e-2, 2e-2)
+
+
+def test_rope_kv_and_cache():
+    T, Hq, Hkv, D, BS, nblk = 37, 8, 2, 128, 32, 6
+    qkv = _bf(T, (Hq + 2 * Hkv) * D, seed=8)
+    pos = torch.randint(0, 500, (T,), dtype=torch.int32, device=DEV)
+    cos, sin = ref.rope_tables(D, 1024, 500000.0, device=DEV)
+    slots = torch.randperm(nblk * BS, device=DEV)[:T].to(torch.int32)
+    slots[3] = -1
+    kc = torch.zeros(nblk, Hkv, BS, D, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros(nblk, Hkv, D, BS, dtype=torch.bfloat16, device=DEV)
+    q2, kc2, vc2 = qkv.clone(), kc.clone(), vc.clone()
+    ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, slots, kc, vc)
+    ref.rope_kv(q2, pos, cos, sin, Hq, Hkv, slots, kc2, vc2)
+    _close(qkv, q2, 1e-2, 1e-2)
+    _close(kc, kc2, 1e-2, 1e-2)
+    _close(vc, vc2, 0, 0)
+
+
+@pytest.mark.parametrize("interleave", [0, 16])
+def test_silu_mul(interleave):
+    gu = _bf(13, 2 * 1024, seed=9)
+    _close(ops.silu_mul(gu, interleave=interleave), ref.silu_mul(gu, interleave=interleave), 1e-2, 1e-2)
+
+
+def test_gelu_add():
+    x, y = _bf(5, 3072, seed=10), _bf(5, 3072, seed=11)
+    _close(ops.gelu(x), ref.gelu(x), 1e-2, 1e-2)
+    _close(ops.add(x, y), ref.add(x, y), 1e-2, 1e-2)
+
+
+def test_embed_vocab_parallel():
+    table = _bf(1000, 512, seed=12)
+    ids = torch.tensor([0, 5, 999, 1000, 1500, 2999, 1234], dtype=torch.int32, device=DEV)
+    _close(ops.embed(ids, table, vstart=1000), ref.embed(ids, table, vstart=1000), 0, 0)
+
+
+@pytest.mark.parametrize("V", [1000, 32000, 128256])
+def test_sample_greedy(V):
+    logits = _bf(6, V, seed=13)
+    ids, scores = ops.sample(logits)
+    exp = logits.float().argmax(-1)
+    assert torch.equal(ids.long().cpu(), exp.cpu())
+    _close(scores, logits.float().max(-1).values, 1e-3, 1e-3)
+
+
+def test_sample_gumbel_matches_reference():
+    V = 4096
+    logits = _bf(3, V, seed=14)
+    temps = torch.tensor([0.0, 0.7, 1.3], device=DEV)
+    seeds = torch.tensor([1, 42, 12345], dtype=torch.int64, device=DEV)
+    ids, _ = ops.sample(logits, temps, seeds, vstart=0)
+    ids_ref, _ = ref.sample(logits.cpu(), temps.cpu(), seeds.cpu(), vstart=0)
+    assert ids.cpu().tolist() == ids_ref.tolist()
+
+
+GEMM_SHAPES = [
+    (1, 256, 1024), (5, 1280, 8192), (16, 4096, 4096), (33, 512, 768), (64, 2048, 1024),
+    (65, 256, 512), (128, 1024, 2048), (300, 384, 640), (1024, 1024, 1024), (7, 128256 // 8, 8192),
+]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+def test_gemm(M, N, K):
+    x = _bf(M, K, seed=15)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=16)
+    y = ops.linear(x, w)
+    _close(y, ref.linear(x, w), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 16, 40, 64, 200])
+def test_gemm_bias_and_silu(M):
+    K, N = 1024, 512
+    x = _bf(M, K, seed=17)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=18)
+    b = _bf(N, seed=19)
+    _close(ops.linear(x, w, bias=b), ref.linear(x, w, bias=b), 2e-2, 2e-2)
+    _close(ops.linear(x, w, epilogue="silu"), ref.linear(x, w, epilogue="silu"), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(8, 2), (4, 4), (64, 8)])
+def test_attn_prefill_varlen_causal(Hq, Hkv):
+    D = 128
+    lens = [1, 37, 128, 200]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    T = sum(lens)
+    qkv = _bf(T, (Hq + 2 * Hkv) * D, seed=20)
+    q = qkv[:, : Hq * D].view(T, Hq, D)
+    k = qkv[:, Hq * D: (Hq + Hkv) * D].view(T, Hkv, D)
+    v = qkv[:, (Hq + Hkv) * D:].view(T, Hkv, D)
+    scale = 1.0 / math.sqrt(D)
+    o = ops.attn_prefill(q, k, v, cu, max(lens), scale, True)
+    _close(o, ref.attn_prefill(q, k, v, cu, max(lens), scale, True), 2e-2, 2e-2)
+
+
+def test_attn_prefill_non_causal():
+    D, Hq, Hkv = 128, 4, 2
+    lens = [70, 130]
+    cu = torch.tensor([0, 70, 200], dtype=torch.int32, device=DEV)
+    q, k, v = _bf(200, Hq, D, seed=21), _bf(200, Hkv, D, seed=22), _bf(200, Hkv, D, seed=23)
+    o = ops.attn_prefill(q, k, v, cu, 130, 0.088, False)
+    _close(o, ref.attn_prefill(q, k, v, cu, 130, 0.088, False), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("part_tokens", [256, 4096])
+@pytest.mark.parametrize("Hq,Hkv", [(16, 2), (8, 8), (64, 8)])
+def test_attn_decode_paged(part_tokens, Hq, Hkv):
+    D, BS = 128, 32
+    lens = [1, 31, 32, 100, 700]
+    B = len(lens)
+    max_blocks = (max(lens) + BS - 1) // BS
+    nblk = B * max_blocks + 3
+    kc = _bf(nblk, Hkv, BS, D, seed=24)
+    vc = _bf(nblk, Hkv, D, BS, seed=25)
+    perm = torch.randperm(nblk)[: B * max_blocks].view(B, max_blocks).to(torch.int32).to(DEV)
+    ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    q = _bf(B, Hq, D, seed=26)
+    scale = 1.0 / math.sqrt(D)
+    o = ops.attn_decode(q, kc, vc, perm, ctx, scale, max(lens), part_tokens)
+    _close(o, ref.attn_decode(q, kc, vc, perm, ctx, scale), 2e-2, 2e-2)
+
+
+def test_attn_decode_strided_q():
+    # q as a view into a fused QKV row (row stride > Hq*D), as the model passes it
+    D, BS, Hq, Hkv, B = 128, 32, 8, 1, 3
+    qkv = _bf(B, (Hq + 2 * Hkv) * D, seed=27)
+    q = qkv[:, : Hq * D].view(B, Hq, D)
+    kc, vc = _bf(8, Hkv, BS, D, seed=28), _bf(8, Hkv, D, BS, seed=29)
+    bt = torch.arange(8, dtype=torch.int32, device=DEV).view(1, 8).repeat(B, 1)
+    ctx = torch.tensor([5, 64, 250], dtype=torch.int32, device=DEV)
+    o = ops.attn_decode(q, kc, vc, bt, ctx, 0.1, 256)
+    _close(o, ref.attn_decode(q, kc, vc, bt, ctx, 0.1), 2e-2, 2e-2)
