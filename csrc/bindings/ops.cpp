@@ -6,8 +6,8 @@
 // (torch.cuda.CUDAGraph on ROCm). Ops write into caller-provided outputs ("out" style): the
 // engine owns static buffers, which is what graph replay needs.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include "bfly_kernels.h"
@@ -16,7 +16,9 @@ namespace {
 
 using at::Tensor;
 
-inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+// torch on ROCm exposes HIP devices as device type 'cuda'; the masquerading stream is the
+// one torch.cuda.current_stream() returns (so ops order correctly with torch's own kernels).
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 inline bfly::bf16* bf(const Tensor& t) { return reinterpret_cast<bfly::bf16*>(t.data_ptr()); }
 
@@ -44,7 +46,7 @@ void rms_norm(const Tensor& x, const Tensor& w, double eps, Tensor& out,
     TORCH_CHECK(r.is_contiguous() && r.size(0) == rows && r.size(1) == dim, "rms_norm: residual");
     res = bf(r);
   }
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   bfly::launch_rmsnorm(bf(x), x.stride(0), res, bf(w), bf(out), out.stride(0), rows, dim,
                        (float)eps, res != nullptr, cur_stream());
 }
@@ -61,7 +63,7 @@ void layer_norm(const Tensor& x, const Tensor& w, const Tensor& b, double eps, T
     TORCH_CHECK(residual->is_contiguous() && residual->sizes() == x.sizes(), "layer_norm: residual");
     res = bf(*residual);
   }
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   bfly::launch_layernorm(bf(x), res, bf(w), bf(b), bf(out), rows, dim, (float)eps, res != nullptr,
                          cur_stream());
 }
@@ -101,7 +103,7 @@ void rope_kv(Tensor& qkv, const Tensor& positions, const Tensor& cos_t, const Te
     vc = bf(V);
     BS = K.size(2);
   }
-  c10::hip::HIPGuard g(qkv.device());
+  c10::DeviceGuard g(qkv.device());
   bfly::launch_rope_kv(bf(qkv), T, num_q_heads, num_kv_heads, D, positions.data_ptr<int>(),
                        cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), sl, kc, vc, BS,
                        cur_stream());
@@ -118,7 +120,7 @@ void kv_append(const Tensor& k, const Tensor& v, const Tensor& slots, Tensor& k_
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "kv_append: k_cache");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == D, "kv_append: v_cache");
   TORCH_CHECK(slots.numel() == T, "kv_append: slots");
-  c10::hip::HIPGuard g(k.device());
+  c10::DeviceGuard g(k.device());
   bfly::launch_kv_append(bf(k), k.stride(0), bf(v), v.stride(0), slots.data_ptr<int>(),
                          bf(k_cache), bf(v_cache), T, Hkv, D, k_cache.size(2), cur_stream());
 }
@@ -131,7 +133,7 @@ void silu_mul(const Tensor& gu, Tensor& out, int64_t interleave) {
   TORCH_CHECK(interleave == 0 || (interleave % 8 == 0 && ffn % interleave == 0), "silu_mul: interleave");
   const long rows = out.numel() / ffn;
   TORCH_CHECK(gu.numel() == rows * 2 * ffn, "silu_mul: rows");
-  c10::hip::HIPGuard g(gu.device());
+  c10::DeviceGuard g(gu.device());
   bfly::launch_silu_mul(bf(gu), bf(out), rows, ffn, interleave, cur_stream());
 }
 
@@ -139,7 +141,7 @@ void gelu(const Tensor& x, Tensor& out) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(out);
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.numel() == out.numel() &&
                   x.numel() % 8 == 0, "gelu: shapes");
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   bfly::launch_gelu(bf(x), bf(out), x.numel(), cur_stream());
 }
 
@@ -148,7 +150,7 @@ void add(const Tensor& a, const Tensor& b, Tensor& out) {
   TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && out.is_contiguous() &&
                   a.numel() == b.numel() && a.numel() == out.numel() && a.numel() % 8 == 0,
               "add: shapes");
-  c10::hip::HIPGuard g(a.device());
+  c10::DeviceGuard g(a.device());
   bfly::launch_add(bf(a), bf(b), bf(out), a.numel(), cur_stream());
 }
 
@@ -157,7 +159,7 @@ void embed(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) 
   TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && out.is_contiguous(), "embed: layout");
   const int T = ids.numel(), dim = table.size(1);
   TORCH_CHECK(dim % 8 == 0 && out.numel() == (long)T * dim, "embed: shapes");
-  c10::hip::HIPGuard g(ids.device());
+  c10::DeviceGuard g(ids.device());
   bfly::launch_embed(ids.data_ptr<int>(), bf(table), bf(out), T, dim, vstart, table.size(0),
                      cur_stream());
 }
@@ -184,7 +186,7 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
     TORCH_CHECK(seeds->scalar_type() == at::kLong && seeds->numel() == rows, "sample: seeds");
     sp = seeds->data_ptr<int64_t>();
   }
-  c10::hip::HIPGuard g(logits.device());
+  c10::DeviceGuard g(logits.device());
   bfly::launch_sample(bf(logits), logits.stride(0), rows, V, vstart, tp, sp,
                       reinterpret_cast<uint64_t*>(workspace.data_ptr()), out_ids.data_ptr<int>(),
                       out_scores.data_ptr<float>(), cur_stream());
@@ -226,7 +228,7 @@ void gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Ten
     ws = reinterpret_cast<float*>(workspace->data_ptr());
     ws_bytes = workspace->numel() * workspace->element_size();
   }
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   const int rc = bfly::launch_gemm(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, epilogue, bp,
                                    bf(out), out.stride(0), ws, ws_bytes, cur_stream());
   TORCH_CHECK(rc == 0, "gemm: unsupported shape M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
@@ -261,7 +263,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
     po = part_o->data_ptr<float>();
     pml = part_ml->data_ptr<float>();
   }
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   const int rc = bfly::launch_attn_decode(bf(q), q.stride(0), bf(k_cache), bf(v_cache),
                                           block_tables.data_ptr<int>(), block_tables.stride(0),
                                           ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale,
@@ -280,11 +282,18 @@ void attn_prefill(const Tensor& q, const Tensor& k, const Tensor& v, const Tenso
   TORCH_CHECK(out.size(1) == Hq && out.size(2) == D && out.size(0) == q.size(0), "attn_prefill: out");
   CHECK_I32(cu_seqlens);
   const int nseq = cu_seqlens.numel() - 1;
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   const int rc = bfly::launch_attn_prefill(bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0),
                                            cu_seqlens.data_ptr<int>(), nseq, max_seqlen, Hq, Hkv, D,
                                            (float)scale, causal, bf(out), out.stride(0), cur_stream());
   TORCH_CHECK(rc == 0, "attn_prefill: unsupported configuration (rc=", rc, ")");
+}
+
+void probe(int64_t which, Tensor& out) {
+  CHECK_GPU(out);
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 64 * 16, "probe: out");
+  c10::DeviceGuard g(out.device());
+  bfly::launch_probe(which, out.data_ptr<float>(), cur_stream());
 }
 
 }  // namespace
@@ -308,6 +317,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
         "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
         "Tensor(c!)? part_ml) -> ()");
+  m.def("probe(int which, Tensor(a!) out) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
         "bool causal, Tensor(a!) out) -> ()");
 }
@@ -325,4 +335,5 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
+  m.impl("probe", &probe);
 }

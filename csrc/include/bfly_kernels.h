@@ -65,4 +65,7 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
                         hipStream_t stream);
 
+// probe.hip
+void launch_probe(int which, float* out, hipStream_t stream);
+
 }  // namespace bfly

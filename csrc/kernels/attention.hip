@@ -25,6 +25,7 @@
 namespace bfly {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4* lds_s4_ptr;
 
 constexpr int kAttnThreads = 256;
@@ -343,12 +344,12 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
                 (lds_s4_ptr)(vb + pf_off(krow, ch) + 8 * (tp & 1)));
             const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (lds_s4_ptr)(vb + pf_off(krow + 8, ch) + 8 * (tp & 1)));
-            bf16x8 vf;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              vf[j] = __builtin_bit_cast(bf16, lo[j]);
-              vf[4 + j] = __builtin_bit_cast(bf16, hi4[j]);
-            }
+            // Assemble the fragment as whole dwords (element-wise bf16 inserts from the
+            // v4i16 result were miscompiled: hipcc kept only the low dword and duplicated it).
+            const u32x2 a2 = __builtin_bit_cast(u32x2, lo);
+            const u32x2 b2 = __builtin_bit_cast(u32x2, hi4);
+            const u32x4 w4 = {a2.x, a2.y, b2.x, b2.y};
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, w4);
             o[dt] = mfma32(vf, pb[kt][s], o[dt]);
           }
       }
