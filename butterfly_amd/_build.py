@@ -38,7 +38,7 @@ def _torch_paths():
 
 
 def _headers() -> list[Path]:
-    return sorted((CSRC / "include").glob("*.h"))
+    return sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "runtime").glob("*.h"))
 
 
 def _digest(src: Path, flags: list[str]) -> str:

@@ -1,0 +1,236 @@
+"""LLMEngine: the distributed inference engine ("Core logic for splitting transformer
+computations across nodes", /root/reference/CLAUDE.md:19) for one rank.
+
+Every rank of a model replica (its TP x PP ranks) runs an identical engine: the same requests,
+the same deterministic C++ scheduler (runtime/scheduler.cpp) and therefore the same step
+plans, so no scheduling messages are exchanged. Data-parallel replicas run independent engines
+on their own request streams.
+
+Per step:
+  prefill  : pack the admitted prompts, run the stage (flash prefill), sample the first tokens
+  decode   : one token per running sequence through the hipGraph-replayed stage
+  PP       : stage s receives the residual stream from s-1 and sends to s+1 (RCCL send/recv
+             over xGMI); the batch is split into microbatches so stages overlap; the last stage
+             samples and broadcasts token ids to the replica's ranks.
+  TP       : handled inside the model (all-reduces) and the sampler (score/id all-gather).
+"""
+from __future__ import annotations
+
+import itertools
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..config import EngineConfig, ModelConfig
+from ..models import Shard, build_model
+from ..parallel.comm import Communicator
+from ..parallel.mesh import Mesh
+from ..utils.metrics import Metrics
+from .kv_cache import KVCache, device_kv_budget, kv_blocks_for_budget
+from .model_runner import ModelRunner
+from .sampler import Sampler, SamplingParams
+
+
+@dataclass
+class Request:
+    rid: int
+    prompt: list
+    params: SamplingParams
+    output: list = field(default_factory=list)
+    arrival: float = 0.0
+    first_token_time: Optional[float] = None
+    finish_time: Optional[float] = None
+    finished: bool = False
+    finish_reason: Optional[str] = None
+
+    @property
+    def tokens(self) -> list:
+        return self.prompt + self.output
+
+
+@dataclass
+class StepOutput:
+    kind: str
+    rids: list
+    new_tokens: list
+    finished: list
+    seconds: float
+
+
+class LLMEngine:
+    def __init__(self, cfg: ModelConfig, mesh: Mesh = Mesh(), engine_cfg: EngineConfig = EngineConfig(),
+                 comm: Optional[Communicator] = None, device=None, stage_layers: Optional[list] = None,
+                 model=None, eos_token_id: Optional[int] = None):
+        self.cfg = cfg
+        self.ecfg = engine_cfg
+        self.mesh = mesh
+        self.comm = comm or Communicator.single()
+        self.rank = self.comm.rank
+        coord = mesh.coord(self.rank)
+        self.coord = coord
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        self.device = torch.device(device)
+        if stage_layers is None:
+            stage_layers = balanced_stages(cfg.num_layers, mesh.pp)
+        a, b = stage_layers[coord.pp]
+        shard = Shard(tp_rank=coord.tp, tp_size=mesh.tp, layer_start=a, layer_end=b,
+                      ep_rank=coord.dp if mesh.ep > 1 else 0, ep_size=mesh.ep)
+        dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        self.model = model or build_model(cfg, shard, device=self.device, dtype=dtype, comm=self.comm)
+        if model is None:
+            self.model.init_random(engine_cfg.seed)
+        self.eos = eos_token_id
+        # ---- KV cache sizing ------------------------------------------------------------
+        bs = engine_cfg.block_size
+        per_tok = self.model.kv_bytes_per_token()
+        if engine_cfg.kv_cache_tokens:
+            nblocks = (engine_cfg.kv_cache_tokens + bs - 1) // bs
+        else:
+            act_reserve = self._activation_reserve()
+            budget = device_kv_budget(self.device, engine_cfg.hbm_utilization, act_reserve)
+            nblocks = kv_blocks_for_budget(budget, per_tok, bs)
+            need = engine_cfg.max_batch * ((engine_cfg.max_seq_len + bs - 1) // bs)
+            nblocks = min(nblocks, max(need, 1))
+        if nblocks <= 0:
+            raise RuntimeError("no HBM left for the KV cache")
+        self.kv = KVCache(self.model, nblocks, bs)
+        native = __import__("butterfly_amd._native_loader", fromlist=["native"]).native()
+        self.scheduler = native.Scheduler(self.kv.manager, engine_cfg.max_batch, engine_cfg.max_prefill_tokens)
+        d = self.model.dims
+        self.sampler = Sampler(self.comm, cfg.vocab_size, d.vocab0, mesh.tp)
+        if self.device.type == "cuda":
+            ops.reserve_workspace(self.device, max_tokens=max(engine_cfg.max_prefill_tokens, engine_cfg.max_batch),
+                                  max_n=self._max_gemm_n(), max_k=self._max_gemm_k(),
+                                  max_batch=max(engine_cfg.graph_batch_sizes + [engine_cfg.max_batch]),
+                                  max_ctx=engine_cfg.max_seq_len, num_kv_heads=d.hkv, head_dim=cfg.head_dim)
+        self.runner = ModelRunner(self.model, self.kv, engine_cfg.max_seq_len, engine_cfg.use_graphs,
+                                  [b for b in engine_cfg.graph_batch_sizes if b <= engine_cfg.max_batch] or [engine_cfg.max_batch],
+                                  max_batch=engine_cfg.max_batch)
+        self.requests: dict[int, Request] = {}
+        self._ids = itertools.count()
+        self.metrics = Metrics()
+        self.pp_first = coord.pp == 0
+        self.pp_last = coord.pp == mesh.pp - 1
+
+    # ------------------------------------------------------------------------------------
+    def _activation_reserve(self) -> int:
+        e, c = self.ecfg, self.cfg
+        T = max(e.max_prefill_tokens, e.max_batch)
+        h = c.hidden_size
+        d = self.model.dims
+        width = max(3 * h, (d.hq + 2 * d.hkv) * c.head_dim, 2 * d.ffn * max(1, d.experts), d.vocab)
+        return int(T * width * 2 * 6) + (2 << 30)
+
+    def _max_gemm_n(self) -> int:
+        c, d = self.cfg, self.model.dims
+        return max((d.hq + 2 * d.hkv) * c.head_dim, c.hidden_size, 2 * d.ffn * max(1, d.experts), d.vocab)
+
+    def _max_gemm_k(self) -> int:
+        c, d = self.cfg, self.model.dims
+        return max(c.hidden_size, d.ffn * max(1, d.experts), d.hq * c.head_dim)
+
+    # ------------------------------------------------------------------------------------
+    def add_request(self, prompt: list, params: Optional[SamplingParams] = None, rid: Optional[int] = None) -> int:
+        rid = next(self._ids) if rid is None else rid
+        params = params or SamplingParams()
+        if len(prompt) + params.max_tokens > self.ecfg.max_seq_len:
+            raise ValueError(f"prompt ({len(prompt)}) + max_tokens ({params.max_tokens}) exceeds max_seq_len")
+        self.requests[rid] = Request(rid, list(prompt), params, arrival=time.perf_counter())
+        self.scheduler.add(rid, len(prompt), params.max_tokens)
+        return rid
+
+    def has_unfinished(self) -> bool:
+        return self.scheduler.num_waiting + self.scheduler.num_running > 0
+
+    def _sample_params(self, rids):
+        temps = [self.requests[r].params.temperature for r in rids]
+        if all(t <= 0 for t in temps):
+            return None, None, None
+        tt = torch.tensor(temps, dtype=torch.float32, device=self.device)
+        seeds = torch.tensor([(self.requests[r].params.seed or r) * 1000003 + len(self.requests[r].output)
+                              for r in rids], dtype=torch.int64, device=self.device)
+        return tt, seeds, [self.requests[r].params for r in rids]
+
+    def step(self) -> StepOutput:
+        t0 = time.perf_counter()
+        plan = self.scheduler.schedule()
+        if plan.kind == 0:
+            return StepOutput("idle", [], [], [], 0.0)
+        rids = list(plan.seq_ids)
+        if plan.cow:
+            self.kv.copy_blocks(list(plan.cow))
+        if plan.kind == 1:
+            fb = self.runner.prefill_batch(plan, lambda r: self.requests[r].tokens)
+            tokens = self._run_stages(lambda h: self.runner.run(fb, h), fb.num_tokens, len(rids), rids)
+            kind = "prefill"
+        else:
+            last = [self.requests[r].tokens[-1] for r in rids]
+            inp = self.runner.decode_inputs(plan, last)
+            tokens = self._run_stages(lambda h: self.runner.run_decode(inp, h), len(rids), len(rids), rids)
+            kind = "decode"
+        new = tokens.tolist()
+        finished = []
+        now = time.perf_counter()
+        for r, t in zip(rids, new):
+            req = self.requests[r]
+            req.output.append(int(t))
+            if req.first_token_time is None:
+                req.first_token_time = now
+            self.scheduler.on_token(r)
+            reason = None
+            if len(req.output) >= req.params.max_tokens:
+                reason = "length"
+            elif not req.params.ignore_eos and (int(t) in req.params.stop_token_ids or
+                                                (self.eos is not None and int(t) == self.eos)):
+                reason = "stop"
+            if reason:
+                req.finished, req.finish_reason, req.finish_time = True, reason, now
+                self.scheduler.finish(r)
+                finished.append(r)
+        dt = time.perf_counter() - t0
+        self.metrics.observe_step(kind, len(rids), dt)
+        return StepOutput(kind, rids, new, finished, dt)
+
+    def _run_stages(self, fn, T: int, R: int, rids) -> torch.Tensor:
+        """Run this rank's pipeline stage; return sampled ids [R] (int32, on every rank)."""
+        m = self.model
+        if self.mesh.pp == 1:
+            logits = fn(None)
+            temps, seeds, params = self._sample_params(rids)
+            return self.sampler.sample(logits, temps, seeds, params)
+        # pipeline: recv residual stream -> compute -> send; last stage samples + broadcasts
+        h = None
+        if not self.pp_first:
+            h = torch.empty(T, self.cfg.hidden_size, dtype=m.dtype, device=self.device)
+            self.comm.recv(h, self.mesh.prev_stage(self.rank))
+        out = fn(h)
+        ids = torch.empty(R, dtype=torch.int32, device=self.device)
+        if not self.pp_last:
+            self.comm.send(out, self.mesh.next_stage(self.rank))
+        else:
+            temps, seeds, params = self._sample_params(rids)
+            ids = self.sampler.sample(out, temps, seeds, params)
+        self.comm.broadcast_(ids, src_in_group=self.mesh.pp - 1, group="pp")
+        return ids
+
+    # ------------------------------------------------------------------------------------
+    def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list:
+        rids = [self.add_request(p, params) for p in prompts]
+        while self.has_unfinished():
+            self.step()
+        return [self.requests[r].output for r in rids]
+
+
+def balanced_stages(num_layers: int, pp: int) -> list:
+    base, extra = divmod(num_layers, pp)
+    out, a = [], 0
+    for s in range(pp):
+        n = base + (1 if s < extra else 0)
+        out.append((a, a + n))
+        a += n
+    return out

@@ -1,0 +1,157 @@
+"""ModelRunner: turns scheduler step plans into device batches and runs the stage, replaying
+hipGraph-captured decode steps ("a single hipGraphLaunch per step per rank").
+
+Decode graphs are captured per batch-size bucket on static input buffers; a step copies its
+inputs into the bucket's buffers (padding rows: slot -1 = no cache write, ctx_len 1) and
+replays. Everything inside — GEMMs, RoPE/KV append, paged attention, norms, TP all-reduces
+(RCCL or the one-shot P2P kernel), the LM head and the TP sampling all-gather — is captured,
+so the host cost per token is one replay.
+"""
+from __future__ import annotations
+
+import bisect
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .batch import ForwardBatch
+
+
+class _DecodeGraph:
+    def __init__(self, bucket: int, max_blocks: int, device, hidden: int, first: bool):
+        i32 = dict(dtype=torch.int32, device=device)
+        self.bucket = bucket
+        self.input_ids = torch.zeros(bucket, **i32)
+        self.positions = torch.zeros(bucket, **i32)
+        self.slots = torch.full((bucket,), -1, **i32)
+        self.block_tables = torch.zeros(bucket, max_blocks, **i32)
+        self.ctx_lens = torch.ones(bucket, **i32)
+        self.hidden_in = None if first else torch.zeros(bucket, hidden, dtype=torch.bfloat16, device=device)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.output: Optional[torch.Tensor] = None
+
+
+class ModelRunner:
+    def __init__(self, model, kv_cache, max_seq_len: int, use_graphs: bool = True,
+                 graph_batch_sizes: Optional[list] = None, post_fn=None, max_batch: int = 256):
+        """`post_fn(output) -> tensor` is captured together with the forward when given (e.g.
+        the TP sampler), so the replay returns the sampled ids directly."""
+        self.model = model
+        self.kv = kv_cache
+        self.device = model.device
+        self.max_seq_len = max_seq_len
+        self.block_size = kv_cache.block_size
+        self.max_blocks = (max_seq_len + self.block_size - 1) // self.block_size
+        self.use_graphs = use_graphs and self.device.type == "cuda" and \
+            os.environ.get("BFLY_DISABLE_GRAPHS", "0") != "1"
+        self.buckets = sorted(graph_batch_sizes or [1, 2, 4, 8, 16, 32, 64])
+        self.graphs: dict[int, _DecodeGraph] = {}
+        self.pool = None
+        self.post_fn = post_fn
+        # host staging buffers (pinned) for per-step inputs
+        hb = max(self.buckets + [max_batch])
+        self._tables_host = np.zeros((hb, self.max_blocks), dtype=np.int32)
+        self._ctx_host = np.zeros((hb,), dtype=np.int32)
+
+    # ------------------------------------------------------------------------------------
+    def prefill_batch(self, plan, tokens_of) -> ForwardBatch:
+        """Batch for a prefill plan; tokens_of(sid) -> full token list to (re)compute."""
+        ids, pos, slots, cu, last = [], [], [], [0], []
+        for sid, sl in zip(plan.seq_ids, plan.prefill_slots):
+            toks = tokens_of(sid)
+            n = len(sl)
+            ids.extend(toks[:n])
+            pos.extend(range(n))
+            slots.extend(sl)
+            cu.append(cu[-1] + n)
+            last.append(cu[-1] - 1)
+        dev = self.device
+        i32 = dict(dtype=torch.int32)
+        return ForwardBatch(
+            input_ids=torch.tensor(ids, **i32).to(dev, non_blocking=True),
+            positions=torch.tensor(pos, **i32).to(dev, non_blocking=True),
+            slots=torch.tensor(slots, **i32).to(dev, non_blocking=True), is_prefill=True,
+            cu_seqlens=torch.tensor(cu, **i32).to(dev, non_blocking=True),
+            max_seqlen=max(cu[i + 1] - cu[i] for i in range(len(cu) - 1)),
+            logits_idx=torch.tensor(last, dtype=torch.int64).to(dev, non_blocking=True))
+
+    def decode_inputs(self, plan, last_tokens: list) -> dict:
+        B = len(plan.seq_ids)
+        self.kv.manager.fill_decode_tables(list(plan.seq_ids), self._tables_host[:B], self._ctx_host[:B])
+        return dict(ids=np.asarray(last_tokens, dtype=np.int32),
+                    pos=np.asarray(plan.decode_positions, dtype=np.int32),
+                    slots=np.asarray(plan.decode_slots, dtype=np.int32),
+                    tables=self._tables_host[:B], ctx=self._ctx_host[:B])
+
+    def decode_batch(self, inp: dict) -> ForwardBatch:
+        dev = self.device
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+        return ForwardBatch(input_ids=t(inp["ids"]), positions=t(inp["pos"]), slots=t(inp["slots"]),
+                            is_prefill=False, block_tables=t(inp["tables"]), ctx_lens=t(inp["ctx"]),
+                            max_ctx=self.max_seq_len, logits_idx=None)
+
+    # ------------------------------------------------------------------------------------
+    def run(self, fb: ForwardBatch, hidden_in=None):
+        out = self.model.forward(fb, self.kv.layers, hidden_in)
+        return self.post_fn(out) if (self.post_fn is not None and self.model.last) else out
+
+    def run_decode(self, inp: dict, hidden_in=None):
+        B = len(inp["ids"])
+        if not self.use_graphs or B > self.buckets[-1]:
+            return self.run(self.decode_batch(inp), hidden_in)
+        bucket = self.buckets[bisect.bisect_left(self.buckets, B)]
+        g = self.graphs.get(bucket)
+        if g is None:
+            g = self._capture(bucket)
+        self._stage(g, inp, hidden_in)
+        g.graph.replay()
+        return g.output[:B]
+
+    def _stage(self, g: _DecodeGraph, inp: dict, hidden_in) -> None:
+        B = len(inp["ids"])
+        dev = self.device
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+        g.input_ids[:B].copy_(t(inp["ids"]))
+        g.positions[:B].copy_(t(inp["pos"]))
+        g.slots[:B].copy_(t(inp["slots"]))
+        g.block_tables[:B].copy_(t(inp["tables"]))
+        g.ctx_lens[:B].copy_(t(inp["ctx"]))
+        if B < g.bucket:
+            g.input_ids[B:].zero_()
+            g.positions[B:].zero_()
+            g.slots[B:].fill_(-1)
+            g.ctx_lens[B:].fill_(1)
+        if g.hidden_in is not None and hidden_in is not None:
+            g.hidden_in[:B].copy_(hidden_in)
+
+    def _graph_batch(self, g: _DecodeGraph) -> ForwardBatch:
+        return ForwardBatch(input_ids=g.input_ids, positions=g.positions, slots=g.slots,
+                            is_prefill=False, block_tables=g.block_tables, ctx_lens=g.ctx_lens,
+                            max_ctx=self.max_seq_len, logits_idx=None)
+
+    def _capture(self, bucket: int) -> _DecodeGraph:
+        m = self.model
+        g = _DecodeGraph(bucket, self.max_blocks, self.device, m.cfg.hidden_size, m.first)
+        fb = self._graph_batch(g)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):   # warm up allocator / workspaces outside capture
+                self.run(fb, g.hidden_in)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, pool=self.pool):
+            g.output = self.run(fb, g.hidden_in)
+        g.graph = graph
+        self.graphs[bucket] = g
+        return g
+
+    def capture_all(self, max_batch: int) -> None:
+        for b in self.buckets:
+            if b <= max_batch and b not in self.graphs:
+                self._capture(b)

@@ -1,0 +1,384 @@
+"""Decoder-only transformer LM covering the Llama-3, Mixtral and GPT-2 families.
+
+One class, arch-specific switches from ModelConfig (norm, position embedding, MLP kind,
+biases, MoE). The model holds only its shard (models/shard.py) and runs one pipeline stage:
+
+  first stage : token (+ learned position) embedding, vocab-parallel (TP all-reduce)
+  every layer : norm -> fused QKV GEMM -> RoPE + paged-KV append -> attention
+                (flash prefill / paged decode) -> O GEMM -> TP all-reduce ->
+                fused residual-add + norm -> FFN (SwiGLU with the activation fused into the
+                gate/up GEMM epilogue | GELU MLP | dense-dispatch MoE) -> TP all-reduce
+  last stage  : final norm on the rows that need logits -> vocab-parallel LM head
+
+The residual stream is carried as (residual, pending delta): each block's "add + norm" is
+ONE kernel (rms_norm with residual=...), so the residual add never costs its own pass.
+
+Weights live in fused local tensors (qkv, interleaved gate/up, stacked experts). The
+checkpoint and the random initialiser work on *logical* parameters (HF-style names, global
+shapes, shard slices) through `logical_params()`, which is what makes a checkpoint written
+under one partition plan loadable under another.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import torch
+
+from .. import ops
+from ..config import ModelConfig
+from ..engine.batch import ForwardBatch
+from ..parallel.comm import Communicator
+from .shard import LocalDims, Shard, local_dims
+
+G16 = ops.SILU_INTERLEAVE
+
+
+@dataclass
+class LogicalParam:
+    name: str
+    global_shape: tuple
+    split_dim: Optional[int]      # dim along which the local piece is a contiguous slice
+    offset: int                   # start of the local piece along split_dim
+    length: int                   # extent of the local piece along split_dim
+    init: str                     # "normal" | "ones" | "zeros"
+    get: Callable[[], torch.Tensor]
+    set: Callable[[torch.Tensor], None]
+    owner: bool = True            # canonical writer of this slice (replicas dedupe on save)
+
+    def local_shape(self) -> tuple:
+        s = list(self.global_shape)
+        if self.split_dim is not None:
+            s[self.split_dim] = self.length
+        return tuple(s)
+
+
+def _name_seed(name: str, seed: int) -> int:
+    return (zlib.crc32(name.encode()) ^ (seed * 0x9E3779B1)) & 0xFFFFFFFF
+
+
+class TransformerLM:
+    def __init__(self, cfg: ModelConfig, shard: Shard = Shard(), device="cpu",
+                 dtype: torch.dtype = torch.bfloat16, comm: Optional[Communicator] = None):
+        self.cfg = cfg
+        self.shard = shard
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.comm = comm or Communicator.single()
+        self.dims: LocalDims = local_dims(cfg, shard)
+        self.layer_ids = list(shard.layers(cfg))
+        self.first = shard.is_first(cfg)
+        self.last = shard.is_last(cfg)
+        self.tp = shard.tp_size
+        self.ep = shard.ep_size
+        if self.device.type == "cuda" and cfg.head_dim != 128:
+            raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
+        self.p: dict[str, torch.Tensor] = {}
+        self._alloc()
+        self.cos = self.sin = None
+        if cfg.pos_emb == "rope":
+            self.cos, self.sin = ops.rope_tables(cfg.head_dim, cfg.max_position, cfg.rope_theta,
+                                                 cfg.rope_scaling, device=self.device)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    # ------------------------------------------------------------------------------------
+    # parameters
+    # ------------------------------------------------------------------------------------
+    def _alloc(self):
+        c, d = self.cfg, self.dims
+        h, D = c.hidden_size, c.head_dim
+        z = lambda *s: torch.zeros(*s, dtype=self.dtype, device=self.device)  # noqa: E731
+        norm_b = c.norm == "layer"
+        if self.first:
+            self.p["embed"] = z(d.vocab, h)
+            if c.pos_emb == "learned":
+                self.p["pos_embed"] = z(c.max_position, h)
+        for i in self.layer_ids:
+            pre = f"l{i}."
+            self.p[pre + "in_w"] = z(h)
+            if norm_b:
+                self.p[pre + "in_b"] = z(h)
+            self.p[pre + "qkv_w"] = z((d.hq + 2 * d.hkv) * D, h)
+            self.p[pre + "o_w"] = z(h, d.hq * D)
+            if c.bias:
+                self.p[pre + "qkv_b"] = z((d.hq + 2 * d.hkv) * D)
+                self.p[pre + "o_b"] = z(h)
+            self.p[pre + "post_w"] = z(h)
+            if norm_b:
+                self.p[pre + "post_b"] = z(h)
+            if c.is_moe:
+                self.p[pre + "router_w"] = z(c.num_experts, h)
+                self.p[pre + "moe_gu_w"] = z(d.experts * 2 * d.ffn, h)
+                self.p[pre + "moe_down_w"] = z(h, d.experts * d.ffn)
+            elif c.act == "silu":
+                self.p[pre + "gu_w"] = z(2 * d.ffn, h)
+                self.p[pre + "down_w"] = z(h, d.ffn)
+            else:
+                self.p[pre + "fc_w"] = z(d.ffn, h)
+                self.p[pre + "proj_w"] = z(h, d.ffn)
+                if c.bias:
+                    self.p[pre + "fc_b"] = z(d.ffn)
+                    self.p[pre + "proj_b"] = z(h)
+        if self.last:
+            self.p["final_w"] = z(h)
+            if norm_b:
+                self.p["final_b"] = z(h)
+            if not c.tie_embeddings:
+                self.p["head"] = z(d.vocab, h)
+            elif not self.first:
+                # tied head on a last stage that does not hold the embedding: its own copy
+                self.p["head"] = z(d.vocab, h)
+
+    @property
+    def head_weight(self) -> torch.Tensor:
+        return self.p["head"] if "head" in self.p else self.p["embed"]
+
+    def local_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.p.values())
+
+    def logical_params(self) -> list[LogicalParam]:
+        """Every logical (HF-style) parameter slice this rank holds."""
+        c, d, s = self.cfg, self.dims, self.shard
+        h, D = c.hidden_size, c.head_dim
+        tp0 = s.tp_rank == 0
+        ep0 = s.ep_rank == 0
+        out: list[LogicalParam] = []
+
+        def rows(t, a, n):
+            return (lambda: t[a:a + n]), (lambda x: t[a:a + n].copy_(x))
+
+        def whole(t):
+            return (lambda: t), (lambda x: t.copy_(x.view(t.shape)))
+
+        def add(name, gshape, split, off, length, init, getset, owner=True):
+            out.append(LogicalParam(name, tuple(gshape), split, off, length, init, getset[0], getset[1], owner))
+
+        norm_b = c.norm == "layer"
+        vlen = max(0, min(c.vocab_size, d.vocab0 + d.vocab) - d.vocab0)
+        if self.first:
+            add("embed_tokens.weight", (c.vocab_size, h), 0, d.vocab0, vlen, "normal",
+                rows(self.p["embed"], 0, vlen), owner=ep0)
+            if c.pos_emb == "learned":
+                add("pos_embed.weight", (c.max_position, h), None, 0, 0, "normal",
+                    whole(self.p["pos_embed"]), owner=tp0 and ep0)
+        kv_rep = max(1, self.tp // c.num_kv_heads)            # tp ranks sharing one kv head
+        kv_owner = (s.tp_rank % kv_rep == 0) and ep0
+        for i in self.layer_ids:
+            pre, L = f"l{i}.", f"layers.{i}."
+            add(L + "input_norm.weight", (h,), None, 0, 0, "ones", whole(self.p[pre + "in_w"]), tp0 and ep0)
+            if norm_b:
+                add(L + "input_norm.bias", (h,), None, 0, 0, "zeros", whole(self.p[pre + "in_b"]), tp0 and ep0)
+            qkv = self.p[pre + "qkv_w"]
+            nq, nkv = d.hq * D, d.hkv * D
+            add(L + "attn.q_proj.weight", (c.q_size, h), 0, d.q_head0 * D, nq, "normal", rows(qkv, 0, nq), ep0)
+            add(L + "attn.k_proj.weight", (c.kv_size, h), 0, d.kv_head0 * D, nkv, "normal", rows(qkv, nq, nkv), kv_owner)
+            add(L + "attn.v_proj.weight", (c.kv_size, h), 0, d.kv_head0 * D, nkv, "normal", rows(qkv, nq + nkv, nkv), kv_owner)
+            if c.bias:
+                qb = self.p[pre + "qkv_b"]
+                add(L + "attn.q_proj.bias", (c.q_size,), 0, d.q_head0 * D, nq, "normal", rows(qb, 0, nq), ep0)
+                add(L + "attn.k_proj.bias", (c.kv_size,), 0, d.kv_head0 * D, nkv, "normal", rows(qb, nq, nkv), kv_owner)
+                add(L + "attn.v_proj.bias", (c.kv_size,), 0, d.kv_head0 * D, nkv, "normal", rows(qb, nq + nkv, nkv), kv_owner)
+            ow = self.p[pre + "o_w"]
+            add(L + "attn.o_proj.weight", (h, c.q_size), 1, d.q_head0 * D, nq, "normal", whole(ow), ep0)
+            if c.bias:
+                add(L + "attn.o_proj.bias", (h,), None, 0, 0, "normal", whole(self.p[pre + "o_b"]), tp0 and ep0)
+            add(L + "post_norm.weight", (h,), None, 0, 0, "ones", whole(self.p[pre + "post_w"]), tp0 and ep0)
+            if norm_b:
+                add(L + "post_norm.bias", (h,), None, 0, 0, "zeros", whole(self.p[pre + "post_b"]), tp0 and ep0)
+            F, Fg = d.ffn, c.intermediate_size
+            if c.is_moe:
+                add(L + "moe.router.weight", (c.num_experts, h), None, 0, 0, "normal",
+                    whole(self.p[pre + "router_w"]), tp0 and ep0)
+                gu, dn = self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"]
+                for el in range(d.experts):
+                    e = d.expert0 + el
+                    E = L + f"moe.experts.{e}."
+                    blk = gu[el * 2 * F:(el + 1) * 2 * F]
+                    add(E + "gate_proj.weight", (Fg, h), 0, d.ffn0, F, "normal", self._gu_getset(blk, 0), True)
+                    add(E + "up_proj.weight", (Fg, h), 0, d.ffn0, F, "normal", self._gu_getset(blk, 1), True)
+                    dcols = dn[:, el * F:(el + 1) * F]
+                    add(E + "down_proj.weight", (h, Fg), 1, d.ffn0, F, "normal",
+                        ((lambda t=dcols: t), (lambda x, t=dcols: t.copy_(x))), True)
+            elif c.act == "silu":
+                gu = self.p[pre + "gu_w"]
+                add(L + "mlp.gate_proj.weight", (Fg, h), 0, d.ffn0, F, "normal", self._gu_getset(gu, 0), ep0)
+                add(L + "mlp.up_proj.weight", (Fg, h), 0, d.ffn0, F, "normal", self._gu_getset(gu, 1), ep0)
+                add(L + "mlp.down_proj.weight", (h, Fg), 1, d.ffn0, F, "normal", whole(self.p[pre + "down_w"]), ep0)
+            else:
+                add(L + "mlp.fc.weight", (Fg, h), 0, d.ffn0, F, "normal", whole(self.p[pre + "fc_w"]), ep0)
+                add(L + "mlp.proj.weight", (h, Fg), 1, d.ffn0, F, "normal", whole(self.p[pre + "proj_w"]), ep0)
+                if c.bias:
+                    add(L + "mlp.fc.bias", (Fg,), 0, d.ffn0, F, "normal", whole(self.p[pre + "fc_b"]), ep0)
+                    add(L + "mlp.proj.bias", (h,), None, 0, 0, "normal", whole(self.p[pre + "proj_b"]), tp0 and ep0)
+        if self.last:
+            add("final_norm.weight", (h,), None, 0, 0, "ones", whole(self.p["final_w"]), tp0 and ep0)
+            if norm_b:
+                add("final_norm.bias", (h,), None, 0, 0, "zeros", whole(self.p["final_b"]), tp0 and ep0)
+            if not c.tie_embeddings:
+                add("lm_head.weight", (c.vocab_size, h), 0, d.vocab0, vlen, "normal",
+                    rows(self.p["head"], 0, vlen), ep0)
+            elif "head" in self.p:
+                # tied copy on a stage without the embedding: same logical tensor, not an owner
+                add("embed_tokens.weight", (c.vocab_size, h), 0, d.vocab0, vlen, "normal",
+                    rows(self.p["head"], 0, vlen), owner=False)
+        return out
+
+    @staticmethod
+    def _gu_getset(gu: torch.Tensor, which: int):
+        """Access the gate (0) or up (1) rows of a 16-row interleaved [2F, h] block."""
+        two_f, h = gu.shape
+        v = gu.view(two_f // (2 * G16), 2, G16, h)[:, which]
+
+        def get():
+            return v.reshape(two_f // 2, h)
+
+        def set_(x):
+            v.copy_(x.view(two_f // (2 * G16), G16, h))
+
+        return get, set_
+
+    @torch.no_grad()
+    def init_random(self, seed: int = 0) -> None:
+        """Deterministic partition-independent random init: the value of every global element
+        depends only on (seed, logical name, global index) — any TP/PP/EP split of the same
+        seed yields identical global weights (tests compare partitions against each other)."""
+        std = self.cfg.init_std
+        amp = std * math.sqrt(3.0)
+        for lp in self.logical_params():
+            if lp.split_dim is not None and lp.length == 0:
+                continue
+            if lp.init == "ones":
+                lp.set(torch.ones(lp.local_shape(), dtype=self.dtype, device=self.device))
+                continue
+            if lp.init == "zeros":
+                lp.set(torch.zeros(lp.local_shape(), dtype=self.dtype, device=self.device))
+                continue
+            shp = lp.local_shape()
+            g = lp.global_shape
+            if len(shp) == 1:
+                buf = torch.empty(1, shp[0], dtype=self.dtype, device=self.device)
+                ops.init_hash_(buf, 0, lp.offset if lp.split_dim == 0 else 0, g[0],
+                               _name_seed(lp.name, seed), amp)
+                lp.set(buf.view(shp))
+                continue
+            buf = torch.empty(shp, dtype=self.dtype, device=self.device)
+            r0 = lp.offset if lp.split_dim == 0 else 0
+            c0 = lp.offset if lp.split_dim == 1 else 0
+            ops.init_hash_(buf, r0, c0, g[1], _name_seed(lp.name, seed), amp)
+            lp.set(buf)
+            del buf
+
+    # ------------------------------------------------------------------------------------
+    # forward
+    # ------------------------------------------------------------------------------------
+    def _norm(self, x, w, b, residual=None):
+        if self.cfg.norm == "rms":
+            return ops.rms_norm(x, w, self.cfg.norm_eps, residual=residual)
+        return ops.layer_norm(x, w, b, self.cfg.norm_eps, residual=residual)
+
+    def embed(self, fb: ForwardBatch) -> torch.Tensor:
+        x = ops.embed(fb.input_ids, self.p["embed"], vstart=self.dims.vocab0)
+        if self.tp > 1:
+            self.comm.all_reduce_(x, "tp")
+        if self.cfg.pos_emb == "learned":
+            pe = ops.embed(fb.positions, self.p["pos_embed"], vstart=0)
+            x = ops.add(x, pe)
+        return x
+
+    def forward(self, fb: ForwardBatch, kv_caches: Optional[list] = None,
+                hidden_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Run this stage. Returns logits [R, vocab_local] on the last stage, else the
+        residual stream [T, hidden] to send to the next stage."""
+        c, d = self.cfg, self.dims
+        residual = self.embed(fb) if self.first else hidden_in
+        if residual is None:
+            raise ValueError("non-first pipeline stage needs hidden_in")
+        if not self.first:
+            residual = residual.clone()   # updated in place by the fused add+norm
+        delta = None
+        T = fb.num_tokens
+        D = c.head_dim
+        for li, i in enumerate(self.layer_ids):
+            pre = f"l{i}."
+            x = self._norm(residual if delta is None else delta, self.p[pre + "in_w"],
+                           self.p.get(pre + "in_b"), residual=None if delta is None else residual)
+            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"))
+            kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
+            slots = fb.slots if kc is not None else None
+            if c.pos_emb == "rope":
+                ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
+            elif kc is not None:
+                k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
+                v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
+                ops.kv_append(k3, v3, fb.slots, kc, vc)
+            q = qkv[:, : d.hq * D].view(T, d.hq, D)
+            if fb.is_prefill:
+                k = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
+                v = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
+                attn = ops.attn_prefill(q, k, v, fb.cu_seqlens, fb.max_seqlen, self.scale, True)
+            else:
+                attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
+            o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
+            o = ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b)
+            if self.tp > 1:
+                self.comm.all_reduce_(o, "tp")
+            x = self._norm(o, self.p[pre + "post_w"], self.p.get(pre + "post_b"), residual=residual)
+            delta = self._ffn(pre, x)
+        if not self.last:
+            return ops.add(residual, delta) if delta is not None else residual
+        idx = fb.logits_idx
+        r = residual if idx is None else residual.index_select(0, idx)
+        if delta is not None:
+            dl = delta if idx is None else delta.index_select(0, idx)
+            if idx is None:
+                r = r.clone()
+            x = self._norm(dl, self.p["final_w"], self.p.get("final_b"), residual=r)
+        else:
+            x = self._norm(r, self.p["final_w"], self.p.get("final_b"))
+        return ops.linear(x, self.head_weight)
+
+    def _ffn(self, pre: str, x: torch.Tensor) -> torch.Tensor:
+        c, d = self.cfg, self.dims
+        if c.is_moe:
+            gates, _, _ = ops.moe_route(x, self.p[pre + "router_w"], c.experts_per_token)
+            xs, gs = x, gates
+            if self.ep > 1:
+                xs = self.comm.all_gather(x, "ep")
+                gs = self.comm.all_gather(gates, "ep")
+            hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
+            ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
+            out = ops.linear(hmid, self.p[pre + "moe_down_w"])
+            if self.ep > 1:
+                out = self.comm.reduce_scatter(out, "ep")
+            elif self.tp > 1:
+                self.comm.all_reduce_(out, "tp")
+            return out
+        if c.act == "silu":
+            hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu")
+            out = ops.linear(hmid, self.p[pre + "down_w"])
+        else:
+            hmid = ops.linear(x, self.p[pre + "fc_w"], bias=self.p.get(pre + "fc_b"))
+            hmid = ops.gelu(hmid)
+            pb = self.p.get(pre + "proj_b") if self.shard.tp_rank == 0 else None
+            out = ops.linear(hmid, self.p[pre + "proj_w"], bias=pb)
+        if self.tp > 1:
+            self.comm.all_reduce_(out, "tp")
+        return out
+
+    # ------------------------------------------------------------------------------------
+    # KV cache layout helpers
+    # ------------------------------------------------------------------------------------
+    def kv_bytes_per_token(self) -> int:
+        """Local KV bytes per cached token (local layers x local kv heads x K,V)."""
+        return 2 * len(self.layer_ids) * self.dims.hkv * self.cfg.head_dim * torch.finfo(self.dtype).bits // 8
+
+    def allocate_kv_cache(self, num_blocks: int, block_size: int) -> list:
+        D, hk = self.cfg.head_dim, self.dims.hkv
+        caches = []
+        for _ in self.layer_ids:
+            k = torch.zeros(num_blocks, hk, block_size, D, dtype=self.dtype, device=self.device)
+            v = torch.zeros(num_blocks, hk, D, block_size, dtype=self.dtype, device=self.device)
+            caches.append((k, v))
+        return caches

@@ -243,3 +243,32 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_c
     torch.ops.bfly.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx,
                                part_tokens, out, po, pml)
     return out
+
+
+def init_hash_(out, grow0: int, gcol0: int, gcols: int, seed: int, amp: float):
+    """Fill a 2-D (view of a) weight shard with partition-independent hashed uniform values."""
+    if not _gpu(out):
+        return ref.init_hash(out, grow0, gcol0, gcols, seed, amp)
+    torch.ops.bfly.init_hash(out, grow0, gcol0, gcols, seed & 0xFFFFFFFF, amp)
+    return out
+
+
+def moe_route(x, wr, top_k: int, gates=None, topk_ids=None, topk_w=None):
+    if not _gpu(x):
+        return ref.moe_route(x, wr, top_k)
+    T, E = x.shape[0], wr.shape[0]
+    if gates is None:
+        gates = torch.empty(T, E, dtype=torch.float32, device=x.device)
+    if topk_ids is None:
+        topk_ids = torch.empty(T, top_k, dtype=torch.int32, device=x.device)
+    if topk_w is None:
+        topk_w = torch.empty(T, top_k, dtype=torch.float32, device=x.device)
+    torch.ops.bfly.moe_route(x, wr, top_k, gates, topk_ids, topk_w)
+    return gates, topk_ids, topk_w
+
+
+def moe_gate_scale_(h, gates, e0: int, num_local: int):
+    if not _gpu(h):
+        return ref.moe_gate_scale(h, gates, e0, num_local)
+    torch.ops.bfly.moe_gate_scale(h, gates, e0, num_local)
+    return h

@@ -254,3 +254,49 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx=None
         return res
     out.copy_(res.view(out.shape))
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# Deterministic init and MoE gating
+# ---------------------------------------------------------------------------------------
+_M32 = 0xFFFFFFFF
+
+
+def _fmix32(h):
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    return h ^ (h >> 16)
+
+
+def init_hash(out, grow0, gcol0, gcols, seed, amp):
+    """Value of global element (r, c) = amp * (2u - 1), u = hash(seed, r*gcols + c)."""
+    rows, cols = out.shape
+    r = torch.arange(rows, dtype=torch.int64).unsqueeze(1) + grow0
+    c = torch.arange(cols, dtype=torch.int64).unsqueeze(0) + gcol0
+    idx = (r * gcols + c) & _M32
+    h = _fmix32((idx * 0x9E3779B1 + seed) & _M32)
+    u = (h >> 8).to(torch.float32) * (1.0 / 16777216.0) + (0.5 / 16777216.0)
+    out.copy_((amp * (2.0 * u - 1.0)).to(out.dtype))
+    return out
+
+
+def moe_route(x, wr, top_k):
+    """-> (gates [T, E] f32 dense, topk_ids [T, k] int32, topk_w [T, k] f32); Mixtral
+    semantics: softmax over all experts, top-k, renormalise over the selected."""
+    logits = x.float() @ wr.float().t()
+    p = torch.softmax(logits, -1)
+    w, ids = torch.topk(p, top_k, -1)
+    w = w / w.sum(-1, keepdim=True)
+    gates = torch.zeros_like(p).scatter_(1, ids, w)
+    return gates, ids.to(torch.int32), w
+
+
+def moe_gate_scale(h, gates, e0, num_local):
+    T = h.shape[0]
+    F = h.shape[1] // num_local
+    g = gates[:, e0:e0 + num_local].to(torch.float32)
+    v = h.float().view(T, num_local, F) * g.unsqueeze(-1)
+    h.copy_(v.view(T, num_local * F).to(h.dtype))
+    return h

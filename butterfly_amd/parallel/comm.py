@@ -1,0 +1,169 @@
+"""Communication layer ("Low-overhead inter-node communication for tensor passing",
+/root/reference/CLAUDE.md:20).
+
+One process per GPU; collectives go through torch.distributed — backend "nccl" is RCCL on
+ROCm (xGMI on MI355X), "gloo" for the CPU plumbing configuration and the control plane.
+`Communicator` binds a rank to the process groups of its mesh axes (tp / pp / dp / ep) and
+exposes the handful of collectives the rank programs need:
+
+  all_reduce_   TP sum after row-parallel O / down projections (and vocab-parallel embed)
+  all_gather    TP sampling (score, id) pairs; EP token gather
+  reduce_scatter EP combine
+  send / recv   PP stage boundary activations and token feedback
+  broadcast_    control-plane metadata
+
+Small TP all-reduces (decode) can be routed to a one-shot peer-to-peer kernel
+(parallel/custom_allreduce.py) instead of RCCL; everything else stays on RCCL.
+Every op is stream-ordered and allocation-free when given outputs, so it can be captured
+in a hipGraph together with the compute kernels.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .mesh import Mesh
+
+
+@dataclass
+class GroupHandle:
+    ranks: list
+    pg: Optional[object]          # torch ProcessGroup, None when size == 1
+    rank_in_group: int
+
+    @property
+    def size(self) -> int:
+        return len(self.ranks)
+
+
+class Communicator:
+    def __init__(self, mesh: Mesh, rank: int, groups: dict[str, GroupHandle]):
+        self.mesh = mesh
+        self.rank = rank
+        self.groups = groups
+        self.custom_ar = None            # optional CustomAllReduce for the tp group
+        self.stats = {"all_reduce_bytes": 0, "send_bytes": 0, "recv_bytes": 0, "calls": 0}
+
+    # -- construction ---------------------------------------------------------------------
+    @classmethod
+    def single(cls) -> "Communicator":
+        m = Mesh()
+        g = GroupHandle([0], None, 0)
+        return cls(m, 0, {"tp": g, "pp": g, "dp": g, "ep": g, "world": g})
+
+    @classmethod
+    def from_mesh(cls, mesh: Mesh) -> "Communicator":
+        """Create every group of the mesh (collective: all ranks must call this)."""
+        if mesh.world_size == 1 or not dist.is_initialized():
+            if mesh.world_size != 1:
+                raise RuntimeError("torch.distributed not initialised for a multi-rank mesh")
+            return cls.single()
+        rank = dist.get_rank()
+        groups: dict[str, GroupHandle] = {}
+        for axis in ("tp", "pp", "dp"):
+            mine = None
+            for ranks in mesh.all_groups(axis):
+                pg = dist.new_group(ranks) if len(ranks) > 1 else None
+                if rank in ranks:
+                    mine = GroupHandle(ranks, pg, ranks.index(rank))
+            groups[axis] = mine
+        groups["ep"] = groups["dp"] if mesh.ep > 1 else GroupHandle([rank], None, 0)
+        groups["world"] = GroupHandle(list(range(mesh.world_size)), dist.group.WORLD, rank)
+        return cls(mesh, rank, groups)
+
+    # -- queries ----------------------------------------------------------------------------
+    def size(self, group: str = "tp") -> int:
+        return self.groups[group].size
+
+    def rank_in(self, group: str = "tp") -> int:
+        return self.groups[group].rank_in_group
+
+    # -- collectives --------------------------------------------------------------------------
+    def all_reduce_(self, t: torch.Tensor, group: str = "tp") -> torch.Tensor:
+        g = self.groups[group]
+        if g.size == 1:
+            return t
+        self.stats["calls"] += 1
+        self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+        if group == "tp" and self.custom_ar is not None and self.custom_ar.should_use(t):
+            return self.custom_ar.all_reduce_(t)
+        dist.all_reduce(t, group=g.pg)
+        return t
+
+    def all_gather(self, t: torch.Tensor, group: str = "tp", out: torch.Tensor | None = None) -> torch.Tensor:
+        g = self.groups[group]
+        if g.size == 1:
+            if out is not None:
+                out.copy_(t)
+                return out
+            return t
+        if out is None:
+            out = torch.empty((g.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=g.pg)
+        return out
+
+    def reduce_scatter(self, t: torch.Tensor, group: str = "ep", out: torch.Tensor | None = None) -> torch.Tensor:
+        g = self.groups[group]
+        if g.size == 1:
+            return t
+        n = t.shape[0] // g.size
+        if out is None:
+            out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, t.contiguous(), group=g.pg)
+        return out
+
+    def send(self, t: torch.Tensor, dst: int) -> None:
+        self.stats["send_bytes"] += t.numel() * t.element_size()
+        dist.send(t.contiguous(), dst)
+
+    def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        self.stats["recv_bytes"] += t.numel() * t.element_size()
+        dist.recv(t, src)
+        return t
+
+    def isend(self, t: torch.Tensor, dst: int):
+        self.stats["send_bytes"] += t.numel() * t.element_size()
+        return dist.isend(t.contiguous(), dst)
+
+    def irecv(self, t: torch.Tensor, src: int):
+        self.stats["recv_bytes"] += t.numel() * t.element_size()
+        return dist.irecv(t, src)
+
+    def broadcast_(self, t: torch.Tensor, src_in_group: int = 0, group: str = "world") -> torch.Tensor:
+        g = self.groups[group]
+        if g.size == 1:
+            return t
+        dist.broadcast(t, g.ranks[src_in_group], group=g.pg)
+        return t
+
+    def barrier(self, group: str = "world") -> None:
+        g = self.groups[group]
+        if g.size > 1:
+            dist.barrier(group=g.pg)
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from the torchrun environment (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR/PORT). Returns (rank, world_size, local_rank). Idempotent; a
+    no-op single-process setup when WORLD_SIZE is absent or 1."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 or dist.is_initialized():
+        return (dist.get_rank(), dist.get_world_size(), local) if dist.is_initialized() else (0, 1, 0)
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    t = timeout_s or float(os.environ.get("BFLY_COMM_TIMEOUT_S", "600"))
+    kwargs = {}
+    if backend == "nccl":
+        kwargs["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=t), **kwargs)
+    return rank, world, local

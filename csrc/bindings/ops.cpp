@@ -154,6 +154,14 @@ void add(const Tensor& a, const Tensor& b, Tensor& out) {
   bfly::launch_add(bf(a), bf(b), bf(out), a.numel(), cur_stream());
 }
 
+void init_hash(Tensor& out, int64_t grow0, int64_t gcol0, int64_t gcols, int64_t seed, double amp) {
+  CHECK_GPU(out); CHECK_BF16(out);
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1, "init_hash: 2-D with unit inner stride");
+  c10::DeviceGuard g(out.device());
+  bfly::launch_init_hash(bf(out), out.size(0), out.size(1), out.stride(0), grow0, gcol0, gcols,
+                         (uint32_t)seed, (float)amp, cur_stream());
+}
+
 void embed(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) {
   CHECK_GPU(ids); CHECK_I32(ids); CHECK_BF16(table); CHECK_BF16(out);
   TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && out.is_contiguous(), "embed: layout");
@@ -289,6 +297,35 @@ void attn_prefill(const Tensor& q, const Tensor& k, const Tensor& v, const Tenso
   TORCH_CHECK(rc == 0, "attn_prefill: unsupported configuration (rc=", rc, ")");
 }
 
+void moe_route(const Tensor& x, const Tensor& wr, int64_t top_k, Tensor& gates, Tensor& topk_ids,
+               Tensor& topk_w) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(wr);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "moe_route: x");
+  TORCH_CHECK(wr.dim() == 2 && wr.is_contiguous() && wr.size(1) == x.size(1), "moe_route: router weight");
+  const int T = x.size(0), H = x.size(1), E = wr.size(0);
+  TORCH_CHECK(gates.scalar_type() == at::kFloat && gates.is_contiguous() && gates.numel() == (long)T * E, "moe_route: gates");
+  CHECK_I32(topk_ids);
+  TORCH_CHECK(topk_ids.numel() == (long)T * top_k && topk_w.numel() == (long)T * top_k &&
+                  topk_w.scalar_type() == at::kFloat, "moe_route: topk outputs");
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_moe_route(bf(x), x.stride(0), bf(wr), T, H, E, top_k, gates.data_ptr<float>(),
+                                        topk_ids.data_ptr<int>(), topk_w.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc == 0, "moe_route: unsupported (E <= 64, k <= 8, H % 8 == 0)");
+}
+
+void moe_gate_scale(Tensor& h, const Tensor& gates, int64_t e0, int64_t num_local) {
+  CHECK_GPU(h); CHECK_BF16(h);
+  TORCH_CHECK(h.dim() == 2 && h.is_contiguous(), "moe_gate_scale: h");
+  TORCH_CHECK(gates.scalar_type() == at::kFloat && gates.dim() == 2 && gates.is_contiguous() &&
+                  gates.size(0) == h.size(0), "moe_gate_scale: gates");
+  const int T = h.size(0), E = gates.size(1);
+  TORCH_CHECK(h.size(1) % num_local == 0 && e0 + num_local <= E, "moe_gate_scale: experts");
+  const int F = h.size(1) / num_local;
+  TORCH_CHECK(F % 8 == 0, "moe_gate_scale: F % 8");
+  c10::DeviceGuard g(h.device());
+  bfly::launch_moe_gate_scale(bf(h), gates.data_ptr<float>(), T, E, e0, num_local, F, cur_stream());
+}
+
 void probe(int64_t which, Tensor& out) {
   CHECK_GPU(out);
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 64 * 16, "probe: out");
@@ -307,6 +344,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("silu_mul(Tensor gu, Tensor(a!) out, int interleave) -> ()");
   m.def("gelu(Tensor x, Tensor(a!) out) -> ()");
   m.def("add(Tensor a, Tensor b, Tensor(a!) out) -> ()");
+  m.def("init_hash(Tensor(a!) out, int grow0, int gcol0, int gcols, int seed, float amp) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vstart) -> ()");
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
         "Tensor(b!) out_scores, Tensor(c!) workspace) -> ()");
@@ -317,6 +355,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
         "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
         "Tensor(c!)? part_ml) -> ()");
+  m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
+  m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
   m.def("probe(int which, Tensor(a!) out) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
         "bool causal, Tensor(a!) out) -> ()");
@@ -331,9 +371,12 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("gelu", &gelu);
   m.impl("add", &add);
   m.impl("embed", &embed);
+  m.impl("init_hash", &init_hash);
   m.impl("sample", &sample);
   m.impl("gemm", &gemm);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("probe", &probe);
+  m.impl("moe_route", &moe_route);
+  m.impl("moe_gate_scale", &moe_gate_scale);
 }

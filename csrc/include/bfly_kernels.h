@@ -38,6 +38,8 @@ void launch_silu_mul(const bf16* gu, bf16* out, long rows, int ffn, int interlea
                      hipStream_t stream);
 void launch_gelu(const bf16* x, bf16* out, long n, hipStream_t stream);
 void launch_add(const bf16* a, const bf16* b, bf16* out, long n, hipStream_t stream);
+void launch_init_hash(bf16* out, long rows, int cols, long ld, long grow0, long gcol0, long gcols,
+                      uint32_t seed, float amp, hipStream_t stream);
 void launch_embed(const int* ids, const bf16* table, bf16* out, int T, int dim, int vstart,
                   int vlocal, hipStream_t stream);
 
@@ -64,6 +66,12 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
                         hipStream_t stream);
+
+// moe.hip
+int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H, int E, int K,
+                     float* gates, int* topk_ids, float* topk_w, hipStream_t stream);
+void launch_moe_gate_scale(bf16* h, const float* gates, long T, int E, int e0, int El, int F,
+                           hipStream_t stream);
 
 // probe.hip
 void launch_probe(int which, float* out, hipStream_t stream);

@@ -86,6 +86,36 @@ __global__ void embed_kernel(const int* __restrict__ ids, const bf16* __restrict
   }
 }
 
+// Deterministic, partition-independent random init: element (global_row, global_col) of a
+// logical weight gets a value that depends only on (seed, global index), so every rank can
+// generate exactly its own shard and any partition reproduces the same global weights.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__global__ void init_hash_kernel(bf16* __restrict__ out, long rows, int cols, long ld, long grow0,
+                                 long gcol0, long gcols, uint32_t seed, float amp) {
+  const long n = rows * cols;
+  for (long e = blockIdx.x * (long)kEwThreads + threadIdx.x; e < n;
+       e += (long)gridDim.x * kEwThreads) {
+    const long r = e / cols;
+    const int c = (int)(e % cols);
+    const uint32_t idx = (uint32_t)((grow0 + r) * gcols + gcol0 + c);
+    const uint32_t h = fmix32(idx * 0x9E3779B1u + seed);
+    const float u = (float)(h >> 8) * (1.0f / 16777216.0f) + (0.5f / 16777216.0f);
+    out[r * ld + c] = f2bf(amp * (2.f * u - 1.f));
+  }
+}
+
+void launch_init_hash(bf16* out, long rows, int cols, long ld, long grow0, long gcol0, long gcols,
+                      uint32_t seed, float amp, hipStream_t stream) {
+  const long n = rows * cols;
+  if (n <= 0) return;
+  long g = (n + kEwThreads - 1) / kEwThreads;
+  if (g > 65536) g = 65536;
+  init_hash_kernel<<<(int)g, kEwThreads, 0, stream>>>(out, rows, cols, ld, grow0, gcol0, gcols, seed, amp);
+}
+
 void launch_silu_mul(const bf16* gu, bf16* out, long rows, int ffn, int interleave,
                      hipStream_t stream) {
   const long nvec = rows * (ffn / 8);

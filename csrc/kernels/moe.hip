@@ -1,0 +1,101 @@
+// Mixture-of-experts kernels (K11 router, K12 gating) for the dense-dispatch MoE path.
+//
+// moe_route: one wave per token. logits[e] = x . Wr[e] (E <= 64 experts, 16-B loads of the
+// token row and of each router row), softmax over experts, top-k selection, renormalisation
+// over the selected experts (Mixtral semantics), and a dense gate row gates[t, e] (0 for
+// experts not selected) used by the fixed-shape expert GEMMs; topk ids/weights are also
+// emitted for the sparse (grouped) path and for routing statistics.
+//
+// moe_gate_scale: h[t, e*F + f] *= gates[t, e0 + e] for the local experts: the gate weight is
+// folded into the intermediate activation so that ONE GEMM over the concatenated local experts
+// (K = E_local * F) both applies every expert's down projection and sums over experts.
+#include "bfly_common.h"
+#include "bfly_kernels.h"
+
+namespace bfly {
+
+constexpr int kMaxExperts = 64;
+
+__global__ void __launch_bounds__(256)
+moe_route_kernel(const bf16* __restrict__ x, long x_stride, const bf16* __restrict__ wr, int T,
+                 int H, int E, int K, float* __restrict__ gates, int* __restrict__ topk_ids,
+                 float* __restrict__ topk_w) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const bf16* xr = x + (long)t * x_stride;
+  float logit[kMaxExperts];
+  for (int e = 0; e < E; ++e) {
+    float acc = 0.f;
+    for (int c = lane * 8; c < H; c += 64 * 8) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(xr + c);
+      const bf16x8 w = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += bf2f(a[j]) * bf2f(w[j]);
+    }
+    logit[e] = wave_sum(acc);
+  }
+  if (lane != 0) return;
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) mx = fmaxf(mx, logit[e]);
+  float den = 0.f;
+  for (int e = 0; e < E; ++e) {
+    logit[e] = __expf(logit[e] - mx);
+    den += logit[e];
+  }
+  for (int e = 0; e < E; ++e) gates[(long)t * E + e] = 0.f;
+  float sel_sum = 0.f;
+  int ids[8];
+  float ws[8];
+  for (int k = 0; k < K; ++k) {
+    int best = 0;
+    float bv = -1.f;
+    for (int e = 0; e < E; ++e)
+      if (logit[e] > bv) { bv = logit[e]; best = e; }
+    ids[k] = best;
+    ws[k] = bv / den;
+    sel_sum += ws[k];
+    logit[best] = -2.f;  // exclude from further selection
+  }
+  for (int k = 0; k < K; ++k) {
+    const float w = ws[k] / sel_sum;
+    topk_ids[(long)t * K + k] = ids[k];
+    topk_w[(long)t * K + k] = w;
+    gates[(long)t * E + ids[k]] = w;
+  }
+}
+
+__global__ void moe_gate_scale_kernel(bf16* __restrict__ h, const float* __restrict__ gates,
+                                      long T, int E, int e0, int El, int F) {
+  const long nvec = T * (long)El * F / 8;
+  const int vpr = El * F / 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += (long)gridDim.x * 256) {
+    const long t = i / vpr;
+    const int c = (int)(i % vpr) * 8;
+    const int e = c / F;
+    const float g = gates[t * E + e0 + e];
+    bf16x8 v = reinterpret_cast<bf16x8*>(h)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) * g);
+    reinterpret_cast<bf16x8*>(h)[i] = v;
+  }
+}
+
+int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H, int E, int K,
+                     float* gates, int* topk_ids, float* topk_w, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (E > kMaxExperts || K > 8 || K > E || H % 8 != 0) return -1;
+  moe_route_kernel<<<(T + 3) / 4, 256, 0, stream>>>(x, x_stride, wr, T, H, E, K, gates, topk_ids, topk_w);
+  return 0;
+}
+
+void launch_moe_gate_scale(bf16* h, const float* gates, long T, int E, int e0, int El, int F,
+                           hipStream_t stream) {
+  const long nvec = T * (long)El * F / 8;
+  if (nvec <= 0) return;
+  long g = (nvec + 255) / 256;
+  if (g > 4096) g = 4096;
+  moe_gate_scale_kernel<<<(int)g, 256, 0, stream>>>(h, gates, T, E, e0, El, F);
+}
+
+}  // namespace bfly

@@ -1,0 +1,155 @@
+// Paged KV-cache block manager (see kv_manager.cpp for the design notes).
+#pragma once
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace bfly_rt {
+
+class KVBlockManager {
+ public:
+  KVBlockManager(int num_blocks, int block_size)
+      : num_blocks_(num_blocks), block_size_(block_size), refcnt_(num_blocks, 0) {
+    if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("bad KV geometry");
+    free_.reserve(num_blocks);
+    for (int b = num_blocks - 1; b >= 0; --b) free_.push_back(b);
+  }
+
+  int num_blocks() const { return num_blocks_; }
+  int block_size() const { return block_size_; }
+  int num_free() const { return (int)free_.size(); }
+  int num_seqs() const { return (int)seqs_.size(); }
+  bool has(int64_t sid) const { return seqs_.count(sid) != 0; }
+
+  int blocks_needed(int64_t tokens) const { return (int)((tokens + block_size_ - 1) / block_size_); }
+  bool can_allocate(int64_t tokens) const { return blocks_needed(tokens) <= num_free(); }
+
+  // Register a sequence with `tokens` tokens to cache; returns their slots.
+  std::vector<int32_t> allocate(int64_t sid, int64_t tokens) {
+    if (seqs_.count(sid)) throw std::invalid_argument("sequence already allocated");
+    const int nb = blocks_needed(tokens);
+    if (nb > num_free()) throw std::runtime_error("KV cache out of blocks");
+    Seq s;
+    s.blocks.reserve(nb + 4);
+    for (int i = 0; i < nb; ++i) s.blocks.push_back(take());
+    s.len = tokens;
+    std::vector<int32_t> slots(tokens);
+    for (int64_t t = 0; t < tokens; ++t) slots[t] = slot_of(s, t);
+    seqs_.emplace(sid, std::move(s));
+    return slots;
+  }
+
+  // Reserve the slot for one more token. Returns (slot, cow_src, cow_dst): when the last page
+  // is shared, a fresh page is taken and the caller must copy cow_src -> cow_dst first.
+  std::tuple<int32_t, int32_t, int32_t> append_slot(int64_t sid) {
+    Seq& s = get(sid);
+    int cow_src = -1, cow_dst = -1;
+    if (s.len % block_size_ == 0) {
+      if (free_.empty()) throw std::runtime_error("KV cache out of blocks");
+      s.blocks.push_back(take());
+    } else if (refcnt_[s.blocks.back()] > 1) {
+      if (free_.empty()) throw std::runtime_error("KV cache out of blocks");
+      cow_src = s.blocks.back();
+      cow_dst = take();
+      --refcnt_[cow_src];
+      s.blocks.back() = cow_dst;
+    }
+    const int32_t slot = slot_of(s, s.len);
+    ++s.len;
+    return {slot, cow_src, cow_dst};
+  }
+
+  // Can every sequence in `sids` append one token without running out of pages?
+  bool can_append(const std::vector<int64_t>& sids) const {
+    int need = 0;
+    for (int64_t sid : sids) {
+      const Seq& s = cget(sid);
+      if (s.len % block_size_ == 0 || refcnt_[s.blocks.back()] > 1) ++need;
+    }
+    return need <= num_free();
+  }
+
+  void fork(int64_t parent, int64_t child) {
+    const Seq& p = cget(parent);
+    if (seqs_.count(child)) throw std::invalid_argument("child exists");
+    Seq c = p;
+    for (int b : c.blocks) ++refcnt_[b];
+    seqs_.emplace(child, std::move(c));
+  }
+
+  void free(int64_t sid) {
+    auto it = seqs_.find(sid);
+    if (it == seqs_.end()) return;
+    for (int b : it->second.blocks) release(b);
+    seqs_.erase(it);
+  }
+
+  std::vector<int32_t> block_table(int64_t sid) const {
+    const Seq& s = cget(sid);
+    return std::vector<int32_t>(s.blocks.begin(), s.blocks.end());
+  }
+  int64_t length(int64_t sid) const { return cget(sid).len; }
+
+  // Decode-step arrays for a batch, written into caller buffers:
+  //   tables [B, max_blocks] (row-major, zero padded), ctx_lens [B] = len after append.
+  // Call after append_slot for this step.
+  void fill_decode_tables(const std::vector<int64_t>& sids,
+                          py::array_t<int32_t, py::array::c_style> tables,
+                          py::array_t<int32_t, py::array::c_style> ctx_lens) const {
+    auto T = tables.mutable_unchecked<2>();
+    auto C = ctx_lens.mutable_unchecked<1>();
+    const int64_t B = (int64_t)sids.size();
+    if (T.shape(0) < B || C.shape(0) < B) throw std::invalid_argument("buffers too small");
+    const int64_t mb = T.shape(1);
+    for (int64_t i = 0; i < B; ++i) {
+      const Seq& s = cget(sids[i]);
+      if ((int64_t)s.blocks.size() > mb) throw std::invalid_argument("block table too narrow");
+      int64_t j = 0;
+      for (; j < (int64_t)s.blocks.size(); ++j) T(i, j) = s.blocks[j];
+      for (; j < mb; ++j) T(i, j) = 0;
+      C(i) = (int32_t)s.len;
+    }
+  }
+
+ private:
+  struct Seq {
+    std::vector<int> blocks;
+    int64_t len = 0;
+  };
+  int take() {
+    const int b = free_.back();
+    free_.pop_back();
+    refcnt_[b] = 1;
+    return b;
+  }
+  void release(int b) {
+    if (--refcnt_[b] == 0) free_.push_back(b);
+  }
+  int32_t slot_of(const Seq& s, int64_t t) const {
+    return (int32_t)(s.blocks[t / block_size_] * block_size_ + t % block_size_);
+  }
+  Seq& get(int64_t sid) {
+    auto it = seqs_.find(sid);
+    if (it == seqs_.end()) throw std::out_of_range("unknown sequence");
+    return it->second;
+  }
+  const Seq& cget(int64_t sid) const {
+    auto it = seqs_.find(sid);
+    if (it == seqs_.end()) throw std::out_of_range("unknown sequence");
+    return it->second;
+  }
+
+  int num_blocks_, block_size_;
+  std::vector<int> free_;
+  std::vector<int> refcnt_;
+  std::unordered_map<int64_t, Seq> seqs_;
+};
+
+}  // namespace bfly_rt

@@ -1,0 +1,151 @@
+// Continuous-batching scheduler core (host runtime, C++) — the "Scheduling System" of the
+// reference's declared architecture (/root/reference/CLAUDE.md:22).
+//
+// Policy (one instance per data-parallel replica; deterministic, so PP/TP ranks that run
+// replicas of it on identical inputs make identical decisions without messaging):
+//   1. prefill first: admit waiting sequences in FIFO order while the batch has room
+//      (max_batch), the step's token budget allows (max_prefill_tokens) and the KV pages for
+//      the whole (re)prompt plus one decode page are free; a step is either all-prefill or
+//      all-decode, so decode steps keep a fixed shape for hipGraph replay;
+//   2. otherwise decode every running sequence; if the KV cache cannot hold one more token
+//      for each of them, preempt the most recently admitted ones (free their pages, requeue
+//      them at the FRONT of the waiting queue for recompute) until it can.
+// The scheduler owns page allocation (through KVBlockManager) and returns the cache slots
+// of every token it schedules.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "kv_manager.h"
+
+#include <algorithm>
+#include <deque>
+#include <stdexcept>
+#include <unordered_map>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace bfly_rt {
+
+struct StepPlan {
+  int kind = 0;  // 0 idle, 1 prefill, 2 decode
+  std::vector<int64_t> seq_ids;
+  std::vector<std::vector<int32_t>> prefill_slots;  // per sequence, every token
+  std::vector<int64_t> prefill_lens;
+  std::vector<int32_t> decode_slots;                // per sequence, the new token
+  std::vector<int32_t> decode_positions;
+  std::vector<std::pair<int32_t, int32_t>> cow;     // page copies to do before the step
+  std::vector<int64_t> preempted;
+};
+
+class Scheduler {
+ public:
+  Scheduler(KVBlockManager& kv, int max_batch, int64_t max_prefill_tokens)
+      : kv_(kv), max_batch_(max_batch), max_prefill_tokens_(max_prefill_tokens) {}
+
+  void add(int64_t sid, int64_t prompt_len, int64_t max_new_tokens) {
+    if (info_.count(sid)) throw std::invalid_argument("duplicate sequence id");
+    info_[sid] = Info{prompt_len, 0, max_new_tokens};
+    waiting_.push_back(sid);
+  }
+
+  // Record one generated token (after a prefill or decode step produced it).
+  void on_token(int64_t sid) { info_.at(sid).generated++; }
+
+  void finish(int64_t sid) {
+    auto it = std::find(running_.begin(), running_.end(), sid);
+    if (it != running_.end()) running_.erase(it);
+    auto wt = std::find(waiting_.begin(), waiting_.end(), sid);
+    if (wt != waiting_.end()) waiting_.erase(wt);
+    kv_.free(sid);
+    info_.erase(sid);
+  }
+
+  int num_waiting() const { return (int)waiting_.size(); }
+  int num_running() const { return (int)running_.size(); }
+  std::vector<int64_t> running() const { return running_; }
+  std::vector<int64_t> waiting() const { return std::vector<int64_t>(waiting_.begin(), waiting_.end()); }
+
+  StepPlan schedule() {
+    StepPlan plan;
+    // --- 1. prefill admission --------------------------------------------------------------
+    int64_t budget = max_prefill_tokens_;
+    int free_pages = kv_.num_free();
+    while (!waiting_.empty() && (int)(running_.size() + plan.seq_ids.size()) < max_batch_) {
+      const int64_t sid = waiting_.front();
+      const Info& in = info_.at(sid);
+      const int64_t len = in.prompt_len + in.generated;   // recompute after preemption
+      if (len > budget && !plan.seq_ids.empty()) break;
+      const int need = kv_.blocks_needed(len + 1);
+      if (need > free_pages) break;
+      waiting_.pop_front();
+      plan.seq_ids.push_back(sid);
+      plan.prefill_lens.push_back(len);
+      plan.prefill_slots.push_back(kv_.allocate(sid, len));
+      free_pages = kv_.num_free();
+      budget -= len;
+      if (budget <= 0) break;
+    }
+    if (!plan.seq_ids.empty()) {
+      plan.kind = 1;
+      for (int64_t sid : plan.seq_ids) running_.push_back(sid);
+      return plan;
+    }
+    if (running_.empty()) return plan;  // idle
+    // --- 2. decode (preempt newest until one token per sequence fits) -------------------------
+    while (!running_.empty() && !kv_.can_append(running_)) {
+      const int64_t victim = running_.back();
+      running_.pop_back();
+      kv_.free(victim);
+      waiting_.push_front(victim);
+      plan.preempted.push_back(victim);
+    }
+    if (running_.empty()) return plan;
+    plan.kind = 2;
+    plan.seq_ids = running_;
+    for (int64_t sid : running_) {
+      auto [slot, src, dst] = kv_.append_slot(sid);
+      plan.decode_slots.push_back(slot);
+      const Info& in = info_.at(sid);
+      plan.decode_positions.push_back((int32_t)(in.prompt_len + in.generated - 1));
+      if (src >= 0) plan.cow.emplace_back(src, dst);
+    }
+    return plan;
+  }
+
+ private:
+  struct Info {
+    int64_t prompt_len, generated, max_new;
+  };
+  KVBlockManager& kv_;
+  int max_batch_;
+  int64_t max_prefill_tokens_;
+  std::deque<int64_t> waiting_;
+  std::vector<int64_t> running_;
+  std::unordered_map<int64_t, Info> info_;
+};
+
+void register_scheduler(py::module_& m) {
+  py::class_<StepPlan>(m, "StepPlan")
+      .def_readonly("kind", &StepPlan::kind)
+      .def_readonly("seq_ids", &StepPlan::seq_ids)
+      .def_readonly("prefill_slots", &StepPlan::prefill_slots)
+      .def_readonly("prefill_lens", &StepPlan::prefill_lens)
+      .def_readonly("decode_slots", &StepPlan::decode_slots)
+      .def_readonly("decode_positions", &StepPlan::decode_positions)
+      .def_readonly("cow", &StepPlan::cow)
+      .def_readonly("preempted", &StepPlan::preempted);
+  py::class_<Scheduler>(m, "Scheduler")
+      .def(py::init<KVBlockManager&, int, int64_t>(), py::arg("kv"), py::arg("max_batch"),
+           py::arg("max_prefill_tokens"), py::keep_alive<1, 2>())
+      .def("add", &Scheduler::add)
+      .def("on_token", &Scheduler::on_token)
+      .def("finish", &Scheduler::finish)
+      .def("schedule", &Scheduler::schedule)
+      .def_property_readonly("num_waiting", &Scheduler::num_waiting)
+      .def_property_readonly("num_running", &Scheduler::num_running)
+      .def("running", &Scheduler::running)
+      .def("waiting", &Scheduler::waiting);
+}
+
+}  // namespace bfly_rt

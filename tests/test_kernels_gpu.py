@@ -186,3 +186,27 @@ def test_attn_decode_strided_q():
     ctx = torch.tensor([5, 64, 250], dtype=torch.int32, device=DEV)
     o = ops.attn_decode(q, kc, vc, bt, ctx, 0.1, 256)
     _close(o, ref.attn_decode(q, kc, vc, bt, ctx, 0.1), 2e-2, 2e-2)
+
+
+def test_init_hash_matches_reference_and_is_partition_independent():
+    full = torch.empty(96, 256, dtype=torch.bfloat16, device=DEV)
+    ops.init_hash_(full, 0, 0, 256, 1234, 0.1)
+    cpu = torch.empty(96, 256, dtype=torch.bfloat16)
+    ref.init_hash(cpu, 0, 0, 256, 1234, 0.1)
+    _close(full, cpu, 1e-3, 1e-2)
+    part = torch.empty(32, 128, dtype=torch.bfloat16, device=DEV)
+    ops.init_hash_(part, 40, 64, 256, 1234, 0.1)
+    assert torch.equal(part.cpu(), full[40:72, 64:192].cpu())
+
+
+def test_moe_route_and_gate_scale():
+    T, H, E, K = 37, 512, 8, 2
+    x, wr = _bf(T, H, seed=30), _bf(E, H, scale=0.05, seed=31)
+    g, ids, w = ops.moe_route(x, wr, K)
+    g2, ids2, w2 = ref.moe_route(x, wr, K)
+    _close(g, g2, 1e-3, 1e-2)
+    h = _bf(T, 3 * 64, seed=32)
+    h2 = h.clone()
+    ops.moe_gate_scale_(h, g, 2, 3)
+    ref.moe_gate_scale(h2, g2, 2, 3)
+    _close(h, h2, 1e-2, 1e-2)
