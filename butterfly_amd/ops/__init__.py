@@ -210,8 +210,9 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None):
 
 def gemm_plan(M: int, N: int, K: int) -> dict:
     load_library()
-    k, mt, nt, bm, bn, sk = torch.ops.bfly.gemm_plan(M, N, K)
-    return {"kind": "skinny" if k == 0 else "tile", "mt": mt, "nt": nt, "bm": bm, "bn": bn, "splitk": sk}
+    k, mt, nt, bm, bn, sk, wk = torch.ops.bfly.gemm_plan(M, N, K)
+    return {"kind": "skinny" if k == 0 else "tile", "mt": mt, "nt": nt, "wk": wk, "bm": bm, "bn": bn,
+            "splitk": sk}
 
 
 def attn_prefill(q, k, v, cu_seqlens, max_seqlen: int, scale: float, causal: bool = True,

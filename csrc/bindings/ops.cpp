@@ -206,7 +206,7 @@ int64_t gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
 
 std::vector<int64_t> gemm_plan(int64_t M, int64_t N, int64_t K) {
   const bfly::GemmPlan p = bfly::plan_gemm(M, N, K);
-  return {p.kind, p.mt, p.nt, p.bm, p.bn, p.sk};
+  return {p.kind, p.mt, p.nt, p.bm, p.bn, p.sk, p.wk};
 }
 
 void gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& bias,
@@ -219,9 +219,7 @@ void gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Ten
   TORCH_CHECK(w.size(1) == K, "gemm: K mismatch");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm: row strides % 8");
   TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64, got ", K);
-  TORCH_CHECK(N % 32 == 0, "gemm: N must be a multiple of 32, got ", N);
-  const bfly::GemmPlan plan = bfly::plan_gemm(M, N, K);
-  if (plan.kind == 1) TORCH_CHECK(N % 128 == 0, "gemm: N must be a multiple of 128 for M > 64, got ", N);
+  TORCH_CHECK(N % 128 == 0, "gemm: N must be a multiple of 128, got ", N);
   const int nout = epilogue == bfly::EPI_SILU ? N / 2 : N;
   TORCH_CHECK(out.size(0) == M && out.size(1) == nout, "gemm: out shape");
   const bfly::bf16* bp = nullptr;
@@ -240,6 +238,30 @@ void gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Ten
   const int rc = bfly::launch_gemm(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, epilogue, bp,
                                    bf(out), out.stride(0), ws, ws_bytes, cur_stream());
   TORCH_CHECK(rc == 0, "gemm: unsupported shape M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
+}
+
+// Benchmark / tuning entry: run an explicit plan [kind, mt, nt, wk, bm, bn, sk].
+void gemm_with_plan(const Tensor& x, const Tensor& w, Tensor& out, std::vector<int64_t> plan,
+                    int64_t epilogue, const c10::optional<Tensor>& workspace) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2 && plan.size() == 7, "gemm_with_plan: args");
+  CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm_with_plan: K mismatch");
+  const int nout = epilogue == bfly::EPI_SILU ? N / 2 : N;
+  TORCH_CHECK(out.size(0) == M && out.size(1) == nout, "gemm_with_plan: out shape");
+  bfly::GemmPlan p{};
+  p.kind = plan[0]; p.mt = plan[1]; p.nt = plan[2]; p.wk = plan[3]; p.bm = plan[4]; p.bn = plan[5]; p.sk = plan[6];
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  if (workspace.has_value()) {
+    ws = reinterpret_cast<float*>(workspace->data_ptr());
+    ws_bytes = workspace->numel() * workspace->element_size();
+  }
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_gemm_plan(p, bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, epilogue,
+                                        nullptr, bf(out), out.stride(0), ws, ws_bytes, cur_stream());
+  TORCH_CHECK(rc == 0, "gemm_with_plan: plan rejected (rc=", rc, ")");
 }
 
 int64_t attn_decode_splits(int64_t max_ctx, int64_t part_tokens) {
@@ -349,6 +371,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
         "Tensor(b!) out_scores, Tensor(c!) workspace) -> ()");
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
+  m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
   m.def("gemm_plan(int M, int N, int K) -> int[]", &gemm_plan);
   m.def("attn_decode_splits(int max_ctx, int part_tokens) -> int", &attn_decode_splits);
@@ -374,6 +397,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("init_hash", &init_hash);
   m.impl("sample", &sample);
   m.impl("gemm", &gemm);
+  m.impl("gemm_with_plan", &gemm_with_plan);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("probe", &probe);

@@ -14,6 +14,7 @@ enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_SILU = 2 };
 struct GemmPlan {
   int kind;  // 0 = skinny (decode), 1 = LDS-tiled
   int mt, nt;
+  int wk;    // skinny: waves splitting K inside a workgroup (1, 2, 4)
   int bm, bn;
   int sk;    // split-K factor
 };
@@ -52,6 +53,9 @@ void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vst
 // gemm.hip
 GemmPlan plan_gemm(int M, int N, int K);
 size_t gemm_workspace_bytes(int M, int N, int K);
+int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
+                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
+                     size_t ws_bytes, hipStream_t stream);
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
                 hipStream_t stream);

@@ -16,9 +16,9 @@
 //    tokens are the B operand, so one weight fragment feeds MT token tiles. The K loop is
 //    split over the 4 waves of a workgroup and, for narrow N, over workgroups (split-K with
 //    f32 partial slabs and a reduce kernel that applies the epilogue).
-//    K permutation: lane group g = lane>>4 loads 64 contiguous bytes (4 sub-steps) of a row
-//    per 128-wide K chunk: physical k = 32g + 8s + j for sub-step s, element j. The same map is
-//    used for both operands, so every product pairs matching k.
+//    K permutation: per 128-wide K chunk, sub-step s, lane group g = lane>>4 and element j
+//    hold physical k = 32s + 8g + j, so each load instruction reads 64 contiguous bytes per
+//    row; the same map is used for both operands, so every product pairs matching k.
 //  * gemm_tile (M > 64, prefill / large-batch decode): BMx128x64 LDS-tiled, 4 waves (2x2),
 //    both operands staged global->LDS by global_load_lds_dwordx4 (no VGPR round trip) into
 //    two buffers (load of tile t+1 overlaps MFMAs on tile t), XOR-swizzled LDS image
@@ -78,21 +78,23 @@ template <int MT, int NT>
 __device__ __forceinline__ void skinny_load(const bf16* __restrict__ W, const bf16* __restrict__ X,
                                             long ldw, long ldx, int n0, int kc, int lane, int M,
                                             bf16x8 (&a)[NT][4], bf16x8 (&b)[MT][4]) {
+  // physical k of (lane group g, sub-step s, element j) = 32 s + 8 g + j: in each load
+  // instruction the 4 lane groups of a row read 64 contiguous bytes.
   const int g = lane >> 4, r = lane & 15;
-  const long kofs = (long)kc * 128 + 32 * g;
+  const long kofs = (long)kc * 128 + 8 * g;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const bf16x8* p = reinterpret_cast<const bf16x8*>(W + (long)(n0 + 16 * t + r) * ldw + kofs);
+    const bf16* p = W + (long)(n0 + 16 * t + r) * ldw + kofs;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) a[t][s] = ld_nt(p + s);
+    for (int s = 0; s < 4; ++s) a[t][s] = ld_nt(reinterpret_cast<const bf16x8*>(p + 32 * s));
   }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int m = 16 * mt + r;
     m = m < M ? m : M - 1;
-    const bf16x8* p = reinterpret_cast<const bf16x8*>(X + (long)m * ldx + kofs);
+    const bf16* p = X + (long)m * ldx + kofs;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) b[mt][s] = p[s];
+    for (int s = 0; s < 4; ++s) b[mt][s] = *reinterpret_cast<const bf16x8*>(p + 32 * s);
   }
 }
 
@@ -107,16 +109,21 @@ __device__ __forceinline__ void skinny_mma(const bf16x8 (&a)[NT][4], const bf16x
       for (int mt = 0; mt < MT; ++mt) acc[t][mt] = mfma16(a[t][s], b[mt][s], acc[t][mt]);
 }
 
-template <int MT, int NT>
+// WK = waves of a workgroup that split K (their partials are summed through LDS); the other
+// 4 / WK waves split N and share the same K range (their X fragments hit the same L1 lines).
+template <int MT, int NT, int WK>
 __global__ void __launch_bounds__(kSkThreads)
 gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                    int M, int N, int K, int epi, const bf16* __restrict__ bias,
                    bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+  constexpr int WN = 4 / WK;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16 * NT;
+  const int wk = wid % WK, wn = wid / WK;
+  const int nb0 = blockIdx.x * 16 * NT * WN;
+  const int n0 = nb0 + wn * 16 * NT;
   const int nchunks = K / 128;
-  const int S = gridDim.y * 4;
-  const int s_idx = blockIdx.y * 4 + wid;
+  const int S = gridDim.y * WK;
+  const int s_idx = blockIdx.y * WK + wk;
   const int c0 = (int)(((long)nchunks * s_idx) / S), c1 = (int)(((long)nchunks * (s_idx + 1)) / S);
 
   f32x4 acc[NT][MT];
@@ -139,7 +146,7 @@ gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict_
     ++c;
   }
 
-  // Cross-wave reduction through LDS: red[wave][t][mt][i][lane].
+  // Cross-wave reduction through LDS: red[wave][t][mt][i][lane], summed over the WK waves.
   constexpr int E = NT * MT * 4 * 64;
   __shared__ float red[4 * E];
 #pragma unroll
@@ -151,20 +158,26 @@ gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict_
   __syncthreads();
 
   const bool silu_epi = epi == EPI_SILU;
-  for (int e = threadIdx.x; e < E; e += kSkThreads) {
+  for (int idx = threadIdx.x; idx < WN * E; idx += kSkThreads) {
+    const int vn = idx / E, e = idx % E;
     const int l = e & 63, i = (e >> 6) & 3, tm = e >> 8;
     const int t = tm / MT, mt = tm % MT;
     const int m = 16 * mt + (l & 15);
     if (m >= M) continue;
-    const int n = n0 + 16 * t + (l >> 4) * 4 + i;
-    const float v = red[e] + red[E + e] + red[2 * E + e] + red[3 * E + e];
+    const int nw0 = nb0 + vn * 16 * NT;
+    const int n = nw0 + 16 * t + (l >> 4) * 4 + i;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < WK; ++k) v += red[(vn * WK + k) * E + e];
     if (part) {
       part[(long)blockIdx.y * M * N + (long)m * N + n] = v;
     } else if (silu_epi) {
       if (t & 1) continue;  // the gate tile's thread combines with its up partner
       const int eu = e + MT * 4 * 64;  // same (mt, i, lane), tile t + 1
-      const float u = red[eu] + red[E + eu] + red[2 * E + eu] + red[3 * E + eu];
-      const int f = n0 / 2 + 16 * (t / 2) + (l >> 4) * 4 + i;
+      float u = 0.f;
+#pragma unroll
+      for (int k = 0; k < WK; ++k) u += red[(vn * WK + k) * E + eu];
+      const int f = nw0 / 2 + 16 * (t / 2) + (l >> 4) * 4 + i;
       store_out(out, ldo, m, f, silu(v) * u);
     } else {
       store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
@@ -182,10 +195,11 @@ template <int ROWS>
 __device__ __forceinline__ void tile_stage(const bf16* __restrict__ src, long ld, int row0,
                                            int row_max, int k0, char* lds, int wid, int lane) {
   // ROWS x 64 bf16 = ROWS x 8 chunks of 16 B; one wave-instruction writes 8 rows (1 KiB).
-  constexpr int kInstr = ROWS / 32;  // per wave (4 waves)
+  constexpr int kInstr = (ROWS + 31) / 32;  // per wave (4 waves)
 #pragma unroll
   for (int i = 0; i < kInstr; ++i) {
     const int blk = i * 4 + wid;             // 8-row block index
+    if (ROWS % 32 != 0 && blk * 8 >= ROWS) break;
     const int row = blk * 8 + (lane >> 3);
     const int slot = lane & 7;
     const int chunk = slot ^ ((row >> 1) & 7);
@@ -201,19 +215,20 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int chunk) 
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + slot * 16);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WMW>
 __global__ void __launch_bounds__(kTileThreads)
 gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
                  bf16* __restrict__ out, long ldo, float* __restrict__ part) {
-  constexpr int WM = BM / 2, WN = BN / 2;    // per-wave output tile
+  constexpr int WNW = 4 / WMW;                // waves along M x waves along N
+  constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
   constexpr int A_BYTES = BM * kBK * 2, B_BYTES = BN * kBK * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;  // one buffer = [A tile | B tile]
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WNW, wn = wid % WNW;
   const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
   const int tile = xcd_remap(blockIdx.x, mtiles * ntiles);
   const int tn = tile / mtiles, tm = tile % mtiles;  // consecutive tiles share a W panel
@@ -289,48 +304,63 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 // ---------------------------------------------------------------------------------------
 static int num_cus() { return 256; }
 
-template <int MT, int NT>
+template <int MT, int NT, int WK>
 static void run_skinny(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                        int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                        hipStream_t stream) {
-  dim3 grid(N / (16 * NT), sk);
-  gemm_skinny_kernel<MT, NT><<<grid, kSkThreads, 0, stream>>>(
+  dim3 grid(N / (16 * NT * (4 / WK)), sk);
+  gemm_skinny_kernel<MT, NT, WK><<<grid, kSkThreads, 0, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? ws : nullptr);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WMW>
 static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                      hipStream_t stream) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const size_t lds = 2 * (BM + BN) * kBK * 2;
   dim3 grid(tiles, sk);
-  gemm_tile_kernel<BM, BN><<<grid, kTileThreads, lds, stream>>>(
+  static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
+  if (!attr_set && lds > 65536) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  gemm_tile_kernel<BM, BN, WMW><<<grid, kTileThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? ws : nullptr);
 }
 
+// Plan selection, from the tools/bench_gemm.py sweep on MI355X (Llama-3-70B TP1/TP8 shapes,
+// weights streamed from HBM): the LDS-tiled kernel with a small BM and split-K beats the
+// register-streaming skinny kernel for every M >= 8 (e.g. down-proj M=64: 90 us = 5.2 TB/s vs
+// 186 us) and ties or beats hipBLASLt; the skinny kernel stays for M <= 4 (GEMV regime).
+// Split-K is sized so the grid has ~448 workgroups (1.75 per CU) with >= 4 K-tiles each.
 GemmPlan plan_gemm(int M, int N, int K) {
   GemmPlan p{};
-  const int target = 2 * num_cus();  // workgroups wanted in flight
-  if (M <= 64 && K % 128 == 0) {
+  const int target = 448;
+  if (M <= 4 && K % 128 == 0 && N % 128 == 0) {
     p.kind = 0;
-    p.mt = (M + 15) / 16;
-    p.nt = (p.mt <= 2 && N % 32 == 0) ? 2 : 1;
-    const int blocks = N / (16 * p.nt);
+    p.mt = 1;
+    p.nt = 4;
+    p.wk = 2;
+    const int blocks = N / (16 * p.nt * (4 / p.wk));
     int sk = 1;
     const int nchunks = K / 128;
-    while (blocks * sk < target && sk * 2 * 4 <= nchunks && sk < 16) sk *= 2;
+    while (blocks * sk < target && sk * 2 * p.wk <= nchunks && sk < 16) sk *= 2;
     p.sk = sk;
-  } else {
-    p.kind = 1;
-    p.bm = M <= 64 ? 64 : 128;
-    p.bn = 128;
-    const int tiles = ((M + p.bm - 1) / p.bm) * (N / p.bn);
-    int sk = 1;
-    const int ktiles = K / kBK;
-    while (tiles * sk < num_cus() && sk * 2 * 4 <= ktiles && sk < 16) sk *= 2;
-    p.sk = sk;
+    return p;
   }
+  p.kind = 1;
+  if (M <= 16) { p.bm = 16; p.wk = 1; }
+  else if (M <= 32) { p.bm = 32; p.wk = 1; }
+  else if (M <= 64) { p.bm = 64; p.wk = 2; }
+  else { p.bm = 128; p.wk = 2; }
+  p.bn = 128;
+  const int tiles = ((M + p.bm - 1) / p.bm) * (N / p.bn);
+  int sk = 1;
+  const int ktiles = K / kBK;
+  while (tiles * sk < target && sk * 2 * 4 <= ktiles && sk < 16) sk *= 2;
+  p.sk = sk;
   return p;
 }
 
@@ -339,24 +369,38 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
   return p.sk > 1 ? (size_t)p.sk * M * N * sizeof(float) : 0;
 }
 
-int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
-                const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
-                hipStream_t stream) {
-  if (M <= 0) return 0;
-  GemmPlan p = plan_gemm(M, N, K);
-  if (p.sk > 1 && (ws == nullptr || ws_bytes < (size_t)p.sk * M * N * sizeof(float))) p.sk = 1;
+static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
+                    int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
+                    hipStream_t stream) {
   if (p.kind == 0) {
-    if (epi == EPI_SILU && p.nt == 1) p.nt = 2;  // SILU pairs gate/up tiles inside a wave
-    if (N % (16 * p.nt) != 0) return -1;
-#define SK_CASE(MT_, NT_) \
-  if (p.mt == MT_ && p.nt == NT_) run_skinny<MT_, NT_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream)
-    SK_CASE(1, 1); SK_CASE(1, 2); SK_CASE(2, 1); SK_CASE(2, 2);
-    SK_CASE(3, 1); SK_CASE(3, 2); SK_CASE(4, 1); SK_CASE(4, 2);
+    if (K % 128 != 0 || M > 16 * p.mt) return -1;
+    if (N % (16 * p.nt * (4 / p.wk)) != 0) return -1;
+    if (epi == EPI_SILU && p.nt % 2 != 0) return -1;
+    bool done = false;
+#define SK_CASE(MT_, NT_, WK_)                                                                   \
+  if (!done && p.mt == MT_ && p.nt == NT_ && p.wk == WK_) {                                       \
+    run_skinny<MT_, NT_, WK_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);    \
+    done = true;                                                                                  \
+  }
+#define SK_WK(MT_, NT_) SK_CASE(MT_, NT_, 1) SK_CASE(MT_, NT_, 2) SK_CASE(MT_, NT_, 4)
+    SK_WK(1, 1) SK_WK(1, 2) SK_WK(1, 4) SK_WK(2, 1) SK_WK(2, 2) SK_WK(2, 4)
+    SK_WK(3, 2) SK_WK(4, 1) SK_WK(4, 2) SK_WK(4, 4)
+#undef SK_WK
 #undef SK_CASE
+    if (!done) return -2;
   } else {
     if (N % p.bn != 0 || K % kBK != 0) return -1;
-    if (p.bm == 64) run_tile<64, 128>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
-    else run_tile<128, 128>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+    bool done = false;
+#define TL_CASE(BM_, BN_, WMW_)                                                                 \
+  if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_) {                                     \
+    run_tile<BM_, BN_, WMW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);    \
+    done = true;                                                                                 \
+  }
+    TL_CASE(16, 128, 1) TL_CASE(16, 256, 1) TL_CASE(32, 128, 1) TL_CASE(32, 256, 1)
+    TL_CASE(64, 128, 1) TL_CASE(64, 128, 2) TL_CASE(64, 256, 1) TL_CASE(64, 256, 2)
+    TL_CASE(128, 128, 2) TL_CASE(128, 256, 2)
+#undef TL_CASE
+    if (!done) return -2;
   }
   if (p.sk > 1) {
     const int nout = epi == EPI_SILU ? N / 2 : N;
@@ -366,6 +410,23 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
     gemm_splitk_reduce_kernel<<<grid, 256, 0, stream>>>(ws, p.sk, M, N, epi, bias, out, ldo);
   }
   return 0;
+}
+
+int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
+                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
+                     size_t ws_bytes, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (p.sk > 1 && (ws == nullptr || ws_bytes < (size_t)p.sk * M * N * sizeof(float))) return -3;
+  return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream);
+}
+
+int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
+                const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
+                hipStream_t stream) {
+  if (M <= 0) return 0;
+  GemmPlan p = plan_gemm(M, N, K);
+  if (p.sk > 1 && (ws == nullptr || ws_bytes < (size_t)p.sk * M * N * sizeof(float))) p.sk = 1;
+  return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream);
 }
 
 }  // namespace bfly

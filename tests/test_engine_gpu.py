@@ -48,7 +48,8 @@ def test_prefill_and_decode_logits_match_reference(preset):
     toks = [int(t) for t in lc[:, :V].argmax(-1)]
     pos = [len(p) for p in prompts]
     sl = [tables[i][pos[i] // bs] * bs + pos[i] % bs for i in range(len(prompts))]
-    db = make_decode_batch(toks, pos, sl, tables, max(len(t) for t in tables), 256)
+    mb = max(len(t) for t in tables)
+    db = make_decode_batch(toks, pos, sl, tables, mb, mb * bs)
     dg = g.forward(db.to("cuda"), kg)
     dc = c.forward(db, kc)
     assert _rel(dg[:, :V], dc[:, :V]) < 3e-2

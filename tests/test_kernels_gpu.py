@@ -112,7 +112,7 @@ def test_sample_gumbel_matches_reference():
 
 GEMM_SHAPES = [
     (1, 256, 1024), (5, 1280, 8192), (16, 4096, 4096), (33, 512, 768), (64, 2048, 1024),
-    (65, 256, 512), (128, 1024, 2048), (300, 384, 640), (1024, 1024, 1024), (7, 128256 // 8, 8192),
+    (65, 256, 512), (128, 1024, 2048), (300, 384, 640), (1024, 1024, 1024), (7, 16128, 8192),
 ]
 
 
@@ -210,3 +210,35 @@ def test_moe_route_and_gate_scale():
     ops.moe_gate_scale_(h, g, 2, 3)
     ref.moe_gate_scale(h2, g2, 2, 3)
     _close(h, h2, 1e-2, 1e-2)
+
+
+TILE_CFGS = [(16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1), (64, 128, 1), (64, 128, 2),
+             (64, 256, 1), (64, 256, 2), (128, 128, 2), (128, 256, 2)]
+
+
+@pytest.mark.parametrize("bm,bn,wmw", TILE_CFGS)
+@pytest.mark.parametrize("epi", ["none", "silu"])
+def test_gemm_tile_plans(bm, bn, wmw, epi):
+    M, N, K = min(bm, 40) if bm < 128 else 200, 512, 1024
+    x = _bf(M, K, seed=40)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=41)
+    nout = N // 2 if epi == "silu" else N
+    for sk in (1, 3):
+        out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+        ws = torch.empty(sk * M * N, dtype=torch.float32, device=DEV)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [1, 0, 0, wmw, bm, bn, sk], ops.EPILOGUES[epi], ws)
+        _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("mt,nt,wk", [(1, 1, 4), (1, 2, 1), (1, 4, 4), (2, 2, 2), (2, 4, 1), (4, 1, 4), (4, 2, 1), (4, 4, 4), (3, 2, 2)])
+def test_gemm_skinny_plans(mt, nt, wk):
+    M, N, K = 16 * mt - 3, 512, 1024
+    x = _bf(M, K, seed=42)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=43)
+    for epi in ("none", "silu") if nt % 2 == 0 else ("none",):
+        nout = N // 2 if epi == "silu" else N
+        for sk in (1, 2):
+            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+            ws = torch.empty(sk * M * N, dtype=torch.float32, device=DEV)
+            torch.ops.bfly.gemm_with_plan(x, w, out, [0, mt, nt, wk, 0, 0, sk], ops.EPILOGUES[epi], ws)
+            _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)

@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""GEMM microbenchmark for the decode / prefill projection shapes of Llama-3-70B.
+
+Weights rotate over enough copies (>= 1 GiB) that every call streams them from HBM (the
+Infinity Cache holds 256 MiB), like a real decode step that touches 80 layers in between.
+Reports time, weight-streaming bandwidth and TFLOP/s for the default plan, optional forced
+plans, and torch.matmul (hipBLASLt) as a yardstick.
+
+usage: python tools/bench_gemm.py [--ms 1,16,64] [--shapes tp1|tp8|all] [--sweep]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from butterfly_amd import ops  # noqa: E402
+
+SHAPES = {
+    "tp1": [("qkv", 10240, 8192, "none"), ("o", 8192, 8192, "none"), ("gate_up", 57344, 8192, "silu"),
+            ("down", 8192, 28672, "none"), ("lm_head", 129024, 8192, "none")],
+    "tp8": [("qkv", 1280, 8192, "none"), ("o", 8192, 1024, "none"), ("gate_up", 7168, 8192, "silu"),
+            ("down", 8192, 3584, "none"), ("lm_head", 16128, 8192, "none")],
+    "8b": [("qkv", 6144, 4096, "none"), ("o", 4096, 4096, "none"), ("gate_up", 28672, 4096, "silu"),
+           ("down", 4096, 14336, "none")],
+}
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn(0)
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for i in range(iters):
+        fn(i)
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ms", default="1,16,32,64,128,256")
+    ap.add_argument("--shapes", default="tp1,tp8")
+    ap.add_argument("--sweep", action="store_true", help="also try alternative skinny plans")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    assert ops.load_library()
+    ms = [int(x) for x in a.ms.split(",")]
+    results = []
+    ws = torch.empty(64 << 20, dtype=torch.float32, device="cuda")
+    for group in a.shapes.split(","):
+        for name, N, K, epi in SHAPES[group]:
+            nbytes = N * K * 2
+            copies = max(2, (1 << 30) // nbytes + 1)
+            Ws = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
+            for M in ms:
+                x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+                nout = N // 2 if epi == "silu" else N
+                out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
+                plan = ops.gemm_plan(M, N, K)
+                t = timeit(lambda i: ops.linear(x, Ws[i % copies], epilogue=epi, out=out))
+                row = {"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": plan, "us": round(t, 2),
+                       "TBps": round(nbytes / t / 1e6, 3), "TFLOPs": round(2 * M * N * K / t / 1e6, 1)}
+                tt = timeit(lambda i: torch.matmul(x, Ws[i % copies].t()))
+                row["torch_us"] = round(tt, 2)
+                if a.sweep:
+                    best = None
+                    mt = (M + 15) // 16
+                    cands = []
+                    for bm in (16, 32, 64, 128):
+                        if bm < M and bm != 128 or (bm == 128 and M <= 64):
+                            continue
+                        for bn, wmw in ((128, 1), (256, 1), (128, 2), (256, 2)):
+                            if (bm, bn, wmw) not in ((16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1),
+                                                     (64, 128, 1), (64, 128, 2), (64, 256, 1), (64, 256, 2),
+                                                     (128, 128, 2), (128, 256, 2)):
+                                continue
+                            if N % bn:
+                                continue
+                            for sk in (1, 2, 4, 8, 16):
+                                if K // 64 < sk * 4:
+                                    continue
+                                cands.append([1, 0, 0, wmw, bm, bn, sk])
+                    for pl in cands:
+                        try:
+                            tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(
+                                x, Ws[i % copies], out, pl, ops.EPILOGUES[epi], ws), iters=10)
+                        except RuntimeError:
+                            continue
+                        if best is None or tv < best[0]:
+                            best = (tv, pl)
+                    for nt in ((1, 2, 4) if M <= 64 else ()):
+                        for wk in (1, 2, 4):
+                            rows = 16 * nt * (4 // wk)
+                            if N % rows or (epi == "silu" and nt % 2):
+                                continue
+                            for sk in (1, 2, 4, 8, 16):
+                                if K // 128 < sk * wk:
+                                    continue
+                                pl = [0, mt, nt, wk, 0, 0, sk]
+                                try:
+                                    tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(
+                                        x, Ws[i % copies], out, pl, ops.EPILOGUES[epi], ws), iters=10)
+                                except RuntimeError:
+                                    continue
+                                if best is None or tv < best[0]:
+                                    best = (tv, pl)
+                    if best:
+                        row["best_us"], row["best_plan"] = round(best[0], 2), best[1]
+                results.append(row)
+                print(json.dumps(row), flush=True)
+            del Ws
+            torch.cuda.empty_cache()
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
