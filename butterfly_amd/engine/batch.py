@@ -21,6 +21,7 @@ class ForwardBatch:
     ctx_lens: Optional[torch.Tensor] = None      # int32 [B] context length incl. the new token
     max_ctx: int = 0                             # static upper bound of ctx_lens
     logits_idx: Optional[torch.Tensor] = None    # int64 [R] rows that need logits (None = all)
+    ep_tokens: int = 0                           # EP: token rows every rank pads to (0 = no pad)
 
     @property
     def num_tokens(self) -> int:
@@ -36,7 +37,7 @@ class ForwardBatch:
         mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
         return ForwardBatch(mv(self.input_ids), mv(self.positions), mv(self.slots), self.is_prefill,
                             mv(self.cu_seqlens), self.max_seqlen, mv(self.block_tables),
-                            mv(self.ctx_lens), self.max_ctx, mv(self.logits_idx))
+                            mv(self.ctx_lens), self.max_ctx, mv(self.logits_idx), self.ep_tokens)
 
 
 def make_prefill_batch(prompts: list[list[int]], slots: list[list[int]], device="cpu",
@@ -71,3 +72,12 @@ def make_decode_batch(tokens: list[int], positions: list[int], slots: list[int],
         slots=torch.tensor(slots, **i32), is_prefill=False, block_tables=bt.to(device),
         ctx_lens=torch.tensor([p + 1 for p in positions], **i32), max_ctx=max_ctx,
         logits_idx=None)
+
+
+def empty_batch(device="cpu", ep_tokens: int = 0) -> ForwardBatch:
+    """A zero-token step: lets an idle expert-parallel rank join its peers' collectives."""
+    i32 = dict(dtype=torch.int32, device=device)
+    return ForwardBatch(input_ids=torch.zeros(0, **i32), positions=torch.zeros(0, **i32),
+                        slots=torch.zeros(0, **i32), is_prefill=True,
+                        cu_seqlens=torch.zeros(1, **i32), max_seqlen=0,
+                        logits_idx=torch.zeros(0, dtype=torch.int64, device=device), ep_tokens=ep_tokens)

@@ -30,6 +30,7 @@ from ..models import Shard, build_model
 from ..parallel.comm import Communicator
 from ..parallel.mesh import Mesh
 from ..utils.metrics import Metrics
+from .batch import empty_batch
 from .kv_cache import KVCache, device_kv_budget, kv_blocks_for_budget
 from .model_runner import ModelRunner
 from .sampler import Sampler, SamplingParams
@@ -159,19 +160,37 @@ class LLMEngine:
     def step(self) -> StepOutput:
         t0 = time.perf_counter()
         plan = self.scheduler.schedule()
-        if plan.kind == 0:
+        ep_pad, any_prefill = 0, plan.kind == 1
+        if self.mesh.ep > 1:
+            # expert-parallel ranks must run the same number of MoE collectives with the same
+            # row count: agree on the padded token count; idle ranks run an empty step.
+            t_local = 0 if plan.kind == 0 else (sum(plan.prefill_lens) if plan.kind == 1 else len(plan.seq_ids))
+            ep_pad, anyp, anyw = self.comm.all_reduce_max_int([t_local, int(plan.kind == 1), int(plan.kind != 0)], "ep")
+            any_prefill = bool(anyp)
+            if not anyw:
+                return StepOutput("idle", [], [], [], 0.0)
+            if plan.kind == 0:
+                self._run_stages(lambda h: self.runner.run(empty_batch(self.device, ep_pad), h), 0, 0, [])
+                return StepOutput("ep-idle", [], [], [], time.perf_counter() - t0)
+        elif plan.kind == 0:
             return StepOutput("idle", [], [], [], 0.0)
         rids = list(plan.seq_ids)
         if plan.cow:
             self.kv.copy_blocks(list(plan.cow))
         if plan.kind == 1:
             fb = self.runner.prefill_batch(plan, lambda r: self.requests[r].tokens)
+            fb.ep_tokens = ep_pad
             tokens = self._run_stages(lambda h: self.runner.run(fb, h), fb.num_tokens, len(rids), rids)
             kind = "prefill"
         else:
             last = [self.requests[r].tokens[-1] for r in rids]
             inp = self.runner.decode_inputs(plan, last)
-            tokens = self._run_stages(lambda h: self.runner.run_decode(inp, h), len(rids), len(rids), rids)
+            if self.mesh.pp > 1:
+                tokens = self._pipeline_decode(inp, rids)
+            else:
+                tokens = self._run_stages(
+                    lambda h: self.runner.run_decode(inp, h, ep_tokens=ep_pad, graphs_ok=not any_prefill),
+                    len(rids), len(rids), rids)
             kind = "decode"
         new = tokens.tolist()
         finished = []
@@ -197,7 +216,8 @@ class LLMEngine:
         return StepOutput(kind, rids, new, finished, dt)
 
     def _run_stages(self, fn, T: int, R: int, rids) -> torch.Tensor:
-        """Run this rank's pipeline stage; return sampled ids [R] (int32, on every rank)."""
+        """Run this rank's pipeline stage on one batch; return sampled ids [R] (int32, on
+        every rank of the replica)."""
         m = self.model
         if self.mesh.pp == 1:
             logits = fn(None)
@@ -215,6 +235,38 @@ class LLMEngine:
         else:
             temps, seeds, params = self._sample_params(rids)
             ids = self.sampler.sample(out, temps, seeds, params)
+        self.comm.broadcast_(ids, src_in_group=self.mesh.pp - 1, group="pp")
+        return ids
+
+    def _pipeline_decode(self, inp: dict, rids) -> torch.Tensor:
+        """Microbatched pipeline decode: the batch is cut into M = pp microbatches; stage s
+        works on microbatch m while stage s+1 works on m-1 (RCCL send/recv of the residual
+        stream over xGMI is stream-ordered, so the overlap needs no host synchronisation).
+        Each microbatch replays its own hipGraph bucket."""
+        B = len(rids)
+        M = max(1, min(self.mesh.pp, B))
+        bounds = [B * i // M for i in range(M + 1)]
+        H = self.cfg.hidden_size
+        reqs, outs = [], []
+        for i in range(M):
+            a, b = bounds[i], bounds[i + 1]
+            sub = {k: v[a:b] for k, v in inp.items()}
+            h = None
+            if not self.pp_first:
+                h = torch.empty(b - a, H, dtype=self.model.dtype, device=self.device)
+                self.comm.recv(h, self.mesh.prev_stage(self.rank))
+            out = self.runner.run_decode(sub, h)
+            if not self.pp_last:
+                # copy out of the graph's static output before the next replay can reuse it
+                snd = out.clone()
+                reqs.append(self.comm.isend(snd, self.mesh.next_stage(self.rank)))
+                outs.append(snd)
+            else:
+                temps, seeds, params = self._sample_params(rids[a:b])
+                outs.append(self.sampler.sample(out, temps, seeds, params))
+        for r in reqs:
+            r.wait()
+        ids = torch.cat(outs) if self.pp_last else torch.empty(B, dtype=torch.int32, device=self.device)
         self.comm.broadcast_(ids, src_in_group=self.mesh.pp - 1, group="pp")
         return ids
 

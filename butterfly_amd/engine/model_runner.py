@@ -85,23 +85,27 @@ class ModelRunner:
                     slots=np.asarray(plan.decode_slots, dtype=np.int32),
                     tables=self._tables_host[:B], ctx=self._ctx_host[:B])
 
-    def decode_batch(self, inp: dict) -> ForwardBatch:
+    def decode_batch(self, inp: dict, ep_tokens: int = 0) -> ForwardBatch:
         dev = self.device
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
         return ForwardBatch(input_ids=t(inp["ids"]), positions=t(inp["pos"]), slots=t(inp["slots"]),
                             is_prefill=False, block_tables=t(inp["tables"]), ctx_lens=t(inp["ctx"]),
-                            max_ctx=self.max_seq_len, logits_idx=None)
+                            max_ctx=self.max_seq_len, logits_idx=None, ep_tokens=ep_tokens)
 
     # ------------------------------------------------------------------------------------
     def run(self, fb: ForwardBatch, hidden_in=None):
         out = self.model.forward(fb, self.kv.layers, hidden_in)
         return self.post_fn(out) if (self.post_fn is not None and self.model.last) else out
 
-    def run_decode(self, inp: dict, hidden_in=None):
+    def run_decode(self, inp: dict, hidden_in=None, ep_tokens: int = 0, graphs_ok: bool = True):
+        """Decode step. With expert parallelism every EP rank must pad to the same row count
+        (`ep_tokens`): the graph bucket is chosen from it, so all EP ranks replay the same
+        shape; steps where some EP rank is prefilling run eagerly (graphs_ok=False)."""
         B = len(inp["ids"])
-        if not self.use_graphs or B > self.buckets[-1]:
-            return self.run(self.decode_batch(inp), hidden_in)
-        bucket = self.buckets[bisect.bisect_left(self.buckets, B)]
+        need = max(B, ep_tokens)
+        if not self.use_graphs or not graphs_ok or need > self.buckets[-1]:
+            return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
+        bucket = self.buckets[bisect.bisect_left(self.buckets, need)]
         g = self.graphs.get(bucket)
         if g is None:
             g = self._capture(bucket)
@@ -129,7 +133,7 @@ class ModelRunner:
     def _graph_batch(self, g: _DecodeGraph) -> ForwardBatch:
         return ForwardBatch(input_ids=g.input_ids, positions=g.positions, slots=g.slots,
                             is_prefill=False, block_tables=g.block_tables, ctx_lens=g.ctx_lens,
-                            max_ctx=self.max_seq_len, logits_idx=None)
+                            max_ctx=self.max_seq_len, logits_idx=None, ep_tokens=g.bucket)
 
     def _capture(self, bucket: int) -> _DecodeGraph:
         m = self.model

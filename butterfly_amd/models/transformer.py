@@ -325,7 +325,7 @@ class TransformerLM:
             if self.tp > 1:
                 self.comm.all_reduce_(o, "tp")
             x = self._norm(o, self.p[pre + "post_w"], self.p.get(pre + "post_b"), residual=residual)
-            delta = self._ffn(pre, x)
+            delta = self._ffn(pre, x, fb)
         if not self.last:
             return ops.add(residual, delta) if delta is not None else residual
         idx = fb.logits_idx
@@ -339,19 +339,27 @@ class TransformerLM:
             x = self._norm(r, self.p["final_w"], self.p.get("final_b"))
         return ops.linear(x, self.head_weight)
 
-    def _ffn(self, pre: str, x: torch.Tensor) -> torch.Tensor:
+    def _ffn(self, pre: str, x: torch.Tensor, fb: ForwardBatch) -> torch.Tensor:
         c, d = self.cfg, self.dims
         if c.is_moe:
             gates, _, _ = ops.moe_route(x, self.p[pre + "router_w"], c.experts_per_token)
             xs, gs = x, gates
+            T = x.shape[0]
             if self.ep > 1:
+                # DP-attention + expert-parallel FFN: every EP rank contributes Tp rows (zero
+                # padded), each computes its local experts on all ranks' tokens, and the
+                # reduce-scatter returns each rank's own rows summed over experts.
+                Tp = max(fb.ep_tokens, T)
+                if Tp > T:
+                    x = torch.cat([x, x.new_zeros(Tp - T, x.shape[1])])
+                    gates = torch.cat([gates, gates.new_zeros(Tp - T, gates.shape[1])])
                 xs = self.comm.all_gather(x, "ep")
                 gs = self.comm.all_gather(gates, "ep")
             hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
             ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
             out = ops.linear(hmid, self.p[pre + "moe_down_w"])
             if self.ep > 1:
-                out = self.comm.reduce_scatter(out, "ep")
+                out = self.comm.reduce_scatter(out, "ep")[:T]
             elif self.tp > 1:
                 self.comm.all_reduce_(out, "tp")
             return out

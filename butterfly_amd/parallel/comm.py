@@ -104,7 +104,10 @@ class Communicator:
             return t
         if out is None:
             out = torch.empty((g.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=g.pg)
+        if t.is_cuda:
+            dist.all_gather_into_tensor(out, t.contiguous(), group=g.pg)
+        else:  # gloo: list form
+            dist.all_gather(list(out.chunk(g.size, 0)), t.contiguous(), group=g.pg)
         return out
 
     def reduce_scatter(self, t: torch.Tensor, group: str = "ep", out: torch.Tensor | None = None) -> torch.Tensor:
@@ -114,8 +117,23 @@ class Communicator:
         n = t.shape[0] // g.size
         if out is None:
             out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.reduce_scatter_tensor(out, t.contiguous(), group=g.pg)
+        if t.is_cuda:
+            dist.reduce_scatter_tensor(out, t.contiguous(), group=g.pg)
+        else:  # gloo has no reduce_scatter: all-reduce then slice
+            full = t.contiguous().clone()
+            dist.all_reduce(full, group=g.pg)
+            out.copy_(full[g.rank_in_group * n:(g.rank_in_group + 1) * n])
         return out
+
+    def all_reduce_max_int(self, values: list, group: str = "world") -> list:
+        """Host-side max of a few integers over a group (control plane, e.g. EP padding)."""
+        g = self.groups[group]
+        if g.size == 1:
+            return list(values)
+        dev = "cuda" if dist.get_backend(g.pg) == "nccl" else "cpu"
+        t = torch.tensor(values, dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.pg)
+        return [int(v) for v in t.tolist()]
 
     def send(self, t: torch.Tensor, dst: int) -> None:
         self.stats["send_bytes"] += t.numel() * t.element_size()
