@@ -114,12 +114,20 @@ class ModelConfig:
         h = hf["hidden_size"]
         nh = hf["num_attention_heads"]
         arch = "mixtral" if mt == "mixtral" else "llama"
+        # rope: older configs carry rope_theta / rope_scaling at top level, newer ones a
+        # "rope_parameters" dict; llama3-style frequency scaling is normalised to our keys
+        rp = dict(hf.get("rope_parameters") or {})
+        theta = rp.get("rope_theta", hf.get("rope_theta", 10000.0))
+        scaling = hf.get("rope_scaling") or (rp if rp.get("rope_type", "default") != "default" else None)
+        if scaling:
+            kind = scaling.get("rope_type", scaling.get("type"))
+            scaling = {"type": kind, **{k: v for k, v in scaling.items() if k not in ("rope_type", "type", "rope_theta")}}
         return cls(name=name, arch=arch, vocab_size=hf["vocab_size"], hidden_size=h,
                    intermediate_size=hf["intermediate_size"], num_layers=hf["num_hidden_layers"],
                    num_heads=nh, num_kv_heads=hf.get("num_key_value_heads", nh),
                    head_dim=hf.get("head_dim", h // nh),
                    max_position=hf.get("max_position_embeddings", 8192),
-                   rope_theta=hf.get("rope_theta", 10000.0), rope_scaling=hf.get("rope_scaling"),
+                   rope_theta=theta, rope_scaling=scaling,
                    norm_eps=hf.get("rms_norm_eps", 1e-5),
                    tie_embeddings=hf.get("tie_word_embeddings", False),
                    num_experts=hf.get("num_local_experts", 0),

@@ -48,6 +48,7 @@ class ModelRunner:
             os.environ.get("BFLY_DISABLE_GRAPHS", "0") != "1"
         self.buckets = sorted(graph_batch_sizes or [1, 2, 4, 8, 16, 32, 64])
         self.graphs: dict[int, _DecodeGraph] = {}
+        self.eager_buckets: set = set()
         self.pool = None
         self.post_fn = post_fn
         # host staging buffers (pinned) for per-step inputs
@@ -106,9 +107,19 @@ class ModelRunner:
         if not self.use_graphs or not graphs_ok or need > self.buckets[-1]:
             return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
         bucket = self.buckets[bisect.bisect_left(self.buckets, need)]
+        if bucket in self.eager_buckets:
+            return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
         g = self.graphs.get(bucket)
         if g is None:
-            g = self._capture(bucket)
+            try:
+                g = self._capture(bucket)
+            except Exception as e:  # capture unsupported here (e.g. a collective): stay eager
+                import warnings
+
+                warnings.warn(f"hipGraph capture of decode bucket {bucket} failed ({e!r}); running eagerly")
+                self.eager_buckets.add(bucket)
+                torch.cuda.synchronize(self.device)
+                return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
         self._stage(g, inp, hidden_in)
         g.graph.replay()
         return g.output[:B]
