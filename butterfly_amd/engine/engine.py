@@ -29,6 +29,8 @@ from ..config import EngineConfig, ModelConfig
 from ..models import Shard, build_model
 from ..parallel.comm import Communicator
 from ..parallel.mesh import Mesh
+from ..utils import trace
+from ..utils.health import FaultInjector
 from ..utils.metrics import Metrics
 from .batch import empty_batch
 from .kv_cache import KVCache, device_kv_budget, kv_blocks_for_budget
@@ -117,6 +119,8 @@ class LLMEngine:
         self.metrics = Metrics()
         self.pp_first = coord.pp == 0
         self.pp_last = coord.pp == mesh.pp - 1
+        self.faults = FaultInjector()
+        self.steps_done = 0
 
     # ------------------------------------------------------------------------------------
     def _activation_reserve(self) -> int:
@@ -158,7 +162,14 @@ class LLMEngine:
         return tt, seeds, [self.requests[r].params for r in rids]
 
     def step(self) -> StepOutput:
+        with trace.range("engine.step", step=self.steps_done):
+            out = self._step()
+        self.steps_done += 1
+        return out
+
+    def _step(self) -> StepOutput:
         t0 = time.perf_counter()
+        self.faults.maybe_inject(self.rank, self.steps_done)
         plan = self.scheduler.schedule()
         ep_pad, any_prefill = 0, plan.kind == 1
         if self.mesh.ep > 1:

@@ -1,0 +1,66 @@
+"""Process launcher: one process per GPU (SURVEY.md §3.2 (1) `bfly launch -n 8 -- ...`).
+
+Starts `nproc` child processes with the torch.distributed environment (RANK, WORLD_SIZE,
+LOCAL_RANK, MASTER_ADDR=127.0.0.1, MASTER_PORT, HSA_ENABLE_IPC_MODE_LEGACY=0 for dmabuf IPC),
+prefixes each child's output with its rank, and fails fast: when any rank exits non-zero the
+others are terminated and the launcher returns that code. The launcher itself never touches
+the GPU, so it can start GPU programs safely.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _pump(stream, prefix: str, out) -> None:
+    for line in iter(stream.readline, b""):
+        out.write(prefix + line.decode(errors="replace"))
+        out.flush()
+
+
+def launch(cmd: list, nproc: int, master_port: int | None = None, env_extra: dict | None = None,
+           prefix_output: bool = True) -> int:
+    port = master_port or _free_port()
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env.update(env_extra or {})
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if prefix_output else None,
+                             stderr=subprocess.STDOUT if prefix_output else None, start_new_session=True)
+        procs.append(p)
+        if prefix_output:
+            threading.Thread(target=_pump, args=(p.stdout, f"[rank{r}] ", sys.stdout), daemon=True).start()
+    code = 0
+    try:
+        while procs:
+            for p in list(procs):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                procs.remove(p)
+                if rc != 0 and code == 0:
+                    code = rc
+                    for q in procs:          # fail fast: take the rest of the job down
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for q in procs:
+            os.killpg(q.pid, signal.SIGTERM)
+        code = 130
+    return code

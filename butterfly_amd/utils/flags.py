@@ -1,0 +1,56 @@
+"""Feature-flag registry ("Use feature flags for incompatible changes during transition",
+/root/reference/CLAUDE.md:81).
+
+Every BFLY_* environment flag the framework reads is declared here once, with its type,
+default and meaning; `dump()` prints the effective values at startup so a run's behaviour is
+reproducible from its log.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Any, Callable
+
+
+@dataclass(frozen=True)
+class Flag:
+    name: str
+    default: Any
+    parse: Callable[[str], Any]
+    help: str
+
+
+def _bool(s: str) -> bool:
+    return s.strip().lower() in ("1", "true", "yes", "on")
+
+
+FLAGS: dict[str, Flag] = {}
+
+
+def define(name: str, default, parse, help: str) -> Flag:
+    f = Flag(name, default, parse, help)
+    FLAGS[name] = f
+    return f
+
+
+define("BFLY_DISABLE_GRAPHS", False, _bool, "run decode steps eagerly instead of replaying hipGraphs")
+define("BFLY_CUSTOM_AR", False, _bool, "use the one-shot IPC all-reduce kernel for small TP all-reduces")
+define("BFLY_CUSTOM_AR_MAX_BYTES", 8 << 20, int, "largest all-reduce (bytes) routed to the IPC kernel")
+define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
+define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
+define("BFLY_FAULT", "", str, "fault injection 'rank:step:kind' (kind: hang|exit|nan) for tests")
+define("BFLY_TRACE", "", str, "write a chrome-trace JSON of engine steps to this path")
+define("BFLY_ROCTX", False, _bool, "emit roctx ranges (visible in rocprofv3 --marker-trace)")
+define("BFLY_LOG_LEVEL", "INFO", str, "log level of the rank-tagged logger")
+define("BFLY_OFFLOAD_ARCH", "gfx950", str, "HIP offload architecture for the kernel build")
+define("BFLY_HOST_CXX", "/opt/rocm/lib/llvm/bin/clang++", str, "host compiler for the torch bindings")
+
+
+def get(name: str):
+    f = FLAGS[name]
+    v = os.environ.get(name)
+    return f.default if v is None or v == "" else f.parse(v)
+
+
+def dump() -> dict:
+    return {n: get(n) for n in sorted(FLAGS)}
