@@ -132,6 +132,6 @@ class PartitionPlan:
 
     @classmethod
     def from_json(cls, path_or_text: str | Path) -> "PartitionPlan":
-        p = Path(str(path_or_text))
-        text = p.read_text() if p.exists() else str(path_or_text)
+        s = str(path_or_text)
+        text = s if s.lstrip().startswith("{") else Path(s).read_text()
         return cls.from_dict(json.loads(text))

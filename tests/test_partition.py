@@ -1,0 +1,53 @@
+"""Partitioning API: plan validity properties, JSON round trip, objective behaviour."""
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from butterfly_amd.config import ModelConfig
+from butterfly_amd.models.shard import local_dims
+from butterfly_amd.partition import PartitionPlan, factorizations, partition
+
+
+@settings(max_examples=30, deadline=None)
+@given(st.sampled_from(["llama3-70b", "llama3-8b", "mixtral-8x7b", "gpt2-small", "llama-tiny"]),
+       st.sampled_from([1, 2, 4, 8]), st.sampled_from(["throughput", "latency"]))
+def test_plans_are_valid(preset, n, objective):
+    cfg = ModelConfig.from_preset(preset)
+    try:
+        plan = partition(cfg, n, objective=objective, batch_per_gpu=16, ctx=512)
+    except ValueError:
+        return  # no feasible layout (e.g. model too big) is a legal answer
+    plan.validate()
+    assert plan.dp * plan.tp * plan.pp == n
+    layers = [l for a, b in plan.stages for l in range(a, b)]
+    assert layers == list(range(cfg.num_layers))            # every layer exactly once, in order
+    assert cfg.num_heads % plan.tp == 0
+    for r in range(n):
+        local_dims(cfg, plan.shard(r))
+        assert plan.weight_bytes[r] <= 288e9                  # fits one MI355X
+    back = PartitionPlan.from_json(plan.to_json())
+    assert back.to_dict() == plan.to_dict()
+
+
+def test_fixed_strategy_and_70b_single_gpu_fits():
+    p = partition("llama3-70b", 8, {"tp": 2, "pp": 4})
+    assert (p.tp, p.pp, p.dp) == (2, 4, 1) and len(p.stages) == 4
+    one = partition("llama3-70b", 1)
+    assert one.weight_bytes[0] > 140e9 and one.weight_bytes[0] < 288e9
+
+
+def test_factorizations():
+    assert sorted(factorizations(4)) == sorted([(4, 1, 1), (2, 2, 1), (2, 1, 2), (1, 4, 1), (1, 2, 2), (1, 1, 4)])
+
+
+def test_invalid_plan_rejected():
+    p = partition("llama-tiny", 2, {"pp": 2})
+    d = p.to_dict()
+    d["stages"] = [[0, 1], [0, 2]]
+    with pytest.raises(ValueError):
+        PartitionPlan.from_dict(d)
+
+
+def test_mixtral_expert_parallel_candidate():
+    p = partition("mixtral-8x7b", 8, {"dp": 8, "ep": 8})
+    assert p.ep == 8 and p.shard(3).ep_rank == 3

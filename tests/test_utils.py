@@ -1,0 +1,56 @@
+"""Observability / health utilities."""
+import json
+import time
+
+import torch.distributed as dist
+
+from butterfly_amd.utils import flags
+from butterfly_amd.utils.health import FaultInjector, HealthMonitor, StepWatchdog
+from butterfly_amd.utils.metrics import Metrics, percentile
+
+from .dist_utils import free_port
+
+
+def test_metrics_export():
+    m = Metrics()
+    for v in (1.0, 2.0, 3.0, 4.0):
+        m.observe("lat", v)
+    m.inc("tokens", 10)
+    s = m.summary()
+    assert s["histograms"]["lat"]["p50"] == 2.5 and s["counters"]["tokens"] == 10
+    assert 'bfly_lat{quantile="0.50"} 2.5' in m.to_prometheus()
+    json.loads(m.to_json())
+    assert percentile([], 50) != percentile([], 50)  # nan
+
+
+def test_flags_registry(monkeypatch):
+    monkeypatch.setenv("BFLY_DISABLE_GRAPHS", "1")
+    assert flags.get("BFLY_DISABLE_GRAPHS") is True
+    assert "BFLY_FAULT" in flags.dump()
+
+
+def test_fault_injector_parse():
+    f = FaultInjector("1:3:nan")
+    assert f.maybe_inject(0, 3) is None and f.maybe_inject(1, 2) is None
+    assert f.maybe_inject(1, 3) == "nan"
+
+
+def test_watchdog_fires():
+    hits = []
+    w = StepWatchdog(0.05, on_failure=hits.append)
+    w.arm("step 7")
+    time.sleep(0.2)
+    assert hits and "step 7" in hits[0]
+    w.arm()
+    w.disarm()
+
+
+def test_health_monitor_detects_dead_rank():
+    store = dist.TCPStore("127.0.0.1", free_port(), 2, True, wait_for_workers=False)
+    failures = []
+    mon = HealthMonitor(store, rank=0, world=2, period=0.05, timeout=0.2, on_failure=failures.append)
+    store.set("bfly/hb/1", repr(time.time() - 10))     # rank 1 went silent 10 s ago
+    mon.start()
+    time.sleep(0.5)
+    mon.stop()
+    assert failures and "rank 1" in failures[0]
