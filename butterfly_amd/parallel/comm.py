@@ -76,6 +76,12 @@ class Communicator:
         groups["world"] = GroupHandle(list(range(mesh.world_size)), dist.group.WORLD, rank)
         return cls(mesh, rank, groups)
 
+    @staticmethod
+    def _nccl(g: GroupHandle) -> bool:
+        # tensor-form collectives on RCCL; list forms on gloo (also used with GPU tensors
+        # when several ranks share one device, which RCCL refuses)
+        return g.pg is not None and dist.get_backend(g.pg) == "nccl"
+
     # -- queries ----------------------------------------------------------------------------
     def size(self, group: str = "tp") -> int:
         return self.groups[group].size
@@ -104,7 +110,7 @@ class Communicator:
             return t
         if out is None:
             out = torch.empty((g.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        if t.is_cuda:
+        if self._nccl(g):
             dist.all_gather_into_tensor(out, t.contiguous(), group=g.pg)
         else:  # gloo: list form
             dist.all_gather(list(out.chunk(g.size, 0)), t.contiguous(), group=g.pg)
@@ -117,7 +123,7 @@ class Communicator:
         n = t.shape[0] // g.size
         if out is None:
             out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        if t.is_cuda:
+        if self._nccl(g):
             dist.reduce_scatter_tensor(out, t.contiguous(), group=g.pg)
         else:  # gloo has no reduce_scatter: all-reduce then slice
             full = t.contiguous().clone()
@@ -135,17 +141,30 @@ class Communicator:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.pg)
         return [int(v) for v in t.tolist()]
 
+    def _world_nccl(self) -> bool:
+        return dist.is_initialized() and dist.get_backend() == "nccl"
+
     def send(self, t: torch.Tensor, dst: int) -> None:
         self.stats["send_bytes"] += t.numel() * t.element_size()
+        if t.is_cuda and not self._world_nccl():   # gloo point-to-point needs host memory
+            dist.send(t.detach().cpu().contiguous(), dst)
+            return
         dist.send(t.contiguous(), dst)
 
     def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
         self.stats["recv_bytes"] += t.numel() * t.element_size()
+        if t.is_cuda and not self._world_nccl():
+            h = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(h, src)
+            t.copy_(h)
+            return t
         dist.recv(t, src)
         return t
 
     def isend(self, t: torch.Tensor, dst: int):
         self.stats["send_bytes"] += t.numel() * t.element_size()
+        if t.is_cuda and not self._world_nccl():
+            return dist.isend(t.detach().cpu().contiguous(), dst)
         return dist.isend(t.contiguous(), dst)
 
     def irecv(self, t: torch.Tensor, src: int):
