@@ -191,15 +191,22 @@ gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict_
 constexpr int kTileThreads = 256;
 constexpr int kBK = 64;
 
+// Loads per wave per stage for a ROWS x 64 tile: every wave issues the same count (small
+// tiles re-issue a piece another wave also loads: identical bytes to the same LDS address),
+// so one compile-time `vmcnt` count is valid for every wave.
+template <int ROWS>
+constexpr int stage_loads() { return (ROWS / 8 + 3) / 4; }
+
 template <int ROWS>
 __device__ __forceinline__ void tile_stage(const bf16* __restrict__ src, long ld, int row0,
                                            int row_max, int k0, char* lds, int wid, int lane) {
   // ROWS x 64 bf16 = ROWS x 8 chunks of 16 B; one wave-instruction writes 8 rows (1 KiB).
-  constexpr int kInstr = (ROWS + 31) / 32;  // per wave (4 waves)
+  constexpr int kBlocks = ROWS / 8;
+  constexpr int kInstr = stage_loads<ROWS>();
 #pragma unroll
   for (int i = 0; i < kInstr; ++i) {
-    const int blk = i * 4 + wid;             // 8-row block index
-    if (ROWS % 32 != 0 && blk * 8 >= ROWS) break;
+    int blk = i * 4 + wid;             // 8-row block index
+    if (kBlocks % 4 != 0) blk %= kBlocks;
     const int row = blk * 8 + (lane >> 3);
     const int slot = lane & 7;
     const int chunk = slot ^ ((row >> 1) & 7);
@@ -210,12 +217,22 @@ __device__ __forceinline__ void tile_stage(const bf16* __restrict__ src, long ld
   }
 }
 
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 __device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int chunk) {
   const int slot = chunk ^ ((row >> 1) & 7);
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + slot * 16);
 }
 
-template <int BM, int BN, int WMW>
+// STAGES-deep glds pipeline: K-tiles kt+1 .. kt+STAGES-1 stay in flight (LDS-DMA) while the
+// MFMAs consume tile kt. Each iteration waits with a COUNTED vmcnt (only tile kt must have
+// landed) and a raw s_barrier (a __syncthreads() would drain every in-flight DMA:
+// cdna_hip_programming.md §5 "Pipelining across barriers"); the buffer refilled in an
+// iteration is the one every wave finished reading in the previous iteration (WAR safe).
+template <int BM, int BN, int WMW, int STAGES>
 __global__ void __launch_bounds__(kTileThreads)
 gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -224,6 +241,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
   constexpr int A_BYTES = BM * kBK * 2, B_BYTES = BN * kBK * 2;
+  constexpr int LPW = stage_loads<BM>() + stage_loads<BN>();  // glds per wave per stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;  // one buffer = [A tile | B tile]
 
@@ -244,20 +262,31 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (kt0 < kt1) {
-    tile_stage<BM>(X, ldx, m0, M, kt0 * kBK, smem, wid, lane);
-    tile_stage<BN>(W, ldw, n0, N, kt0 * kBK, smem + A_BYTES, wid, lane);
-  }
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < kt1) {
-      char* nb = smem + (cur ^ 1) * STAGE_BYTES;
-      tile_stage<BM>(X, ldx, m0, M, (kt + 1) * kBK, nb, wid, lane);
-      tile_stage<BN>(W, ldw, n0, N, (kt + 1) * kBK, nb + A_BYTES, wid, lane);
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (kt0 + s < kt1) {
+      char* b = smem + s * STAGE_BYTES;
+      tile_stage<BM>(X, ldx, m0, M, (kt0 + s) * kBK, b, wid, lane);
+      tile_stage<BN>(W, ldw, n0, N, (kt0 + s) * kBK, b + A_BYTES, wid, lane);
     }
-    const char* As = smem + cur * STAGE_BYTES;
+  }
+  int buf = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    // tiles issued after kt: min(STAGES - 2, kt1 - 1 - kt); wait until only those are pending
+    const int after = min(STAGES - 2, kt1 - 1 - kt);
+    if (STAGES >= 4 && after >= 2) vm_wait<(STAGES >= 4 ? 2 : 0) * LPW>();
+    else if (STAGES >= 3 && after >= 1) vm_wait<LPW>();
+    else vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < kt1) {
+      int nbuf = buf + STAGES - 1;
+      if (nbuf >= STAGES) nbuf -= STAGES;
+      char* nb = smem + nbuf * STAGE_BYTES;
+      tile_stage<BM>(X, ldx, m0, M, (kt + STAGES - 1) * kBK, nb, wid, lane);
+      tile_stage<BN>(W, ldw, n0, N, (kt + STAGES - 1) * kBK, nb + A_BYTES, wid, lane);
+    }
+    const char* As = smem + buf * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -271,6 +300,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
+    if (++buf == STAGES) buf = 0;
   }
 
   // Epilogue: acc[i][j][r] = C[m = m0 + wm*WM + 16i + (lane>>4)*4 + r][n = n0 + wn*WN + 16j + (lane&15)]
@@ -313,20 +343,20 @@ static void run_skinny(const bf16* X, long ldx, const bf16* W, long ldw, int M, 
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? ws : nullptr);
 }
 
-template <int BM, int BN, int WMW>
+template <int BM, int BN, int WMW, int STAGES>
 static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                      hipStream_t stream) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  const size_t lds = 2 * (BM + BN) * kBK * 2;
+  const size_t lds = (size_t)STAGES * (BM + BN) * kBK * 2;
   dim3 grid(tiles, sk);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
   if (!attr_set && lds > 65536) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW, STAGES>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  gemm_tile_kernel<BM, BN, WMW><<<grid, kTileThreads, lds, stream>>>(
+  gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? ws : nullptr);
 }
 
@@ -338,19 +368,24 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
 GemmPlan plan_gemm(int M, int N, int K) {
   GemmPlan p{};
   const int target = 448;
-  if (M <= 4 && K % 128 == 0 && N % 128 == 0) {
+  const bool skinny_ok = K % 128 == 0 && N % 128 == 0;
+  // register-streaming kernel: GEMV-like M, and short-K shapes (row-parallel projections
+  // after TP splits K) where the LDS pipeline cannot fill before the K loop ends
+  if (skinny_ok && (M <= 4 || (M <= 64 && K <= 1024))) {
     p.kind = 0;
-    p.mt = 1;
-    p.nt = 4;
-    p.wk = 2;
+    p.mt = (M + 15) / 16;
+    const bool long_k = K > 4096;
+    p.nt = M <= 4 ? (long_k ? 4 : 1) : 2;
+    p.wk = long_k ? 2 : 4;
     const int blocks = N / (16 * p.nt * (4 / p.wk));
     int sk = 1;
     const int nchunks = K / 128;
-    while (blocks * sk < target && sk * 2 * p.wk <= nchunks && sk < 16) sk *= 2;
+    while (long_k && blocks * sk < target && sk * 2 * p.wk <= nchunks && sk < 16) sk *= 2;
     p.sk = sk;
     return p;
   }
   p.kind = 1;
+  p.mt = 3;   // tile plans: `mt` = pipeline depth (K-tiles in flight + 1)
   if (M <= 16) { p.bm = 16; p.wk = 1; }
   else if (M <= 32) { p.bm = 32; p.wk = 1; }
   else if (M <= 64) { p.bm = 64; p.wk = 2; }
@@ -391,14 +426,17 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
   } else {
     if (N % p.bn != 0 || K % kBK != 0) return -1;
     bool done = false;
-#define TL_CASE(BM_, BN_, WMW_)                                                                 \
-  if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_) {                                     \
-    run_tile<BM_, BN_, WMW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);    \
-    done = true;                                                                                 \
+    const int st = p.mt > 0 ? p.mt : 2;   // tile plans reuse `mt` as the pipeline depth
+#define TL_CASE(BM_, BN_, WMW_, ST_)                                                            \
+  if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_ && st == ST_) {                       \
+    run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream); \
+    done = true;                                                                                \
   }
-    TL_CASE(16, 128, 1) TL_CASE(16, 256, 1) TL_CASE(32, 128, 1) TL_CASE(32, 256, 1)
-    TL_CASE(64, 128, 1) TL_CASE(64, 128, 2) TL_CASE(64, 256, 1) TL_CASE(64, 256, 2)
-    TL_CASE(128, 128, 2) TL_CASE(128, 256, 2)
+#define TL_ST(BM_, BN_, WMW_) TL_CASE(BM_, BN_, WMW_, 2) TL_CASE(BM_, BN_, WMW_, 3) TL_CASE(BM_, BN_, WMW_, 4)
+    TL_ST(16, 128, 1) TL_ST(16, 256, 1) TL_ST(32, 128, 1) TL_ST(32, 256, 1)
+    TL_ST(64, 128, 1) TL_ST(64, 128, 2) TL_ST(64, 256, 1) TL_ST(64, 256, 2)
+    TL_ST(128, 128, 2) TL_ST(128, 256, 2)
+#undef TL_ST
 #undef TL_CASE
     if (!done) return -2;
   }

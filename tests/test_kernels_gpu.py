@@ -223,11 +223,14 @@ def test_gemm_tile_plans(bm, bn, wmw, epi):
     x = _bf(M, K, seed=40)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=41)
     nout = N // 2 if epi == "silu" else N
-    for sk in (1, 3):
-        out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-        ws = torch.empty(sk * M * N, dtype=torch.float32, device=DEV)
-        torch.ops.bfly.gemm_with_plan(x, w, out, [1, 0, 0, wmw, bm, bn, sk], ops.EPILOGUES[epi], ws)
-        _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+    for st in (2, 3, 4):
+        if st * (bm + bn) * 128 > 160 * 1024:
+            continue
+        for sk in (1, 3, 5):   # uneven K splits: 16 k-tiles over 3 / 5 workgroups (1..4 deep)
+            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+            ws = torch.empty(sk * M * N, dtype=torch.float32, device=DEV)
+            torch.ops.bfly.gemm_with_plan(x, w, out, [1, st, 0, wmw, bm, bn, sk], ops.EPILOGUES[epi], ws)
+            _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
 
 
 @pytest.mark.parametrize("mt,nt,wk", [(1, 1, 4), (1, 2, 1), (1, 4, 4), (2, 2, 2), (2, 4, 1), (4, 1, 4), (4, 2, 1), (4, 4, 4), (3, 2, 2)])

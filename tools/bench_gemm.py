@@ -84,7 +84,10 @@ def main():
                             for sk in (1, 2, 4, 8, 16):
                                 if K // 64 < sk * 4:
                                     continue
-                                cands.append([1, 0, 0, wmw, bm, bn, sk])
+                                for st in (2, 3, 4):
+                                    if st * (bm + bn) * 128 > 160 * 1024:
+                                        continue
+                                    cands.append([1, st, 0, wmw, bm, bn, sk])
                     for pl in cands:
                         try:
                             tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(
