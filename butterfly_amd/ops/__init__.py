@@ -23,7 +23,7 @@ _loaded = False
 _load_error: str | None = None
 
 EPILOGUES = {"none": 0, "bias": 1, "silu": 2}
-DECODE_PART_TOKENS = 256
+DECODE_PART_TOKENS = 0   # 0 = pick the context split per call (attn_decode_part_tokens)
 
 
 def load_library(path: str | os.PathLike | None = None) -> bool:
@@ -96,7 +96,8 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
         ws = max(ws, torch.ops.bfly.gemm_workspace_size(m, max_n, max_k))
     _arena.get(device, "gemm", ws // 4 + 1, torch.float32)
     if max_batch and max_ctx:
-        ns = torch.ops.bfly.attn_decode_splits(max_ctx, DECODE_PART_TOKENS)
+        ns = max(torch.ops.bfly.attn_decode_splits(max_ctx, torch.ops.bfly.attn_decode_part_tokens(b, num_kv_heads, max_ctx))
+                 for b in range(1, max_batch + 1))
         _arena.get(device, "attn_o", max_batch * num_kv_heads * ns * 16 * head_dim, torch.float32)
         _arena.get(device, "attn_ml", max_batch * num_kv_heads * ns * 16 * 2, torch.float32)
     _arena.get(device, "sample", max(max_batch, max_tokens, 1) * 64, torch.int64)
@@ -236,6 +237,8 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_c
     Hkv = k_cache.shape[1]
     if out is None:
         out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
+    if part_tokens <= 0:
+        part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
     ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
     po = pml = None
     if ns > 1:

@@ -268,6 +268,10 @@ int64_t attn_decode_splits(int64_t max_ctx, int64_t part_tokens) {
   return bfly::attn_decode_splits(max_ctx, part_tokens);
 }
 
+int64_t attn_decode_part_tokens(int64_t B, int64_t Hkv, int64_t max_ctx) {
+  return bfly::attn_decode_part_tokens(B, Hkv, max_ctx);
+}
+
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& block_tables, const Tensor& ctx_lens, double scale,
                  int64_t max_ctx, int64_t part_tokens, Tensor& out,
@@ -284,6 +288,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
               "attn_decode: block_tables");
   TORCH_CHECK(ctx_lens.numel() >= B, "attn_decode: ctx_lens");
   TORCH_CHECK((long)block_tables.size(1) * BS >= max_ctx, "attn_decode: block table too narrow for max_ctx");
+  if (part_tokens <= 0) part_tokens = bfly::attn_decode_part_tokens(B, Hkv, max_ctx);
   const int nsplit = bfly::attn_decode_splits(max_ctx, part_tokens);
   float *po = nullptr, *pml = nullptr;
   if (nsplit > 1) {
@@ -375,6 +380,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
   m.def("gemm_plan(int M, int N, int K) -> int[]", &gemm_plan);
   m.def("attn_decode_splits(int max_ctx, int part_tokens) -> int", &attn_decode_splits);
+  m.def("attn_decode_part_tokens(int B, int Hkv, int max_ctx) -> int", &attn_decode_part_tokens);
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
         "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
         "Tensor(c!)? part_ml) -> ()");

@@ -62,6 +62,7 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 
 // attention.hip
 int attn_decode_splits(int max_ctx, int part_tokens);
+int attn_decode_part_tokens(int B, int Hkv, int max_ctx);
 int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,

@@ -63,14 +63,16 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
   }
 
   const int g = lane >> 4, r = lane & 15;
-  // Q^T fragment (B operand): lane holds Q[row r][d = 32g + 8ds + j]; rows >= G are zero.
+  // d permutation: sub-step ds, lane group g, element j hold d = 32 ds + 8 g + j, so each K
+  // load instruction reads 64 contiguous bytes of every key row (full cache-line pairs).
+  // Q^T fragment (B operand): lane holds Q[row r][d]; rows >= G are zero.
   bf16x8 qf[4];
   {
     const int qr = r < G ? r : 0;
-    const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (long)b * q_stride + (long)(h * G + qr) * D + 32 * g);
+    const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D + 8 * g;
 #pragma unroll
     for (int ds = 0; ds < 4; ++ds) {
-      qf[ds] = qp[ds];
+      qf[ds] = *reinterpret_cast<const bf16x8*>(qp + 32 * ds);
       if (r >= G) qf[ds] = bf16x8{};
     }
   }
@@ -82,25 +84,25 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
 
   const int p0 = tok0 / BS, p1 = (tok1 + BS - 1) / BS;
   const int* bt = block_tables + (long)b * bt_stride;
-  for (int p = p0 + wid; p < p1; p += 4) {
+
+  // K rows: tile kt, lane row r -> key sigma(kt, r) = 8*(r>>2) + 4*kt + (r&3)
+  auto load_page = [&](int p, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
     const long blk = bt[p];
-    const bf16* kb = k_cache + ((blk * Hkv + h) * BS) * D;
+    const bf16* kb = k_cache + ((blk * Hkv + h) * BS) * D + 8 * g;
     const bf16* vb = v_cache + (blk * Hkv + h) * (long)D * BS;
-    // K rows: tile kt, lane row r -> key sigma(kt, r) = 8*(r>>2) + 4*kt + (r&3)
-    bf16x8 kf[2][4];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const int key = 8 * (r >> 2) + 4 * kt + (r & 3);
-      const bf16x8* kp = reinterpret_cast<const bf16x8*>(kb + key * D + 32 * g);
 #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) kf[kt][ds] = ld_nt(kp + ds);
+      for (int ds = 0; ds < 4; ++ds)
+        kf[kt][ds] = ld_nt(reinterpret_cast<const bf16x8*>(kb + key * D + 32 * ds));
     }
     // V^T rows: d = 16dt + r, keys 8g .. 8g+7
-    bf16x8 vf[8];
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
       vf[dt] = ld_nt(reinterpret_cast<const bf16x8*>(vb + (16 * dt + r) * BS + 8 * g));
-
+  };
+  auto compute_page = [&](int p, const bf16x8 (&kf)[2][4], const bf16x8 (&vf)[8]) {
     f32x4 st[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -140,6 +142,21 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
       o[dt] *= alpha;
       o[dt] = mfma16(vf[dt], pb, o[dt]);
     }
+  };
+
+  // software pipeline over this wave's pages (p0 + wid, +4, ...): the next page's K/V loads
+  // are in flight while the current page is computed; two named register sets (rule 20).
+  bf16x8 kA[2][4], vA[8], kB[2][4], vB[8];
+  int p = p0 + wid;
+  if (p < p1) load_page(p, kA, vA);
+  while (p < p1) {
+    if (p + 4 < p1) load_page(p + 4, kB, vB);
+    compute_page(p, kA, vA);
+    p += 4;
+    if (p >= p1) break;
+    if (p + 4 < p1) load_page(p + 4, kA, vA);
+    compute_page(p, kB, vB);
+    p += 4;
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -181,28 +198,38 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
   }
 }
 
+// One workgroup per (query row, kv head, sequence); thread = head dim element. The split
+// maxima are reduced once per workgroup through LDS, then every thread streams its column.
 template <int D>
-__global__ void __launch_bounds__(kAttnThreads)
+__global__ void __launch_bounds__(D)
 attn_decode_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
                            int nsplit, int Hq, int Hkv, bf16* __restrict__ out) {
-  const int h = blockIdx.x, b = blockIdx.y;
+  __shared__ float s_w[256];
+  __shared__ float s_inv;
+  const int qr = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int G = Hq / Hkv;
   const long base = (long)(b * Hkv + h) * nsplit;
-  for (int e = threadIdx.x; e < G * D; e += kAttnThreads) {
-    const int qr = e / D, d = e % D;
+  const int d = threadIdx.x;
+  if (threadIdx.x == 0) {
     float M = kNegInf;
     for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[((base + s) * 16 + qr) * 2]);
     const float Mb = M == kNegInf ? 0.f : M;
-    float L = 0.f, O = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
+    float L = 0.f;
+    for (int s = 0; s < nsplit && s < 256; ++s) {
       const float ms = part_ml[((base + s) * 16 + qr) * 2];
-      if (ms == kNegInf) continue;
-      const float f = exp2f(ms - Mb);
-      L += f * part_ml[((base + s) * 16 + qr) * 2 + 1];
-      O += f * part_o[((base + s) * 16 + qr) * D + d];
+      const float w = ms == kNegInf ? 0.f : exp2f(ms - Mb);
+      s_w[s] = w;
+      L += w * part_ml[((base + s) * 16 + qr) * 2 + 1];
     }
-    out[((long)b * Hq + h * G + qr) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+    s_inv = L > 0.f ? 1.f / L : 0.f;
   }
+  __syncthreads();
+  float O = 0.f;
+  for (int s = 0; s < nsplit && s < 256; ++s) {
+    const float w = s_w[s];
+    if (w != 0.f) O += w * part_o[((base + s) * 16 + qr) * D + d];
+  }
+  out[((long)b * Hq + h * G + qr) * D + d] = f2bf(O * s_inv);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -380,13 +407,28 @@ int attn_decode_splits(int max_ctx, int part_tokens) {
   return (max_ctx + part_tokens - 1) / part_tokens;
 }
 
+// Context split size: enough (b, kv-head, split) workgroups to cover the 256 CUs ~4x, but
+// splits of >= 128 tokens (4 pages per workgroup, one per wave) so each wave streams a page.
+int attn_decode_part_tokens(int B, int Hkv, int max_ctx) {
+  const int want_wg = 1024;
+  const int bh = B * Hkv > 0 ? B * Hkv : 1;
+  int splits = (want_wg + bh - 1) / bh;
+  int part = (max_ctx + splits - 1) / splits;
+  part = (part + 31) / 32 * 32;
+  if (part < 128) part = 128;
+  while ((max_ctx + part - 1) / part > 256) part += 32;   // combine kernel: <= 256 splits
+  return part;
+}
+
 int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
                        bf16* out, float* part_o, float* part_ml, hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || block_size != 32 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
+  if (part_tokens <= 0) part_tokens = attn_decode_part_tokens(B, Hkv, max_ctx);
   if (part_tokens % block_size != 0) return -2;
+  if (attn_decode_splits(max_ctx, part_tokens) > 256) return -4;
   const int nsplit = attn_decode_splits(max_ctx, part_tokens);
   if (nsplit > 1 && (part_o == nullptr || part_ml == nullptr)) return -3;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -395,9 +437,8 @@ int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const 
       q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, Hq, Hkv, scale_log2,
       part_tokens, out, part_o, part_ml);
   if (nsplit > 1) {
-    dim3 g2(Hkv, B);
-    attn_decode_combine_kernel<128><<<g2, kAttnThreads, 0, stream>>>(part_o, part_ml, nsplit, Hq,
-                                                                     Hkv, out);
+    dim3 g2(Hq / Hkv, Hkv, B);
+    attn_decode_combine_kernel<128><<<g2, 128, 0, stream>>>(part_o, part_ml, nsplit, Hq, Hkv, out);
   }
   return 0;
 }

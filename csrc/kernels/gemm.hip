@@ -385,7 +385,7 @@ GemmPlan plan_gemm(int M, int N, int K) {
     return p;
   }
   p.kind = 1;
-  p.mt = 3;   // tile plans: `mt` = pipeline depth (K-tiles in flight + 1)
+  p.mt = M >= 512 ? 2 : 3;   // tile plans: `mt` = pipeline depth (K-tiles in flight + 1)
   if (M <= 16) { p.bm = 16; p.wk = 1; }
   else if (M <= 32) { p.bm = 32; p.wk = 1; }
   else if (M <= 64) { p.bm = 64; p.wk = 2; }

@@ -158,7 +158,7 @@ def test_attn_prefill_non_causal():
     _close(o, ref.attn_prefill(q, k, v, cu, 130, 0.088, False), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("part_tokens", [256, 4096])
+@pytest.mark.parametrize("part_tokens", [0, 128, 256, 4096])
 @pytest.mark.parametrize("Hq,Hkv", [(16, 2), (8, 8), (64, 8)])
 def test_attn_decode_paged(part_tokens, Hq, Hkv):
     D, BS = 128, 32
