@@ -165,6 +165,8 @@ class LLMEngine:
         with trace.range("engine.step", step=self.steps_done):
             out = self._step()
         self.steps_done += 1
+        if self.steps_done % 256 == 0:
+            self.comm.check_health()
         return out
 
     def _step(self) -> StepOutput:

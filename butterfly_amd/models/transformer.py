@@ -297,13 +297,15 @@ class TransformerLM:
             raise ValueError("non-first pipeline stage needs hidden_in")
         if not self.first:
             residual = residual.clone()   # updated in place by the fused add+norm
-        delta = None
+        delta, partial = None, False      # FFN output of the previous layer (un-reduced if partial)
         T = fb.num_tokens
         D = c.head_dim
         for li, i in enumerate(self.layer_ids):
             pre = f"l{i}."
-            x = self._norm(residual if delta is None else delta, self.p[pre + "in_w"],
-                           self.p.get(pre + "in_b"), residual=None if delta is None else residual)
+            if delta is None:
+                x = self._norm(residual, self.p[pre + "in_w"], self.p.get(pre + "in_b"))
+            else:
+                x = self._add_norm(delta, pre + "in", residual, partial)
             qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"))
             kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
             slots = fb.slots if kc is not None else None
@@ -322,24 +324,39 @@ class TransformerLM:
                 attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
             o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
             o = ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b)
-            if self.tp > 1:
-                self.comm.all_reduce_(o, "tp")
-            x = self._norm(o, self.p[pre + "post_w"], self.p.get(pre + "post_b"), residual=residual)
-            delta = self._ffn(pre, x, fb)
+            x = self._add_norm(o, pre + "post", residual, self.tp > 1)
+            delta, partial = self._ffn(pre, x, fb)
         if not self.last:
-            return ops.add(residual, delta) if delta is not None else residual
+            if delta is None:
+                return residual
+            if partial:
+                self.comm.all_reduce_(delta, "tp")
+            return ops.add(residual, delta)
         idx = fb.logits_idx
         r = residual if idx is None else residual.index_select(0, idx)
         if delta is not None:
+            # all-reduce is linear: select the sampled rows first and reduce only those
             dl = delta if idx is None else delta.index_select(0, idx)
             if idx is None:
                 r = r.clone()
-            x = self._norm(dl, self.p["final_w"], self.p.get("final_b"), residual=r)
+            x = self._add_norm(dl, "final", r, partial)
         else:
             x = self._norm(r, self.p["final_w"], self.p.get("final_b"))
         return ops.linear(x, self.head_weight)
 
-    def _ffn(self, pre: str, x: torch.Tensor, fb: ForwardBatch) -> torch.Tensor:
+    def _add_norm(self, t: torch.Tensor, prefix: str, residual: torch.Tensor, partial: bool) -> torch.Tensor:
+        """residual += (all_reduce(t) if partial else t); return norm(residual). With TP the
+        all-reduce and the add+norm run as one fused kernel when the IPC all-reduce is on."""
+        w, b = self.p[prefix + "_w"], self.p.get(prefix + "_b")
+        if partial:
+            if self.cfg.norm == "rms":
+                return self.comm.all_reduce_rms_norm_(t, w, self.cfg.norm_eps, residual, "tp")
+            self.comm.all_reduce_(t, "tp")
+        return self._norm(t, w, b, residual=residual)
+
+    def _ffn(self, pre: str, x: torch.Tensor, fb: ForwardBatch) -> tuple:
+        """Returns (out, partial): `partial` means `out` still needs the TP all-reduce, which
+        the caller fuses with the next residual add + norm."""
         c, d = self.cfg, self.dims
         if c.is_moe:
             gates, _, _ = ops.moe_route(x, self.p[pre + "router_w"], c.experts_per_token)
@@ -359,10 +376,8 @@ class TransformerLM:
             ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
             out = ops.linear(hmid, self.p[pre + "moe_down_w"])
             if self.ep > 1:
-                out = self.comm.reduce_scatter(out, "ep")[:T]
-            elif self.tp > 1:
-                self.comm.all_reduce_(out, "tp")
-            return out
+                return self.comm.reduce_scatter(out, "ep")[:T], False
+            return out, self.tp > 1
         if c.act == "silu":
             hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu")
             out = ops.linear(hmid, self.p[pre + "down_w"])
@@ -371,9 +386,7 @@ class TransformerLM:
             hmid = ops.gelu(hmid)
             pb = self.p.get(pre + "proj_b") if self.shard.tp_rank == 0 else None
             out = ops.linear(hmid, self.p[pre + "proj_w"], bias=pb)
-        if self.tp > 1:
-            self.comm.all_reduce_(out, "tp")
-        return out
+        return out, self.tp > 1
 
     # ------------------------------------------------------------------------------------
     # KV cache layout helpers

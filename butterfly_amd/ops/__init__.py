@@ -44,6 +44,12 @@ def load_library(path: str | os.PathLike | None = None) -> bool:
     return _loaded
 
 
+def require_library() -> None:
+    """Raise unless the HIP kernel library is loaded (GPU-only features call this)."""
+    if not load_library():
+        raise RuntimeError(f"butterfly_amd HIP kernels unavailable: {_load_error}")
+
+
 def native_available() -> bool:
     return load_library()
 

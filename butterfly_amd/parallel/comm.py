@@ -74,7 +74,12 @@ class Communicator:
             groups[axis] = mine
         groups["ep"] = groups["dp"] if mesh.ep > 1 else GroupHandle([rank], None, 0)
         groups["world"] = GroupHandle(list(range(mesh.world_size)), dist.group.WORLD, rank)
-        return cls(mesh, rank, groups)
+        comm = cls(mesh, rank, groups)
+        from ..utils import flags
+
+        if flags.get("BFLY_CUSTOM_AR") and mesh.tp > 1 and torch.cuda.is_available():
+            comm.enable_custom_all_reduce(flags.get("BFLY_CUSTOM_AR_MAX_BYTES"))
+        return comm
 
     @staticmethod
     def _nccl(g: GroupHandle) -> bool:
@@ -100,6 +105,42 @@ class Communicator:
             return self.custom_ar.all_reduce_(t)
         dist.all_reduce(t, group=g.pg)
         return t
+
+    def all_reduce_rms_norm_(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor,
+                             group: str = "tp") -> torch.Tensor:
+        """residual += all_reduce(t); return rms_norm(residual) * w — one fused kernel on the
+        IPC path (the all-reduce feeding every transformer block's add+norm), else RCCL
+        all-reduce followed by the fused add+norm kernel."""
+        g = self.groups[group]
+        car = self.custom_ar
+        if g.size > 1 and group == "tp" and car is not None and car.should_use(t):
+            self.stats["calls"] += 1
+            self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+            return car.all_reduce_rms_norm_(t, w, eps, residual)
+        from .. import ops
+
+        self.all_reduce_(t, group)
+        return ops.rms_norm(t, w, eps, residual=residual)
+
+    def enable_custom_all_reduce(self, max_bytes: int) -> bool:
+        """Set up the one-shot IPC all-reduce for the TP group (collective over the group).
+        Returns True when it passed its self-test and will be used."""
+        g = self.groups["tp"]
+        if g.size not in (2, 4, 8) or not torch.cuda.is_available():
+            return False
+        from .custom_allreduce import CustomAllReduce
+
+        car = CustomAllReduce(g.ranks, g.rank_in_group, g.pg, max_bytes=max_bytes)
+        self.custom_ar = car if car.ok else None
+        if not car.ok:
+            car.close()
+        return self.custom_ar is not None
+
+    def check_health(self) -> None:
+        """Raise if the IPC all-reduce recorded a peer-wait timeout (a rank stopped arriving:
+        its results since then are not trustworthy). Cheap: one 4-byte device read."""
+        if self.custom_ar is not None and self.custom_ar.error():
+            raise RuntimeError(f"rank {self.rank}: custom all-reduce peer wait timed out")
 
     def all_gather(self, t: torch.Tensor, group: str = "tp", out: torch.Tensor | None = None) -> torch.Tensor:
         g = self.groups[group]

@@ -1,0 +1,126 @@
+"""One-shot IPC all-reduce for the TP group.
+
+Each rank allocates one uncached device buffer, exports it with hipIpcGetMemHandle, and the
+group exchanges handles over the (already initialised) process group. The all-reduce itself
+is one HIP kernel (csrc/kernels/allreduce.hip): publish own rows, flag every peer, read the
+peers' rows directly over xGMI and sum in fixed rank order, so all ranks hold bitwise
+identical results. `all_reduce_rms_norm_` additionally fuses the residual add and RMSNorm
+that follow every TP all-reduce in the transformer block, removing one kernel and one pass
+over the activations per all-reduce.
+
+Only messages up to `max_bytes` (default BFLY_CUSTOM_AR_MAX_BYTES) go here — the decode
+all-reduces; larger ones (prefill) stay on RCCL. Construction runs a self-test; if the IPC
+mapping, the kernel or the flag protocol misbehave on this machine, the instance reports
+`ok = False` and the communicator keeps using RCCL.
+"""
+from __future__ import annotations
+
+import logging
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+log = logging.getLogger("butterfly_amd.comm")
+
+
+class CustomAllReduce:
+    def __init__(self, ranks: list, rank_in_group: int, pg, max_bytes: int = 8 << 20,
+                 device: torch.device | None = None):
+        ops.require_library()
+        self.world = len(ranks)
+        self.rank = rank_in_group
+        self.cap = int(max_bytes)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        if self.world not in (2, 4, 8):
+            raise ValueError("custom all-reduce supports groups of 2, 4 or 8 ranks")
+        L = torch.ops.bfly
+        self._ptr = 0
+        self._opened = []
+        self.bases = []
+        self.ok = False
+        # every step below is collective: a local failure is voted on, never raised alone
+        handle = None
+        try:
+            self._ptr = L.car_alloc(L.car_buffer_bytes(self.cap))
+            handle = bytes(L.car_ipc_handle(self._ptr).tolist())
+        except Exception as e:  # noqa: BLE001
+            log.warning("custom all-reduce: buffer export failed (%r)", e)
+        handles: list = [None] * self.world
+        dist.all_gather_object(handles, handle, group=pg)
+        local_ok = all(h is not None for h in handles)
+        if local_ok:
+            try:
+                for r, h in enumerate(handles):
+                    if r == self.rank:
+                        self.bases.append(self._ptr)
+                    else:
+                        p = L.car_ipc_open(torch.tensor(list(h), dtype=torch.uint8))
+                        self._opened.append(p)
+                        self.bases.append(p)
+            except Exception as e:  # noqa: BLE001
+                log.warning("custom all-reduce: opening a peer buffer failed (%r)", e)
+                local_ok = False
+        if self._vote(local_ok, pg):
+            self.ok = self._self_test(pg)
+
+    # ---------------------------------------------------------------------------------------
+    def should_use(self, t: torch.Tensor) -> bool:
+        return (self.ok and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2
+                and t.is_contiguous() and t.shape[1] % 8 == 0 and t.shape[1] <= 16384
+                and t.numel() * 2 <= self.cap and t.data_ptr() % 16 == 0)
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        torch.ops.bfly.custom_all_reduce(t, t, None, None, 0.0, self.bases, self.rank, self.cap)
+        return t
+
+    def all_reduce_rms_norm_(self, t: torch.Tensor, w: torch.Tensor, eps: float,
+                             residual: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """residual += all_reduce(t) (bf16), returns rms_norm(residual) * w."""
+        if out is None:
+            out = torch.empty_like(t)
+        torch.ops.bfly.custom_all_reduce(t, out, residual, w, float(eps), self.bases, self.rank, self.cap)
+        return out
+
+    def error(self) -> int:
+        """Sticky device error word (non-zero after a flag-wait timeout)."""
+        return int(torch.ops.bfly.car_error(self._ptr))
+
+    def _vote(self, good: bool, pg) -> bool:
+        """True iff `good` on every rank of the group."""
+        flag = torch.tensor([1 if good else 0], dtype=torch.int32,
+                            device=self.device if dist.get_backend(pg) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=pg)
+        return bool(flag.item())
+
+    def _self_test(self, pg) -> bool:
+        good = True
+        try:
+            for rows, dim in ((3, 64), (130, 4096)):
+                x = torch.arange(rows * dim, device=self.device, dtype=torch.float32).view(rows, dim)
+                x = ((x % 17) + self.rank).to(torch.bfloat16)
+                want = sum(((x.float() - self.rank) + r) for r in range(self.world)).to(torch.bfloat16)
+                for _ in range(3):      # exercise both buffer parities
+                    y = x.clone()
+                    self.all_reduce_(y)
+                torch.cuda.synchronize(self.device)
+                good &= bool(torch.equal(y, want)) and self.error() == 0
+        except Exception as e:  # noqa: BLE001 — any failure means: keep RCCL
+            log.warning("custom all-reduce self-test raised %r", e)
+            good = False
+        ok = self._vote(good, pg)
+        if not ok:
+            log.warning("custom all-reduce self-test failed on some rank; using RCCL")
+        return ok
+
+    def close(self) -> None:
+        L = torch.ops.bfly
+        for p in self._opened:
+            L.car_ipc_close(p)
+        self._opened = []
+        if self._ptr:
+            torch.cuda.synchronize(self.device)
+            L.car_free(self._ptr)
+            self._ptr = 0
+        self.ok = False

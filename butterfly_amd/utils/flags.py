@@ -34,7 +34,8 @@ def define(name: str, default, parse, help: str) -> Flag:
 
 
 define("BFLY_DISABLE_GRAPHS", False, _bool, "run decode steps eagerly instead of replaying hipGraphs")
-define("BFLY_CUSTOM_AR", False, _bool, "use the one-shot IPC all-reduce kernel for small TP all-reduces")
+define("BFLY_CUSTOM_AR", True, _bool, "use the one-shot IPC all-reduce kernel (self-tested at start-up, "
+       "RCCL otherwise) for small TP all-reduces")
 define("BFLY_CUSTOM_AR_MAX_BYTES", 8 << 20, int, "largest all-reduce (bytes) routed to the IPC kernel")
 define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")

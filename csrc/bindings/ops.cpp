@@ -360,6 +360,68 @@ void probe(int64_t which, Tensor& out) {
   bfly::launch_probe(which, out.data_ptr<float>(), cur_stream());
 }
 
+// ---- one-shot IPC all-reduce -------------------------------------------------------------
+// Buffers are raw device pointers carried as int64 (they are shared with peer processes via
+// hipIpc handles and live for the communicator's lifetime, outside torch's allocator).
+int64_t car_alloc(int64_t bytes) {
+  TORCH_CHECK(bytes > 0, "car_alloc: bytes");
+  void* p = bfly::car_alloc((size_t)bytes);
+  TORCH_CHECK(p != nullptr, "car_alloc: hipExtMallocWithFlags(uncached) failed");
+  return reinterpret_cast<int64_t>(p);
+}
+void car_free(int64_t p) { bfly::car_free(reinterpret_cast<void*>(p)); }
+Tensor car_ipc_handle(int64_t p) {
+  Tensor h = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  TORCH_CHECK(bfly::car_ipc_handle(reinterpret_cast<void*>(p), h.data_ptr<uint8_t>()) == 0,
+              "car_ipc_handle: hipIpcGetMemHandle failed");
+  return h;
+}
+int64_t car_ipc_open(const Tensor& h) {
+  TORCH_CHECK(h.scalar_type() == at::kByte && h.numel() == 64 && h.is_contiguous() && !h.is_cuda(),
+              "car_ipc_open: expects a 64-byte CPU uint8 handle");
+  void* p = bfly::car_ipc_open(h.data_ptr<uint8_t>());
+  TORCH_CHECK(p != nullptr, "car_ipc_open: hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+void car_ipc_close(int64_t p) { bfly::car_ipc_close(reinterpret_cast<void*>(p)); }
+int64_t car_error(int64_t p) { return bfly::car_error(reinterpret_cast<const void*>(p)); }
+
+void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tensor>& residual,
+                       const c10::optional<Tensor>& w, double eps, at::IntArrayRef bases,
+                       int64_t rank, int64_t cap) {
+  CHECK_GPU(inp); CHECK_BF16(inp); CHECK_BF16(out);
+  TORCH_CHECK(inp.dim() == 2 && inp.is_contiguous() && out.is_contiguous() &&
+                  out.sizes() == inp.sizes(), "custom_all_reduce: 2-D contiguous, same shape");
+  CHECK_ALIGN16(inp); CHECK_ALIGN16(out);
+  const int world = (int)bases.size();
+  TORCH_CHECK(world == 2 || world == 4 || world == 8, "custom_all_reduce: world must be 2, 4 or 8");
+  TORCH_CHECK(rank >= 0 && rank < world, "custom_all_reduce: rank");
+  const int rows = inp.size(0), dim = inp.size(1);
+  TORCH_CHECK(dim % 8 == 0 && dim <= 16384, "custom_all_reduce: dim % 8 == 0 and <= 16384");
+  TORCH_CHECK((int64_t)rows * dim * 2 <= cap, "custom_all_reduce: message larger than the buffer");
+  bfly::ArPeers peers{};
+  for (int i = 0; i < world; ++i) {
+    TORCH_CHECK(bases[i] != 0, "custom_all_reduce: null peer buffer");
+    peers.base[i] = reinterpret_cast<char*>(bases[i]);
+  }
+  bfly::bf16* res = nullptr;
+  const bfly::bf16* wp = nullptr;
+  if (residual.has_value()) {
+    TORCH_CHECK(w.has_value(), "custom_all_reduce: norm weight required with residual");
+    const Tensor& r = *residual;
+    CHECK_BF16(r); CHECK_BF16((*w));
+    TORCH_CHECK(r.is_contiguous() && r.sizes() == inp.sizes(), "custom_all_reduce: residual shape");
+    TORCH_CHECK(w->numel() == dim && w->is_contiguous(), "custom_all_reduce: weight shape");
+    TORCH_CHECK(out.data_ptr() != inp.data_ptr(), "custom_all_reduce: fused norm cannot run in place");
+    res = bf(r);
+    wp = bf(*w);
+  }
+  c10::DeviceGuard g(inp.device());
+  const int rc = bfly::launch_custom_allreduce(bf(inp), bf(out), res, wp, (float)eps, rows, dim,
+                                               peers, world, (int)rank, cap, cur_stream());
+  TORCH_CHECK(rc == 0, "custom_all_reduce: launch rejected (", rc, ")");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(bfly, m) {
@@ -379,6 +441,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
   m.def("gemm_plan(int M, int N, int K) -> int[]", &gemm_plan);
+  m.def("gemm_check(int M, int N, int K, int epilogue) -> int",
+        [](int64_t M, int64_t N, int64_t K, int64_t e) -> int64_t { return bfly::gemm_check(M, N, K, e); });
   m.def("attn_decode_splits(int max_ctx, int part_tokens) -> int", &attn_decode_splits);
   m.def("attn_decode_part_tokens(int B, int Hkv, int max_ctx) -> int", &attn_decode_part_tokens);
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
@@ -387,6 +451,15 @@ TORCH_LIBRARY(bfly, m) {
   m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
   m.def("probe(int which, Tensor(a!) out) -> ()");
+  m.def("car_alloc(int bytes) -> int", &car_alloc);
+  m.def("car_free(int ptr) -> ()", &car_free);
+  m.def("car_ipc_handle(int ptr) -> Tensor", &car_ipc_handle);
+  m.def("car_ipc_open(Tensor handle) -> int", &car_ipc_open);
+  m.def("car_ipc_close(int ptr) -> ()", &car_ipc_close);
+  m.def("car_error(int ptr) -> int", &car_error);
+  m.def("car_buffer_bytes(int cap) -> int", [](int64_t cap) -> int64_t { return bfly::car_buffer_bytes(cap); });
+  m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, Tensor(b!)? residual, Tensor? w, float eps, "
+        "int[] bases, int rank, int cap) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
         "bool causal, Tensor(a!) out) -> ()");
 }
@@ -407,6 +480,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("probe", &probe);
+  m.impl("custom_all_reduce", &custom_all_reduce);
   m.impl("moe_route", &moe_route);
   m.impl("moe_gate_scale", &moe_gate_scale);
 }

@@ -56,6 +56,7 @@ size_t gemm_workspace_bytes(int M, int N, int K);
 int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                      int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                      size_t ws_bytes, hipStream_t stream);
+int gemm_check(int M, int N, int K, int epi);   // 0 if the auto plan can run this shape
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
                 hipStream_t stream);
@@ -71,6 +72,22 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
                         hipStream_t stream);
+
+// allreduce.hip — one-shot IPC all-reduce (+ fused residual add / RMSNorm)
+constexpr int kArBlocks = 128;
+constexpr int kArMaxWorld = 8;
+constexpr long kArDataOff = 65536;
+struct ArPeers { char* base[kArMaxWorld]; };
+inline long car_buffer_bytes(long cap) { return kArDataOff + 2 * cap; }
+int launch_custom_allreduce(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
+                            int rows, int dim, const ArPeers& peers, int world, int rank,
+                            long cap, hipStream_t stream);
+void* car_alloc(size_t bytes);
+void car_free(void* p);
+int car_ipc_handle(void* p, unsigned char* out64);
+void* car_ipc_open(const unsigned char* h64);
+void car_ipc_close(void* p);
+int car_error(const void* base);
 
 // moe.hip
 int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H, int E, int K,

@@ -375,7 +375,7 @@ GemmPlan plan_gemm(int M, int N, int K) {
     p.kind = 0;
     p.mt = (M + 15) / 16;
     const bool long_k = K > 4096;
-    p.nt = M <= 4 ? (long_k ? 4 : 1) : 2;
+    p.nt = M <= 4 ? (long_k ? 4 : 2) : 2;   // even: the SiLU epilogue pairs gate/up groups
     p.wk = long_k ? 2 : 4;
     const int blocks = N / (16 * p.nt * (4 / p.wk));
     int sk = 1;
@@ -404,9 +404,10 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
   return p.sk > 1 ? (size_t)p.sk * M * N * sizeof(float) : 0;
 }
 
+// `dry`: validate only (the plan is supported for this shape/epilogue) without launching.
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
-                    hipStream_t stream) {
+                    hipStream_t stream, bool dry = false) {
   if (p.kind == 0) {
     if (K % 128 != 0 || M > 16 * p.mt) return -1;
     if (N % (16 * p.nt * (4 / p.wk)) != 0) return -1;
@@ -414,7 +415,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     bool done = false;
 #define SK_CASE(MT_, NT_, WK_)                                                                   \
   if (!done && p.mt == MT_ && p.nt == NT_ && p.wk == WK_) {                                       \
-    run_skinny<MT_, NT_, WK_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);    \
+    if (!dry) run_skinny<MT_, NT_, WK_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream); \
     done = true;                                                                                  \
   }
 #define SK_WK(MT_, NT_) SK_CASE(MT_, NT_, 1) SK_CASE(MT_, NT_, 2) SK_CASE(MT_, NT_, 4)
@@ -429,7 +430,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     const int st = p.mt > 0 ? p.mt : 2;   // tile plans reuse `mt` as the pipeline depth
 #define TL_CASE(BM_, BN_, WMW_, ST_)                                                            \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_ && st == ST_) {                       \
-    run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream); \
+    if (!dry) run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream); \
     done = true;                                                                                \
   }
 #define TL_ST(BM_, BN_, WMW_) TL_CASE(BM_, BN_, WMW_, 2) TL_CASE(BM_, BN_, WMW_, 3) TL_CASE(BM_, BN_, WMW_, 4)
@@ -440,7 +441,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1) {
+  if (p.sk > 1 && !dry) {
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);
@@ -456,6 +457,12 @@ int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, 
   if (M <= 0) return 0;
   if (p.sk > 1 && (ws == nullptr || ws_bytes < (size_t)p.sk * M * N * sizeof(float))) return -3;
   return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream);
+}
+
+int gemm_check(int M, int N, int K, int epi) {
+  if (M <= 0) return 0;
+  return run_plan(plan_gemm(M, N, K), nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0,
+                  nullptr, nullptr, true);
 }
 
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,

@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""GPU check + microbenchmark of the one-shot IPC all-reduce (csrc/kernels/allreduce.hip).
+
+N ranks share cuda:0 (gloo carries only the handle exchange): exercises the IPC mapping,
+the flag protocol, both buffer parities, the fused add+RMSNorm epilogue, hipGraph capture
+and replay, and times the kernel.  On a multi-GPU node the same script runs one rank per GPU.
+usage: python -m butterfly_amd launch -n 2 -- python tools/car_check.py [--bench]"""
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from butterfly_amd import ops  # noqa: E402
+from butterfly_amd.parallel.custom_allreduce import CustomAllReduce  # noqa: E402
+
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+local = int(os.environ.get("LOCAL_RANK", "0"))
+dev_idx = local if torch.cuda.device_count() > local and os.environ.get("BFLY_CAR_SHARED") != "1" else 0
+torch.cuda.set_device(dev_idx)
+dev = torch.device("cuda", dev_idx)
+dist.init_process_group("gloo", rank=rank, world_size=world)
+car = CustomAllReduce(list(range(world)), rank, dist.group.WORLD, max_bytes=8 << 20, device=dev)
+fails = []
+if not car.ok:
+    print(f"rank {rank}: custom all-reduce self-test FAILED", flush=True)
+    sys.exit(1)
+
+
+def data(rows, dim, r, salt):
+    g = torch.Generator(device="cpu").manual_seed(1000 * salt + r)
+    return (torch.randn(rows, dim, generator=g) * (r + 1)).to(torch.bfloat16).to(dev)
+
+
+# 1. plain sums, many shapes (every rank computes the same expected value)
+for salt, (rows, dim) in enumerate([(1, 8192), (7, 8192), (64, 8192), (128, 8192), (129, 1024),
+                                    (256, 8192), (512, 4096), (1, 16384)]):
+    xs = [data(rows, dim, r, salt) for r in range(world)]
+    want = torch.zeros(rows, dim, device=dev)
+    for x in xs:
+        want += x.float()
+    want = want.to(torch.bfloat16)
+    y = xs[rank].clone()
+    car.all_reduce_(y)
+    torch.cuda.synchronize()
+    if not torch.equal(y, want):
+        fails.append(f"sum {rows}x{dim}: max err {(y.float() - want.float()).abs().max().item():.3e}")
+
+# 2. fused residual add + RMSNorm == all-reduce then rms_norm(residual=...)
+for salt, (rows, dim) in enumerate([(64, 8192), (3, 4096), (200, 8192)]):
+    xs = [data(rows, dim, r, 50 + salt) for r in range(world)]
+    res0 = data(rows, dim, 99, 50 + salt)
+    w = data(1, dim, 77, 50 + salt).view(dim)
+    s = torch.zeros(rows, dim, device=dev)
+    for x in xs:
+        s += x.float()
+    s = s.to(torch.bfloat16)
+    res_ref = res0.clone()
+    y_ref = ops.rms_norm(s, w, 1e-5, residual=res_ref)
+    res = res0.clone()
+    y = car.all_reduce_rms_norm_(xs[rank].clone(), w, 1e-5, res)
+    torch.cuda.synchronize()
+    if not torch.equal(res, res_ref):
+        fails.append(f"fused residual {rows}x{dim}")
+    err = (y.float() - y_ref.float()).abs().max().item()
+    if err > 1e-2 * max(1.0, y_ref.float().abs().max().item()):
+        fails.append(f"fused norm {rows}x{dim}: {err:.3e}")
+
+# 3. graph capture / replay
+x = data(64, 8192, rank, 7)
+buf = x.clone()
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    car.all_reduce_(buf)         # warm-up on the capture stream
+torch.cuda.current_stream().wait_stream(s)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    car.all_reduce_(buf)
+want = torch.zeros(64, 8192, device=dev)
+for r in range(world):
+    want += data(64, 8192, r, 7).float()
+want = want.to(torch.bfloat16)
+for it in range(5):
+    buf.copy_(x)
+    g.replay()
+    torch.cuda.synchronize()
+    if not torch.equal(buf, want):
+        fails.append(f"graph replay {it}")
+        break
+if car.error():
+    fails.append(f"device error word {car.error()}")
+
+# 4. timing (kernel alone, back-to-back)
+if "--bench" in sys.argv:
+    for rows in (1, 16, 64, 128, 256):
+        t = data(rows, 8192, rank, 3)
+        for _ in range(10):
+            car.all_reduce_(t)
+        torch.cuda.synchronize()
+        dist.barrier()
+        n = 200
+        t0 = time.perf_counter()
+        for _ in range(n):
+            car.all_reduce_(t)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) / n * 1e6
+        if rank == 0:
+            print(f"custom all-reduce world={world} rows={rows} dim=8192 ({rows * 16} KiB): {us:.1f} us/call", flush=True)
+
+car.close()
+print(f"rank {rank}: custom all-reduce world={world} -> {'PASS' if not fails else 'FAIL ' + '; '.join(fails)}", flush=True)
+dist.destroy_process_group()
+sys.exit(0 if not fails else 1)
