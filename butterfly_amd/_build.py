@@ -38,7 +38,8 @@ def _torch_paths():
 
 
 def _headers() -> list[Path]:
-    return sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "runtime").glob("*.h"))
+    return (sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "runtime").glob("*.h"))
+            + sorted((CSRC / "kernels").glob("*.inc")))
 
 
 def _digest(src: Path, flags: list[str]) -> str:

@@ -74,7 +74,7 @@ class _Arena:
         self.bufs: dict[tuple, torch.Tensor] = {}
         self.frozen = False
 
-    def get(self, device, name: str, numel: int, dtype) -> torch.Tensor:
+    def get(self, device, name: str, numel: int, dtype, zero: bool = False) -> torch.Tensor:
         key = (str(device), name, dtype)
         buf = self.bufs.get(key)
         if buf is None or buf.numel() < numel:
@@ -82,7 +82,7 @@ class _Arena:
                 raise RuntimeError(
                     f"workspace '{name}' needs {numel} elements but is frozen/capturing; "
                     "call ops.reserve_workspace() before capture")
-            buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
+            buf = (torch.zeros if zero else torch.empty)(max(numel, 1), dtype=dtype, device=device)
             self.bufs[key] = buf
         return buf
 
@@ -100,7 +100,7 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
         if m > max_tokens:
             continue
         ws = max(ws, torch.ops.bfly.gemm_workspace_size(m, max_n, max_k))
-    _arena.get(device, "gemm", ws // 4 + 1, torch.float32)
+    _arena.get(device, "gemm", ws // 4 + 1, torch.float32, zero=True)
     if max_batch and max_ctx:
         ns = max(torch.ops.bfly.attn_decode_splits(max_ctx, torch.ops.bfly.attn_decode_part_tokens(b, num_kv_heads, max_ctx))
                  for b in range(1, max_batch + 1))
@@ -210,7 +210,9 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None):
     if out is None:
         out = torch.empty(M, nout, dtype=x.dtype, device=x.device)
     need = torch.ops.bfly.gemm_workspace_size(M, N, x.shape[1])
-    ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32) if need else None
+    # zero-initialised once: its head holds the split-K arrival counters, which every GEMM
+    # leaves re-armed at zero
+    ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True) if need else None
     torch.ops.bfly.gemm(x, w, out, bias, epi, ws)
     return out
 

@@ -441,6 +441,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
   m.def("gemm_plan(int M, int N, int K) -> int[]", &gemm_plan);
+  m.def("gemm_set_splitk_fixup(bool on) -> ()", [](bool on) { bfly::gemm_set_splitk_fixup(on); });
   m.def("gemm_check(int M, int N, int K, int epilogue) -> int",
         [](int64_t M, int64_t N, int64_t K, int64_t e) -> int64_t { return bfly::gemm_check(M, N, K, e); });
   m.def("attn_decode_splits(int max_ctx, int part_tokens) -> int", &attn_decode_splits);

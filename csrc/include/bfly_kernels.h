@@ -56,7 +56,8 @@ size_t gemm_workspace_bytes(int M, int N, int K);
 int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                      int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                      size_t ws_bytes, hipStream_t stream);
-int gemm_check(int M, int N, int K, int epi);   // 0 if the auto plan can run this shape
+int gemm_check(int M, int N, int K, int epi);
+void gemm_set_splitk_fixup(bool on);   // in-kernel split-K reduction (default: env / off)   // 0 if the auto plan can run this shape
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
                 hipStream_t stream);

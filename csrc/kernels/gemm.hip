@@ -69,6 +69,77 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int SK
   }
 }
 
+// In-kernel split-K fixup ("last workgroup reduces"): every split writes its f32 partial,
+// publishes it (device-scope release) and bumps the tile's arrival counter; the split that
+// arrives last sums all partials in split order 0..SK-1 (deterministic, independent of which
+// split finished last), applies the epilogue, writes bf16 and re-arms the counter to 0 for the
+// next GEMM. Removes the separate reduce launch and its kernel boundary, and the reduction of
+// early tiles overlaps the MFMA work of late ones. Counters live at a fixed place (the start
+// of the workspace), so every GEMM on the stream shares them and always leaves them zeroed.
+constexpr int kSplitCounters = 16384;
+constexpr size_t kCounterBytes = kSplitCounters * sizeof(int);
+
+// Hand-off recipe of cdna_hip_programming.md §5 (split-K item 2): plain slab stores, every
+// wave drains its stores, barrier, ONE agent-scope release + relaxed ticket by lane 0; the
+// last arriver does ONE agent-scope acquire. `flag` is a word of the kernel's existing LDS
+// array (a second __shared__ object would perturb the k-loop's waits: item 4a).
+__device__ __forceinline__ bool splitk_arrive(int* counter, int sk, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == sk - 1;
+    if (last) {
+      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+__device__ __forceinline__ void splitk_fixup(const float* __restrict__ part, int SK, int M, int N,
+                                             int m0, int m1, int n0, int n1, int epi,
+                                             const bf16* __restrict__ bias, bf16* __restrict__ out,
+                                             long ldo) {
+  const long slab = (long)M * N;
+  if (m1 > M) m1 = M;
+  if (epi == EPI_SILU) {
+    const int f0 = n0 / 2, nf = (n1 - n0) / 2;   // output columns of this tile
+    const int total = (m1 - m0) * (nf / 4);
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int m = m0 + e / (nf / 4), f = f0 + (e % (nf / 4)) * 4;
+      const long gi = (long)m * N + (f >> 4) * 32 + (f & 15), ui = gi + 16;
+      f32x4 g = {0.f, 0.f, 0.f, 0.f}, u = g;
+      for (int sp = 0; sp < SK; ++sp) {
+        g += *reinterpret_cast<const f32x4*>(part + sp * slab + gi);
+        u += *reinterpret_cast<const f32x4*>(part + sp * slab + ui);
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(silu(g[j]) * u[j]);
+      *reinterpret_cast<bf16x4*>(out + (long)m * ldo + f) = o;
+    }
+  } else {
+    const int nc = (n1 - n0) / 4;
+    const int total = (m1 - m0) * nc;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int m = m0 + e / nc, n = n0 + (e % nc) * 4;
+      const long i = (long)m * N + n;
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < SK; ++sp) a += *reinterpret_cast<const f32x4*>(part + sp * slab + i);
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(epi == EPI_BIAS ? a[j] + bf2f(bias[n + j]) : a[j]);
+      *reinterpret_cast<bf16x4*>(out + (long)m * ldo + n) = o;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Skinny (decode) GEMM
 // ---------------------------------------------------------------------------------------
@@ -115,7 +186,8 @@ template <int MT, int NT, int WK>
 __global__ void __launch_bounds__(kSkThreads)
 gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                    int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                   bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+                   bf16* __restrict__ out, long ldo, float* __restrict__ part,
+                   int* __restrict__ counters) {
   constexpr int WN = 4 / WK;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wk = wid % WK, wn = wid / WK;
@@ -183,6 +255,8 @@ gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict_
       store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
     }
   }
+  if (part && counters && splitk_arrive(counters + blockIdx.x, gridDim.y, reinterpret_cast<int*>(red)))
+    splitk_fixup(part, gridDim.y, M, N, 0, M, nb0, nb0 + 16 * NT * WN, epi, bias, out, ldo);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -236,7 +310,8 @@ template <int BM, int BN, int WMW, int STAGES>
 __global__ void __launch_bounds__(kTileThreads)
 gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                 bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+                 bf16* __restrict__ out, long ldo, float* __restrict__ part,
+                 int* __restrict__ counters) {
   constexpr int WNW = 4 / WMW;                // waves along M x waves along N
   constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
@@ -327,6 +402,8 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
       }
     }
   }
+  if (part && counters && splitk_arrive(counters + tile, gridDim.y, reinterpret_cast<int*>(smem)))
+    splitk_fixup(part, gridDim.y, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -334,13 +411,30 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 // ---------------------------------------------------------------------------------------
 static int num_cus() { return 256; }
 
+// Workspace layout: [kCounterBytes of zeroed split counters | SK x M x N f32 partials].
+static float* splitk_part(float* ws) { return ws + kCounterBytes / sizeof(float); }
+
+// BFLY_GEMM_SPLITK_FIXUP=1 reduces split-K partials inside the GEMM (last-arriver fixup)
+// instead of a separate reduce kernel. Off by default: it only pays when SK x slab bytes per
+// tile is a few tens of KB (the decode plans use SK=8 on 64x128 tiles = 256 KB per tile).
+static int g_fixup = -1;   // -1: not yet read from the environment
+static bool fixup_enabled() {
+  if (g_fixup < 0) {
+    const char* e = getenv("BFLY_GEMM_SPLITK_FIXUP");
+    g_fixup = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_fixup == 1;
+}
+void gemm_set_splitk_fixup(bool on) { g_fixup = on ? 1 : 0; }
+
 template <int MT, int NT, int WK>
 static void run_skinny(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                        int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                        hipStream_t stream) {
   dim3 grid(N / (16 * NT * (4 / WK)), sk);
   gemm_skinny_kernel<MT, NT, WK><<<grid, kSkThreads, 0, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? ws : nullptr);
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
+      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr);
 }
 
 template <int BM, int BN, int WMW, int STAGES>
@@ -357,7 +451,8 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
     attr_set = true;
   }
   gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? ws : nullptr);
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
+      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr);
 }
 
 // Plan selection, from the tools/bench_gemm.py sweep on MI355X (Llama-3-70B TP1/TP8 shapes,
@@ -365,7 +460,40 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
 // register-streaming skinny kernel for every M >= 8 (e.g. down-proj M=64: 90 us = 5.2 TB/s vs
 // 186 us) and ties or beats hipBLASLt; the skinny kernel stays for M <= 4 (GEMV regime).
 // Split-K is sized so the grid has ~448 workgroups (1.75 per CU) with >= 4 K-tiles each.
+// Measured plan table (tools/gen_gemm_table.py from the profiles/gemm_tune_*.json sweeps of
+// tools/bench_gemm.py --sweep on MI355X): the fastest plan per model projection shape and
+// token-count bucket (entries exist only where the sweep beat the heuristic by > 3%).
+struct TunedPlan { int N, K, M, kind, mt, nt, wk, bm, bn, sk; };
+static const TunedPlan kTuned[] = {
+#include "gemm_tuned.inc"
+};
+
+static GemmPlan plan_gemm_heuristic(int M, int N, int K);
+
+static bool tuned_enabled() {   // BFLY_GEMM_TUNED=0: heuristic plans only (A/B runs)
+  static const bool on = [] {
+    const char* e = getenv("BFLY_GEMM_TUNED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 GemmPlan plan_gemm(int M, int N, int K) {
+  if (!tuned_enabled()) return plan_gemm_heuristic(M, N, K);
+  // token-count buckets of the sweep: M uses the entry of its bucket, or the heuristic plan
+  // when the sweep found nothing better there
+  static const int kBuckets[] = {1, 16, 32, 64, 128, 256};
+  int bucket = 0;
+  for (int b : kBuckets)
+    if (b >= M) { bucket = b; break; }
+  if (bucket == 0) return plan_gemm_heuristic(M, N, K);
+  for (const TunedPlan& t : kTuned)
+    if (t.N == N && t.K == K && t.M == bucket)
+      return GemmPlan{t.kind, t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
+  return plan_gemm_heuristic(M, N, K);
+}
+
+static GemmPlan plan_gemm_heuristic(int M, int N, int K) {
   GemmPlan p{};
   const int target = 448;
   const bool skinny_ok = K % 128 == 0 && N % 128 == 0;
@@ -399,9 +527,15 @@ GemmPlan plan_gemm(int M, int N, int K) {
   return p;
 }
 
+static size_t plan_ws_bytes(const GemmPlan& p, int M, int N) {
+  return p.sk > 1 ? kCounterBytes + (size_t)p.sk * M * N * sizeof(float) : 0;
+}
+
+// Enough for the tuned plan and for the heuristic plan it may fall back to (below).
 size_t gemm_workspace_bytes(int M, int N, int K) {
-  const GemmPlan p = plan_gemm(M, N, K);
-  return p.sk > 1 ? (size_t)p.sk * M * N * sizeof(float) : 0;
+  const size_t a = plan_ws_bytes(plan_gemm(M, N, K), M, N);
+  const size_t b = plan_ws_bytes(plan_gemm_heuristic(M, N, K), M, N);
+  return a > b ? a : b;
 }
 
 // `dry`: validate only (the plan is supported for this shape/epilogue) without launching.
@@ -412,6 +546,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     if (K % 128 != 0 || M > 16 * p.mt) return -1;
     if (N % (16 * p.nt * (4 / p.wk)) != 0) return -1;
     if (epi == EPI_SILU && p.nt % 2 != 0) return -1;
+    if (p.sk > 1 && N / (16 * p.nt * (4 / p.wk)) > kSplitCounters) return -1;
     bool done = false;
 #define SK_CASE(MT_, NT_, WK_)                                                                   \
   if (!done && p.mt == MT_ && p.nt == NT_ && p.wk == WK_) {                                       \
@@ -426,6 +561,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     if (!done) return -2;
   } else {
     if (N % p.bn != 0 || K % kBK != 0) return -1;
+    if (p.sk > 1 && (long)((M + p.bm - 1) / p.bm) * (N / p.bn) > kSplitCounters) return -1;
     bool done = false;
     const int st = p.mt > 0 ? p.mt : 2;   // tile plans reuse `mt` as the pipeline depth
 #define TL_CASE(BM_, BN_, WMW_, ST_)                                                            \
@@ -441,12 +577,13 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry) {
+  if (p.sk > 1 && !dry && !fixup_enabled()) {
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);
     if (grid > 4096) grid = 4096;
-    gemm_splitk_reduce_kernel<<<grid, 256, 0, stream>>>(ws, p.sk, M, N, epi, bias, out, ldo);
+    gemm_splitk_reduce_kernel<<<grid, 256, 0, stream>>>(splitk_part(ws), p.sk, M, N, epi, bias,
+                                                         out, ldo);
   }
   return 0;
 }
@@ -455,22 +592,33 @@ int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, 
                      int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                      size_t ws_bytes, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (p.sk > 1 && (ws == nullptr || ws_bytes < (size_t)p.sk * M * N * sizeof(float))) return -3;
+  if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
+    return -3;
   return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream);
+}
+
+// The plan for this call: the tuned/heuristic plan, or the heuristic one when a table entry
+// measured for another epilogue cannot run this one (e.g. odd skinny NT with SiLU).
+static GemmPlan select_plan(int M, int N, int K, int epi) {
+  GemmPlan p = plan_gemm(M, N, K);
+  if (run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true) != 0)
+    p = plan_gemm_heuristic(M, N, K);
+  return p;
 }
 
 int gemm_check(int M, int N, int K, int epi) {
   if (M <= 0) return 0;
-  return run_plan(plan_gemm(M, N, K), nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0,
-                  nullptr, nullptr, true);
+  return run_plan(select_plan(M, N, K, epi), nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr,
+                  0, nullptr, nullptr, true);
 }
 
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
                 hipStream_t stream) {
   if (M <= 0) return 0;
-  GemmPlan p = plan_gemm(M, N, K);
-  if (p.sk > 1 && (ws == nullptr || ws_bytes < (size_t)p.sk * M * N * sizeof(float))) p.sk = 1;
+  GemmPlan p = select_plan(M, N, K, epi);
+  if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
+    p.sk = 1;
   return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream);
 }
 

@@ -227,10 +227,16 @@ def test_gemm_tile_plans(bm, bn, wmw, epi):
         if st * (bm + bn) * 128 > 160 * 1024:
             continue
         for sk in (1, 3, 5):   # uneven K splits: 16 k-tiles over 3 / 5 workgroups (1..4 deep)
-            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-            ws = torch.empty(sk * M * N, dtype=torch.float32, device=DEV)
-            torch.ops.bfly.gemm_with_plan(x, w, out, [1, st, 0, wmw, bm, bn, sk], ops.EPILOGUES[epi], ws)
-            _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+            for fixup in (False, True) if sk > 1 else (False,):
+                torch.ops.bfly.gemm_set_splitk_fixup(fixup)
+                out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+                ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)  # [split counters | partials]
+                try:
+                    for _ in range(2):   # second call checks the counters were re-armed
+                        torch.ops.bfly.gemm_with_plan(x, w, out, [1, st, 0, wmw, bm, bn, sk], ops.EPILOGUES[epi], ws)
+                finally:
+                    torch.ops.bfly.gemm_set_splitk_fixup(False)
+                _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
 
 
 @pytest.mark.parametrize("mt,nt,wk", [(1, 1, 4), (1, 2, 1), (1, 4, 4), (2, 2, 2), (2, 4, 1), (4, 1, 4), (4, 2, 1), (4, 4, 4), (3, 2, 2)])
@@ -241,7 +247,13 @@ def test_gemm_skinny_plans(mt, nt, wk):
     for epi in ("none", "silu") if nt % 2 == 0 else ("none",):
         nout = N // 2 if epi == "silu" else N
         for sk in (1, 2):
-            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-            ws = torch.empty(sk * M * N, dtype=torch.float32, device=DEV)
-            torch.ops.bfly.gemm_with_plan(x, w, out, [0, mt, nt, wk, 0, 0, sk], ops.EPILOGUES[epi], ws)
-            _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+            for fixup in (False, True) if sk > 1 else (False,):
+                torch.ops.bfly.gemm_set_splitk_fixup(fixup)
+                out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+                ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)  # [split counters | partials]
+                try:
+                    for _ in range(2):
+                        torch.ops.bfly.gemm_with_plan(x, w, out, [0, mt, nt, wk, 0, 0, sk], ops.EPILOGUES[epi], ws)
+                finally:
+                    torch.ops.bfly.gemm_set_splitk_fixup(False)
+                _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)

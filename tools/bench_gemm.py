@@ -21,14 +21,37 @@ from butterfly_amd import ops  # noqa: E402
 SHAPES = {
     "tp1": [("qkv", 10240, 8192, "none"), ("o", 8192, 8192, "none"), ("gate_up", 57344, 8192, "silu"),
             ("down", 8192, 28672, "none"), ("lm_head", 129024, 8192, "none")],
+    "tp2": [("qkv", 5120, 8192, "none"), ("o", 8192, 4096, "none"), ("gate_up", 28672, 8192, "silu"),
+            ("down", 8192, 14336, "none")],
     "tp8": [("qkv", 1280, 8192, "none"), ("o", 8192, 1024, "none"), ("gate_up", 7168, 8192, "silu"),
             ("down", 8192, 3584, "none"), ("lm_head", 16128, 8192, "none")],
+    "tp4": [("qkv", 2560, 8192, "none"), ("o", 8192, 2048, "none"), ("gate_up", 14336, 8192, "silu"),
+            ("down", 8192, 7168, "none"), ("lm_head", 32256, 8192, "none")],
     "8b": [("qkv", 6144, 4096, "none"), ("o", 4096, 4096, "none"), ("gate_up", 28672, 4096, "silu"),
-           ("down", 4096, 14336, "none")],
+           ("down", 4096, 14336, "none"), ("lm_head", 128256, 4096, "none")],
+    "mixtral": [("lm_head", 32000, 4096, "none")],
 }
 
 
-def timeit(fn, iters=20):
+SERIAL = False
+LOG = None
+
+
+def timeit(fn, iters=20, tag=None):
+    if SERIAL:
+        # one call at a time (synchronised), so no two GEMMs overlap: per-dispatch durations
+        # come from the rocprofv3 kernel trace; the log line lets tools/gemm_trace_tune.py map
+        # dispatches (in order) back to candidates
+        n = 3 + iters
+        fn(0)                      # raises (before any launch) for an unsupported plan
+        torch.cuda.synchronize()
+        if LOG is not None and tag is not None:
+            LOG.write(json.dumps({"tag": tag, "calls": n}) + "\n")
+            LOG.flush()
+        for i in range(1, n):
+            fn(i)
+            torch.cuda.synchronize()
+        return float("nan")      # real durations come from the trace
     for _ in range(3):
         fn(0)
     torch.cuda.synchronize()
@@ -47,11 +70,15 @@ def main():
     ap.add_argument("--shapes", default="tp1,tp8")
     ap.add_argument("--sweep", action="store_true", help="also try alternative skinny plans")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--serial", default=None, help="serialised mode for rocprofv3: write the candidate log here")
     a = ap.parse_args()
+    global SERIAL, LOG
+    if a.serial:
+        SERIAL, LOG = True, open(a.serial, "w")
     assert ops.load_library()
     ms = [int(x) for x in a.ms.split(",")]
     results = []
-    ws = torch.empty(64 << 20, dtype=torch.float32, device="cuda")
+    ws = torch.zeros(64 << 20, dtype=torch.float32, device="cuda")  # head = split-K counters (kept zeroed)
     for group in a.shapes.split(","):
         for name, N, K, epi in SHAPES[group]:
             nbytes = N * K * 2
@@ -62,17 +89,22 @@ def main():
                 nout = N // 2 if epi == "silu" else N
                 out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
                 plan = ops.gemm_plan(M, N, K)
-                t = timeit(lambda i: ops.linear(x, Ws[i % copies], epilogue=epi, out=out))
+                auto = [0 if plan["kind"] == "skinny" else 1, plan["mt"], plan["nt"], plan["wk"], plan["bm"],
+                        plan["bn"], plan["splitk"]]
+                t = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, Ws[i % copies], out, auto, ops.EPILOGUES[epi], ws),
+                           tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": auto, "auto": True})
                 row = {"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": plan, "us": round(t, 2),
                        "TBps": round(nbytes / t / 1e6, 3), "TFLOPs": round(2 * M * N * K / t / 1e6, 1)}
-                tt = timeit(lambda i: torch.matmul(x, Ws[i % copies].t()))
-                row["torch_us"] = round(tt, 2)
+                if not SERIAL:
+                    tt = timeit(lambda i: torch.matmul(x, Ws[i % copies].t()))
+                    row["torch_us"] = round(tt, 2)
                 if a.sweep:
                     best = None
+                    top = []
                     mt = (M + 15) // 16
                     cands = []
                     for bm in (16, 32, 64, 128):
-                        if bm < M and bm != 128 or (bm == 128 and M <= 64):
+                        if (bm == 128 and M <= 64) or (M + bm - 1) // bm > 8:
                             continue
                         for bn, wmw in ((128, 1), (256, 1), (128, 2), (256, 2)):
                             if (bm, bn, wmw) not in ((16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1),
@@ -91,9 +123,11 @@ def main():
                     for pl in cands:
                         try:
                             tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(
-                                x, Ws[i % copies], out, pl, ops.EPILOGUES[epi], ws), iters=10)
+                                x, Ws[i % copies], out, pl, ops.EPILOGUES[epi], ws), iters=10,
+                                tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": pl})
                         except RuntimeError:
                             continue
+                        top.append((round(tv, 2), pl))
                         if best is None or tv < best[0]:
                             best = (tv, pl)
                     for nt in ((1, 2, 4) if M <= 64 else ()):
@@ -107,13 +141,15 @@ def main():
                                 pl = [0, mt, nt, wk, 0, 0, sk]
                                 try:
                                     tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(
-                                        x, Ws[i % copies], out, pl, ops.EPILOGUES[epi], ws), iters=10)
+                                        x, Ws[i % copies], out, pl, ops.EPILOGUES[epi], ws), iters=10,
+                                        tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": pl})
                                 except RuntimeError:
                                     continue
                                 if best is None or tv < best[0]:
                                     best = (tv, pl)
                     if best:
                         row["best_us"], row["best_plan"] = round(best[0], 2), best[1]
+                        row["top_tile"] = sorted(top)[:4]
                 results.append(row)
                 print(json.dumps(row), flush=True)
             del Ws
