@@ -292,6 +292,8 @@ class LLMEngine:
 
 
 def balanced_stages(num_layers: int, pp: int) -> list:
+    if not 1 <= pp <= num_layers:
+        raise ValueError(f"cannot split {num_layers} layers into {pp} pipeline stages")
     base, extra = divmod(num_layers, pp)
     out, a = [], 0
     for s in range(pp):

@@ -14,6 +14,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 
 from ..config import ModelConfig
+from ..models.ir import OpSpec, build_ir
 from .hw import MI355X, Hardware
 
 
@@ -29,6 +30,8 @@ class CostModel:
         self.cfg = cfg
         self.hw = hw
         self.oneshot = oneshot_allreduce
+        self._irs: dict = {}
+        self._cur_ep = 1
 
     # ---- primitives ------------------------------------------------------------------------
     def gemm(self, M: int, N: int, K: int) -> float:
@@ -49,67 +52,67 @@ class CostModel:
     def p2p(self, nbytes: float) -> float:
         return self.hw.p2p_latency_s + nbytes / self.hw.xgmi_link_bw
 
-    # ---- model pieces ------------------------------------------------------------------------
+    # ---- model pieces (priced from the model IR: models/ir.py) ---------------------------------
+    def _ir(self, tp: int, ep: int):
+        key = (tp, ep)
+        if key not in self._irs:
+            self._irs[key] = build_ir(self.cfg, tp, ep)
+        return self._irs[key]
+
     def layer_weight_bytes(self, tp: int, ep: int = 1) -> float:
-        c = self.cfg
-        h, D = c.hidden_size, c.head_dim
-        hkv_l = max(1, c.num_kv_heads // tp)
-        attn = (c.num_heads // tp + 2 * hkv_l) * D * h + (c.num_heads // tp) * D * h
-        mlp_cols = c.intermediate_size // (tp if ep == 1 else 1)
-        mlp = (3 if c.act == "silu" else 2) * h * mlp_cols
-        if c.is_moe:
-            mlp *= c.num_experts // ep
-            mlp += c.num_experts * h
-        return 2.0 * (attn + mlp)
+        return 2.0 * self._ir(tp, ep).layers[0].param_elems
+
+    def op_time(self, op: OpSpec, tokens: int, ctx: int, decode: bool, seqs: int, tp: int) -> float:
+        """Seconds for one IR op on one rank (collectives priced against xGMI)."""
+        hw, c = self.hw, self.cfg
+        if op.kind == "gemm":
+            return self.gemm(tokens * op.m_scale, op.n, op.k)
+        if op.kind == "attn":
+            D = c.head_dim
+            hq_l = c.num_heads // tp
+            hkv_l = max(1, c.num_kv_heads // tp)
+            if decode:
+                kv_bytes = 2.0 * tokens * ctx * hkv_l * D * 2
+                flops = 4.0 * tokens * ctx * hq_l * D
+                return max(kv_bytes / hw.hbm_bw_eff, flops / hw.bf16_flops_eff) + hw.kernel_overhead_s
+            L = tokens / max(seqs, 1)
+            flops = 2.0 * tokens * L * hq_l * D   # causal: half of 4*T*L*H*D
+            return flops / (0.6 * hw.bf16_flops_eff) + hw.kernel_overhead_s
+        if op.kind == "collective":
+            nbytes = 2.0 * tokens * op.width
+            if op.collective == "all_reduce":
+                return self.allreduce(nbytes, tp)
+            g = tp if op.group == "tp" else max(2, self._cur_ep)
+            return hw.collective_latency_s + (g - 1) * nbytes / hw.xgmi_link_bw
+        # memory-bound elementwise / norm / rope / routing ops
+        byts = op.act_bytes(tokens) + 2.0 * op.param_elems
+        return byts / hw.hbm_bw_eff + hw.kernel_overhead_s
 
     def layer_time(self, tokens: int, tp: int, ctx: int, decode: bool, seqs: int = 0,
                    ep: int = 1) -> LayerCost:
         """One transformer layer on `tokens` tokens (decode: one per sequence, each attending
         to `ctx` cached tokens; prefill: `seqs` causal sequences of tokens/seqs each)."""
-        c = self.cfg
-        h, D = c.hidden_size, c.head_dim
-        hq_l = c.num_heads // tp
-        hkv_l = max(1, c.num_kv_heads // tp)
-        t = 0.0
-        t += self.gemm(tokens, (hq_l + 2 * hkv_l) * D, h)                # QKV
-        t += self.gemm(tokens, h, hq_l * D)                               # O
-        if c.is_moe:
-            e_l = c.num_experts // ep
-            f = c.intermediate_size // (tp if ep == 1 else 1)
-            tt = tokens * ep
-            t += self.gemm(tt, 2 * f * e_l, h) + self.gemm(tt, h, f * e_l)
-        else:
-            f = c.intermediate_size // tp
-            n_up = 2 * f if c.act == "silu" else f
-            t += self.gemm(tokens, n_up, h) + self.gemm(tokens, h, f)
-        if decode:
-            kv_bytes = 2.0 * tokens * ctx * hkv_l * D * 2
-            flops = 4.0 * tokens * ctx * hq_l * D
-            t += max(kv_bytes / self.hw.hbm_bw_eff, flops / self.hw.bf16_flops_eff) + self.hw.kernel_overhead_s
-        else:
-            L = tokens / max(seqs, 1)
-            flops = 2.0 * tokens * L * hq_l * D   # causal: half of 4*T*L*H*D
-            t += flops / (0.6 * self.hw.bf16_flops_eff) + self.hw.kernel_overhead_s
-        t += 6 * self.hw.kernel_overhead_s                                 # norms, rope, act
-        ar_bytes = 2.0 * tokens * h
-        comm = 0.0
-        if tp > 1:
-            comm = 2 * self.allreduce(ar_bytes, tp)
-        if c.is_moe and ep > 1:
-            comm += 2 * (self.hw.collective_latency_s + (ep - 1) / ep * ar_bytes * ep / self.hw.xgmi_link_bw)
-        return LayerCost(t + comm, self.layer_weight_bytes(tp, ep), ar_bytes * 2 * (tp > 1))
+        self._cur_ep = ep
+        layer = self._ir(tp, ep).layers[0]
+        t = comm = 0.0
+        comm_bytes = 0.0
+        for op in layer.ops:
+            dt = self.op_time(op, tokens, ctx, decode, seqs, tp)
+            if op.kind == "collective":
+                comm += dt
+                comm_bytes += 2.0 * tokens * op.width
+            else:
+                t += dt
+        return LayerCost(t + comm, 2.0 * layer.param_elems, comm_bytes)
 
     def embed_head_time(self, tokens: int, logits_rows: int, tp: int) -> tuple[float, float]:
-        c = self.cfg
-        v_l = c.vocab_size / tp
-        first = 2.0 * tokens * c.hidden_size / self.hw.hbm_bw_eff + self.hw.kernel_overhead_s
-        if tp > 1:
-            first += self.allreduce(2.0 * tokens * c.hidden_size, tp)
-        last = self.gemm(logits_rows, int(v_l), c.hidden_size) + 3 * self.hw.kernel_overhead_s
+        ir = self._ir(tp, 1)
+        first = sum(self.op_time(o, tokens, 0, True, 1, tp) for o in ir.embed)
+        last = sum(self.op_time(o, logits_rows, 0, True, 1, tp) for o in ir.head) + 2 * self.hw.kernel_overhead_s
         return first, last
 
     def embed_head_bytes(self, tp: int) -> tuple[float, float]:
-        c = self.cfg
-        emb = 2.0 * c.vocab_size * c.hidden_size / tp
-        head = 0.0 if c.tie_embeddings else emb
+        ir = self._ir(tp, 1)
+        emb = 2.0 * sum(o.param_elems for o in ir.embed)
+        head = 2.0 * sum(o.param_elems for o in ir.head if o.kind == "gemm")
         return emb, head
