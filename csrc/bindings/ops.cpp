@@ -242,7 +242,8 @@ void gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Ten
 
 // Benchmark / tuning entry: run an explicit plan [kind, mt, nt, wk, bm, bn, sk].
 void gemm_with_plan(const Tensor& x, const Tensor& w, Tensor& out, std::vector<int64_t> plan,
-                    int64_t epilogue, const c10::optional<Tensor>& workspace) {
+                    int64_t epilogue, const c10::optional<Tensor>& workspace,
+                    const c10::optional<Tensor>& bias) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2 && plan.size() == 7, "gemm_with_plan: args");
   CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out);
@@ -258,9 +259,16 @@ void gemm_with_plan(const Tensor& x, const Tensor& w, Tensor& out, std::vector<i
     ws = reinterpret_cast<float*>(workspace->data_ptr());
     ws_bytes = workspace->numel() * workspace->element_size();
   }
+  const bfly::bf16* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(epilogue == bfly::EPI_BIAS && bias->numel() == N && bias->is_contiguous(), "gemm_with_plan: bias");
+    CHECK_BF16(*bias);
+    bp = bf(*bias);
+  }
+  TORCH_CHECK(epilogue != bfly::EPI_BIAS || bp != nullptr, "gemm_with_plan: bias epilogue needs a bias");
   c10::DeviceGuard g(x.device());
   const int rc = bfly::launch_gemm_plan(p, bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, epilogue,
-                                        nullptr, bf(out), out.stride(0), ws, ws_bytes, cur_stream());
+                                        bp, bf(out), out.stride(0), ws, ws_bytes, cur_stream());
   TORCH_CHECK(rc == 0, "gemm_with_plan: plan rejected (rc=", rc, ")");
 }
 
@@ -438,7 +446,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
         "Tensor(b!) out_scores, Tensor(c!) workspace) -> ()");
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
-  m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace) -> ()");
+  m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace, "
+        "Tensor? bias=None) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
   m.def("gemm_plan(int M, int N, int K) -> int[]", &gemm_plan);
   m.def("gemm_set_splitk_fixup(bool on) -> ()", [](bool on) { bfly::gemm_set_splitk_fixup(on); });

@@ -407,6 +407,160 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// Big-tile GEMM (prefill / large M): 256x256 tile, 8 waves (2 along M x 4 along N, each
+// owning a 128x64 output block = 8x4 MFMA 16x16x32 accumulators), BK = 32, 4-stage ring of
+// glds-staged K-tiles (4 x 32 KiB = 128 KiB LDS, one workgroup per CU). Per K-step a wave
+// issues 12 ds_read_b128 and 32 MFMAs (half the LDS bytes per MFMA of the 128x128 tile), waits
+// for its K-tile with a counted vmcnt (two K-tiles stay in flight across the raw barrier),
+// and runs the MFMA cluster at raised priority (cdna_hip_programming.md T3/T4 + setprio).
+// LDS rows are 64 B; slot = chunk ^ ((row >> 2) & 3) makes every 16-lane ds_read_b128 group
+// hit 16 distinct 16-B slots of the bank row (the DMA writes lane-linearly, so the swizzle is
+// applied on the per-lane SOURCE address). Tiles are walked in GROUP_M super-rows inside each
+// XCD's contiguous range, so the 32 CUs of an XCD share X and W panels in their L2.
+// ---------------------------------------------------------------------------------------
+constexpr int kBigThreads = 512;
+constexpr int kBigBK = 32;
+constexpr int kBigStages = 4;
+constexpr int kBigGroupM = 8;
+
+__device__ __forceinline__ void big_stage(const bf16* __restrict__ src, long ld, int row0,
+                                          int row_max, int k0, char* lds, int wid, int lane) {
+  // 256 rows x 32 bf16 = 16 KiB = 16 wave-instructions of 16 rows (4 lanes x 16 B per row)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = i * 8 + wid;
+    const int row = blk * 16 + (lane >> 2);
+    const int slot = lane & 3;
+    const int chunk = slot ^ ((row >> 2) & 3);
+    int gr = row0 + row;
+    gr = gr < row_max ? gr : row_max - 1;
+    const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 big_frag(const char* lds, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(lds + row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4));
+}
+
+__global__ void __launch_bounds__(kBigThreads)
+gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
+                int M, int N, int K, int epi, const bf16* __restrict__ bias,
+                bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+  constexpr int BM = 256, BN = 256, TI = 8, TJ = 4;
+  constexpr int A_BYTES = BM * kBigBK * 2, STAGE_BYTES = 2 * A_BYTES;
+  constexpr int LPW = 4;   // glds per wave per stage (2 for X, 2 for W)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int ntile_all = mtiles * ntiles;
+  const int t = xcd_remap(blockIdx.x, ntile_all);
+  // GROUP_M ordering: consecutive tiles walk GROUP_M row-tiles of one column, then the next
+  const int per_group = kBigGroupM * ntiles;
+  const int g = t / per_group, first_m = g * kBigGroupM;
+  const int gsize = min(mtiles - first_m, kBigGroupM);
+  const int tm = first_m + (t % per_group) % gsize;
+  const int tn = (t % per_group) / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int ktiles = K / kBigBK;
+  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
+  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Ping-pong schedule: the two wave groups (wm = 0 / 1, one wave of each per SIMD) run
+  // staggered by one barrier, so one group's MFMA cluster overlaps the other group's
+  // ds_read + glds phase. Barrier b splits group 0 as load(k) | 2k | mfma(k) | 2k+1 and
+  // group 1 as load(k) | 2k+1 | mfma(k) | 2k+2. Each load(k) waits (counted vmcnt) for
+  // stage k+1, reads stage k (waited one step earlier by BOTH groups, before a barrier the
+  // reader has passed), refills the buffer of stage k-1 (read by both groups before barriers
+  // they passed, lgkmcnt(0) retired) with stage k+3, and retires its ds_reads before the
+  // barrier that ends the phase.
+#pragma unroll
+  for (int s = 0; s < kBigStages - 1; ++s) {
+    if (kt0 + s < kt1) {
+      char* b = smem + s * STAGE_BYTES;
+      big_stage(X, ldx, m0, M, (kt0 + s) * kBigBK, b, wid, lane);
+      big_stage(W, ldw, n0, N, (kt0 + s) * kBigBK, b + A_BYTES, wid, lane);
+    }
+  }
+  {
+    const int issued = min(kBigStages - 1, kt1 - kt0);   // stages in flight; stage 0 must land
+    if (issued >= 3) vm_wait<2 * LPW>();
+    else if (issued == 2) vm_wait<LPW>();
+    else vm_wait<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+  int buf = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    // load phase
+    const char* As = smem + buf * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
+    bf16x8 bfr[TJ], af[TI];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) bfr[j] = big_frag(Bs, wn * 64 + 16 * j + (lane & 15), lane >> 4);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) af[i] = big_frag(As, wm * 128 + 16 * i + (lane & 15), lane >> 4);
+    if (kt + kBigStages - 1 < kt1) {
+      int nbuf = buf + kBigStages - 1;
+      if (nbuf >= kBigStages) nbuf -= kBigStages;
+      char* nb = smem + nbuf * STAGE_BYTES;
+      big_stage(X, ldx, m0, M, (kt + kBigStages - 1) * kBigBK, nb, wid, lane);
+      big_stage(W, ldw, n0, N, (kt + kBigStages - 1) * kBigBK, nb + A_BYTES, wid, lane);
+    }
+    // stage kt+1 must have landed; stages kt+2 / kt+3 (just issued) may still fly
+    if (kt + 3 < kt1) vm_wait<2 * LPW>();
+    else if (kt + 2 < kt1) vm_wait<LPW>();
+    else vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // MFMA phase
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    if (++buf == kBigStages) buf = 0;
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
+
+  // Epilogue: acc[i][j][r] = C[m0 + wm*128 + 16i + (lane>>4)*4 + r][n0 + wn*64 + 16j + (lane&15)]
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * 128 + 16 * i + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int n = n0 + wn * 64 + 16 * j + (lane & 15);
+        const float v = acc[i][j][r];
+        if (part) {
+          part[(long)blockIdx.y * M * N + (long)m * N + n] = v;
+        } else if (epi == EPI_SILU) {
+          if (j & 1) continue;
+          const float u = acc[i][j + 1][r];
+          const int f = (n0 + wn * 64) / 2 + 16 * (j / 2) + (lane & 15);
+          store_out(out, ldo, m, f, silu(v) * u);
+        } else {
+          store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Host dispatch
 // ---------------------------------------------------------------------------------------
 static int num_cus() { return 256; }
@@ -454,6 +608,24 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
       sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr);
 }
+
+static void run_big(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                    int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
+                    hipStream_t stream) {
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  const size_t lds = (size_t)kBigStages * 2 * 256 * kBigBK * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid(tiles, sk);
+  gemm_big_kernel<<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo,
+                                                      sk > 1 ? splitk_part(ws) : nullptr);
+}
+
+
 
 // Plan selection, from the tools/bench_gemm.py sweep on MI355X (Llama-3-70B TP1/TP8 shapes,
 // weights streamed from HBM): the LDS-tiled kernel with a small BM and split-K beats the
@@ -512,6 +684,17 @@ static GemmPlan plan_gemm_heuristic(int M, int N, int K) {
     p.sk = sk;
     return p;
   }
+  if (M > 256 && N % 256 == 0 && K % kBigBK == 0) {
+    // prefill / large batch: 256x256 ping-pong tile (~1.27 PF at M = 8192 on MI355X vs ~0.9 for
+    // the 128x128 tile); split K only when the tile grid cannot fill the 256 CUs
+    p.kind = 2;
+    p.bm = p.bn = 256;
+    const int tiles = ((M + 255) / 256) * (N / 256);
+    int sk = 1;
+    while (tiles * sk < 256 && K / kBigBK >= sk * 2 * 8 && sk < 8) sk *= 2;
+    p.sk = sk;
+    return p;
+  }
   p.kind = 1;
   p.mt = M >= 512 ? 2 : 3;   // tile plans: `mt` = pipeline depth (K-tiles in flight + 1)
   if (M <= 16) { p.bm = 16; p.wk = 1; }
@@ -542,7 +725,11 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                     hipStream_t stream, bool dry = false) {
-  if (p.kind == 0) {
+  if (p.kind == 2) {
+    if (N % 256 != 0 || K % kBigBK != 0) return -1;
+    if (p.sk > 1 && (long)((M + 255) / 256) * (N / 256) > kSplitCounters) return -1;
+    if (!dry) run_big(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+  } else if (p.kind == 0) {
     if (K % 128 != 0 || M > 16 * p.mt) return -1;
     if (N % (16 * p.nt * (4 / p.wk)) != 0) return -1;
     if (epi == EPI_SILU && p.nt % 2 != 0) return -1;
@@ -577,7 +764,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry && !fixup_enabled()) {
+  if (p.sk > 1 && !dry && (!fixup_enabled() || p.kind >= 2)) {   // big kernel: no fixup path
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);

@@ -16,6 +16,12 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _kernels_loaded():
+    # GPU tests must run the HIP kernels: fail loudly if the library is missing
+    assert ops.load_library(), "butterfly_amd/_C.so not built or failed to load"
+
+
 def _bf(*shape, scale=1.0, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(DEV)
@@ -210,6 +216,26 @@ def test_moe_route_and_gate_scale():
     ops.moe_gate_scale_(h, g, 2, 3)
     ref.moe_gate_scale(h2, g2, 2, 3)
     _close(h, h2, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(600, 512, 1024), (256, 768, 160), (77, 256, 96), (1000, 1280, 4096),
+                                   (300, 512, 64), (520, 512, 32)])
+@pytest.mark.parametrize("epi", ["none", "bias", "silu"])
+def test_gemm_big_tile(M, N, K, epi, kind=2):
+    """256x256 8-wave kernel (plan kind 2): ragged M, K-tile counts below / above the ring
+    depth, split-K, all epilogues, asymmetric operands."""
+    x = _bf(M, K, seed=60)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=61)
+    b = _bf(N, seed=62) if epi == "bias" else None
+    nout = N // 2 if epi == "silu" else N
+    want = ref.linear(x, w, b, "silu" if epi == "silu" else "none")
+    for sk in (1, 2, 3):
+        if K // 32 < sk:
+            continue
+        out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+        ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+        _close(out, want, 2e-2, 2e-2)
 
 
 TILE_CFGS = [(16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1), (64, 128, 1), (64, 128, 2),

@@ -104,7 +104,7 @@ def main():
                     mt = (M + 15) // 16
                     cands = []
                     for bm in (16, 32, 64, 128):
-                        if (bm == 128 and M <= 64) or (M + bm - 1) // bm > 8:
+                        if (bm == 128 and M <= 64) or ((M + bm - 1) // bm > 8 and bm != 128):
                             continue
                         for bn, wmw in ((128, 1), (256, 1), (128, 2), (256, 2)):
                             if (bm, bn, wmw) not in ((16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1),
@@ -113,13 +113,17 @@ def main():
                                 continue
                             if N % bn:
                                 continue
-                            for sk in (1, 2, 4, 8, 16):
+                            for sk in ((1, 2, 4, 8, 16) if M <= 256 else (1,)):
                                 if K // 64 < sk * 4:
                                     continue
                                 for st in (2, 3, 4):
                                     if st * (bm + bn) * 128 > 160 * 1024:
                                         continue
                                     cands.append([1, st, 0, wmw, bm, bn, sk])
+                    if M >= 128 and N % 256 == 0:
+                        for sk in (1, 2, 4):
+                            if K // 32 >= sk * 8:
+                                cands.append([2, 0, 0, 0, 256, 256, sk])
                     for pl in cands:
                         try:
                             tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(
