@@ -77,7 +77,9 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = True) -> P
     tinc, tlib = _torch_paths()
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{CSRC / 'include'}", "-Wno-unused-result",
               "-D__HIP_PLATFORM_AMD__=1"]
-    kflags = [HIPCC, f"--offload-arch={ARCH}", "-ffast-math", "-fno-gpu-rdc", *common]
+    # fast-math for contraction / reassociation, but infinities stay meaningful: the attention
+    # kernels use -inf as the empty-score sentinel
+    kflags = [HIPCC, f"--offload-arch={ARCH}", "-ffast-math", "-fno-finite-math-only", "-fno-gpu-rdc", *common]
     # Host-only C++ for the bindings: ROCm's clang (x86 __bf16 support, libstdc++ ABI).
     hostcxx = os.environ.get("BFLY_HOST_CXX", "/opt/rocm/lib/llvm/bin/clang++")
     bflags = [hostcxx, "-x", "c++", *common, "-I/opt/rocm/include", f"-I{tinc}", f"-I{tinc / 'torch/csrc/api/include'}",

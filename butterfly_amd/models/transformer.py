@@ -28,6 +28,7 @@ from typing import Callable, Optional
 import torch
 
 from .. import ops
+from ..utils import flags
 from ..config import ModelConfig
 from ..engine.batch import ForwardBatch
 from ..parallel.comm import Communicator
@@ -73,6 +74,10 @@ class TransformerLM:
         self.last = shard.is_last(cfg)
         self.tp = shard.tp_size
         self.ep = shard.ep_size
+        # fuse split-K GEMM reduces into the consuming norm / rope kernels (GPU, no TP
+        # all-reduce in between, RMSNorm models)
+        self.defer_reduce = (self.device.type == "cuda" and self.tp == 1 and cfg.norm == "rms"
+                             and flags.get("BFLY_DEFER_REDUCE"))
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
@@ -306,11 +311,14 @@ class TransformerLM:
                 x = self._norm(residual, self.p[pre + "in_w"], self.p.get(pre + "in_b"))
             else:
                 x = self._add_norm(delta, pre + "in", residual, partial)
-            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"))
+            # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
+            # when no all-reduce sits in between (tp == 1)
+            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"),
+                             defer=self.defer_reduce and c.pos_emb == "rope")
             kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
             slots = fb.slots if kc is not None else None
             if c.pos_emb == "rope":
-                ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
+                qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
             elif kc is not None:
                 k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
                 v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
@@ -323,7 +331,7 @@ class TransformerLM:
             else:
                 attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
             o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
-            o = ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b)
+            o = ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce)
             x = self._add_norm(o, pre + "post", residual, self.tp > 1)
             delta, partial = self._ffn(pre, x, fb)
         if not self.last:
@@ -336,7 +344,7 @@ class TransformerLM:
         r = residual if idx is None else residual.index_select(0, idx)
         if delta is not None:
             # all-reduce is linear: select the sampled rows first and reduce only those
-            dl = delta if idx is None else delta.index_select(0, idx)
+            dl = delta if idx is None else ops.materialize(delta).index_select(0, idx)
             if idx is None:
                 r = r.clone()
             x = self._add_norm(dl, "final", r, partial)
@@ -380,7 +388,7 @@ class TransformerLM:
             return out, self.tp > 1
         if c.act == "silu":
             hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu")
-            out = ops.linear(hmid, self.p[pre + "down_w"])
+            out = ops.linear(hmid, self.p[pre + "down_w"], defer=self.defer_reduce)
         else:
             hmid = ops.linear(x, self.p[pre + "fc_w"], bias=self.p.get(pre + "fc_b"))
             hmid = ops.gelu(hmid)

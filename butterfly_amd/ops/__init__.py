@@ -112,9 +112,39 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
 # ---------------------------------------------------------------------------------------
 # Ops
 # ---------------------------------------------------------------------------------------
+class Partial:
+    """Output of a split-K GEMM whose reduce was deferred to its consumer (`linear(...,
+    defer=True)`): `slabs` [sk, M, N] f32 live in the shared GEMM workspace and must be consumed
+    (rms_norm / rope_kv fuse the reduce) or `materialize()`d before the next GEMM runs.
+    `out` is the bf16 [M, N] buffer the result belongs in."""
+
+    __slots__ = ("slabs", "out")
+
+    def __init__(self, slabs: torch.Tensor, out: torch.Tensor):
+        self.slabs, self.out = slabs, out
+
+    @property
+    def shape(self):
+        return self.out.shape
+
+    def materialize(self) -> torch.Tensor:
+        torch.ops.bfly.splitk_reduce(self.slabs, self.out)
+        return self.out
+
+
+def materialize(x):
+    return x.materialize() if isinstance(x, Partial) else x
+
+
 def rms_norm(x, w, eps: float, out=None, residual=None):
     """y = x * rsqrt(mean(x^2) + eps) * w; with `residual`: residual += x first (in place)
-    and y is the norm of the updated residual (the fused add+norm of every block)."""
+    and y is the norm of the updated residual (the fused add+norm of every block). `x` may be
+    a deferred split-K GEMM output (`Partial`): its reduce is fused into this kernel."""
+    if isinstance(x, Partial):
+        if out is None:
+            out = torch.empty_like(x.out)
+        torch.ops.bfly.rms_norm_partial(x.slabs, w, eps, out, residual)
+        return out
     if not _gpu(x):
         return ref.rms_norm(x, w, eps, out, residual)
     if out is None:
@@ -134,7 +164,11 @@ def layer_norm(x, w, b, eps: float, out=None, residual=None):
 
 def rope_kv(qkv, positions, cos, sin, n_q: int, n_kv: int, slots=None, k_cache=None,
             v_cache=None):
-    """In-place RoPE on the Q/K heads of a fused QKV row; optional paged KV append."""
+    """In-place RoPE on the Q/K heads of a fused QKV row; optional paged KV append. Returns the
+    (bf16) QKV rows; `qkv` may be a deferred split-K GEMM output whose reduce is fused here."""
+    if isinstance(qkv, Partial):
+        torch.ops.bfly.rope_kv(qkv.out, positions, cos, sin, n_q, n_kv, slots, k_cache, v_cache, qkv.slabs)
+        return qkv.out
     if not _gpu(qkv):
         return ref.rope_kv(qkv, positions, cos, sin, n_q, n_kv, slots, k_cache, v_cache)
     torch.ops.bfly.rope_kv(qkv, positions, cos, sin, n_q, n_kv, slots, k_cache, v_cache)
@@ -166,6 +200,7 @@ def gelu(x, out=None):
 
 
 def add(a, b, out=None):
+    b = materialize(b)
     if not _gpu(a):
         return ref.add(a, b, out)
     if out is None:
@@ -197,11 +232,23 @@ def sample(logits, temps=None, seeds=None, vstart: int = 0, out_ids=None, out_sc
     return out_ids, out_scores
 
 
-def linear(x, w, bias=None, epilogue: str = "none", out=None):
+def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = False):
     """y = x @ w.T (+ bias) with optional fused SwiGLU epilogue ('silu': w rows gate/up
-    interleaved in 16-row groups, output width w.shape[0] // 2)."""
+    interleaved in 16-row groups, output width w.shape[0] // 2). `defer=True` (no bias /
+    epilogue): when the plan splits K, return a `Partial` whose reduce the consumer fuses."""
     if not _gpu(x):
         return ref.linear(x, w, bias, epilogue, out)
+    if defer and bias is None and epilogue == "none":
+        M, N = x.shape[0], w.shape[0]
+        if out is None:
+            out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        need = torch.ops.bfly.gemm_workspace_size(M, N, x.shape[1])
+        ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
+        sk = torch.ops.bfly.gemm_deferred(x, w, out, ws)
+        if sk == 1:
+            return out
+        off = torch.ops.bfly.gemm_slab_offset()
+        return Partial(ws[off:off + sk * M * N].view(sk, M, N), out)
     epi = EPILOGUES["bias"] if (bias is not None and epilogue == "none") else EPILOGUES[epilogue]
     if epilogue == "silu" and bias is not None:
         raise ValueError("bias + silu epilogue not supported")

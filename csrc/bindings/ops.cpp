@@ -70,7 +70,8 @@ void layer_norm(const Tensor& x, const Tensor& w, const Tensor& b, double eps, T
 
 void rope_kv(Tensor& qkv, const Tensor& positions, const Tensor& cos_t, const Tensor& sin_t,
              int64_t num_q_heads, int64_t num_kv_heads, const c10::optional<Tensor>& slots,
-             const c10::optional<Tensor>& k_cache, const c10::optional<Tensor>& v_cache) {
+             const c10::optional<Tensor>& k_cache, const c10::optional<Tensor>& v_cache,
+             const c10::optional<Tensor>& partial) {
   CHECK_GPU(qkv); CHECK_BF16(qkv);
   TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous(), "rope_kv: qkv must be 2-D contiguous");
   const int T = qkv.size(0);
@@ -103,10 +104,19 @@ void rope_kv(Tensor& qkv, const Tensor& positions, const Tensor& cos_t, const Te
     vc = bf(V);
     BS = K.size(2);
   }
+  const float* part = nullptr;
+  int sk = 0;
+  if (partial.has_value()) {
+    const Tensor& P = *partial;
+    TORCH_CHECK(P.scalar_type() == at::kFloat && P.dim() == 3 && P.is_contiguous() && P.size(1) == T &&
+                    P.size(2) == qkv.size(1), "rope_kv: partial slabs must be [sk, T, row] f32");
+    part = P.data_ptr<float>();
+    sk = P.size(0);
+  }
   c10::DeviceGuard g(qkv.device());
   bfly::launch_rope_kv(bf(qkv), T, num_q_heads, num_kv_heads, D, positions.data_ptr<int>(),
                        cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), sl, kc, vc, BS,
-                       cur_stream());
+                       cur_stream(), part, sk);
 }
 
 void kv_append(const Tensor& k, const Tensor& v, const Tensor& slots, Tensor& k_cache,
@@ -270,6 +280,55 @@ void gemm_with_plan(const Tensor& x, const Tensor& w, Tensor& out, std::vector<i
   const int rc = bfly::launch_gemm_plan(p, bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, epilogue,
                                         bp, bf(out), out.stride(0), ws, ws_bytes, cur_stream());
   TORCH_CHECK(rc == 0, "gemm_with_plan: plan rejected (rc=", rc, ")");
+}
+
+// GEMM whose split-K reduce is left to the consumer: returns the split count (slabs in the
+// workspace) or 1 (out written).
+int64_t gemm_deferred(const Tensor& x, const Tensor& w, Tensor& out, Tensor& workspace) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm_deferred: 2-D operands");
+  CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 128 == 0, "gemm_deferred: shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_deferred: row strides % 8");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.is_contiguous(), "gemm_deferred: out");
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_contiguous(), "gemm_deferred: workspace");
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_gemm_deferred(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, bf(out),
+                                            out.stride(0), workspace.data_ptr<float>(),
+                                            workspace.numel() * 4, cur_stream());
+  TORCH_CHECK(rc > 0, "gemm_deferred: unsupported shape M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
+  return rc;
+}
+
+void splitk_reduce(const Tensor& slabs, Tensor& out) {
+  CHECK_GPU(slabs);
+  TORCH_CHECK(slabs.scalar_type() == at::kFloat && slabs.dim() == 3 && slabs.is_contiguous(), "splitk_reduce: slabs [sk, M, N] f32");
+  CHECK_BF16(out);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == slabs.size(1) && out.size(1) == slabs.size(2) && out.is_contiguous(), "splitk_reduce: out");
+  c10::DeviceGuard g(out.device());
+  bfly::launch_splitk_reduce(slabs.data_ptr<float>(), slabs.size(0), slabs.size(1), slabs.size(2), bf(out),
+                             out.stride(0), cur_stream());
+}
+
+void rms_norm_partial(const Tensor& slabs, const Tensor& w, double eps, Tensor& out,
+                      const c10::optional<Tensor>& residual) {
+  CHECK_GPU(slabs);
+  TORCH_CHECK(slabs.scalar_type() == at::kFloat && slabs.dim() == 3 && slabs.is_contiguous(), "rms_norm_partial: slabs [sk, rows, dim]");
+  const int sk = slabs.size(0), rows = slabs.size(1), dim = slabs.size(2);
+  CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(dim % 8 == 0 && dim <= 16384 && w.numel() == dim, "rms_norm_partial: dim");
+  TORCH_CHECK(out.is_contiguous() && out.size(0) == rows && out.size(1) == dim, "rms_norm_partial: out");
+  bfly::bf16* res = nullptr;
+  if (residual.has_value()) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) == rows && residual->size(1) == dim, "rms_norm_partial: residual");
+    res = bf(*residual);
+  }
+  c10::DeviceGuard g(out.device());
+  bfly::launch_rmsnorm(nullptr, dim, res, bf(w), bf(out), dim, rows, dim, (float)eps, res != nullptr,
+                       cur_stream(), slabs.data_ptr<float>(), sk);
 }
 
 int64_t attn_decode_splits(int64_t max_ctx, int64_t part_tokens) {
@@ -436,7 +495,11 @@ TORCH_LIBRARY(bfly, m) {
   m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out, Tensor(b!)? residual) -> ()");
   m.def("layer_norm(Tensor x, Tensor w, Tensor b, float eps, Tensor(a!) out, Tensor(b!)? residual) -> ()");
   m.def("rope_kv(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, int num_q_heads, "
-        "int num_kv_heads, Tensor? slots, Tensor(b!)? k_cache, Tensor(c!)? v_cache) -> ()");
+        "int num_kv_heads, Tensor? slots, Tensor(b!)? k_cache, Tensor(c!)? v_cache, Tensor? partial=None) -> ()");
+  m.def("gemm_deferred(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) workspace) -> int");
+  m.def("splitk_reduce(Tensor slabs, Tensor(a!) out) -> ()");
+  m.def("rms_norm_partial(Tensor slabs, Tensor w, float eps, Tensor(a!) out, Tensor(b!)? residual) -> ()");
+  m.def("gemm_slab_offset() -> int", []() -> int64_t { return (int64_t)bfly::gemm_slab_offset_floats(); });
   m.def("kv_append(Tensor k, Tensor v, Tensor slots, Tensor(a!) k_cache, Tensor(b!) v_cache) -> ()");
   m.def("silu_mul(Tensor gu, Tensor(a!) out, int interleave) -> ()");
   m.def("gelu(Tensor x, Tensor(a!) out) -> ()");
@@ -487,6 +550,9 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("sample", &sample);
   m.impl("gemm", &gemm);
   m.impl("gemm_with_plan", &gemm_with_plan);
+  m.impl("gemm_deferred", &gemm_deferred);
+  m.impl("splitk_reduce", &splitk_reduce);
+  m.impl("rms_norm_partial", &rms_norm_partial);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("probe", &probe);

@@ -20,16 +20,21 @@ struct GemmPlan {
 };
 
 // norm.hip
+// `part` (optional): x is instead the sum of `sk` f32 split-K slabs [sk][rows][dim] of the
+// producing GEMM (its deferred reduce fused here)
 void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y,
                     long y_stride, int rows, int dim, float eps, bool add_residual,
-                    hipStream_t stream);
+                    hipStream_t stream, const float* part = nullptr, int sk = 0);
 void launch_layernorm(const bf16* x, bf16* residual, const bf16* w, const bf16* b, bf16* y,
                       int rows, int dim, float eps, bool add_residual, hipStream_t stream);
 
 // rope.hip
+// `part` (optional): the QKV row is the sum of `sk` f32 split-K slabs [sk][T][row] of the
+// GEMM (deferred reduce fused here); the bf16 row is written to `qkv` as well
 void launch_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* positions,
                     const float* cos_t, const float* sin_t, const int* slots, bf16* k_cache,
-                    bf16* v_cache, int block_size, hipStream_t stream);
+                    bf16* v_cache, int block_size, hipStream_t stream,
+                    const float* part = nullptr, int sk = 0);
 void launch_kv_append(const bf16* k, long k_stride, const bf16* v, long v_stride,
                       const int* slots, bf16* k_cache, bf16* v_cache, int T, int Hkv, int D,
                       int block_size, hipStream_t stream);
@@ -57,6 +62,14 @@ int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, 
                      int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                      size_t ws_bytes, hipStream_t stream);
 int gemm_check(int M, int N, int K, int epi);
+// Y = X W^T without epilogue; when the plan splits K, the f32 slabs are left in the workspace
+// (at gemm_slab_offset_floats(), layout [sk][M][N]) for the consumer kernel to reduce, and the
+// split count is returned; otherwise `out` is written and 1 is returned. < 0: error.
+int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                         bf16* out, long ldo, float* ws, size_t ws_bytes, hipStream_t stream);
+size_t gemm_slab_offset_floats();
+void launch_splitk_reduce(const float* part, int sk, int M, int N, bf16* out, long ldo,
+                          hipStream_t stream);
 void gemm_set_splitk_fixup(bool on);   // in-kernel split-K reduction (default: env / off)   // 0 if the auto plan can run this shape
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,

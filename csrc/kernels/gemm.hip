@@ -724,7 +724,7 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 // `dry`: validate only (the plan is supported for this shape/epilogue) without launching.
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
-                    hipStream_t stream, bool dry = false) {
+                    hipStream_t stream, bool dry = false, bool defer = false) {
   if (p.kind == 2) {
     if (N % 256 != 0 || K % kBigBK != 0) return -1;
     if (p.sk > 1 && (long)((M + 255) / 256) * (N / 256) > kSplitCounters) return -1;
@@ -764,7 +764,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry && (!fixup_enabled() || p.kind >= 2)) {   // big kernel: no fixup path
+  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind >= 2)) {   // big kernel: no fixup path
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);
@@ -797,6 +797,29 @@ int gemm_check(int M, int N, int K, int epi) {
   if (M <= 0) return 0;
   return run_plan(select_plan(M, N, K, epi), nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr,
                   0, nullptr, nullptr, true);
+}
+
+int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                         bf16* out, long ldo, float* ws, size_t ws_bytes, hipStream_t stream) {
+  if (M <= 0) return 1;
+  GemmPlan p = select_plan(M, N, K, EPI_NONE);
+  if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
+    p.sk = 1;
+  const bool defer = p.sk > 1 && !(fixup_enabled() && p.kind < 2);
+  const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, out, ldo, ws, stream,
+                          false, defer);
+  if (rc != 0) return rc;
+  return defer ? p.sk : 1;
+}
+
+size_t gemm_slab_offset_floats() { return kCounterBytes / sizeof(float); }
+
+void launch_splitk_reduce(const float* part, int sk, int M, int N, bf16* out, long ldo,
+                          hipStream_t stream) {
+  long total = (long)M * N;
+  int grid = (int)((total + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  gemm_splitk_reduce_kernel<<<grid, 256, 0, stream>>>(part, sk, M, N, EPI_NONE, nullptr, out, ldo);
 }
 
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,

@@ -64,6 +64,71 @@ rmsnorm_kernel(const bf16* __restrict__ x, long x_stride, bf16* __restrict__ res
   }
 }
 
+// Add + RMSNorm whose input is the f32 split-K slabs [sk][rows][dim] of the producing GEMM
+// (its deferred reduce fused here). 1024 threads per row and every slab load of a thread
+// issued before the adds: at decode the rows are few (the batch), so each workgroup must keep
+// many loads in flight to stream its sk x dim x 4 bytes.
+constexpr int kNormPartThreads = 1024;
+
+template <int NV>
+__global__ void __launch_bounds__(kNormPartThreads)
+rmsnorm_partial_kernel(const float* __restrict__ part, int sk, long slab, bf16* __restrict__ residual,
+                       const bf16* __restrict__ w, bf16* __restrict__ y, int dim, float eps,
+                       int add_residual) {
+  __shared__ float red[16];
+  const long row = blockIdx.x;
+  const int nvec = dim >> 3;
+  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + row * (long)dim);
+  float v[NV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * kNormPartThreads;
+    if (c < nvec) {
+      const float* pr = part + row * (long)dim + c * 8;
+      f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+#pragma unroll 8
+      for (int k = 1; k < sk; ++k) {
+        lo += *reinterpret_cast<const f32x4*>(pr + k * slab);
+        hi += *reinterpret_cast<const f32x4*>(pr + k * slab + 4);
+      }
+      bf16x8 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { a[j] = f2bf(lo[j]); a[j + 4] = f2bf(hi[j]); }
+      if (add_residual) {
+        const bf16x8 r = rr[c];
+        bf16x8 sm;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sm[j] = f2bf(bf2f(a[j]) + bf2f(r[j]));
+          v[i][j] = bf2f(sm[j]);
+        }
+        rr[c] = sm;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(a[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)dim + eps);
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + row * (long)dim);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * kNormPartThreads;
+    if (c < nvec) {
+      const bf16x8 g = wr[c];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
+      yr[c] = o;
+    }
+  }
+}
+
 template <int NV>
 __global__ void __launch_bounds__(kNormThreads)
 layernorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ residual,
@@ -128,7 +193,18 @@ layernorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ residual,
 
 void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y,
                     long y_stride, int rows, int dim, float eps, bool add_residual,
-                    hipStream_t stream) {
+                    hipStream_t stream, const float* part, int sk) {
+  if (part != nullptr) {
+    if (rows <= 0) return;
+    const long slab = (long)rows * dim;
+    const int nv = (dim / 8 + kNormPartThreads - 1) / kNormPartThreads;
+    const int ar = add_residual ? 1 : 0;
+    if (nv <= 1)
+      rmsnorm_partial_kernel<1><<<rows, kNormPartThreads, 0, stream>>>(part, sk, slab, residual, w, y, dim, eps, ar);
+    else
+      rmsnorm_partial_kernel<2><<<rows, kNormPartThreads, 0, stream>>>(part, sk, slab, residual, w, y, dim, eps, ar);
+    return;
+  }
   if (rows <= 0) return;
   const int nvec = dim / 8;
   const int nv = (nvec + kNormThreads - 1) / kNormThreads;

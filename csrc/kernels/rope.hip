@@ -15,29 +15,52 @@ namespace bfly {
 
 constexpr int kRopeThreads = 256;
 
+// Grid (T, ceil(items / 256)): item i < Hrot*LPH rotates 8 pairs of one Q/K head, the rest copy
+// 8 elements of one V head (so a token's work spreads over several workgroups: at decode T is
+// only the batch size). With `part` the row is first assembled from the f32 split-K slabs of
+// the QKV GEMM (its deferred reduce fused here) and written back to `qkv` in bf16.
+template <int D>
+__device__ __forceinline__ bf16x8 rope_load(const bf16* __restrict__ row, const float* __restrict__ prow,
+                                            int sk, long slab, int col) {
+  if (!prow) return *reinterpret_cast<const bf16x8*>(row + col);
+  f32x4 lo = *reinterpret_cast<const f32x4*>(prow + col), hi = *reinterpret_cast<const f32x4*>(prow + col + 4);
+  for (int k = 1; k < sk; ++k) {
+    lo += *reinterpret_cast<const f32x4*>(prow + k * slab + col);
+    hi += *reinterpret_cast<const f32x4*>(prow + k * slab + col + 4);
+  }
+  bf16x8 a;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { a[j] = f2bf(lo[j]); a[j + 4] = f2bf(hi[j]); }
+  return a;
+}
+
 template <int D>
 __global__ void __launch_bounds__(kRopeThreads)
 rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
                const float* __restrict__ cos_t, const float* __restrict__ sin_t,
                const int* __restrict__ slots, bf16* __restrict__ k_cache,
-               bf16* __restrict__ v_cache, int Hq, int Hkv, int BS) {
+               bf16* __restrict__ v_cache, int Hq, int Hkv, int BS,
+               const float* __restrict__ part, int sk, long slab) {
   constexpr int H2 = D / 2;        // rotation pairs per head
   constexpr int LPH = H2 / 8;      // lanes per head (each lane: 8 pairs)
+  constexpr int LPV = D / 8;
   const int t = blockIdx.x;
+  const int i = blockIdx.y * kRopeThreads + threadIdx.x;
+  const int nrot = (Hq + Hkv) * LPH, nv = Hkv * LPV;
+  if (i >= nrot + nv) return;
   const long row_stride = (long)(Hq + 2 * Hkv) * D;
   bf16* row = qkv + (long)t * row_stride;
-  const int pos = positions[t];
-  const float* cr = cos_t + (long)pos * H2;
-  const float* sr = sin_t + (long)pos * H2;
+  const float* prow = part ? part + (long)t * row_stride : nullptr;
   const int slot = slots ? slots[t] : -1;
   const int blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
-  const int nrot = (Hq + Hkv) * LPH;
-  for (int i = threadIdx.x; i < nrot; i += kRopeThreads) {
+  if (i < nrot) {
+    const int pos = positions[t];
+    const float* cr = cos_t + (long)pos * H2;
+    const float* sr = sin_t + (long)pos * H2;
     const int h = i / LPH, p0 = (i % LPH) * 8;
-    bf16* hp = row + (long)h * D;
-    bf16x8 a = *reinterpret_cast<const bf16x8*>(hp + p0);
-    bf16x8 b = *reinterpret_cast<const bf16x8*>(hp + p0 + H2);
+    const bf16x8 a = rope_load<D>(row, prow, sk, slab, h * D + p0);
+    const bf16x8 b = rope_load<D>(row, prow, sk, slab, h * D + p0 + H2);
     const f32x4 c0 = *reinterpret_cast<const f32x4*>(cr + p0);
     const f32x4 c1 = *reinterpret_cast<const f32x4*>(cr + p0 + 4);
     const f32x4 s0 = *reinterpret_cast<const f32x4*>(sr + p0);
@@ -51,6 +74,7 @@ rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
       oa[j] = f2bf(x0 * c - x1 * s);
       ob[j] = f2bf(x1 * c + x0 * s);
     }
+    bf16* hp = row + (long)h * D;
     *reinterpret_cast<bf16x8*>(hp + p0) = oa;
     *reinterpret_cast<bf16x8*>(hp + p0 + H2) = ob;
     if (h >= Hq && slot >= 0 && k_cache) {
@@ -59,18 +83,18 @@ rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
       *reinterpret_cast<bf16x8*>(kp + p0) = oa;
       *reinterpret_cast<bf16x8*>(kp + p0 + H2) = ob;
     }
+    return;
   }
+  // V heads: (materialise and) copy into the transposed cache page (8 scattered 2-B stores)
+  const int iv = i - nrot;
+  const int kh = iv / LPV, d0 = (iv % LPV) * 8;
+  const int col = (Hq + Hkv + kh) * D + d0;
+  const bf16x8 v = rope_load<D>(row, prow, sk, slab, col);
+  if (prow) *reinterpret_cast<bf16x8*>(row + col) = v;
   if (slot < 0 || !v_cache) return;
-  // V heads: copy into the transposed cache page (8 scattered 2-B stores per lane).
-  constexpr int LPV = D / 8;
-  const int nv = Hkv * LPV;
-  for (int i = threadIdx.x; i < nv; i += kRopeThreads) {
-    const int kh = i / LPV, d0 = (i % LPV) * 8;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + (long)(Hq + Hkv + kh) * D + d0);
-    bf16* vp = v_cache + ((long)blk * Hkv + kh) * D * BS + off;
+  bf16* vp = v_cache + ((long)blk * Hkv + kh) * D * BS + off;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vp[(long)(d0 + j) * BS] = v[j];
-  }
+  for (int j = 0; j < 8; ++j) vp[(long)(d0 + j) * BS] = v[j];
 }
 
 // Standalone paged-cache append for already-rotated K and V ([T, Hkv, D] each, any row
@@ -98,14 +122,17 @@ kv_append_kernel(const bf16* __restrict__ k, long k_stride, const bf16* __restri
 
 void launch_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* positions,
                     const float* cos_t, const float* sin_t, const int* slots, bf16* k_cache,
-                    bf16* v_cache, int block_size, hipStream_t stream) {
+                    bf16* v_cache, int block_size, hipStream_t stream, const float* part, int sk) {
   if (T <= 0) return;
+  const long slab = (long)T * (Hq + 2 * Hkv) * D;
+  const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+  const dim3 grid(T, (items + kRopeThreads - 1) / kRopeThreads);
   if (D == 128) {
-    rope_kv_kernel<128><<<T, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots,
-                                                       k_cache, v_cache, Hq, Hkv, block_size);
+    rope_kv_kernel<128><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, k_cache,
+                                                          v_cache, Hq, Hkv, block_size, part, sk, slab);
   } else if (D == 64) {
-    rope_kv_kernel<64><<<T, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots,
-                                                      k_cache, v_cache, Hq, Hkv, block_size);
+    rope_kv_kernel<64><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, k_cache,
+                                                         v_cache, Hq, Hkv, block_size, part, sk, slab);
   }
 }
 

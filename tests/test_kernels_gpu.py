@@ -283,3 +283,42 @@ def test_gemm_skinny_plans(mt, nt, wk):
                 finally:
                     torch.ops.bfly.gemm_set_splitk_fixup(False)
                 _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 8192, 8192), (7, 1280, 8192), (64, 10240, 8192)])
+def test_gemm_deferred_reduce_fusions(M, N, K):
+    """A split-K GEMM left unreduced (Partial) must give the same result through every fused
+    consumer as the plain GEMM followed by the unfused op."""
+    x = _bf(M, K, seed=70)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=71)
+    full = ops.linear(x, w)
+    p = ops.linear(x, w, defer=True)
+    if not isinstance(p, ops.Partial):
+        pytest.skip("plan does not split K for this shape")
+    got = ops.linear(x, w, defer=True).materialize()
+    torch.testing.assert_close(got, full, atol=0, rtol=0)
+    # (fused consumers may sum the slabs in another association order under -ffast-math:
+    # equal up to one bf16 rounding step)
+    # add + rmsnorm with the reduce fused in
+    if N == 8192:
+        wn = _bf(N, seed=72)
+        r0 = _bf(M, N, seed=73)
+        ra, rb = r0.clone(), r0.clone()
+        ya = ops.rms_norm(full, wn, 1e-5, residual=ra)
+        yb = ops.rms_norm(ops.linear(x, w, defer=True), wn, 1e-5, residual=rb)
+        torch.testing.assert_close(rb, ra, atol=1e-2, rtol=1e-2)
+        torch.testing.assert_close(yb, ya, atol=2e-2, rtol=2e-2)
+    # rope + KV append with the reduce fused in
+    if N == 10240:
+        hq, hkv, D, BS = 64, 8, 128, 32
+        cos, sin = ref.rope_tables(D, 4096, 500000.0)
+        cos, sin = cos.to(DEV), sin.to(DEV)
+        pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+        slots = torch.randperm(8 * BS, device=DEV)[:M].to(torch.int32)
+        kc = [torch.zeros(8, hkv, BS, D, dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+        vc = [torch.zeros(8, hkv, D, BS, dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+        qa = ops.rope_kv(full.clone(), pos, cos, sin, hq, hkv, slots, kc[0], vc[0])
+        qb = ops.rope_kv(ops.linear(x, w, defer=True), pos, cos, sin, hq, hkv, slots, kc[1], vc[1])
+        torch.testing.assert_close(qb, qa, atol=2e-2, rtol=2e-2)
+        torch.testing.assert_close(kc[1], kc[0], atol=2e-2, rtol=2e-2)
+        torch.testing.assert_close(vc[1], vc[0], atol=2e-2, rtol=2e-2)
