@@ -760,6 +760,9 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     TL_ST(16, 128, 1) TL_ST(16, 256, 1) TL_ST(32, 128, 1) TL_ST(32, 256, 1)
     TL_ST(64, 128, 1) TL_ST(64, 128, 2) TL_ST(64, 256, 1) TL_ST(64, 256, 2)
     TL_ST(128, 128, 2) TL_ST(128, 256, 2)
+    // CU-balanced decode tiles: N/224 or N/160 tiles x split-K land on exactly 256 workgroups
+    // for the Llama-3-70B projections (gate/up 57344 = 256 x 224, QKV 10240 = 64 x 160)
+    TL_ST(64, 224, 4) TL_ST(64, 160, 4)
 #undef TL_ST
 #undef TL_CASE
     if (!done) return -2;

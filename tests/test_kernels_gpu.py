@@ -239,13 +239,13 @@ def test_gemm_big_tile(M, N, K, epi, kind=2):
 
 
 TILE_CFGS = [(16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1), (64, 128, 1), (64, 128, 2),
-             (64, 256, 1), (64, 256, 2), (128, 128, 2), (128, 256, 2)]
+             (64, 256, 1), (64, 256, 2), (128, 128, 2), (128, 256, 2), (64, 224, 4), (64, 160, 4)]
 
 
 @pytest.mark.parametrize("bm,bn,wmw", TILE_CFGS)
 @pytest.mark.parametrize("epi", ["none", "silu"])
 def test_gemm_tile_plans(bm, bn, wmw, epi):
-    M, N, K = min(bm, 40) if bm < 128 else 200, 512, 1024
+    M, N, K = min(bm, 40) if bm < 128 else 200, 512 if bn in (128, 256) else 3 * bn, 1024
     x = _bf(M, K, seed=40)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=41)
     nout = N // 2 if epi == "silu" else N

@@ -106,10 +106,10 @@ def main():
                     for bm in (16, 32, 64, 128):
                         if (bm == 128 and M <= 64) or ((M + bm - 1) // bm > 8 and bm != 128):
                             continue
-                        for bn, wmw in ((128, 1), (256, 1), (128, 2), (256, 2)):
+                        for bn, wmw in ((128, 1), (256, 1), (128, 2), (256, 2), (224, 4), (160, 4)):
                             if (bm, bn, wmw) not in ((16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1),
                                                      (64, 128, 1), (64, 128, 2), (64, 256, 1), (64, 256, 2),
-                                                     (128, 128, 2), (128, 256, 2)):
+                                                     (128, 128, 2), (128, 256, 2), (64, 224, 4), (64, 160, 4)):
                                 continue
                             if N % bn:
                                 continue
