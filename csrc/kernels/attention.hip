@@ -13,12 +13,12 @@
 //   operand is then one 16-B load.
 //   Split-K over the context (flash-decoding) with an f32 partial combine kernel.
 //
-// Prefill (attn_prefill_kernel): causal varlen flash attention. Workgroup = 128 query rows
-// of one head (4 waves x 32 rows), KV tiles of 64 keys register-staged into a double-buffered,
-// XOR-swizzled LDS image (cdna_hip_programming.md T10 image (b)): K is read by ds_read_b128
-// as the 32x32x16 A operand of S^T = K . Q^T, V by ds_read_b64_tr_b16 as the A operand of
-// O^T = V^T . P^T; the S^T accumulator is converted in registers into the P^T B operand
-// (§3 "An accumulator tile as the next MFMA's operand").
+// Prefill (attn_prefill_kernel): causal varlen flash attention. Workgroup = 256 query rows
+// of one head (8 waves x 32 rows, 2 waves per SIMD), KV tiles of 64 keys staged by LDS-DMA
+// into a 3-deep ring of XOR-swizzled LDS images (cdna_hip_programming.md T10 image (b)): K is
+// read by ds_read_b128 as the 32x32x16 A operand of S^T = K . Q^T, V by ds_read_b64_tr_b16 as
+// the A operand of O^T = V^T . P^T; the S^T accumulator is converted in registers into the
+// P^T B operand (§3 "An accumulator tile as the next MFMA's operand").
 #include "bfly_common.h"
 #include "bfly_kernels.h"
 
@@ -235,24 +235,58 @@ attn_decode_combine_kernel(const float* __restrict__ part_o, const float* __rest
 // ---------------------------------------------------------------------------------------
 // Prefill
 // ---------------------------------------------------------------------------------------
-constexpr int kPfBQ = 128, kPfBKV = 64;
+constexpr int kPfBQ = 256, kPfBKV = 64, kPfWaves = 8, kPfStages = 3;
+constexpr int kPfThreads = kPfWaves * 64;
 
 // Byte offset of 16-B chunk `ch` (0..15) of row `row` in a [rows][128 x bf16] LDS image
 // (T10 image (b): conflict-free for 32x32x16 row reads and for the transposed reads).
-__device__ __forceinline__ int pf_off(int row, int ch) {
-  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+__device__ __forceinline__ int pf_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int pf_off(int row, int ch) { return row * 256 + 16 * (ch ^ pf_swz(row)); }
+
+typedef __attribute__((address_space(3))) void* pf_lds_t;
+typedef __attribute__((address_space(1))) void* pf_gbl_t;
+
+template <int N>
+__device__ __forceinline__ void pf_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Stage one 64-key K/V tile (2 x 16 KiB) by LDS-DMA: each wave-instruction writes 4 rows
+// (1 KiB) lane-linearly; the XOR image is produced by swizzling the per-lane SOURCE chunk.
+__device__ __forceinline__ void pf_stage(const bf16* __restrict__ k, long k_stride,
+                                         const bf16* __restrict__ v, long v_stride, int s0, int L,
+                                         int kh, int t, char* kb, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = i * kPfWaves + wid;          // 16 pieces of 4 rows
+    const int row = piece * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ pf_swz(row);
+    int key = t * kPfBKV + row;
+    key = key < L ? key : L - 1;
+    const long ko = (long)(s0 + key);
+    __builtin_amdgcn_global_load_lds((pf_gbl_t)(k + ko * k_stride + (long)kh * 128 + ch * 8),
+                                     (pf_lds_t)(kb + piece * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((pf_gbl_t)(v + ko * v_stride + (long)kh * 128 + ch * 8),
+                                     (pf_lds_t)(kb + kPfBKV * 256 + piece * 1024), 16, 0, 0);
+  }
+}
+
+// Causal varlen flash attention. Workgroup = 256 query rows of one head (8 waves x 32 rows,
+// two waves per SIMD so one wave's softmax overlaps the other's MFMAs); 64-key K/V tiles in a
+// 3-deep LDS-DMA ring (counted vmcnt, one raw barrier per tile). Per wave: S^T = K Q^T on
+// 32x32x16 MFMAs (the lane owns one query column: row max/sum are lane-local plus one swap),
+// P^T built in registers from the accumulator, O^T += V^T P^T with V fed by transposed LDS
+// reads (ds_read_b64_tr_b16).
 template <int D>
-__global__ void __launch_bounds__(kAttnThreads)
+__global__ void __launch_bounds__(kPfThreads)
 attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
                     long k_stride, const bf16* __restrict__ v, long v_stride,
                     const int* __restrict__ cu_seqlens, int Hq, int Hkv, float scale_log2,
                     int causal, bf16* __restrict__ out, long o_stride) {
   static_assert(D == 128, "prefill kernel is specialised for D=128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TILE_BYTES = kPfBKV * D * 2;  // 16 KiB
-  // smem = [K0 | V0 | K1 | V1]
+  constexpr int STAGE_BYTES = 2 * kPfBKV * D * 2;  // K | V, 32 KiB
+  constexpr int LPW = 4;                            // glds per wave per stage
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int seq = blockIdx.y, h = blockIdx.z;
   const int s0 = cu_seqlens[seq];
@@ -281,61 +315,49 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   const int ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
   const int wave_qmax = q0 + 32 * wid + 31;
 
-  // Register staging: 64 rows x 16 chunks = 1024 chunks per tile; 4 per thread per operand.
-  bf16x8 rk[4], rv[4];
-  auto load_tile = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cl = i * kAttnThreads + threadIdx.x;
-      const int row = cl >> 4, ch = cl & 15;
-      int key = t * kPfBKV + row;
-      key = key < L ? key : L - 1;
-      rk[i] = *reinterpret_cast<const bf16x8*>(k + (long)(s0 + key) * k_stride + (long)kh * D + ch * 8);
-      rv[i] = *reinterpret_cast<const bf16x8*>(v + (long)(s0 + key) * v_stride + (long)kh * D + ch * 8);
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* kb = smem + buf * 2 * TILE_BYTES;
-    char* vb = kb + TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cl = i * kAttnThreads + threadIdx.x;
-      const int row = cl >> 4, ch = cl & 15;
-      *reinterpret_cast<bf16x8*>(kb + pf_off(row, ch)) = rk[i];
-      *reinterpret_cast<bf16x8*>(vb + pf_off(row, ch)) = rv[i];
-    }
-  };
-
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
+  for (int st = 0; st < kPfStages - 1; ++st)
+    if (st < ntiles) pf_stage(k, k_stride, v, v_stride, s0, L, kh, st, smem + st * STAGE_BYTES, wid, lane);
+  int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) load_tile(t + 1);
+    if (t + 1 < ntiles) pf_vm_wait<LPW>();   // tile t landed; tile t+1 may still fly
+    else pf_vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + kPfStages - 1 < ntiles) {
+      int nb = buf + kPfStages - 1;
+      if (nb >= kPfStages) nb -= kPfStages;
+      pf_stage(k, k_stride, v, v_stride, s0, L, kh, t + kPfStages - 1, smem + nb * STAGE_BYTES, wid, lane);
+    }
     const int kv0 = t * kPfBKV;
-    const char* kb = smem + (t & 1) * 2 * TILE_BYTES;
-    const char* vb = kb + TILE_BYTES;
+    const char* kb = smem + buf * STAGE_BYTES;
+    const char* vb = kb + kPfBKV * 256;
     if (!(causal && kv0 > wave_qmax)) {
       // S^T tiles: st[kt][r] = S[key = kv0 + 32kt + (r&3) + 8(r>>2) + 4hi][query c]
-      f32x16 st[2];
+      f32x16 sc[2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        st[kt] = f32x16{};
+        sc[kt] = f32x16{};
         const int row = 32 * kt + c;
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + pf_off(row, 2 * ks + hi));
-          st[kt] = mfma32(kf, qf[ks], st[kt]);
+          sc[kt] = mfma32(kf, qf[ks], sc[kt]);
         }
       }
+      const bool full = !causal || kv0 + kPfBKV - 1 <= q0 + 32 * wid;   // no masking needed
       float tmax = kNegInf;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int key = kv0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          const bool ok = key < L && (!causal || key <= qrow);
-          const float xv = ok ? st[kt][r] * scale_log2 : kNegInf;
-          st[kt][r] = xv;
+          float xv = sc[kt][r] * scale_log2;
+          if (!full || kv0 + kPfBKV > L) {
+            const int key = kv0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            const bool ok = key < L && (!causal || key <= qrow);
+            xv = ok ? xv : kNegInf;
+          }
+          sc[kt][r] = xv;
           tmax = fmaxf(tmax, xv);
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
@@ -351,7 +373,7 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
         for (int s = 0; s < 2; ++s)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float pv = exp2f(st[kt][8 * s + j] - mb);
+            const float pv = exp2f(sc[kt][8 * s + j] - mb);
             ps += pv;
             pb[kt][s][j] = f2bf(pv);
           }
@@ -381,8 +403,7 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
           }
       }
     }
-    if (t + 1 < ntiles) store_tile((t + 1) & 1);
-    __syncthreads();
+    if (++buf == kPfStages) buf = 0;
   }
   lsum += __shfl_xor(lsum, 32, 64);
   if (qrow >= L) return;
@@ -451,8 +472,14 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid((max_seqlen + kPfBQ - 1) / kPfBQ, nseq, Hq);
-  const size_t lds = 4 * kPfBKV * D * 2;  // 64 KiB: K,V x 2 buffers
-  attn_prefill_kernel<128><<<grid, kAttnThreads, lds, stream>>>(
+  const size_t lds = (size_t)kPfStages * 2 * kPfBKV * D * 2;  // 96 KiB: 3 x (K | V)
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_kernel<128>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  attn_prefill_kernel<128><<<grid, kPfThreads, lds, stream>>>(
       q, q_stride, k, k_stride, v, v_stride, cu_seqlens, Hq, Hkv, scale_log2, causal ? 1 : 0,
       out, o_stride);
   return 0;

@@ -14,8 +14,32 @@ from butterfly_amd import ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="64:1024:64:8,64:1024:8:1,256:1024:64:8,1:8192:64:8,16:4096:64:8")
+    ap.add_argument("--prefill", default="16:1024:64:8,4:4096:64:8,1:16384:64:8",
+                    help="prefill cases seqs:len:Hq:Hkv ('' to skip)")
     a = ap.parse_args()
     ops.load_library()
+    for case in filter(None, a.prefill.split(",")):
+        n, Ls, Hq, Hkv = map(int, case.split(":"))
+        D, T = 128, n * Ls
+        q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16)
+        k = torch.randn(T, Hkv, D, device="cuda", dtype=torch.bfloat16)
+        v = torch.randn(T, Hkv, D, device="cuda", dtype=torch.bfloat16)
+        cu = torch.arange(0, T + 1, Ls, dtype=torch.int32, device="cuda")
+        out = torch.empty_like(q)
+        f = lambda: ops.attn_prefill(q, k, v, cu, Ls, 0.088, True, out=out)  # noqa: E731
+        for _ in range(2):
+            f()
+        torch.cuda.synchronize()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        it = 5
+        st.record()
+        for _ in range(it):
+            f()
+        en.record()
+        torch.cuda.synchronize()
+        us = st.elapsed_time(en) / it * 1e3
+        flops = 4.0 * n * Ls * Ls / 2 * Hq * D          # causal useful FLOPs
+        print(json.dumps({"prefill": case, "us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}), flush=True)
     for case in a.cases.split(","):
         B, ctx, Hq, Hkv = map(int, case.split(":"))
         D, BS = 128, 32
