@@ -367,9 +367,11 @@ class TransformerLM:
         the caller fuses with the next residual add + norm."""
         c, d = self.cfg, self.dims
         if c.is_moe:
-            gates, _, _ = ops.moe_route(x, self.p[pre + "router_w"], c.experts_per_token)
-            xs, gs = x, gates
+            gates, topk_ids, topk_w = ops.moe_route(x, self.p[pre + "router_w"], c.experts_per_token)
             T = x.shape[0]
+            # prefill: token-routed sparse experts (K12/K13: only routed rows are computed);
+            # decode: dense fixed-shape path (weight-streaming bound either way, graph friendly)
+            sparse = fb.is_prefill and self.device.type == "cuda" and flags.get("BFLY_MOE_SPARSE")
             if self.ep > 1:
                 # DP-attention + expert-parallel FFN: every EP rank contributes Tp rows (zero
                 # padded), each computes its local experts on all ranks' tokens, and the
@@ -378,11 +380,22 @@ class TransformerLM:
                 if Tp > T:
                     x = torch.cat([x, x.new_zeros(Tp - T, x.shape[1])])
                     gates = torch.cat([gates, gates.new_zeros(Tp - T, gates.shape[1])])
+                    topk_ids = torch.cat([topk_ids, topk_ids.new_full((Tp - T, topk_ids.shape[1]), -1)])
+                    topk_w = torch.cat([topk_w, topk_w.new_zeros(Tp - T, topk_w.shape[1])])
                 xs = self.comm.all_gather(x, "ep")
-                gs = self.comm.all_gather(gates, "ep")
-            hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
-            ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
-            out = ops.linear(hmid, self.p[pre + "moe_down_w"])
+                if sparse:
+                    ids_s, w_s = self.comm.all_gather(topk_ids, "ep"), self.comm.all_gather(topk_w, "ep")
+                else:
+                    gs = self.comm.all_gather(gates, "ep")
+            else:
+                xs, gs, ids_s, w_s = x, gates, topk_ids, topk_w
+            if sparse:
+                out = ops.moe_sparse_ffn(xs, ids_s, w_s, self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"],
+                                         d.expert0, d.experts, d.ffn)
+            else:
+                hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
+                ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
+                out = ops.linear(hmid, self.p[pre + "moe_down_w"])
             if self.ep > 1:
                 return self.comm.reduce_scatter(out, "ep")[:T], False
             return out, self.tp > 1

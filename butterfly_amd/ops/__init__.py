@@ -326,6 +326,33 @@ def moe_route(x, wr, top_k: int, gates=None, topk_ids=None, topk_w=None):
     return gates, topk_ids, topk_w
 
 
+def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, ffn: int):
+    """Routed expert FFN: permute the (token, k) pairs of the local experts into per-expert
+    row slots (moe_align), grouped gate/up GEMM with fused SiLU over gathered token rows,
+    grouped down GEMM, weighted combine back to token order. Only routed rows are computed
+    (the dense path computes every local expert for every token)."""
+    if not _gpu(x):
+        return ref.moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0, num_local, ffn)
+    T, H = x.shape
+    k = topk_ids.shape[1]
+    TK = T * k
+    L = torch.ops.bfly
+    dev = x.device
+    rows = _arena.get(dev, "moe_rows", TK, torch.int32)[:TK]
+    slot_of = _arena.get(dev, "moe_slot", TK, torch.int32)[:TK]
+    nt = L.moe_max_tiles(TK, num_local)
+    tiles = _arena.get(dev, "moe_tiles", nt * 4, torch.int32)[:nt * 4].view(nt, 4)
+    count = _arena.get(dev, "moe_count", 1, torch.int32)[:1]
+    L.moe_align(topk_ids, e0, num_local, rows, slot_of, tiles, count)
+    hmid = torch.empty(TK, ffn, dtype=x.dtype, device=dev)
+    L.moe_grouped_gemm(x, gu_w, hmid, rows, tiles, count, 2 * ffn * H, 2 * ffn, H, num_local, EPILOGUES["silu"])
+    y = torch.empty(TK, H, dtype=x.dtype, device=dev)
+    L.moe_grouped_gemm(hmid, down_w, y, None, tiles, count, ffn, H, ffn, num_local, EPILOGUES["none"])
+    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    L.moe_combine(y, slot_of, topk_w, out)
+    return out
+
+
 def moe_gate_scale_(h, gates, e0: int, num_local: int):
     if not _gpu(h):
         return ref.moe_gate_scale(h, gates, e0, num_local)

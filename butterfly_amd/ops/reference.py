@@ -300,3 +300,22 @@ def moe_gate_scale(h, gates, e0, num_local):
     v = h.float().view(T, num_local, F) * g.unsqueeze(-1)
     h.copy_(v.view(T, num_local * F).to(h.dtype))
     return h
+
+
+def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, ffn: int):
+    """Token-routed expert FFN over the local experts (SwiGLU, gate/up interleaved rows):
+    out[t] = sum_j w[t, j] * down_e(silu(g_e x_t) * u_e x_t) for j with local e = ids[t, j]."""
+    T, H = x.shape
+    out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
+    ids = topk_ids.long() - e0
+    for el in range(num_local):
+        hit = (ids == el)
+        tok = hit.any(-1).nonzero().flatten()
+        if tok.numel() == 0:
+            continue
+        w_e = (topk_w * hit).sum(-1)[tok]
+        gu = gu_w[el * 2 * ffn:(el + 1) * 2 * ffn]
+        h = linear(x[tok], gu, epilogue="silu")
+        y = linear(h, down_w[:, el * ffn:(el + 1) * ffn].contiguous())
+        out[tok] += w_e.unsqueeze(-1).float() * y.float()
+    return out.to(x.dtype)

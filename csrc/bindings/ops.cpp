@@ -407,6 +407,65 @@ void moe_route(const Tensor& x, const Tensor& wr, int64_t top_k, Tensor& gates, 
   TORCH_CHECK(rc == 0, "moe_route: unsupported (E <= 64, k <= 8, H % 8 == 0)");
 }
 
+int64_t moe_max_tiles(int64_t TK, int64_t El) { return bfly::moe_max_tiles(TK, El, bfly::kMoeGroupBM); }
+
+void moe_align(const Tensor& topk_ids, int64_t e0, int64_t num_local, Tensor& rows, Tensor& slot_of,
+               Tensor& tiles, Tensor& count) {
+  CHECK_GPU(topk_ids); CHECK_I32(topk_ids); CHECK_I32(rows); CHECK_I32(slot_of); CHECK_I32(tiles); CHECK_I32(count);
+  TORCH_CHECK(topk_ids.dim() == 2 && topk_ids.is_contiguous(), "moe_align: topk_ids [T, k]");
+  const int T = topk_ids.size(0), K = topk_ids.size(1);
+  TORCH_CHECK(num_local > 0 && num_local <= 64, "moe_align: 1..64 local experts");
+  TORCH_CHECK(rows.numel() >= (long)T * K && slot_of.numel() == (long)T * K, "moe_align: rows / slot_of size");
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 4 && tiles.is_contiguous() &&
+                  tiles.size(0) >= bfly::moe_max_tiles(T * K, num_local, bfly::kMoeGroupBM), "moe_align: tiles [max_tiles, 4]");
+  TORCH_CHECK(count.numel() == 1, "moe_align: count");
+  c10::DeviceGuard g(topk_ids.device());
+  const int rc = bfly::launch_moe_align(topk_ids.data_ptr<int>(), T, K, e0, num_local, bfly::kMoeGroupBM,
+                                        rows.data_ptr<int>(), slot_of.data_ptr<int>(),
+                                        reinterpret_cast<int4*>(tiles.data_ptr<int>()), count.data_ptr<int>(), cur_stream());
+  TORCH_CHECK(rc == 0, "moe_align: rejected (", rc, ")");
+}
+
+void moe_grouped_gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& rows,
+                      const Tensor& tiles, const Tensor& count, int64_t w_estride, int64_t n, int64_t k,
+                      int64_t num_experts, int64_t epilogue) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_I32(tiles); CHECK_I32(count);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) >= k, "moe_grouped_gemm: x");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0, "moe_grouped_gemm: w");
+  TORCH_CHECK(n % 128 == 0 && k % 64 == 0, "moe_grouped_gemm: N % 128, K % 64");
+  TORCH_CHECK(epilogue == bfly::EPI_NONE || epilogue == bfly::EPI_SILU, "moe_grouped_gemm: epilogue");
+  const long ldw = w.stride(0);
+  const long last = (num_experts - 1) * w_estride + (n - 1) * ldw + k;
+  TORCH_CHECK(num_experts > 0 && last <= w.numel(), "moe_grouped_gemm: expert slices exceed w");
+  const int nout = epilogue == bfly::EPI_SILU ? n / 2 : n;
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(1) == nout, "moe_grouped_gemm: out");
+  const int* rp = nullptr;
+  if (rows.has_value()) {
+    CHECK_I32(*rows);
+    rp = rows->data_ptr<int>();
+  } else {
+    TORCH_CHECK(x.size(0) >= out.size(0), "moe_grouped_gemm: slot rows");
+  }
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 4, "moe_grouped_gemm: tiles");
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_gemm_grouped(bf(x), x.stride(0), bf(w), ldw, w_estride, n, k, epilogue, rp,
+                                           reinterpret_cast<const int4*>(tiles.data_ptr<int>()), count.data_ptr<int>(),
+                                           tiles.size(0), bf(out), out.stride(0), cur_stream());
+  TORCH_CHECK(rc == 0, "moe_grouped_gemm: rejected (", rc, ")");
+}
+
+void moe_combine(const Tensor& y, const Tensor& slot_of, const Tensor& topk_w, Tensor& out) {
+  CHECK_GPU(y); CHECK_BF16(y); CHECK_I32(slot_of); CHECK_BF16(out);
+  TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.dim() == 2 && topk_w.is_contiguous(), "moe_combine: topk_w");
+  const int T = topk_w.size(0), K = topk_w.size(1), H = out.size(1);
+  TORCH_CHECK(slot_of.numel() == (long)T * K && out.size(0) == T && out.is_contiguous() && y.is_contiguous() &&
+                  y.size(1) == H, "moe_combine: shapes");
+  c10::DeviceGuard g(y.device());
+  const int rc = bfly::launch_moe_combine(bf(y), slot_of.data_ptr<int>(), topk_w.data_ptr<float>(), T, K, H, bf(out),
+                                          cur_stream());
+  TORCH_CHECK(rc == 0, "moe_combine: H % 8");
+}
+
 void moe_gate_scale(Tensor& h, const Tensor& gates, int64_t e0, int64_t num_local) {
   CHECK_GPU(h); CHECK_BF16(h);
   TORCH_CHECK(h.dim() == 2 && h.is_contiguous(), "moe_gate_scale: h");
@@ -523,6 +582,12 @@ TORCH_LIBRARY(bfly, m) {
         "Tensor(c!)? part_ml) -> ()");
   m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
+  m.def("moe_max_tiles(int tk, int num_local) -> int", &moe_max_tiles);
+  m.def("moe_align(Tensor topk_ids, int e0, int num_local, Tensor(a!) rows, Tensor(b!) slot_of, Tensor(c!) tiles, "
+        "Tensor(d!) count) -> ()");
+  m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? rows, Tensor tiles, Tensor count, int w_estride, "
+        "int n, int k, int num_experts, int epilogue) -> ()");
+  m.def("moe_combine(Tensor y, Tensor slot_of, Tensor topk_w, Tensor(a!) out) -> ()");
   m.def("probe(int which, Tensor(a!) out) -> ()");
   m.def("car_alloc(int bytes) -> int", &car_alloc);
   m.def("car_free(int ptr) -> ()", &car_free);
@@ -559,4 +624,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("custom_all_reduce", &custom_all_reduce);
   m.impl("moe_route", &moe_route);
   m.impl("moe_gate_scale", &moe_gate_scale);
+  m.impl("moe_align", &moe_align);
+  m.impl("moe_grouped_gemm", &moe_grouped_gemm);
+  m.impl("moe_combine", &moe_combine);
 }

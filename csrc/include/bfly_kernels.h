@@ -109,6 +109,17 @@ int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H,
 void launch_moe_gate_scale(bf16* h, const float* gates, long T, int E, int e0, int El, int F,
                            hipStream_t stream);
 
+// sparse MoE (moe.hip + gemm.hip grouped tiles)
+int moe_max_tiles(int TK, int El, int BM);
+int launch_moe_align(const int* topk_ids, int T, int K, int e0, int El, int BM, int* rows,
+                     int* slot_of, int4* tiles, int* count, hipStream_t stream);
+int launch_moe_combine(const bf16* y, const int* slot_of, const float* w, int T, int K, int H,
+                       bf16* out, hipStream_t stream);
+constexpr int kMoeGroupBM = 64;
+int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w_estride, int N,
+                        int K, int epi, const int* rows, const int4* tiles, const int* count,
+                        int max_tiles, bf16* out, long ldo, hipStream_t stream);
+
 // probe.hip
 void launch_probe(int which, float* out, hipStream_t stream);
 

@@ -271,9 +271,10 @@ constexpr int kBK = 64;
 template <int ROWS>
 constexpr int stage_loads() { return (ROWS / 8 + 3) / 4; }
 
-template <int ROWS>
+template <int ROWS, bool GATHER = false>
 __device__ __forceinline__ void tile_stage(const bf16* __restrict__ src, long ld, int row0,
-                                           int row_max, int k0, char* lds, int wid, int lane) {
+                                           int row_max, int k0, char* lds, int wid, int lane,
+                                           const int* __restrict__ rows = nullptr) {
   // ROWS x 64 bf16 = ROWS x 8 chunks of 16 B; one wave-instruction writes 8 rows (1 KiB).
   constexpr int kBlocks = ROWS / 8;
   constexpr int kInstr = stage_loads<ROWS>();
@@ -286,6 +287,9 @@ __device__ __forceinline__ void tile_stage(const bf16* __restrict__ src, long ld
     const int chunk = slot ^ ((row >> 1) & 7);
     int gr = row0 + row;
     gr = gr < row_max ? gr : row_max - 1;
+    if constexpr (GATHER) {
+      if (rows) gr = rows[gr];   // grouped GEMM: row slot -> source token
+    }
     const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
     __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 0);
   }
@@ -306,12 +310,19 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int chunk) 
 // landed) and a raw s_barrier (a __syncthreads() would drain every in-flight DMA:
 // cdna_hip_programming.md §5 "Pipelining across barriers"); the buffer refilled in an
 // iteration is the one every wave finished reading in the previous iteration (WAR safe).
-template <int BM, int BN, int WMW, int STAGES>
+//
+// GROUPED (MoE expert GEMM, K13): blockIdx.x indexes a device-built tile list
+// gtiles[i] = {expert, first row slot, end row slot} (count in *gcount; excess workgroups
+// exit), blockIdx.z the N tile; the expert selects W + expert * w_estride and A rows are
+// gathered through grows[slot] (nullptr: slots are rows). Output rows are row slots.
+template <int BM, int BN, int WMW, int STAGES, bool GROUPED = false>
 __global__ void __launch_bounds__(kTileThreads)
 gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
                  bf16* __restrict__ out, long ldo, float* __restrict__ part,
-                 int* __restrict__ counters) {
+                 int* __restrict__ counters, const int* __restrict__ grows = nullptr,
+                 const int4* __restrict__ gtiles = nullptr, const int* __restrict__ gcount = nullptr,
+                 long w_estride = 0) {
   constexpr int WNW = 4 / WMW;                // waves along M x waves along N
   constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
@@ -322,10 +333,22 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
-  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-  const int tile = xcd_remap(blockIdx.x, mtiles * ntiles);
-  const int tn = tile / mtiles, tm = tile % mtiles;  // consecutive tiles share a W panel
-  const int m0 = tm * BM, n0 = tn * BN;
+  int tile, m0, n0;
+  if constexpr (GROUPED) {
+    if ((int)blockIdx.x >= *gcount) return;
+    const int4 info = gtiles[blockIdx.x];
+    W += (long)info.x * w_estride;
+    m0 = info.y;
+    M = info.z;                     // rows [m0, M) of the permuted slot space
+    n0 = blockIdx.z * BN;
+    tile = 0;
+  } else {
+    const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+    tile = xcd_remap(blockIdx.x, mtiles * ntiles);
+    const int tn = tile / mtiles, tm = tile % mtiles;  // consecutive tiles share a W panel
+    m0 = tm * BM;
+    n0 = tn * BN;
+  }
 
   const int ktiles = K / kBK;
   const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
@@ -341,7 +364,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   for (int s = 0; s < STAGES - 1; ++s) {
     if (kt0 + s < kt1) {
       char* b = smem + s * STAGE_BYTES;
-      tile_stage<BM>(X, ldx, m0, M, (kt0 + s) * kBK, b, wid, lane);
+      tile_stage<BM, GROUPED>(X, ldx, m0, M, (kt0 + s) * kBK, b, wid, lane, grows);
       tile_stage<BN>(W, ldw, n0, N, (kt0 + s) * kBK, b + A_BYTES, wid, lane);
     }
   }
@@ -358,7 +381,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
       int nbuf = buf + STAGES - 1;
       if (nbuf >= STAGES) nbuf -= STAGES;
       char* nb = smem + nbuf * STAGE_BYTES;
-      tile_stage<BM>(X, ldx, m0, M, (kt + STAGES - 1) * kBK, nb, wid, lane);
+      tile_stage<BM, GROUPED>(X, ldx, m0, M, (kt + STAGES - 1) * kBK, nb, wid, lane, grows);
       tile_stage<BN>(W, ldw, n0, N, (kt + STAGES - 1) * kBK, nb + A_BYTES, wid, lane);
     }
     const char* As = smem + buf * STAGE_BYTES;
@@ -794,6 +817,28 @@ static GemmPlan select_plan(int M, int N, int K, int epi) {
   if (run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true) != 0)
     p = plan_gemm_heuristic(M, N, K);
   return p;
+}
+
+// Grouped expert GEMM (MoE): fixed 64x128 tile, 3-stage pipeline; grid = (max tiles, 1,
+// N / 128) with the device tile list deciding which workgroups run.
+constexpr int kGroupBM = 64;
+int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w_estride, int N,
+                        int K, int epi, const int* rows, const int4* tiles, const int* count,
+                        int max_tiles, bf16* out, long ldo, hipStream_t stream) {
+  if (N % 128 != 0 || K % kBK != 0 || max_tiles <= 0) return -1;
+  if (epi != EPI_NONE && epi != EPI_SILU) return -1;
+  constexpr int BM = kGroupBM, BN = 128, WMW = 2, ST = 3;
+  const size_t lds = (size_t)ST * (BM + BN) * kBK * 2;
+  static bool attr_set = false;
+  if (!attr_set && lds > 65536) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW, ST, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid(max_tiles, 1, N / BN);
+  gemm_tile_kernel<BM, BN, WMW, ST, true><<<grid, kTileThreads, lds, stream>>>(
+      X, ldx, W, ldw, 0, N, K, epi, nullptr, out, ldo, nullptr, nullptr, rows, tiles, count, w_estride);
+  return 0;
 }
 
 int gemm_check(int M, int N, int K, int epi) {

@@ -9,6 +9,15 @@
 // moe_gate_scale: h[t, e*F + f] *= gates[t, e0 + e] for the local experts: the gate weight is
 // folded into the intermediate activation so that ONE GEMM over the concatenated local experts
 // (K = E_local * F) both applies every expert's down projection and sums over experts.
+//
+// Sparse path (K12 permute / K13 grouped GEMM / weighted combine), used for prefill where the
+// dense path would spend E/top_k times the FLOPs:
+//   moe_align:   counting sort of the (token, k) pairs routed to local experts into per-expert
+//                contiguous row slots; emits rows[slot] = token, slot_of[pair] (-1: not local)
+//                and the grouped-GEMM tile list {expert, first slot, end slot} (+ its count),
+//                all on the device so the whole layer is graph-capturable with fixed grids.
+//   (grouped gate/up GEMM with SiLU, grouped down GEMM: gemm.hip GROUPED tile kernel)
+//   moe_combine: out[t] = sum_j w[t, j] * Y[slot_of[t, j]] (f32, fixed j order).
 #include "bfly_common.h"
 #include "bfly_kernels.h"
 
@@ -79,6 +88,79 @@ __global__ void moe_gate_scale_kernel(bf16* __restrict__ h, const float* __restr
     for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) * g);
     reinterpret_cast<bf16x8*>(h)[i] = v;
   }
+}
+
+__global__ void __launch_bounds__(1024)
+moe_align_kernel(const int* __restrict__ topk_ids, int TK, int K, int e0, int El, int BM,
+                 int* __restrict__ rows, int* __restrict__ slot_of, int4* __restrict__ tiles,
+                 int* __restrict__ count) {
+  __shared__ int cnt[kMaxExperts], cur[kMaxExperts];
+  for (int e = threadIdx.x; e < El; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < TK; i += blockDim.x) {
+    const int e = topk_ids[i] - e0;
+    if (e >= 0 && e < El) atomicAdd(&cnt[e], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int off = 0, nt = 0;
+    for (int e = 0; e < El; ++e) {
+      cur[e] = off;
+      for (int r = off; r < off + cnt[e]; r += BM) tiles[nt++] = int4{e, r, min(r + BM, off + cnt[e]), 0};
+      off += cnt[e];
+    }
+    *count = nt;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TK; i += blockDim.x) {
+    const int e = topk_ids[i] - e0;
+    if (e >= 0 && e < El) {
+      const int pos = atomicAdd(&cur[e], 1);
+      rows[pos] = i / K;
+      slot_of[i] = pos;
+    } else {
+      slot_of[i] = -1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+moe_combine_kernel(const bf16* __restrict__ y, const int* __restrict__ slot_of,
+                   const float* __restrict__ w, int K, int H, bf16* __restrict__ out) {
+  const long t = blockIdx.x;
+  for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < K; ++j) {
+      const int sl = slot_of[t * K + j];
+      if (sl < 0) continue;
+      const float g = w[t * K + j];
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(y + (long)sl * H + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += g * bf2f(v[q]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
+    *reinterpret_cast<bf16x8*>(out + t * H + c) = o;
+  }
+}
+
+int moe_max_tiles(int TK, int El, int BM) { return (TK + BM - 1) / BM + El; }
+
+int launch_moe_align(const int* topk_ids, int T, int K, int e0, int El, int BM, int* rows,
+                     int* slot_of, int4* tiles, int* count, hipStream_t stream) {
+  if (El <= 0 || El > kMaxExperts || BM <= 0) return -1;
+  if (T <= 0) return 0;
+  moe_align_kernel<<<1, 1024, 0, stream>>>(topk_ids, T * K, K, e0, El, BM, rows, slot_of, tiles, count);
+  return 0;
+}
+
+int launch_moe_combine(const bf16* y, const int* slot_of, const float* w, int T, int K, int H,
+                       bf16* out, hipStream_t stream) {
+  if (H % 8 != 0) return -1;
+  if (T <= 0) return 0;
+  moe_combine_kernel<<<T, 256, 0, stream>>>(y, slot_of, w, K, H, out);
+  return 0;
 }
 
 int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H, int E, int K,
