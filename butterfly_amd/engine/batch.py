@@ -22,6 +22,7 @@ class ForwardBatch:
     max_ctx: int = 0                             # static upper bound of ctx_lens
     logits_idx: Optional[torch.Tensor] = None    # int64 [R] rows that need logits (None = all)
     ep_tokens: int = 0                           # EP: token rows every rank pads to (0 = no pad)
+    ep_alltoall: bool = False                    # EP: this step dispatches tokens by all-to-all
 
     @property
     def num_tokens(self) -> int:
@@ -37,7 +38,8 @@ class ForwardBatch:
         mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
         return ForwardBatch(mv(self.input_ids), mv(self.positions), mv(self.slots), self.is_prefill,
                             mv(self.cu_seqlens), self.max_seqlen, mv(self.block_tables),
-                            mv(self.ctx_lens), self.max_ctx, mv(self.logits_idx), self.ep_tokens)
+                            mv(self.ctx_lens), self.max_ctx, mv(self.logits_idx), self.ep_tokens,
+                            self.ep_alltoall)
 
 
 def make_prefill_batch(prompts: list[list[int]], slots: list[list[int]], device="cpu",

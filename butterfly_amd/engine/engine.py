@@ -183,7 +183,9 @@ class LLMEngine:
             if not anyw:
                 return StepOutput("idle", [], [], [], 0.0)
             if plan.kind == 0:
-                self._run_stages(lambda h: self.runner.run(empty_batch(self.device, ep_pad), h), 0, 0, [])
+                eb = empty_batch(self.device, ep_pad)
+                eb.ep_alltoall = any_prefill
+                self._run_stages(lambda h: self.runner.run(eb, h), 0, 0, [])
                 return StepOutput("ep-idle", [], [], [], time.perf_counter() - t0)
         elif plan.kind == 0:
             return StepOutput("idle", [], [], [], 0.0)
@@ -193,6 +195,7 @@ class LLMEngine:
         if plan.kind == 1:
             fb = self.runner.prefill_batch(plan, lambda r: self.requests[r].tokens)
             fb.ep_tokens = ep_pad
+            fb.ep_alltoall = self.mesh.ep > 1
             tokens = self._run_stages(lambda h: self.runner.run(fb, h), fb.num_tokens, len(rids), rids)
             kind = "prefill"
         else:
@@ -202,7 +205,8 @@ class LLMEngine:
                 tokens = self._pipeline_decode(inp, rids)
             else:
                 tokens = self._run_stages(
-                    lambda h: self.runner.run_decode(inp, h, ep_tokens=ep_pad, graphs_ok=not any_prefill),
+                    lambda h: self.runner.run_decode(inp, h, ep_tokens=ep_pad, graphs_ok=not any_prefill,
+                                                     ep_alltoall=self.mesh.ep > 1 and any_prefill),
                     len(rids), len(rids), rids)
             kind = "decode"
         new = tokens.tolist()

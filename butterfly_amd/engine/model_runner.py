@@ -98,14 +98,17 @@ class ModelRunner:
         out = self.model.forward(fb, self.kv.layers, hidden_in)
         return self.post_fn(out) if (self.post_fn is not None and self.model.last) else out
 
-    def run_decode(self, inp: dict, hidden_in=None, ep_tokens: int = 0, graphs_ok: bool = True):
+    def run_decode(self, inp: dict, hidden_in=None, ep_tokens: int = 0, graphs_ok: bool = True,
+                   ep_alltoall: bool = False):
         """Decode step. With expert parallelism every EP rank must pad to the same row count
         (`ep_tokens`): the graph bucket is chosen from it, so all EP ranks replay the same
         shape; steps where some EP rank is prefilling run eagerly (graphs_ok=False)."""
         B = len(inp["ids"])
         need = max(B, ep_tokens)
-        if not self.use_graphs or not graphs_ok or need > self.buckets[-1]:
-            return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
+        if not self.use_graphs or not graphs_ok or need > self.buckets[-1] or ep_alltoall:
+            fb = self.decode_batch(inp, ep_tokens)
+            fb.ep_alltoall = ep_alltoall
+            return self.run(fb, hidden_in)
         bucket = self.buckets[bisect.bisect_left(self.buckets, need)]
         if bucket in self.eager_buckets:
             return self.run(self.decode_batch(inp, ep_tokens), hidden_in)

@@ -372,6 +372,8 @@ class TransformerLM:
             # prefill: token-routed sparse experts (K12/K13: only routed rows are computed);
             # decode: dense fixed-shape path (weight-streaming bound either way, graph friendly)
             sparse = fb.is_prefill and self.device.type == "cuda" and flags.get("BFLY_MOE_SPARSE")
+            if self.ep > 1 and fb.ep_alltoall and flags.get("BFLY_EP_ALLTOALL"):
+                return self._moe_alltoall(pre, x, topk_ids, topk_w), False
             if self.ep > 1:
                 # DP-attention + expert-parallel FFN: every EP rank contributes Tp rows (zero
                 # padded), each computes its local experts on all ranks' tokens, and the
@@ -408,6 +410,34 @@ class TransformerLM:
             pb = self.p.get(pre + "proj_b") if self.shard.tp_rank == 0 else None
             out = ops.linear(hmid, self.p[pre + "proj_w"], bias=pb)
         return out, self.tp > 1
+
+    def _moe_alltoall(self, pre: str, x: torch.Tensor, topk_ids: torch.Tensor,
+                      topk_w: torch.Tensor) -> torch.Tensor:
+        """Expert-parallel MoE with token dispatch by all-to-all:
+        each token travels only to the EP ranks that own one of its top-k experts (once per
+        rank), the receiver runs its local experts on the routed rows (permute + grouped GEMM),
+        and a second all-to-all returns the weighted partial outputs to be summed at the
+        source. Used on steps where some EP rank prefills (variable-size exchange)."""
+        d = self.dims
+        T, H = x.shape
+        k = topk_ids.shape[1]
+        El, ep = d.experts, self.ep
+        dest = torch.div(topk_ids.long().clamp(min=0), El, rounding_mode="floor").clamp(max=ep - 1)
+        hit = torch.zeros(T, ep, dtype=torch.bool, device=x.device)
+        if T:
+            hit.scatter_(1, dest, True)
+        r_idx, t_idx = hit.t().nonzero(as_tuple=True)        # grouped by destination rank
+        splits = hit.sum(0).tolist()
+        meta = torch.cat([topk_ids.float(), topk_w.float()], 1)[t_idx]   # ids exact in f32
+        xr, rsplits = self.comm.all_to_all_v(x[t_idx], splits, "ep")
+        mr, _ = self.comm.all_to_all_v(meta, splits, "ep")
+        yr = ops.moe_sparse_ffn(xr, mr[:, :k].round().to(torch.int32).contiguous(), mr[:, k:].contiguous(),
+                                self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"], d.expert0, El, d.ffn)
+        back, _ = self.comm.all_to_all_v(yr, rsplits, "ep")
+        out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
+        if T:
+            out.index_add_(0, t_idx, back.float())
+        return out.to(x.dtype)
 
     # ------------------------------------------------------------------------------------
     # KV cache layout helpers

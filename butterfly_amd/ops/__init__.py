@@ -336,6 +336,8 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
     T, H = x.shape
     k = topk_ids.shape[1]
     TK = T * k
+    if TK == 0:
+        return torch.zeros(T, H, dtype=x.dtype, device=x.device)
     L = torch.ops.bfly
     dev = x.device
     rows = _arena.get(dev, "moe_rows", TK, torch.int32)[:TK]

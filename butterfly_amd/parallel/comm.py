@@ -172,6 +172,26 @@ class Communicator:
             out.copy_(full[g.rank_in_group * n:(g.rank_in_group + 1) * n])
         return out
 
+    def all_to_all_v(self, t: torch.Tensor, send_splits: list, group: str = "ep") -> tuple:
+        """Variable-size all-to-all along dim 0 (EP token dispatch / return): rows
+        [sum(send_splits[:r]), +send_splits[r]) go to group rank r. Returns (received rows in
+        source-rank order, recv_splits). The split sizes are exchanged first (host sync), so
+        this is an eager (prefill) primitive; decode keeps fixed-shape collectives."""
+        g = self.groups[group]
+        if g.size == 1:
+            return t, list(send_splits)
+        dev = t.device if self._nccl(g) else torch.device("cpu")
+        sc = torch.tensor(send_splits, dtype=torch.int64, device=dev)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=g.pg)
+        recv_splits = [int(v) for v in rc.tolist()]
+        src = t.contiguous() if self._nccl(g) else t.detach().cpu().contiguous()
+        out = torch.empty((sum(recv_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+        dist.all_to_all_single(out, src, output_split_sizes=recv_splits, input_split_sizes=list(send_splits),
+                               group=g.pg)
+        self.stats["calls"] += 1
+        return out.to(t.device), recv_splits
+
     def all_reduce_max_int(self, values: list, group: str = "world") -> list:
         """Host-side max of a few integers over a group (control plane, e.g. EP padding)."""
         g = self.groups[group]

@@ -182,6 +182,26 @@ class FakeComm(Communicator):
         out.copy_(part)
         return out
 
+    def all_to_all_v(self, t, send_splits, group="ep"):
+        g = self.groups[group]
+        if g.size == 1:
+            return t, list(send_splits)
+        me = g.rank_in_group
+        # split sizes meet in a checked collective; the ragged row blocks travel through the
+        # (src, dst) queues, so a shape mismatch on either side is reported by recv()
+        splits_all = self._coll(group, "a2a_splits", torch.tensor(send_splits, dtype=torch.int64),
+                                lambda xs: torch.stack(xs))
+        off = 0
+        for r, n in enumerate(send_splits):
+            self.world.send(self.rank, g.ranks[r], t[off:off + n])
+            off += n
+        recv_splits = [int(splits_all[r][me]) for r in range(g.size)]
+        parts = []
+        for r, n in enumerate(recv_splits):
+            like = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype)
+            parts.append(self.world.recv(g.ranks[r], self.rank, like))
+        return torch.cat(parts, 0).to(t.device), recv_splits
+
     def all_reduce_max_int(self, values, group="world"):
         g = self.groups[group]
         if g.size == 1:

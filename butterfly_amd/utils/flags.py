@@ -41,6 +41,7 @@ define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0:
 define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
 define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped expert GEMMs instead of the dense path")
+define("BFLY_EP_ALLTOALL", True, _bool, "EP MoE on prefill steps: dispatch tokens by all-to-all (else all-gather / reduce-scatter)")
 define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
 define("BFLY_FAULT", "", str, "fault injection 'rank:step:kind' (kind: hang|exit|nan) for tests")

@@ -150,7 +150,7 @@ int moe_max_tiles(int TK, int El, int BM) { return (TK + BM - 1) / BM + El; }
 int launch_moe_align(const int* topk_ids, int T, int K, int e0, int El, int BM, int* rows,
                      int* slot_of, int4* tiles, int* count, hipStream_t stream) {
   if (El <= 0 || El > kMaxExperts || BM <= 0) return -1;
-  if (T <= 0) return 0;
+  if (T <= 0) return (int)hipMemsetAsync(count, 0, sizeof(int), stream);   // no tiles
   moe_align_kernel<<<1, 1024, 0, stream>>>(topk_ids, T * K, K, e0, El, BM, rows, slot_of, tiles, count);
   return 0;
 }
