@@ -23,7 +23,12 @@ _loaded = False
 _load_error: str | None = None
 
 EPILOGUES = {"none": 0, "bias": 1, "silu": 2}
-DECODE_PART_TOKENS = 0   # 0 = pick the context split per call (attn_decode_part_tokens)
+DECODE_PART_TOKENS = 0
+# Split combine inside the decode kernel (last-arriver merge) instead of the combine kernel.
+# Off: measured 2x slower on MI355X (B=64 ctx 1024: 104 vs 53 us; B=1 ctx 8192: 168 vs 47 us)
+# — the per-workgroup agent-scope release (L2 write-back) and the serial merge in one
+# workgroup cost more than the separate, fully parallel combine launch.
+FUSED_DECODE_COMBINE = False   # 0 = pick the context split per call (attn_decode_part_tokens)
 
 
 def load_library(path: str | os.PathLike | None = None) -> bool:
@@ -106,6 +111,7 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
                  for b in range(1, max_batch + 1))
         _arena.get(device, "attn_o", max_batch * num_kv_heads * ns * 16 * head_dim, torch.float32)
         _arena.get(device, "attn_ml", max_batch * num_kv_heads * ns * 16 * 2, torch.float32)
+        _arena.get(device, "attn_cnt", max_batch * num_kv_heads, torch.int32, zero=True)
     _arena.get(device, "sample", max(max_batch, max_tokens, 1) * 64, torch.int64)
 
 
@@ -295,12 +301,15 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_c
     if part_tokens <= 0:
         part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
     ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
-    po = pml = None
+    po = pml = cnt = None
     if ns > 1:
         po = _arena.get(q.device, "attn_o", B * Hkv * ns * 16 * D, torch.float32)
         pml = _arena.get(q.device, "attn_ml", B * Hkv * ns * 16 * 2, torch.float32)
+        if FUSED_DECODE_COMBINE:
+            # zeroed once; the kernel's last-arriving split re-arms every counter it used
+            cnt = _arena.get(q.device, "attn_cnt", B * Hkv, torch.int32, zero=True)
     torch.ops.bfly.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx,
-                               part_tokens, out, po, pml)
+                               part_tokens, out, po, pml, cnt)
     return out
 
 

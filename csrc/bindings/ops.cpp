@@ -342,7 +342,8 @@ int64_t attn_decode_part_tokens(int64_t B, int64_t Hkv, int64_t max_ctx) {
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& block_tables, const Tensor& ctx_lens, double scale,
                  int64_t max_ctx, int64_t part_tokens, Tensor& out,
-                 const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml) {
+                 const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml,
+                 const c10::optional<Tensor>& counters) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "attn_decode: q [B, Hq, D]");
   const int B = q.size(0), Hq = q.size(1), D = q.size(2);
@@ -365,11 +366,17 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
     po = part_o->data_ptr<float>();
     pml = part_ml->data_ptr<float>();
   }
+  int* cnt = nullptr;
+  if (counters.has_value()) {
+    CHECK_I32(*counters);
+    TORCH_CHECK(counters->numel() >= (long)B * Hkv && counters->is_contiguous(), "attn_decode: counters [B*Hkv] (zeroed)");
+    cnt = counters->data_ptr<int>();
+  }
   c10::DeviceGuard g(q.device());
   const int rc = bfly::launch_attn_decode(bf(q), q.stride(0), bf(k_cache), bf(v_cache),
                                           block_tables.data_ptr<int>(), block_tables.stride(0),
                                           ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale,
-                                          max_ctx, part_tokens, bf(out), po, pml, cur_stream());
+                                          max_ctx, part_tokens, bf(out), po, pml, cur_stream(), cnt);
   TORCH_CHECK(rc == 0, "attn_decode: unsupported configuration (rc=", rc, ")");
 }
 
@@ -579,7 +586,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("attn_decode_part_tokens(int B, int Hkv, int max_ctx) -> int", &attn_decode_part_tokens);
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
         "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
-        "Tensor(c!)? part_ml) -> ()");
+        "Tensor(c!)? part_ml, Tensor(d!)? counters=None) -> ()");
   m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
   m.def("moe_max_tiles(int tk, int num_local) -> int", &moe_max_tiles);

@@ -81,7 +81,8 @@ int attn_decode_part_tokens(int B, int Hkv, int max_ctx);
 int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
-                       bf16* out, float* part_o, float* part_ml, hipStream_t stream);
+                       bf16* out, float* part_o, float* part_ml, hipStream_t stream,
+                       int* counters = nullptr);   // zeroed [B*Hkv]: fused split combine
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,

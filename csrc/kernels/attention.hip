@@ -34,13 +34,62 @@ constexpr float kNegInf = -INFINITY;
 // ---------------------------------------------------------------------------------------
 // Decode
 // ---------------------------------------------------------------------------------------
+// Split combine fused into the decode kernel: every split of a (sequence, kv head) publishes
+// its partial (O, m, l) and takes a ticket; the split that arrives last merges all partials
+// (fixed split order: deterministic) and writes the output, then re-arms the counter for the
+// next call. Hand-off per cdna_hip_programming.md §5 split-K item 2 (stores drained, barrier,
+// one agent-scope release + relaxed ticket; one agent-scope acquire in the last arriver). The
+// partials are 8 KiB per split, so the serial merge is short; it replaces a separate combine
+// launch and its kernel boundary.
+__device__ __forceinline__ void decode_split_done(const float* __restrict__ part_o,
+                                                  const float* __restrict__ part_ml,
+                                                  int* __restrict__ counters, int b, int h,
+                                                  int nsplit, int G, int Hq, int Hkv,
+                                                  bf16* __restrict__ out, int* s_last) {
+  constexpr int D = 128;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* cnt = counters + b * Hkv + h;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == nsplit - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *s_last = last;
+  }
+  __syncthreads();
+  if (!*s_last) return;
+  const long base = (long)(b * Hkv + h) * nsplit;
+  for (int e = threadIdx.x; e < G * D; e += blockDim.x) {
+    const int qr = e / D, d = e % D;
+    float M = kNegInf;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[((base + s) * 16 + qr) * 2]);
+    const float Mb = M == kNegInf ? 0.f : M;
+    float L = 0.f, O = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const float ms = part_ml[((base + s) * 16 + qr) * 2];
+      if (ms == kNegInf) continue;
+      const float w = exp2f(ms - Mb);
+      L += w * part_ml[((base + s) * 16 + qr) * 2 + 1];
+      O += w * part_o[((base + s) * 16 + qr) * D + d];
+    }
+    out[((long)b * Hq + h * G + qr) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+}
+
 template <int D, int BS>
 __global__ void __launch_bounds__(kAttnThreads)
 attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k_cache,
                    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables,
                    int bt_stride, const int* __restrict__ ctx_lens, int Hq, int Hkv,
                    float scale_log2, int part_tokens, bf16* __restrict__ out,
-                   float* __restrict__ part_o, float* __restrict__ part_ml) {
+                   float* __restrict__ part_o, float* __restrict__ part_ml,
+                   int* __restrict__ counters) {
   static_assert(D == 128 && BS == 32, "decode kernel is specialised for D=128, BS=32");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -53,12 +102,14 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
 
   __shared__ float s_o[4][8][4][64];
   __shared__ float s_m[4][16], s_l[4][16];
+  __shared__ int s_last;
 
-  if (tok0 >= tok1) {  // empty split: mark it so the combine kernel skips it
+  if (tok0 >= tok1) {  // empty split: mark it so the combine skips it
     if (nsplit > 1 && threadIdx.x < 16) {
       part_ml[(part_base * 16 + threadIdx.x) * 2 + 0] = kNegInf;
       part_ml[(part_base * 16 + threadIdx.x) * 2 + 1] = 0.f;
     }
+    if (nsplit > 1 && counters) decode_split_done(part_o, part_ml, counters, b, h, nsplit, G, Hq, Hkv, out, &s_last);
     return;
   }
 
@@ -196,6 +247,7 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
       }
     }
   }
+  if (nsplit > 1 && counters) decode_split_done(part_o, part_ml, counters, b, h, nsplit, G, Hq, Hkv, out, &s_last);
 }
 
 // One workgroup per (query row, kv head, sequence); thread = head dim element. The split
@@ -444,7 +496,8 @@ int attn_decode_part_tokens(int B, int Hkv, int max_ctx) {
 int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
-                       bf16* out, float* part_o, float* part_ml, hipStream_t stream) {
+                       bf16* out, float* part_o, float* part_ml, hipStream_t stream,
+                       int* counters) {
   if (B <= 0) return 0;
   if (D != 128 || block_size != 32 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
   if (part_tokens <= 0) part_tokens = attn_decode_part_tokens(B, Hkv, max_ctx);
@@ -456,8 +509,8 @@ int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const 
   dim3 grid(nsplit, Hkv, B);
   attn_decode_kernel<128, 32><<<grid, kAttnThreads, 0, stream>>>(
       q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, Hq, Hkv, scale_log2,
-      part_tokens, out, part_o, part_ml);
-  if (nsplit > 1) {
+      part_tokens, out, part_o, part_ml, nsplit > 1 ? counters : nullptr);
+  if (nsplit > 1 && counters == nullptr) {
     dim3 g2(Hq / Hkv, Hkv, B);
     attn_decode_combine_kernel<128><<<g2, 128, 0, stream>>>(part_o, part_ml, nsplit, Hq, Hkv, out);
   }

@@ -164,9 +164,10 @@ def test_attn_prefill_non_causal():
     _close(o, ref.attn_prefill(q, k, v, cu, 130, 0.088, False), 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("part_tokens", [0, 128, 256, 4096])
 @pytest.mark.parametrize("Hq,Hkv", [(16, 2), (8, 8), (64, 8)])
-def test_attn_decode_paged(part_tokens, Hq, Hkv):
+def test_attn_decode_paged(part_tokens, Hq, Hkv, fused, monkeypatch):
     D, BS = 128, 32
     lens = [1, 31, 32, 100, 700]
     B = len(lens)
@@ -178,8 +179,11 @@ def test_attn_decode_paged(part_tokens, Hq, Hkv):
     ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
     q = _bf(B, Hq, D, seed=26)
     scale = 1.0 / math.sqrt(D)
-    o = ops.attn_decode(q, kc, vc, perm, ctx, scale, max(lens), part_tokens)
-    _close(o, ref.attn_decode(q, kc, vc, perm, ctx, scale), 2e-2, 2e-2)
+    monkeypatch.setattr(ops, "FUSED_DECODE_COMBINE", fused)
+    want = ref.attn_decode(q, kc, vc, perm, ctx, scale)
+    for _ in range(2):   # the fused combine must leave its split counters re-armed
+        o = ops.attn_decode(q, kc, vc, perm, ctx, scale, max(lens), part_tokens)
+        _close(o, want, 2e-2, 2e-2)
 
 
 def test_attn_decode_strided_q():
