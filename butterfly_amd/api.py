@@ -25,6 +25,7 @@ from .engine.engine import LLMEngine
 from .engine.sampler import SamplingParams
 from .parallel.comm import Communicator, init_distributed
 from .partition import PartitionPlan, partition
+from .utils import flags
 from .utils.tokenizer import load_tokenizer
 
 
@@ -68,6 +69,17 @@ class LLM:
         self.engine = LLMEngine(cfg, plan.mesh, ecfg, comm=self.comm, device=device,
                                 stage_layers=plan.stages, model=None if ckpt is None else self._load(ckpt, plan, device))
         self.tokenizer = load_tokenizer(tokenizer)
+        self.health = None
+        period = flags.get("BFLY_HEARTBEAT_S")
+        if world > 1 and period > 0:
+            # rank heartbeats through the job's TCPStore: a dead or wedged rank aborts the
+            # whole job instead of leaving its peers blocked in a collective
+            import torch.distributed as dist
+
+            from .utils.health import HealthMonitor
+
+            self.health = HealthMonitor(dist.distributed_c10d._get_default_store(), rank, world,
+                                        period=period, timeout=max(30.0, 6 * period)).start()
 
     def _load(self, path, plan, device):
         from .ckpt import load_into

@@ -29,8 +29,8 @@ from ..config import EngineConfig, ModelConfig
 from ..models import Shard, build_model
 from ..parallel.comm import Communicator
 from ..parallel.mesh import Mesh
-from ..utils import trace
-from ..utils.health import FaultInjector
+from ..utils import flags, trace
+from ..utils.health import FaultInjector, StepWatchdog
 from ..utils.metrics import Metrics
 from .batch import empty_batch
 from .kv_cache import KVCache, device_kv_budget, kv_blocks_for_budget
@@ -120,6 +120,10 @@ class LLMEngine:
         self.pp_first = coord.pp == 0
         self.pp_last = coord.pp == mesh.pp - 1
         self.faults = FaultInjector()
+        # a step that outlives BFLY_STEP_TIMEOUT_S (hung collective, wedged GPU) dumps every
+        # thread's stack and terminates the rank (0 = off; first steps include graph capture)
+        st = flags.get("BFLY_STEP_TIMEOUT_S")
+        self.watchdog = StepWatchdog(st) if st > 0 else None
         self.steps_done = 0
 
     # ------------------------------------------------------------------------------------
@@ -162,8 +166,12 @@ class LLMEngine:
         return tt, seeds, [self.requests[r].params for r in rids]
 
     def step(self) -> StepOutput:
+        if self.watchdog is not None:
+            self.watchdog.arm(f"engine step {self.steps_done}")
         with trace.range("engine.step", step=self.steps_done):
             out = self._step()
+        if self.watchdog is not None:
+            self.watchdog.disarm()
         self.steps_done += 1
         if self.steps_done % 256 == 0:
             self.comm.check_health()

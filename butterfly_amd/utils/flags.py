@@ -45,6 +45,7 @@ define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped
 define("BFLY_EP_ALLTOALL", True, _bool, "EP MoE on prefill steps: dispatch tokens by all-to-all (else all-gather / reduce-scatter)")
 define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
+define("BFLY_STEP_TIMEOUT_S", 0.0, float, "engine step watchdog: terminate a rank whose step exceeds this (0 = off)")
 define("BFLY_FAULT", "", str, "fault injection 'rank:step:kind' (kind: hang|exit|nan) for tests")
 define("BFLY_TRACE", "", str, "write a chrome-trace JSON of engine steps to this path")
 define("BFLY_ROCTX", False, _bool, "emit roctx ranges (visible in rocprofv3 --marker-trace)")
