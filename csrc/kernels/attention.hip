@@ -480,15 +480,18 @@ int attn_decode_splits(int max_ctx, int part_tokens) {
   return (max_ctx + part_tokens - 1) / part_tokens;
 }
 
-// Context split size: enough (b, kv-head, split) workgroups to cover the 256 CUs ~4x, but
-// splits of >= 128 tokens (4 pages per workgroup, one per wave) so each wave streams a page.
+// Context split size, from a split-size sweep on MI355X (tools/bench_attn.py --parts): aim at
+// ~256 (b, kv-head, split) workgroups (one per CU), splitting the context evenly and never
+// below 256 tokens per split; a single split skips the combine launch entirely.
+//   B=64 Hkv=8 ctx 1K: 1 split 46 us (2 splits 53);  B=8 ctx 4K: 4 splits 30 us (16: 38);
+//   B=64 Hkv=1: 4 splits 13.5 us (8: 15.4);        B=1 ctx 8K: 32 splits 27 us (64: 43).
 int attn_decode_part_tokens(int B, int Hkv, int max_ctx) {
-  const int want_wg = 1024;
-  const int bh = B * Hkv > 0 ? B * Hkv : 1;
-  int splits = (want_wg + bh - 1) / bh;
+  const int pairs = B * Hkv > 0 ? B * Hkv : 1;
+  const int splits = (256 + pairs - 1) / pairs;
   int part = (max_ctx + splits - 1) / splits;
   part = (part + 31) / 32 * 32;
-  if (part < 128) part = 128;
+  if (splits > 1 && part < 256) part = 256;
+  if (part < 32) part = 32;
   while ((max_ctx + part - 1) / part > 256) part += 32;   // combine kernel: <= 256 splits
   return part;
 }

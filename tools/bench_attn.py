@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--cases", default="64:1024:64:8,64:1024:8:1,256:1024:64:8,1:8192:64:8,16:4096:64:8")
     ap.add_argument("--prefill", default="16:1024:64:8,4:4096:64:8,1:16384:64:8",
                     help="prefill cases seqs:len:Hq:Hkv ('' to skip)")
+    ap.add_argument("--parts", default="0", help="decode split sizes to try (0 = auto)")
     a = ap.parse_args()
     ops.load_library()
     for case in filter(None, a.prefill.split(",")):
@@ -50,23 +51,23 @@ def main():
         cl = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
         q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
         out = torch.empty_like(q)
-        f = lambda: ops.attn_decode(q, kc, vc, bt, cl, 0.088, ctx, out=out)  # noqa: E731
-        for _ in range(3):
-            f()
-        torch.cuda.synchronize()
-        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        it = 20
-        st.record()
-        for _ in range(it):
-            f()
-        en.record()
-        torch.cuda.synchronize()
-        us = st.elapsed_time(en) / it * 1e3
-        byts = 2 * B * ctx * Hkv * D * 2
-        print(json.dumps({"B": B, "ctx": ctx, "Hq": Hq, "Hkv": Hkv, "us": round(us, 2),
-                          "TBps": round(byts / us / 1e6, 3),
-                          "part_tokens": torch.ops.bfly.attn_decode_part_tokens(B, Hkv, ctx)}), flush=True)
-
+        for pt in [int(x) for x in a.parts.split(",")]:
+            f = lambda: ops.attn_decode(q, kc, vc, bt, cl, 0.088, ctx, part_tokens=pt, out=out)  # noqa: E731
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            it = 20
+            st.record()
+            for _ in range(it):
+                f()
+            en.record()
+            torch.cuda.synchronize()
+            us = st.elapsed_time(en) / it * 1e3
+            byts = 2 * B * ctx * Hkv * D * 2
+            used = pt if pt > 0 else torch.ops.bfly.attn_decode_part_tokens(B, Hkv, ctx)
+            print(json.dumps({"B": B, "ctx": ctx, "Hq": Hq, "Hkv": Hkv, "us": round(us, 2),
+                              "TBps": round(byts / us / 1e6, 3), "part_tokens": used}), flush=True)
 
 if __name__ == "__main__":
     main()
