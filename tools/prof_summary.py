@@ -27,7 +27,9 @@ def main():
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    last_prefill = max((i for i, r in enumerate(rows) if "attn_prefill" in r["Kernel_Name"]), default=-1)
+    # the decode window starts after the prefill's last attention AND its trailing big-tile GEMMs
+    last_prefill = max((i for i, r in enumerate(rows) if "attn_prefill" in r["Kernel_Name"]
+                        or "gemm_big_kernel" in r["Kernel_Name"]), default=-1)
     dec = rows[last_prefill + 1:]
     agg = defaultdict(lambda: [0, 0.0])
     for r in dec:
