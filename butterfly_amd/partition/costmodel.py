@@ -11,7 +11,10 @@ it must fit the usable HBM (288 GB per MI355X).
 """
 from __future__ import annotations
 
+import json
 from dataclasses import dataclass
+from pathlib import Path
+from typing import Optional
 
 from ..config import ModelConfig
 from ..models.ir import OpSpec, build_ir
@@ -25,26 +28,53 @@ class LayerCost:
     comm_bytes: float
 
 
+_CALIB = Path(__file__).resolve().parent / "calibration" / "mi355x_gemm.json"
+_M_BUCKETS = (1, 16, 32, 64, 128, 256, 512)
+
+
+def _load_gemm_calibration() -> dict:
+    try:
+        d = json.loads(_CALIB.read_text())
+    except (OSError, ValueError):
+        return {}
+    out = {}
+    for key, us in d.get("gemm", {}).items():
+        n, k, m = (int(v) for v in key.split("x"))
+        out[(n, k, m)] = us * 1e-6
+    return out
+
+
 class CostModel:
+    """GEMM times come from the measured MI355X table (partition/calibration, produced by
+    tools/gemm_tune.sh) when the shape is known, otherwise from max(FLOPs / eff(M), bytes /
+    bandwidth) with an M-dependent MFMA efficiency fitted to the same measurements."""
+    _calib: Optional[dict] = None
+
     def __init__(self, cfg: ModelConfig, hw: Hardware = MI355X, oneshot_allreduce: bool = True):
         self.cfg = cfg
         self.hw = hw
         self.oneshot = oneshot_allreduce
+        if CostModel._calib is None:
+            CostModel._calib = _load_gemm_calibration()
         self._irs: dict = {}
         self._cur_ep = 1
 
     # ---- primitives ------------------------------------------------------------------------
     def gemm(self, M: int, N: int, K: int) -> float:
         hw = self.hw
+        bucket = next((b for b in _M_BUCKETS if b >= M), None)
+        if bucket is not None and (N, K, bucket) in self._calib:
+            return self._calib[(N, K, bucket)] + hw.kernel_overhead_s
         flops = 2.0 * M * N * K
         byts = 2.0 * (N * K + M * K + M * N)
-        return max(flops / hw.bf16_flops_eff, byts / hw.hbm_bw_eff) + hw.kernel_overhead_s
+        eff = hw.bf16_flops_eff * M / (M + 110.0)     # fit: 0.66 PF @128 ... 1.27 PF @8192
+        return max(flops / eff, byts / hw.hbm_bw_eff) + hw.kernel_overhead_s
 
     def allreduce(self, nbytes: float, n: int) -> float:
         if n <= 1:
             return 0.0
         hw = self.hw
-        if self.oneshot and nbytes <= 512 * 1024:
+        if self.oneshot and nbytes <= hw.oneshot_ar_max_bytes:
             # one-shot: every rank reads the n-1 peer buffers over n-1 distinct links at once
             return hw.oneshot_ar_latency_s + nbytes / hw.xgmi_link_bw
         return hw.collective_latency_s + 2.0 * (n - 1) / n * nbytes / hw.xgmi_link_bw

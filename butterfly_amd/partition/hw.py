@@ -19,15 +19,16 @@ class Hardware:
     gpus_per_node: int = 8
     hbm_bytes: float = 288e9
     hbm_bw: float = 6.29e12            # measured copy bandwidth
-    hbm_bw_eff: float = 5.0e12          # sustained by weight-streaming GEMMs / paged attention
+    hbm_bw_eff: float = 5.7e12          # sustained by weight-streaming GEMMs / paged attention (measured)
     bf16_flops: float = 2.5e15          # dense spec
-    bf16_flops_eff: float = 0.9e15      # sustained by our MFMA GEMMs (large M)
+    bf16_flops_eff: float = 1.3e15      # large-M asymptote of our 256x256 MFMA GEMM (measured 1.27 PF @8192)
     xgmi_links: int = 7                 # per GPU, full mesh within a node
     xgmi_link_bw: float = 153e9         # bytes/s per link per direction
     kernel_overhead_s: float = 1.5e-6   # dependent kernel boundary inside a graph
     collective_latency_s: float = 12e-6  # small-message RCCL all-reduce
     p2p_latency_s: float = 8e-6         # RCCL send/recv hop
     oneshot_ar_latency_s: float = 5e-6  # one-shot IPC all-reduce (small messages)
+    oneshot_ar_max_bytes: float = 8 << 20  # larger all-reduces go to RCCL (BFLY_CUSTOM_AR_MAX_BYTES)
     usable_hbm_fraction: float = 0.92
 
     def to_dict(self) -> dict:

@@ -699,7 +699,7 @@ GemmPlan plan_gemm(int M, int N, int K) {
   if (!tuned_enabled()) return plan_gemm_heuristic(M, N, K);
   // token-count buckets of the sweep: M uses the entry of its bucket, or the heuristic plan
   // when the sweep found nothing better there
-  static const int kBuckets[] = {1, 16, 32, 64, 128, 256};
+  static const int kBuckets[] = {1, 16, 32, 64, 128, 256, 512};
   int bucket = 0;
   for (int b : kBuckets)
     if (b >= M) { bucket = b; break; }
