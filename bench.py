@@ -102,9 +102,14 @@ def main():
     # prefill (untimed; reported separately)
     tp0 = time.perf_counter()
     prefill_tokens = 0
-    while eng.scheduler.num_waiting > 0:
+    # with the asynchronous pipeline (pp > 1) one step advances every stage by one request
+    # group (replica_batch / pp sequences) and each sequence gets a token every pp steps
+    groups = mesh.pp if eng.async_pp else 1
+    decode_streak = 0
+    while eng.scheduler.num_waiting > 0 or decode_streak < groups:
         out = eng.step()
         prefill_tokens += sum(len(eng.requests[r].prompt) for r in out.rids) if out.kind == "prefill" else 0
+        decode_streak = decode_streak + 1 if out.kind == "decode" else 0
     torch.cuda.synchronize()
     prefill_s = time.perf_counter() - tp0
     log(f"prefill {prefill_tokens} tokens in {prefill_s:.2f}s ({prefill_tokens / prefill_s:.0f} tok/s/replica)", rank)
@@ -114,24 +119,30 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     step_times = []
+    gen_tokens = 0
     t_start = time.perf_counter()
     for _ in range(a.steps):
         ts = time.perf_counter()
         out = eng.step()
         step_times.append(time.perf_counter() - ts)
-        assert out.kind == "decode" and len(out.rids) == replica_batch, (out.kind, len(out.rids))
+        assert out.kind == "decode", out.kind
+        gen_tokens += len(out.new_tokens)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    if replica_batch % groups == 0:   # every step carried one full group
+        assert gen_tokens == a.steps * replica_batch // groups, (gen_tokens, a.steps, replica_batch, groups)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, gen_tokens], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    tokens = a.steps * replica_batch * mesh.dp
+        elapsed = float(t[0].item())
+    # tokens of the whole node: every DP replica generates gen_tokens (same work per replica)
+    tokens = gen_tokens * mesh.dp
     value = tokens / elapsed
-    p50 = statistics.median(step_times) * 1e3
-    p99 = sorted(step_times)[max(0, int(len(step_times) * 0.99) - 1)] * 1e3
+    # per-token latency of a sequence = `groups` steps (one step when pp == 1)
+    p50 = statistics.median(step_times) * 1e3 * groups
+    p99 = sorted(step_times)[max(0, int(len(step_times) * 0.99) - 1)] * 1e3 * groups
     with open(BASELINE) as f:
         base = json.load(f)
     pub = base.get("published") or {}
@@ -155,7 +166,7 @@ def main():
         "config": {"model": "Llama-3-70B" if a.model == "llama3-70b" else a.model,
                    "global_batch": a.batch_per_gpu * a.gpus, "seq_len": a.prompt_len,
                    "parallelism": plan.name, "stages": [list(s) for s in plan.stages],
-                   "hipgraph": not a.no_graphs},
+                   "hipgraph": not a.no_graphs, "pp_async_groups": groups if groups > 1 else None},
     }
     if rank == 0:
         line = json.dumps(res)

@@ -10,8 +10,10 @@ Per step:
   prefill  : pack the admitted prompts, run the stage (flash prefill), sample the first tokens
   decode   : one token per running sequence through the hipGraph-replayed stage
   PP       : stage s receives the residual stream from s-1 and sends to s+1 (RCCL send/recv
-             over xGMI); the batch is split into microbatches so stages overlap; the last stage
-             samples and broadcasts token ids to the replica's ranks.
+             over xGMI); the last stage samples and broadcasts token ids to the replica's
+             ranks. Default (BFLY_PP_ASYNC): pp request groups stay in flight across steps,
+             one step = one tick in which every stage advances one group (engine/pipeline.py);
+             otherwise each step splits the batch into microbatches (fill/drain per step).
   TP       : handled inside the model (all-reduces) and the sampler (score/id all-gather).
 """
 from __future__ import annotations
@@ -35,6 +37,7 @@ from ..utils.metrics import Metrics
 from .batch import empty_batch
 from .kv_cache import KVCache, device_kv_budget, kv_blocks_for_budget
 from .model_runner import ModelRunner
+from .pipeline import GroupedScheduler, PipePlan
 from .sampler import Sampler, SamplingParams
 
 
@@ -103,7 +106,18 @@ class LLMEngine:
             raise RuntimeError("no HBM left for the KV cache")
         self.kv = KVCache(self.model, nblocks, bs)
         native = __import__("butterfly_amd._native_loader", fromlist=["native"]).native()
-        self.scheduler = native.Scheduler(self.kv.manager, engine_cfg.max_batch, engine_cfg.max_prefill_tokens)
+        # pipeline parallelism without per-step fill/drain: pp request groups in flight
+        # (engine/pipeline.py); EP layouts keep the synchronous path (EP collectives span DP ranks)
+        self.async_pp = mesh.pp > 1 and mesh.ep == 1 and flags.get("BFLY_PP_ASYNC")
+        if self.async_pp:
+            self.scheduler = GroupedScheduler(native, self.kv.manager, mesh.pp, engine_cfg.max_batch,
+                                              engine_cfg.max_prefill_tokens)
+        else:
+            self.scheduler = native.Scheduler(self.kv.manager, engine_cfg.max_batch, engine_cfg.max_prefill_tokens)
+        self._tick = 0
+        self._inflight: list = []        # PipePlans entered at ticks k-pp+1 .. k
+        self._pending: Optional[PipePlan] = None   # left the last stage; ids not yet applied
+        self._sends: list = []
         d = self.model.dims
         self.sampler = Sampler(self.comm, cfg.vocab_size, d.vocab0, mesh.tp)
         if self.device.type == "cuda":
@@ -111,9 +125,11 @@ class LLMEngine:
                                   max_n=self._max_gemm_n(), max_k=self._max_gemm_k(),
                                   max_batch=max(engine_cfg.graph_batch_sizes + [engine_cfg.max_batch]),
                                   max_ctx=engine_cfg.max_seq_len, num_kv_heads=d.hkv, head_dim=cfg.head_dim)
+        buckets = [b for b in engine_cfg.graph_batch_sizes if b <= engine_cfg.max_batch] or [engine_cfg.max_batch]
+        if self.async_pp and self.scheduler.group_batch not in buckets:
+            buckets.append(self.scheduler.group_batch)    # a full group replays one graph
         self.runner = ModelRunner(self.model, self.kv, engine_cfg.max_seq_len, engine_cfg.use_graphs,
-                                  [b for b in engine_cfg.graph_batch_sizes if b <= engine_cfg.max_batch] or [engine_cfg.max_batch],
-                                  max_batch=engine_cfg.max_batch)
+                                  buckets, max_batch=engine_cfg.max_batch)
         self.requests: dict[int, Request] = {}
         self._ids = itertools.count()
         self.metrics = Metrics()
@@ -180,6 +196,8 @@ class LLMEngine:
     def _step(self) -> StepOutput:
         t0 = time.perf_counter()
         self.faults.maybe_inject(self.rank, self.steps_done)
+        if self.async_pp:
+            return self._pp_tick(t0)
         plan = self.scheduler.schedule()
         ep_pad, any_prefill = 0, plan.kind == 1
         if self.mesh.ep > 1:
@@ -217,7 +235,10 @@ class LLMEngine:
                                                      ep_alltoall=self.mesh.ep > 1 and any_prefill),
                     len(rids), len(rids), rids)
             kind = "decode"
-        new = tokens.tolist()
+        return self._apply_tokens(kind, rids, tokens.tolist(), t0)
+
+    def _apply_tokens(self, kind: str, rids: list, new: list, t0: float) -> StepOutput:
+        """Append one sampled token per sequence, retire finished ones, record metrics."""
         finished = []
         now = time.perf_counter()
         for r, t in zip(rids, new):
@@ -264,7 +285,8 @@ class LLMEngine:
         return ids
 
     def _pipeline_decode(self, inp: dict, rids) -> torch.Tensor:
-        """Microbatched pipeline decode: the batch is cut into M = pp microbatches; stage s
+        """Synchronous pipeline decode (BFLY_PP_ASYNC=0, and EP layouts): the batch is cut
+        into M = pp microbatches; stage s
         works on microbatch m while stage s+1 works on m-1 (RCCL send/recv of the residual
         stream over xGMI is stream-ordered, so the overlap needs no host synchronisation).
         Each microbatch replays its own hipGraph bucket."""
@@ -294,6 +316,70 @@ class LLMEngine:
         ids = torch.cat(outs) if self.pp_last else torch.empty(B, dtype=torch.int32, device=self.device)
         self.comm.broadcast_(ids, src_in_group=self.mesh.pp - 1, group="pp")
         return ids
+
+    # ------------------------------------------------------------------------------------
+    # asynchronous pipeline (engine/pipeline.py): one tick = every stage advances one group
+    def _pp_tick(self, t0: float) -> StepOutput:
+        """Tick k: stage s runs the group that entered at tick k - s. Returns the tokens of the
+        group that left the last stage at tick k - 1 (applied now, right before that group is
+        scheduled again), or an empty 'pipeline' output while the pipe fills."""
+        pp, s = self.mesh.pp, self.coord.pp
+        k = self._tick
+        self._tick += 1
+        # sends of the previous tick: the next stage posted (or is about to post) their recvs
+        # at the start of its tick k, which depends on nothing this rank does in tick k
+        for w in self._sends:
+            w.wait()
+        self._sends = []
+        # this rank's stage works on the plan that entered s ticks ago; stages >= 1 enqueue
+        # their device work before blocking on the previous tick's ids (keeps the GPU fed)
+        mine = next((p for p in self._inflight if p.tick == k - s), None)
+        if s > 0 and mine is not None:
+            self._pp_stage_work(mine)
+        out = StepOutput("pipeline", [], [], [], 0.0)
+        if self._pending is not None:
+            p, self._pending = self._pending, None
+            out = self._apply_tokens(p.kind, p.rids, p.ids.tolist(), t0)
+        # schedule the group entering stage 0 (every rank: replicated deterministic state)
+        g = k % pp
+        plan = self.scheduler.groups[g].schedule()
+        if plan.kind != 0:
+            rids = list(plan.seq_ids)
+            T = sum(plan.prefill_lens) if plan.kind == 1 else len(rids)
+            self._inflight.append(PipePlan(k, g, plan, rids, T, list(plan.cow)))
+            if s == 0:
+                self._pp_stage_work(self._inflight[-1])
+        # the plan that entered pp-1 ticks ago leaves the last stage now: broadcast its ids
+        leaving = next((p for p in self._inflight if p.tick == k - pp + 1), None)
+        if leaving is not None:
+            self._inflight.remove(leaving)
+            if leaving.ids is None:
+                leaving.ids = torch.empty(len(leaving.rids), dtype=torch.int32, device=self.device)
+            self.comm.broadcast_(leaving.ids, src_in_group=pp - 1, group="pp")
+            self._pending = leaving
+        out.seconds = time.perf_counter() - t0
+        return out
+
+    def _pp_stage_work(self, p: PipePlan) -> None:
+        """recv the residual stream (stage > 0) -> run this stage -> isend (not last) or sample
+        (last stage: ids kept on the plan for the broadcast)."""
+        h = None
+        if not self.pp_first:
+            h = torch.empty(p.tokens, self.cfg.hidden_size, dtype=self.model.dtype, device=self.device)
+            self.comm.recv(h, self.mesh.prev_stage(self.rank))
+        if p.cow:
+            self.kv.copy_blocks(p.cow)
+        if p.plan.kind == 1:
+            out = self.runner.run(self.runner.prefill_batch(p.plan, lambda r: self.requests[r].tokens), h)
+        else:
+            inp = self.runner.decode_inputs(p.plan, [self.requests[r].tokens[-1] for r in p.rids])
+            out = self.runner.run_decode(inp, h)
+        if not self.pp_last:
+            snd = out.clone() if p.plan.kind == 2 else out   # graph outputs are reused by the next replay
+            self._sends.append(self.comm.isend(snd, self.mesh.next_stage(self.rank)))
+        else:
+            temps, seeds, params = self._sample_params(p.rids)
+            p.ids = self.sampler.sample(out, temps, seeds, params)
 
     # ------------------------------------------------------------------------------------
     def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list:

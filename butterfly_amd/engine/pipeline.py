@@ -1,0 +1,77 @@
+"""Asynchronous pipeline-parallel decode: `pp` request groups in flight across engine steps.
+
+Per-step microbatching (engine._pipeline_decode) pays a fill/drain bubble every step — with
+M = pp microbatches a step lasts (M + pp - 1) stage-slots for M slots of work, and every
+microbatch re-streams the stage's weights from HBM. Here the replica's sequences are split
+into `pp` groups, each with its own continuous-batching scheduler over the shared KV block
+manager, and the engine advances in ticks: at tick k group (k mod pp) enters stage 0 while
+stage s works on the group that entered at tick k - s. In steady state every stage streams
+its weights once per tick for one group, and one group's tokens leave the last stage per tick
+— no bubble, and the same RCCL send/recv of the residual stream between neighbouring stages
+(SURVEY.md §2.6 PP row, §3.2 (4) "PP steady-state loop").
+
+Determinism across ranks: every rank of the replica runs the same tick loop, schedules the
+entering group itself (the schedulers are replicated, as in the synchronous engine), receives
+the sampled ids of the group leaving the last stage by a broadcast over the pp group, and
+applies them to its scheduler at the start of the next tick — which is exactly when that group
+is scheduled again (it entered pp ticks earlier). A group's block tables, positions and tokens
+only change at its own scheduling / completion, so a plan made at tick k stays valid while
+stages 1..pp-1 process it at ticks k+1..k+pp-1.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+
+class GroupedScheduler:
+    """`groups` replicated C++ schedulers (runtime/scheduler.cpp) sharing one KV block manager;
+    new requests go to the least-loaded group (deterministic: ties -> lowest index)."""
+
+    def __init__(self, native, kv_manager, groups: int, max_batch: int, max_prefill_tokens: int):
+        self.group_batch = max(1, -(-max_batch // groups))
+        self.groups = [native.Scheduler(kv_manager, self.group_batch, max_prefill_tokens)
+                       for _ in range(groups)]
+        self.owner: dict[int, int] = {}
+
+    def add(self, rid: int, prompt_len: int, max_new: int) -> None:
+        g = min(range(len(self.groups)),
+                key=lambda i: (self.groups[i].num_running + self.groups[i].num_waiting, i))
+        self.groups[g].add(rid, prompt_len, max_new)
+        self.owner[rid] = g
+
+    def on_token(self, rid: int) -> None:
+        self.groups[self.owner[rid]].on_token(rid)
+
+    def finish(self, rid: int) -> None:
+        self.groups[self.owner.pop(rid)].finish(rid)
+
+    @property
+    def num_waiting(self) -> int:
+        return sum(g.num_waiting for g in self.groups)
+
+    @property
+    def num_running(self) -> int:
+        return sum(g.num_running for g in self.groups)
+
+    def running(self) -> list:
+        return [r for g in self.groups for r in g.running()]
+
+    def waiting(self) -> list:
+        return [r for g in self.groups for r in g.waiting()]
+
+
+@dataclass
+class PipePlan:
+    """One group's step plan travelling through the stages."""
+    tick: int                 # tick at which it entered stage 0
+    group: int
+    plan: object              # native StepPlan (kind 1 prefill / 2 decode)
+    rids: list
+    tokens: int               # rows of the residual stream between stages
+    cow: list = field(default_factory=list)
+    ids: Optional[object] = None   # sampled ids tensor (last stage / after broadcast)
+
+    @property
+    def kind(self) -> str:
+        return "prefill" if self.plan.kind == 1 else "decode"

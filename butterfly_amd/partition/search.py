@@ -8,8 +8,9 @@ compatible with the kv heads, pp <= layers, ep in {1, dp} for MoE):
      (runtime/partition_search.cpp), charging the embedding to stage 0, the LM head to the
      last stage and a boundary transfer to each cut, under the per-GPU memory capacity
      (weights + the stage's KV for its sequences);
-  3. estimate the steady-state step: pp == 1 -> the stage time; pp > 1 -> microbatched
-     pipeline, bounded by the slowest stage plus the fill/drain share;
+  3. estimate the steady-state step: pp == 1 -> the stage time; pp > 1 -> the asynchronous
+     pipeline's ticks (slowest stage x groups; engine/pipeline.py), or with BFLY_PP_ASYNC=0
+     the per-step microbatched pipeline, slowest stage plus the fill/drain share;
   4. score: throughput = generated tokens / s for the node, latency = step time.
 xGMI placement: a full mesh gives every GPU pair its own link, so no two logical edges
 (ring all-reduce neighbours, pipeline neighbours) ever share a link; the plan records the
@@ -23,6 +24,7 @@ from typing import Optional, Union
 from .._native_loader import native
 from ..config import ModelConfig
 from ..models.shard import Shard, local_dims
+from ..utils import flags
 from .costmodel import CostModel
 from .hw import MI355X, Hardware
 from .plan import PartitionPlan
@@ -78,9 +80,15 @@ def evaluate(cfg: ModelConfig, dp: int, tp: int, pp: int, ep: int, *, batch_per_
         stage_t.append(t)
     if pp == 1:
         step = stage_t[0]
+        step_latency = step
+    elif decode and ep == 1 and flags.get("BFLY_PP_ASYNC"):
+        # asynchronous pipeline (engine/pipeline.py): mb = pp groups in flight, one tick per
+        # group per stage, no fill/drain; a sequence gets a token every pp ticks
+        step = max(stage_t) * mb
+        step_latency = max(stage_t) * pp
     else:
         step = max(stage_t) * (mb + pp - 1) / mb * mb   # all microbatches through the pipe
-    step_latency = sum(stage_t) if pp > 1 else step
+        step_latency = sum(stage_t)
     tokens_per_step = global_batch if decode else global_batch * ctx
     tps = tokens_per_step / step
     weight_bytes, kv_budget = [], []

@@ -12,10 +12,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", ["tp2", "pp2", "dp2xep2"])
-def test_sharded_layout_on_one_gpu(layout):
+@pytest.mark.parametrize("layout,extra", [("tp2", []), ("pp2", []), ("dp2xep2", []),
+                                          ("pp2", ["-", "graphs"])])
+def test_sharded_layout_on_one_gpu(layout, extra):
     r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", "2", "--",
-                        sys.executable, os.path.join(ROOT, "tools", "gpu_dist_check.py"), layout],
+                        sys.executable, os.path.join(ROOT, "tools", "gpu_dist_check.py"), layout] + extra,
                        cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert r.stdout.count("PASS") == 2, r.stdout[-4000:]

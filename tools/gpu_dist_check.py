@@ -2,7 +2,7 @@
 """Sharded GPU model check on ONE GPU: N ranks share cuda:0 over gloo (RCCL refuses two ranks
 on one device), each runs its TP/PP shard through the HIP kernels, and the generated tokens
 must equal a single-process run of the same (partition-independent) weights.
-usage: python -m butterfly_amd launch -n 2 -- python tools/gpu_dist_check.py tp2|pp2|dp2ep2"""
+usage: python -m butterfly_amd launch -n 2 -- python tools/gpu_dist_check.py tp2|pp2|dp2ep2 [preset|-] [graphs]"""
 import os
 import sys
 
@@ -17,7 +17,8 @@ from butterfly_amd.parallel.comm import Communicator  # noqa: E402
 from butterfly_amd.parallel.mesh import Mesh  # noqa: E402
 
 layout = sys.argv[1]
-preset = sys.argv[2] if len(sys.argv) > 2 else ("mixtral-tiny" if "ep" in layout else "llama-small")
+preset = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "-" else ("mixtral-tiny" if "ep" in layout else "llama-small")
+graphs = len(sys.argv) > 3 and sys.argv[3] == "graphs"   # hipGraph decode (PP: per-group buckets)
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 torch.cuda.set_device(0)
 dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -28,7 +29,7 @@ for part in layout.split("x"):
 mesh = Mesh(**kw)
 cfg = ModelConfig.from_preset(preset)
 prompts = [[(7 * i + 3 * j) % cfg.vocab_size + 1 for j in range(5 + 3 * i)] for i in range(6)]
-ecfg = EngineConfig(max_batch=8, max_seq_len=256, kv_cache_tokens=4096, use_graphs=False, seed=3)
+ecfg = EngineConfig(max_batch=8, max_seq_len=256, kv_cache_tokens=4096, use_graphs=graphs, seed=3)
 params = SamplingParams(max_tokens=10, ignore_eos=True)
 dp = mesh.coord(rank).dp
 mine = prompts[dp::mesh.dp]
