@@ -440,6 +440,148 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// Decode ring GEMM (kind 3; decode batches of 65-256 rows, e.g. TP2 replicas at 128 rows).
+//
+// Measured on MI355X (tools/exp_dec.py, N 57344 x K 8192): gemm_tile at BM = 128 streams
+// weights at ~4.9-5.3 TB/s for ANY M (the time is flat in M: the kernel shape, not the
+// arithmetic, is the limit), while 64-row tiles at two 4-wave workgroups per CU reach
+// ~6.0 TB/s — but only for M <= 64 (a second row tile re-reads W through the per-CU load
+// path: 3.9 TB/s at M = 128). The per-CU LDS-DMA stream scales with the number of waves
+// issuing it, and X staged per K-tile competes with W for it. So this kernel:
+//  * runs 8 waves per workgroup (NWM along M x NWN along N), one workgroup per CU;
+//  * keeps X and W in separate LDS rings: X (L2-resident) needs 3 slots, W gets SW slots
+//    (up to 160 KiB in all), so SW-1 weight K-tiles stream while the MFMAs consume tile kt;
+//  * uses wide N tiles (BN up to 256: 224 makes N = 57344 exactly 256 tiles) so X is at most
+//    half of the staged bytes at BM = 128.
+// Issue order per iteration is W(kt+SW-1) then X(kt+2), so X(kt) is always the later of the
+// two loads tile kt needs and one counted vmcnt covers both: LW + LX loads were issued after
+// X(kt) in steady state; in the tail the wait is exact or conservative.
+// ---------------------------------------------------------------------------------------
+template <int ROWS, int NW>
+constexpr int ring_loads() { return (ROWS / 8 + NW - 1) / NW; }
+
+template <int ROWS, int NW>
+__device__ __forceinline__ void ring_stage(const bf16* __restrict__ src, long ld, int row0, int row_max,
+                                           int k0, char* lds, int wid, int lane, bool nt) {
+  constexpr int kBlocks = ROWS / 8;   // 8-row blocks of 1 KiB; one wave-instruction each
+#pragma unroll
+  for (int i = 0; i < ring_loads<ROWS, NW>(); ++i) {
+    int blk = i * NW + wid;
+    if (kBlocks % NW != 0) blk %= kBlocks;   // surplus lanes re-load a block (same bytes)
+    const int row = blk * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    int gr = row0 + row;
+    gr = gr < row_max ? gr : row_max - 1;
+    const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
+    if (nt)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 2);
+    else
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 0);
+  }
+}
+
+constexpr int kDecThreads = 512;
+
+template <int BM, int BN, int NWM, int NWN, int SW>
+__global__ void __launch_bounds__(kDecThreads)
+gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
+                int M, int N, int K, int epi, const bf16* __restrict__ bias,
+                bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+  constexpr int SX = 3, NW = NWM * NWN;
+  static_assert(NW * 64 <= kDecThreads && SW >= SX, "decode ring configuration");
+  constexpr int WM = BM / NWM, WN = BN / NWN;   // per-wave output block
+  constexpr int TI = WM / 16, TJ = WN / 16;
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "per-wave block must be whole MFMA tiles");
+  constexpr int XB = BM * kBK * 2, WB = BN * kBK * 2;
+  constexpr int LX = ring_loads<BM, NW>(), LW = ring_loads<BN, NW>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const xs = smem;
+  char* const wsm = smem + SX * XB;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / NWN, wn = wid % NWN;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int tile = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int tn = tile / mtiles, tm = tile % mtiles;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ktiles = K / kBK;
+  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
+  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
+  const bool w_nt = mtiles == 1 && g_tile_w_nt;   // each weight byte read by one workgroup
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue = the issue pattern of virtual iterations kt0-SW+1 .. kt0-1: W(kt0 .. kt0+SW-2)
+  // and, lagging by SW-SX, X(kt0 .. kt0+1). Slot of K-tile t: (t - kt0) mod S.
+#pragma unroll
+  for (int v = 0; v < SW - 1; ++v) {
+    if (kt0 + v < kt1) ring_stage<BN, NW>(W, ldw, n0, N, (kt0 + v) * kBK, wsm + v * WB, wid, lane, w_nt);
+    const int xv = v - (SW - SX);
+    if (xv >= 0 && kt0 + xv < kt1) ring_stage<BM, NW>(X, ldx, m0, M, (kt0 + xv) * kBK, xs + xv * XB, wid, lane, false);
+  }
+  int xslot = 0, wslot = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    // loads issued after X(kt): iteration kt-1's W(kt+SW-2) (if any) and X(kt+1) (if any)
+    if (kt + SW - 2 < kt1) vm_wait<LW + LX>();
+    else if (kt + 1 < kt1) vm_wait<LX>();
+    else vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // refill the slots every wave finished reading in iteration kt-1
+    const int wfill = wslot == 0 ? SW - 1 : wslot - 1;
+    const int xfill = xslot == 0 ? SX - 1 : xslot - 1;
+    if (kt + SW - 1 < kt1) ring_stage<BN, NW>(W, ldw, n0, N, (kt + SW - 1) * kBK, wsm + wfill * WB, wid, lane, w_nt);
+    if (kt + SX - 1 < kt1) ring_stage<BM, NW>(X, ldx, m0, M, (kt + SX - 1) * kBK, xs + xfill * XB, wid, lane, false);
+    const char* As = xs + xslot * XB;
+    const char* Bs = wsm + wslot * WB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TI];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = lds_frag(As, wm * WM + 16 * i + (lane & 15), ks * 4 + (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const bf16x8 b = lds_frag(Bs, wn * WN + 16 * j + (lane & 15), ks * 4 + (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < TI; ++i) acc[i][j] = mfma16(af[i], b, acc[i][j]);
+      }
+    }
+    if (++xslot == SX) xslot = 0;
+    if (++wslot == SW) wslot = 0;
+  }
+
+  // Epilogue: acc[i][j][r] = C[m0 + wm*WM + 16i + (lane>>4)*4 + r][n0 + wn*WN + 16j + (lane&15)]
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * WM + 16 * i + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int n = n0 + wn * WN + 16 * j + (lane & 15);
+        const float v = acc[i][j][r];
+        if (part) {
+          part[(long)blockIdx.y * M * N + (long)m * N + n] = v;
+        } else if (epi == EPI_SILU) {
+          if constexpr (TJ % 2 == 0) {   // gate/up 16-row groups pair up inside the wave
+            if (j & 1) continue;
+            const float u = acc[i][j + 1][r];
+            store_out(out, ldo, m, (n0 + wn * WN) / 2 + 16 * (j / 2) + (lane & 15), silu(v) * u);
+          }
+        } else {
+          store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Big-tile GEMM (prefill / large M): 256x256 tile, 8 waves (2 along M x 4 along N, each
 // owning a 128x64 output block = 8x4 MFMA 16x16x32 accumulators), BK = 32, 4-stage ring of
 // glds-staged K-tiles (4 x 32 KiB = 128 KiB LDS, one workgroup per CU). Per K-step a wave
@@ -654,6 +796,25 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
       sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr);
 }
 
+template <int BM, int BN, int NWM, int NWN, int SW>
+static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                    int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
+                    hipStream_t stream) {
+  init_nt_policy();
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  constexpr size_t lds = (size_t)(3 * BM + SW * BN) * kBK * 2;
+  static_assert(lds <= 160 * 1024, "decode GEMM rings exceed the 160 KiB LDS");
+  static bool attr_set = false;
+  if (!attr_set && lds > 65536) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_dec_kernel<BM, BN, NWM, NWN, SW>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid(tiles, sk);
+  gemm_dec_kernel<BM, BN, NWM, NWN, SW><<<grid, NWM * NWN * 64, lds, stream>>>(
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr);
+}
+
 static void run_big(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                     hipStream_t stream) {
@@ -774,6 +935,24 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     if (N % 256 != 0 || K % kBigBK != 0) return -1;
     if (p.sk > 1 && (long)((M + 255) / 256) * (N / 256) > kSplitCounters) return -1;
     if (!dry) run_big(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+  } else if (p.kind == 3) {
+    // decode ring GEMM: plan {3, SW (weight ring depth), waves, waves along M, BM, BN, sk}
+    if (N % p.bn != 0 || K % kBK != 0 || K / kBK < p.sk * 2) return -1;
+    const int nwn = p.wk > 0 ? p.nt / p.wk : 0;
+    if (epi == EPI_SILU && (nwn <= 0 || (p.bn / nwn) % 32 != 0)) return -1;
+    bool done = false;
+#define DEC_CASE(BM_, BN_, NWM_, NWN_, SW_)                                                      \
+  if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == NWM_ && p.nt == NWM_ * NWN_ && p.mt == SW_) { \
+    if (!dry) run_dec<BM_, BN_, NWM_, NWN_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream); \
+    done = true;                                                                                 \
+  }
+    DEC_CASE(128, 224, 8, 1, 4) DEC_CASE(128, 224, 8, 1, 3) DEC_CASE(128, 256, 8, 1, 3)
+    DEC_CASE(128, 256, 4, 2, 3) DEC_CASE(128, 128, 8, 1, 5) DEC_CASE(128, 128, 4, 2, 5)
+    DEC_CASE(128, 160, 8, 1, 4) DEC_CASE(128, 80, 8, 1, 6) DEC_CASE(128, 64, 8, 1, 8)
+    DEC_CASE(128, 64, 4, 2, 8) DEC_CASE(64, 128, 4, 2, 6) DEC_CASE(64, 256, 4, 2, 4)
+    DEC_CASE(64, 224, 4, 1, 4) DEC_CASE(64, 160, 4, 2, 5) DEC_CASE(64, 64, 4, 2, 8)
+#undef DEC_CASE
+    if (!done) return -2;
   } else if (p.kind == 0) {
     if (K % 128 != 0 || M > 16 * p.mt) return -1;
     if (N % (16 * p.nt * (4 / p.wk)) != 0) return -1;

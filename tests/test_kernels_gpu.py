@@ -269,6 +269,34 @@ def test_gemm_tile_plans(bm, bn, wmw, epi):
                 _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
 
 
+DEC_CFGS = [(128, 224, 8, 1, 4), (128, 224, 8, 1, 3), (128, 256, 8, 1, 3), (128, 256, 4, 2, 3), (128, 128, 8, 1, 5),
+            (128, 128, 4, 2, 5), (128, 160, 8, 1, 4), (128, 80, 8, 1, 6), (128, 64, 8, 1, 8), (128, 64, 4, 2, 8),
+            (64, 128, 4, 2, 6), (64, 256, 4, 2, 4), (64, 224, 4, 1, 4), (64, 160, 4, 2, 5), (64, 64, 4, 2, 8)]
+
+
+@pytest.mark.parametrize("bm,bn,nwm,nwn,sw", DEC_CFGS)
+def test_gemm_decode_ring_plans(bm, bn, nwm, nwn, sw):
+    """Decode ring GEMM (plan kind 3, separate X / W LDS rings): ragged M (< BM, and > BM so
+    two row tiles share a weight panel), K-tile counts shorter than the weight ring (tail
+    waits), uneven split-K, all epilogues that the tile width allows."""
+    N = 3 * bn
+    for M, K in ((bm - 5, 1024), (bm + 9, 192), (bm // 2, 4096)):
+        x = _bf(M, K, seed=44)
+        w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=45)
+        b = _bf(N, seed=46)
+        for epi in ("none", "bias", "silu") if (bn // nwn) % 32 == 0 else ("none", "bias"):
+            nout = N // 2 if epi == "silu" else N
+            want = ref.linear(x, w, b if epi == "bias" else None, "silu" if epi == "silu" else "none")
+            for sk in (1, 3):
+                if K // 64 < 2 * sk:
+                    continue
+                out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+                ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
+                torch.ops.bfly.gemm_with_plan(x, w, out, [3, sw, nwm * nwn, nwm, bm, bn, sk], ops.EPILOGUES[epi], ws,
+                                              b if epi == "bias" else None)
+                _close(out, want, 2e-2, 2e-2)
+
+
 @pytest.mark.parametrize("mt,nt,wk", [(1, 1, 4), (1, 2, 1), (1, 4, 4), (2, 2, 2), (2, 4, 1), (4, 1, 4), (4, 2, 1), (4, 4, 4), (3, 2, 2)])
 def test_gemm_skinny_plans(mt, nt, wk):
     M, N, K = 16 * mt - 3, 512, 1024

@@ -33,6 +33,10 @@ SHAPES = {
 }
 
 
+DEC_CFGS = [(128, 224, 8, 1, 4), (128, 224, 8, 1, 3), (128, 256, 8, 1, 3), (128, 256, 4, 2, 3), (128, 128, 8, 1, 5),
+            (128, 128, 4, 2, 5), (128, 160, 8, 1, 4), (128, 80, 8, 1, 6), (128, 64, 8, 1, 8), (128, 64, 4, 2, 8),
+            (64, 128, 4, 2, 6), (64, 256, 4, 2, 4), (64, 224, 4, 1, 4), (64, 160, 4, 2, 5), (64, 64, 4, 2, 8)]
+
 SERIAL = False
 LOG = None
 
@@ -89,7 +93,7 @@ def main():
                 nout = N // 2 if epi == "silu" else N
                 out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
                 plan = ops.gemm_plan(M, N, K)
-                auto = [("skinny", "tile", "big").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
+                auto = [("skinny", "tile", "big", "dec").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
                         plan["bn"], plan["splitk"]]
                 t = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, Ws[i % copies], out, auto, ops.EPILOGUES[epi], ws),
                            tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": auto, "auto": True})
@@ -120,6 +124,13 @@ def main():
                                     if st * (bm + bn) * 128 > 160 * 1024:
                                         continue
                                     cands.append([1, st, 0, wmw, bm, bn, sk])
+                    # decode ring GEMM (kind 3): separate activation / weight LDS rings
+                    for bm, bn, nwm, nwn, sw in DEC_CFGS if 16 < M <= 256 else ():
+                        if N % bn or (bm == 128 and M <= 48) or (epi == "silu" and (bn // nwn) % 32):
+                            continue
+                        for sk in (1, 2, 4, 8):
+                            if K // 64 >= sk * 8:
+                                cands.append([3, sw, nwm * nwn, nwm, bm, bn, sk])
                     if M >= 128 and N % 256 == 0:
                         for sk in (1, 2, 4):
                             if K // 32 >= sk * 8:
