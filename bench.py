@@ -49,6 +49,11 @@ def parse_plan(s: str, n: int):
     return d
 
 
+def sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 def log(msg, rank=0):
     if rank == 0:
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -71,7 +76,8 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        # one GPU per rank; ranks sharing a GPU (gloo test mode) all use device 0
+        torch.cuda.set_device(local % torch.cuda.device_count())
     cfg = ModelConfig.from_preset(a.model)
     plan = partition(cfg, a.gpus, parse_plan(a.plan, a.gpus), batch_per_gpu=a.batch_per_gpu,
                      ctx=a.prompt_len + a.warmup + a.steps)
@@ -89,7 +95,7 @@ def main():
                         graph_batch_sizes=[replica_batch])
     t0 = time.perf_counter()
     eng = LLMEngine(cfg, mesh, ecfg, comm=comm, stage_layers=plan.stages)
-    torch.cuda.synchronize()
+    sync()
     log(f"engine ready in {time.perf_counter() - t0:.1f}s: {eng.model.local_bytes() / 1e9:.1f} GB weights/rank, "
         f"KV {eng.kv.bytes() / 1e9:.1f} GB ({eng.kv.capacity_tokens} tokens)", rank)
 
@@ -110,14 +116,14 @@ def main():
         out = eng.step()
         prefill_tokens += sum(len(eng.requests[r].prompt) for r in out.rids) if out.kind == "prefill" else 0
         decode_streak = decode_streak + 1 if out.kind == "decode" else 0
-    torch.cuda.synchronize()
+    sync()
     prefill_s = time.perf_counter() - tp0
     log(f"prefill {prefill_tokens} tokens in {prefill_s:.2f}s ({prefill_tokens / prefill_s:.0f} tok/s/replica)", rank)
     for _ in range(a.warmup):
         eng.step()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     step_times = []
     gen_tokens = 0
     t_start = time.perf_counter()
@@ -127,14 +133,15 @@ def main():
         step_times.append(time.perf_counter() - ts)
         assert out.kind == "decode", out.kind
         gen_tokens += len(out.new_tokens)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if replica_batch % groups == 0:   # every step carried one full group
         assert gen_tokens == a.steps * replica_batch // groups, (gen_tokens, a.steps, replica_batch, groups)
     if world > 1:
-        t = torch.tensor([elapsed, gen_tokens], dtype=torch.float64, device="cuda")
+        dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed, gen_tokens], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0].item())
     # tokens of the whole node: every DP replica generates gen_tokens (same work per replica)
@@ -160,13 +167,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": (value / ref) if ref else None,
-        "dtype": "bf16",
+        "dtype": {torch.bfloat16: "bf16", torch.float32: "fp32"}.get(eng.model.dtype, str(eng.model.dtype)),
         "data": "synthetic random prompts; random-init weights (deterministic hash init)",
         "prefill_tokens_per_s_per_replica": round(prefill_tokens / prefill_s, 1),
         "config": {"model": "Llama-3-70B" if a.model == "llama3-70b" else a.model,
                    "global_batch": a.batch_per_gpu * a.gpus, "seq_len": a.prompt_len,
                    "parallelism": plan.name, "stages": [list(s) for s in plan.stages],
-                   "hipgraph": not a.no_graphs, "pp_async_groups": groups if groups > 1 else None},
+                   "hipgraph": eng.runner.use_graphs, "pp_async_groups": groups if groups > 1 else None},
     }
     if rank == 0:
         line = json.dumps(res)

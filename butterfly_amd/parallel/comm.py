@@ -255,7 +255,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] =
     if world == 1 or dist.is_initialized():
         return (dist.get_rank(), dist.get_world_size(), local) if dist.is_initialized() else (0, 1, 0)
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        from ..utils import flags
+
+        backend = flags.get("BFLY_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     t = timeout_s or float(os.environ.get("BFLY_COMM_TIMEOUT_S", "600"))

@@ -45,6 +45,8 @@ define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped
 define("BFLY_EP_ALLTOALL", True, _bool, "EP MoE on prefill steps: dispatch tokens by all-to-all (else all-gather / reduce-scatter)")
 define("BFLY_PP_ASYNC", True, _bool, "pipeline parallelism: keep pp decode groups in flight across steps "
        "(one group per stage per tick, no fill/drain bubble) instead of per-step microbatching")
+define("BFLY_DIST_BACKEND", "", str, "torch.distributed backend override for init_distributed (default: nccl "
+       "= RCCL with a GPU, gloo without; gloo lets several ranks share one GPU in tests)")
 define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
 define("BFLY_STEP_TIMEOUT_S", 0.0, float, "engine step watchdog: terminate a rank whose step exceeds this (0 = off)")

@@ -20,3 +20,22 @@ def test_sharded_layout_on_one_gpu(layout, extra):
                        cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert r.stdout.count("PASS") == 2, r.stdout[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plan", ["tp2", "pp2"])
+def test_bench_two_ranks_on_one_gpu(plan):
+    """bench.py's multi-rank path on the GPU (ranks share cuda:0 over gloo): hipGraph decode,
+    the IPC all-reduce (tp2) / asynchronous pipeline (pp2), rank 0's JSON line."""
+    import json
+
+    env = dict(os.environ, BFLY_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", "2", "--",
+                        sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "llama-small",
+                        "--plan", plan, "--steps", "8", "--warmup", "2", "--batch-per-gpu", "8",
+                        "--prompt-len", "64"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    lines = [l.split("] ", 1)[1] for l in r.stdout.splitlines() if l.startswith("[rank0] {")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["config"]["parallelism"] == plan and res["value"] > 0 and res["dtype"] == "bf16"
