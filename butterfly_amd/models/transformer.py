@@ -74,10 +74,13 @@ class TransformerLM:
         self.last = shard.is_last(cfg)
         self.tp = shard.tp_size
         self.ep = shard.ep_size
-        # fuse split-K GEMM reduces into the consuming norm / rope kernels (GPU, no TP
-        # all-reduce in between, RMSNorm models)
-        self.defer_reduce = (self.device.type == "cuda" and self.tp == 1 and cfg.norm == "rms"
-                             and flags.get("BFLY_DEFER_REDUCE"))
+        # fuse split-K GEMM reduces into the consuming kernels: QKV -> rope_kv always (no
+        # collective in between), O / down -> add+rmsnorm when no TP all-reduce sits between
+        defer = self.device.type == "cuda" and flags.get("BFLY_DEFER_REDUCE")
+        self.defer_qkv = defer and cfg.pos_emb == "rope"
+        # (tp > 1: the IPC all-reduce takes the split-K slabs and reduces them in its publish)
+        self.defer_reduce = defer and cfg.norm == "rms" and (
+            self.tp == 1 or getattr(self.comm, "custom_ar", None) is not None)
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
@@ -313,8 +316,7 @@ class TransformerLM:
                 x = self._add_norm(delta, pre + "in", residual, partial)
             # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
             # when no all-reduce sits in between (tp == 1)
-            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"),
-                             defer=self.defer_reduce and c.pos_emb == "rope")
+            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
             kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
             slots = fb.slots if kc is not None else None
             if c.pos_emb == "rope":
@@ -338,8 +340,8 @@ class TransformerLM:
             if delta is None:
                 return residual
             if partial:
-                self.comm.all_reduce_(delta, "tp")
-            return ops.add(residual, delta)
+                delta = self.comm.all_reduce_(delta, "tp")
+            return ops.add(residual, ops.materialize(delta))
         idx = fb.logits_idx
         r = residual if idx is None else residual.index_select(0, idx)
         if delta is not None:
@@ -359,7 +361,7 @@ class TransformerLM:
         if partial:
             if self.cfg.norm == "rms":
                 return self.comm.all_reduce_rms_norm_(t, w, self.cfg.norm_eps, residual, "tp")
-            self.comm.all_reduce_(t, "tp")
+            t = self.comm.all_reduce_(t, "tp")
         return self._norm(t, w, b, residual=residual)
 
     def _ffn(self, pre: str, x: torch.Tensor, fb: ForwardBatch) -> tuple:

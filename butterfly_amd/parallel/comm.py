@@ -95,14 +95,21 @@ class Communicator:
         return self.groups[group].rank_in_group
 
     # -- collectives --------------------------------------------------------------------------
-    def all_reduce_(self, t: torch.Tensor, group: str = "tp") -> torch.Tensor:
+    def all_reduce_(self, t, group: str = "tp") -> torch.Tensor:
+        """In-place sum over the group; returns the reduced tensor. `t` may be a deferred
+        split-K GEMM output (ops.Partial): the IPC kernel reduces its slabs while publishing,
+        any other path materialises it first."""
+        from .. import ops
+
         g = self.groups[group]
         if g.size == 1:
-            return t
+            return ops.materialize(t)
         self.stats["calls"] += 1
-        self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+        self.stats["all_reduce_bytes"] += t.shape[0] * t.shape[1] * 2 if isinstance(t, ops.Partial) \
+            else t.numel() * t.element_size()
         if group == "tp" and self.custom_ar is not None and self.custom_ar.should_use(t):
             return self.custom_ar.all_reduce_(t)
+        t = ops.materialize(t)
         dist.all_reduce(t, group=g.pg)
         return t
 
@@ -111,15 +118,15 @@ class Communicator:
         """residual += all_reduce(t); return rms_norm(residual) * w — one fused kernel on the
         IPC path (the all-reduce feeding every transformer block's add+norm), else RCCL
         all-reduce followed by the fused add+norm kernel."""
+        from .. import ops
+
         g = self.groups[group]
         car = self.custom_ar
         if g.size > 1 and group == "tp" and car is not None and car.should_use(t):
             self.stats["calls"] += 1
-            self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
+            self.stats["all_reduce_bytes"] += t.shape[0] * t.shape[1] * 2
             return car.all_reduce_rms_norm_(t, w, eps, residual)
-        from .. import ops
-
-        self.all_reduce_(t, group)
+        t = self.all_reduce_(t, group)
         return ops.rms_norm(t, w, eps, residual=residual)
 
     def enable_custom_all_reduce(self, max_bytes: int) -> bool:

@@ -66,21 +66,32 @@ class CustomAllReduce:
             self.ok = self._self_test(pg)
 
     # ---------------------------------------------------------------------------------------
-    def should_use(self, t: torch.Tensor) -> bool:
+    def should_use(self, t) -> bool:
+        if isinstance(t, ops.Partial):   # split-K slabs: reduced inside the all-reduce kernel
+            t = t.out
         return (self.ok and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2
                 and t.is_contiguous() and t.shape[1] % 8 == 0 and t.shape[1] <= 16384
                 and t.numel() * 2 <= self.cap and t.data_ptr() % 16 == 0)
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce_(self, t) -> torch.Tensor:
+        """In place; `t` may be a deferred split-K GEMM output (ops.Partial), whose reduce the
+        kernel fuses into its publish step (the result lands in t.out)."""
+        if isinstance(t, ops.Partial):
+            torch.ops.bfly.custom_all_reduce(t.out, t.out, None, None, 0.0, self.bases, self.rank, self.cap, t.slabs)
+            return t.out
         torch.ops.bfly.custom_all_reduce(t, t, None, None, 0.0, self.bases, self.rank, self.cap)
         return t
 
-    def all_reduce_rms_norm_(self, t: torch.Tensor, w: torch.Tensor, eps: float,
+    def all_reduce_rms_norm_(self, t, w: torch.Tensor, eps: float,
                              residual: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """residual += all_reduce(t) (bf16), returns rms_norm(residual) * w."""
+        """residual += all_reduce(t) (bf16), returns rms_norm(residual) * w. `t` may be an
+        ops.Partial (split-K slabs reduced in the kernel)."""
+        slabs = None
+        if isinstance(t, ops.Partial):
+            t, slabs = t.out, t.slabs
         if out is None:
             out = torch.empty_like(t)
-        torch.ops.bfly.custom_all_reduce(t, out, residual, w, float(eps), self.bases, self.rank, self.cap)
+        torch.ops.bfly.custom_all_reduce(t, out, residual, w, float(eps), self.bases, self.rank, self.cap, slabs)
         return out
 
     def error(self) -> int:

@@ -521,7 +521,7 @@ int64_t car_error(int64_t p) { return bfly::car_error(reinterpret_cast<const voi
 
 void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tensor>& residual,
                        const c10::optional<Tensor>& w, double eps, at::IntArrayRef bases,
-                       int64_t rank, int64_t cap) {
+                       int64_t rank, int64_t cap, const c10::optional<Tensor>& slabs) {
   CHECK_GPU(inp); CHECK_BF16(inp); CHECK_BF16(out);
   TORCH_CHECK(inp.dim() == 2 && inp.is_contiguous() && out.is_contiguous() &&
                   out.sizes() == inp.sizes(), "custom_all_reduce: 2-D contiguous, same shape");
@@ -549,9 +549,20 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tenso
     res = bf(r);
     wp = bf(*w);
   }
+  const float* sp = nullptr;
+  int sk = 0;
+  if (slabs.has_value()) {   // inp is then only the shape / output placeholder
+    const Tensor& sl = *slabs;
+    CHECK_GPU(sl);
+    TORCH_CHECK(sl.scalar_type() == at::kFloat && sl.dim() == 3 && sl.is_contiguous() &&
+                    sl.size(1) == rows && sl.size(2) == dim, "custom_all_reduce: slabs [sk, rows, dim] f32");
+    CHECK_ALIGN16(sl);
+    sp = sl.data_ptr<float>();
+    sk = (int)sl.size(0);
+  }
   c10::DeviceGuard g(inp.device());
   const int rc = bfly::launch_custom_allreduce(bf(inp), bf(out), res, wp, (float)eps, rows, dim,
-                                               peers, world, (int)rank, cap, cur_stream());
+                                               peers, world, (int)rank, cap, cur_stream(), sp, sk);
   TORCH_CHECK(rc == 0, "custom_all_reduce: launch rejected (", rc, ")");
 }
 
@@ -604,7 +615,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("car_error(int ptr) -> int", &car_error);
   m.def("car_buffer_bytes(int cap) -> int", [](int64_t cap) -> int64_t { return bfly::car_buffer_bytes(cap); });
   m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, Tensor(b!)? residual, Tensor? w, float eps, "
-        "int[] bases, int rank, int cap) -> ()");
+        "int[] bases, int rank, int cap, Tensor? slabs=None) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
         "bool causal, Tensor(a!) out) -> ()");
 }

@@ -55,7 +55,7 @@ template <int W, int MODE, int NV>
 __global__ void __launch_bounds__(kArThreads)
 allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __restrict__ residual,
                  const bf16* __restrict__ w, float eps, int rows, int dim, ArPeers peers,
-                 int rank, long cap) {
+                 int rank, long cap, const float* __restrict__ slabs, int sk) {
   __shared__ uint32_t s_epoch;
   __shared__ float red[16];
   const int b = blockIdx.x;
@@ -67,13 +67,35 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
   const long data_off = kArDataOff + (long)(e & 1) * cap;
   const int nvec = dim >> 3;
 
-  // 1. publish this rank's rows
+  // 1. publish this rank's rows. With `slabs` the input is a split-K GEMM's f32 partials
+  // [sk][rows][dim]: their reduce (rounded to bf16, exactly what the reduce kernel would
+  // have written) is fused into the publish, and the local operand is read back from `mine`.
   bf16* mine = reinterpret_cast<bf16*>(my + data_off);
+  const long slab = (long)rows * dim;
   for (int r = b; r < rows; r += kArBlocks) {
-    const bf16x8* src = reinterpret_cast<const bf16x8*>(in + (long)r * dim);
     bf16x8* dst = reinterpret_cast<bf16x8*>(mine + (long)r * dim);
-    for (int c = threadIdx.x; c < nvec; c += kArThreads) dst[c] = src[c];
+    if (slabs != nullptr) {
+      for (int c = threadIdx.x; c < nvec; c += kArThreads) {
+        const float* sp = slabs + (long)r * dim + c * 8;
+        f32x4 lo = *reinterpret_cast<const f32x4*>(sp), hi = *reinterpret_cast<const f32x4*>(sp + 4);
+        for (int q = 1; q < sk; ++q) {
+          lo += *reinterpret_cast<const f32x4*>(sp + q * slab);
+          hi += *reinterpret_cast<const f32x4*>(sp + q * slab + 4);
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = f2bf(lo[j]);
+          o[j + 4] = f2bf(hi[j]);
+        }
+        dst[c] = o;
+      }
+    } else {
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(in + (long)r * dim);
+      for (int c = threadIdx.x; c < nvec; c += kArThreads) dst[c] = src[c];
+    }
   }
+  const bf16* own = slabs != nullptr ? mine : in;   // this rank's operand for the sum
   __threadfence_system();
   __syncthreads();
 
@@ -98,7 +120,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
         bf16x8 v[W];
 #pragma unroll
         for (int p = 0; p < W; ++p)
-          v[p] = p == rank ? reinterpret_cast<const bf16x8*>(in + ro)[c]
+          v[p] = p == rank ? reinterpret_cast<const bf16x8*>(own + ro)[c]
                            : reinterpret_cast<const bf16x8*>(src[p] + ro)[c];
         float acc[8];
 #pragma unroll
@@ -122,7 +144,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
           bf16x8 x[W];
 #pragma unroll
           for (int p = 0; p < W; ++p)
-            x[p] = p == rank ? reinterpret_cast<const bf16x8*>(in + ro)[c]
+            x[p] = p == rank ? reinterpret_cast<const bf16x8*>(own + ro)[c]
                              : reinterpret_cast<const bf16x8*>(src[p] + ro)[c];
           const bf16x8 rr = reinterpret_cast<const bf16x8*>(residual + ro)[c];
           bf16x8 s;
@@ -159,24 +181,25 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
 
 template <int W>
 int launch_w(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps, int rows,
-             int dim, const ArPeers& peers, int rank, long cap, hipStream_t stream) {
+             int dim, const ArPeers& peers, int rank, long cap, const float* slabs, int sk,
+             hipStream_t stream) {
   const dim3 grid(kArBlocks), block(kArThreads);
   if (residual == nullptr) {
     allreduce_kernel<W, 0, 1><<<grid, block, 0, stream>>>(in, out, nullptr, nullptr, 0.f, rows,
-                                                          dim, peers, rank, cap);
+                                                          dim, peers, rank, cap, slabs, sk);
     return 0;
   }
   const int nv = (dim / 8 + kArThreads - 1) / kArThreads;
 #define AR_NV(N)                                                                          \
   case N:                                                                                 \
     allreduce_kernel<W, 1, N><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, \
-                                                          dim, peers, rank, cap);         \
+                                                          dim, peers, rank, cap, slabs, sk); \
     return 0;
   switch (nv) {
     AR_NV(1) AR_NV(2) AR_NV(4) AR_NV(8)
-    case 3: allreduce_kernel<W, 1, 4><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, dim, peers, rank, cap); return 0;
+    case 3: allreduce_kernel<W, 1, 4><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk); return 0;
     case 5: case 6: case 7:
-      allreduce_kernel<W, 1, 8><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, dim, peers, rank, cap);
+      allreduce_kernel<W, 1, 8><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk);
       return 0;
     default: return -1;
   }
@@ -187,14 +210,15 @@ int launch_w(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps
 
 int launch_custom_allreduce(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
                             int rows, int dim, const ArPeers& peers, int world, int rank,
-                            long cap, hipStream_t stream) {
+                            long cap, hipStream_t stream, const float* slabs, int sk) {
   if (dim % 8 != 0 || dim > 16384 || rows < 0) return -2;
+  if (slabs != nullptr && sk < 1) return -6;
   if ((long)rows * dim * 2 > cap) return -3;
   if (rank < 0 || rank >= world) return -4;
   switch (world) {
-    case 2: return launch_w<2>(in, out, residual, w, eps, rows, dim, peers, rank, cap, stream);
-    case 4: return launch_w<4>(in, out, residual, w, eps, rows, dim, peers, rank, cap, stream);
-    case 8: return launch_w<8>(in, out, residual, w, eps, rows, dim, peers, rank, cap, stream);
+    case 2: return launch_w<2>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+    case 4: return launch_w<4>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+    case 8: return launch_w<8>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
     default: return -5;
   }
 }

@@ -68,6 +68,45 @@ for salt, (rows, dim) in enumerate([(64, 8192), (3, 4096), (200, 8192)]):
     if err > 1e-2 * max(1.0, y_ref.float().abs().max().item()):
         fails.append(f"fused norm {rows}x{dim}: {err:.3e}")
 
+# 2b. split-K slab input (ops.Partial): the kernel reduces the f32 slabs while publishing;
+#     equal to splitk_reduce -> all-reduce (-> add + RMSNorm)
+for salt, (sk, rows, dim) in enumerate([(4, 64, 8192), (3, 5, 4096), (8, 128, 8192)]):
+    slabs = [(torch.randn(sk, rows, dim, generator=torch.Generator().manual_seed(300 + 10 * salt + r)) * 0.3)
+             .to(dev) for r in range(world)]
+    parts = []
+    for r in range(world):
+        o = torch.empty(rows, dim, dtype=torch.bfloat16, device=dev)
+        torch.ops.bfly.splitk_reduce(slabs[r].contiguous(), o)
+        parts.append(o)
+    s = torch.zeros(rows, dim, device=dev)
+    for o in parts:
+        s += o.float()
+    s = s.to(torch.bfloat16)
+    y = car.all_reduce_(ops.Partial(slabs[rank].contiguous(), torch.empty(rows, dim, dtype=torch.bfloat16, device=dev)))
+    torch.cuda.synchronize()
+    # the slab sum may round differently from splitk_reduce's (fast-math reassociation): within
+    # one bf16 ulp of it, and bitwise identical on every rank
+    err = (y.float() - s.float()).abs().max().item()
+    if err > 8e-3 * max(1.0, s.float().abs().max().item()):
+        fails.append(f"slab sum sk={sk} {rows}x{dim}: max err {err:.3e}")
+    ys = [torch.empty_like(y).cpu() for _ in range(world)]
+    dist.all_gather(ys, y.cpu())
+    if not all(torch.equal(ys[0], t) for t in ys):
+        fails.append(f"slab sum sk={sk} {rows}x{dim}: ranks disagree")
+    w = data(1, dim, 78, 60 + salt).view(dim)
+    res0 = data(rows, dim, 98, 60 + salt)
+    res_ref = res0.clone()
+    y_ref = ops.rms_norm(s, w, 1e-5, residual=res_ref)
+    res = res0.clone()
+    y = car.all_reduce_rms_norm_(ops.Partial(slabs[rank].contiguous(), torch.empty(rows, dim, dtype=torch.bfloat16,
+                                                                                    device=dev)), w, 1e-5, res)
+    torch.cuda.synchronize()
+    if (res.float() - res_ref.float()).abs().max().item() > 1.6e-2 * max(1.0, res_ref.float().abs().max().item()):
+        fails.append(f"slab fused residual sk={sk} {rows}x{dim}")
+    err = (y.float() - y_ref.float()).abs().max().item()
+    if err > 1e-2 * max(1.0, y_ref.float().abs().max().item()):
+        fails.append(f"slab fused norm sk={sk} {rows}x{dim}: {err:.3e}")
+
 # 3. graph capture / replay
 x = data(64, 8192, rank, 7)
 buf = x.clone()
