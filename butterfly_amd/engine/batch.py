@@ -23,6 +23,7 @@ class ForwardBatch:
     logits_idx: Optional[torch.Tensor] = None    # int64 [R] rows that need logits (None = all)
     ep_tokens: int = 0                           # EP: token rows every rank pads to (0 = no pad)
     ep_alltoall: bool = False                    # EP: this step dispatches tokens by all-to-all
+    cp: Optional[object] = None                  # prefill over a context-parallel group (CPContext)
 
     @property
     def num_tokens(self) -> int:
@@ -39,7 +40,7 @@ class ForwardBatch:
         return ForwardBatch(mv(self.input_ids), mv(self.positions), mv(self.slots), self.is_prefill,
                             mv(self.cu_seqlens), self.max_seqlen, mv(self.block_tables),
                             mv(self.ctx_lens), self.max_ctx, mv(self.logits_idx), self.ep_tokens,
-                            self.ep_alltoall)
+                            self.ep_alltoall, self.cp)
 
 
 def make_prefill_batch(prompts: list[list[int]], slots: list[list[int]], device="cpu",

@@ -329,7 +329,12 @@ class TransformerLM:
             if fb.is_prefill:
                 k = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
                 v = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
-                attn = ops.attn_prefill(q, k, v, fb.cu_seqlens, fb.max_seqlen, self.scale, True)
+                if fb.cp is not None:   # context parallel: K/V chunks circulate over the group
+                    from ..parallel.context_parallel import ring_attention
+
+                    attn = ring_attention(q, k, v, fb.cp, self.scale)
+                else:
+                    attn = ops.attn_prefill(q, k, v, fb.cu_seqlens, fb.max_seqlen, self.scale, True)
             else:
                 attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
             o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None

@@ -278,13 +278,27 @@ def gemm_plan(M: int, N: int, K: int) -> dict:
 
 
 def attn_prefill(q, k, v, cu_seqlens, max_seqlen: int, scale: float, causal: bool = True,
-                 out=None):
+                 out=None, cu_seqlens_k=None, return_lse: bool = False):
+    """Varlen flash attention (K3). `cu_seqlens_k`: keys of each sequence come from other
+    rows than its queries (non-causal; context-parallel ring steps). `return_lse`: also return
+    the per-(row, head) natural-log sum-exp of the scaled scores [T, Hq] f32 (-inf: no keys),
+    which `attn_lse_merge_` uses to combine attention over key chunks."""
     if not _gpu(q):
-        return ref.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out)
+        return ref.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out, cu_seqlens_k, return_lse)
     if out is None:
         out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
-    torch.ops.bfly.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out)
-    return out
+    lse = torch.empty(q.shape[0], q.shape[1], dtype=torch.float32, device=q.device) if return_lse else None
+    torch.ops.bfly.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out, cu_seqlens_k, lse)
+    return (out, lse) if return_lse else out
+
+
+def attn_lse_merge_(acc_o, acc_lse, o, lse):
+    """K16: fold a partial attention result (o bf16 [T, H, D], lse [T, H]) into running f32
+    accumulators (acc_o [T, H, D], acc_lse [T, H]) in place."""
+    if not _gpu(acc_o):
+        return ref.attn_lse_merge_(acc_o, acc_lse, o, lse)
+    torch.ops.bfly.attn_lse_merge(acc_o, acc_lse, o, lse)
+    return acc_o, acc_lse
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_ctx: int,

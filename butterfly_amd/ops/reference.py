@@ -205,31 +205,50 @@ def linear(x, w, bias=None, epilogue="none", out=None):
     return out
 
 
-def attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal=True, out=None):
-    """q [T, Hq, D], k/v [T, Hkv, D]; varlen sequences given by cu_seqlens (int32)."""
+def attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal=True, out=None, cu_seqlens_k=None,
+                 return_lse=False):
+    """q [T, Hq, D], k/v [Tk, Hkv, D]; varlen sequences given by cu_seqlens (int32), keys by
+    cu_seqlens_k (default: the same rows). With return_lse also returns ln sum exp(scaled
+    scores) per (row, head) [T, Hq] f32, -inf where a row sees no key."""
     T, Hq, D = q.shape
     Hkv = k.shape[1]
     G = Hq // Hkv
-    res = torch.empty(T, Hq, D, dtype=q.dtype, device=q.device)
+    res = torch.zeros(T, Hq, D, dtype=q.dtype, device=q.device)
+    lse = torch.full((T, Hq), float("-inf"), dtype=torch.float32, device=q.device)
     cu = cu_seqlens.tolist()
+    cuk = cu_seqlens_k.tolist() if cu_seqlens_k is not None else cu
     for i in range(len(cu) - 1):
         a, b = cu[i], cu[i + 1]
-        if b <= a:
+        ka, kb = cuk[i], cuk[i + 1]
+        if b <= a or kb <= ka:
             continue
         qs = q[a:b].float().transpose(0, 1)                       # [Hq, L, D]
-        ks = k[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
-        vs = v[a:b].float().transpose(0, 1).repeat_interleave(G, 0)
+        ks = k[ka:kb].float().transpose(0, 1).repeat_interleave(G, 0)
+        vs = v[ka:kb].float().transpose(0, 1).repeat_interleave(G, 0)
         s = (qs @ ks.transpose(1, 2)) * scale
         if causal:
             L = b - a
-            mask = torch.ones(L, L, dtype=torch.bool, device=q.device).triu(1)
+            mask = torch.ones(L, kb - ka, dtype=torch.bool, device=q.device).triu(1)
             s = s.masked_fill(mask, float("-inf"))
+        lse[a:b] = torch.logsumexp(s, -1).transpose(0, 1)
         p = torch.softmax(s, -1)
         res[a:b] = (p @ vs).transpose(0, 1).to(q.dtype)
-    if out is None:
-        return res
-    out.copy_(res)
-    return out
+    if out is not None:
+        out.copy_(res)
+        res = out
+    return (res, lse) if return_lse else res
+
+
+def attn_lse_merge_(acc_o, acc_lse, o, lse):
+    """acc_lse <- log(e^acc_lse + e^lse); acc_o <- weighted mix of acc_o and o (in place)."""
+    new = torch.logaddexp(acc_lse, lse)
+    ok = new > float("-inf")
+    wa = torch.where(ok, torch.exp(acc_lse - new), torch.zeros_like(new))
+    wb = torch.where(ok, torch.exp(lse - new), torch.zeros_like(new))
+    mixed = acc_o * wa.unsqueeze(-1) + o.float() * wb.unsqueeze(-1)
+    acc_o.copy_(torch.where(ok.unsqueeze(-1), mixed, acc_o))
+    acc_lse.copy_(torch.where(ok, new, acc_lse))
+    return acc_o, acc_lse
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx=None,

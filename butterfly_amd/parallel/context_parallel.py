@@ -1,0 +1,160 @@
+"""Context parallelism (CP): one long prompt's prefill split by sequence position over a group
+of ranks, with ring attention (SURVEY.md §2.6 "CP / ring attention", §5.7; K16 LSE merge).
+
+Layout: every sequence of the batch is cut into `cp` contiguous chunks, chunk r on cp rank r
+(the remainder goes to the LAST ranks, so the final token — the one that needs logits — is on
+the last rank for every non-empty sequence). Each rank runs the full model (weights replicated
+over the CP group; TP inside it is orthogonal) on its own tokens only: projections, MLP and
+norms touch 1/cp of the tokens and the KV cache holds only the rank's chunk.
+
+Attention (`ring_attention`): the local queries first attend causally to the local keys; then
+the K/V chunks travel around the ring (rank r sends to r+1 and receives from r-1, cp-1 steps).
+A chunk that came from an earlier position (source rank < r) is fully visible: non-causal flash
+attention over it returns a partial output and its log-sum-exp, merged into f32 accumulators by
+the LSE-merge kernel; chunks from later positions are masked entirely and only relayed. The
+transfer of step j+1 is posted before step j's attention runs, so on RCCL the K/V hop over
+xGMI overlaps the flash-attention kernel. The result equals single-device causal attention up to
+floating-point reassociation (tests/test_context_parallel.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+
+def split_lengths(L: int, cp: int) -> list[int]:
+    """Chunk lengths of an L-token sequence over cp ranks (remainder to the last ranks)."""
+    base, extra = divmod(L, cp)
+    return [base + (1 if r >= cp - extra else 0) for r in range(cp)]
+
+
+@dataclass
+class CPContext:
+    """Static description of one context-parallel prefill step on one rank."""
+    ranks: list                  # global ranks of the CP group, in chunk order
+    rank: int                    # this rank's index in the group (= its chunk)
+    pg: Optional[object]         # torch process group of `ranks` (None when cp == 1)
+    lens: list                   # lens[r][i] = tokens of sequence i held by cp rank r
+
+    @property
+    def size(self) -> int:
+        return len(self.ranks)
+
+    def cu(self, r: int, device) -> torch.Tensor:
+        c = [0]
+        for n in self.lens[r]:
+            c.append(c[-1] + n)
+        return torch.tensor(c, dtype=torch.int32, device=device)
+
+    def tokens(self, r: int) -> int:
+        return sum(self.lens[r])
+
+    def max_len(self, r: int) -> int:
+        return max(self.lens[r]) if self.lens[r] else 0
+
+
+def _nccl(pg) -> bool:
+    return pg is not None and dist.get_backend(pg) == "nccl"
+
+
+class _RingHop:
+    """Send `t` to the next rank and receive the previous rank's chunk into `out`. RCCL: one
+    grouped isend/irecv pair (stream-ordered, overlaps the caller's compute until `wait`).
+    gloo (CPU tests / ranks sharing a GPU): blocking, even ranks send first, odd ranks receive
+    first, host-staged for device tensors."""
+
+    def __init__(self, ctx: CPContext, t: torch.Tensor, out: torch.Tensor):
+        n, r = ctx.size, ctx.rank
+        dst, src = ctx.ranks[(r + 1) % n], ctx.ranks[(r - 1) % n]
+        self.out, self.reqs = out, []
+        if _nccl(ctx.pg):
+            ops_ = [dist.P2POp(dist.isend, t.contiguous(), dst, ctx.pg),
+                    dist.P2POp(dist.irecv, out, src, ctx.pg)]
+            self.reqs = dist.batch_isend_irecv(ops_)
+            return
+        host_t = t.detach().cpu().contiguous()
+        host_o = torch.empty(out.shape, dtype=out.dtype)
+        if r % 2 == 0:
+            dist.send(host_t, dst, group=ctx.pg)
+            dist.recv(host_o, src, group=ctx.pg)
+        else:
+            dist.recv(host_o, src, group=ctx.pg)
+            dist.send(host_t, dst, group=ctx.pg)
+        out.copy_(host_o)
+
+    def wait(self) -> torch.Tensor:
+        for q in self.reqs:
+            q.wait()
+        return self.out
+
+
+def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CPContext,
+                   scale: float) -> torch.Tensor:
+    """Causal attention of this rank's query chunk against the whole sequence, whose K/V chunks
+    live on the other CP ranks. q [T, Hq, D], k/v [T, Hkv, D] (this rank's tokens, packed per
+    sequence as ctx.lens[rank]); returns [T, Hq, D] in q's dtype."""
+    r, n = ctx.rank, ctx.size
+    dev = q.device
+    cu_r = ctx.cu(r, dev)
+    out, lse = ops.attn_prefill(q, k, v, cu_r, ctx.max_len(r), scale, True, return_lse=True)
+    if n == 1:
+        return out
+    acc_o, acc_lse = out.float(), lse
+    Hkv, D = k.shape[1], k.shape[2]
+    cur = torch.stack([k, v], 1).contiguous()         # [T, 2, Hkv, D]: one message per hop
+    for j in range(1, n):
+        src = (r - j) % n                              # whose chunk arrives at step j
+        nxt = torch.empty(ctx.tokens(src), 2, Hkv, D, dtype=k.dtype, device=dev)
+        hop = _RingHop(ctx, cur, nxt)
+        cur = hop.wait()
+        if src < r and ctx.tokens(src) > 0:            # earlier positions: fully visible
+            o_j, lse_j = ops.attn_prefill(q, cur[:, 0], cur[:, 1], cu_r, ctx.max_len(r), scale, False,
+                                          cu_seqlens_k=ctx.cu(src, dev), return_lse=True)
+            ops.attn_lse_merge_(acc_o, acc_lse, o_j, lse_j)
+    return acc_o.to(q.dtype)
+
+
+def cp_prefill(model, prompts: list, ctx_ranks: list, rank_in_group: int, pg=None,
+               kv_caches: Optional[list] = None, slots: Optional[list] = None) -> torch.Tensor:
+    """Context-parallel prefill of `prompts` (token lists) by the CP group `ctx_ranks`; this
+    rank processes its chunk of every prompt. `slots[i]` (optional) are the paged-cache slots of
+    THIS rank's chunk of prompt i in `kv_caches` (its local KV shard). Returns the last-token
+    logits [nseq, vocab_local] on every rank of the group (broadcast from the last rank)."""
+    from ..engine.batch import ForwardBatch
+
+    cp = len(ctx_ranks)
+    per_seq = [split_lengths(len(p), cp) for p in prompts]
+    lens = [[per_seq[i][r] for i in range(len(prompts))] for r in range(cp)]
+    ctx = CPContext(list(ctx_ranks), rank_in_group, pg, lens)
+    ids, pos, sl = [], [], []
+    for i, p in enumerate(prompts):
+        a = sum(per_seq[i][:rank_in_group])
+        n = per_seq[i][rank_in_group]
+        ids.extend(p[a:a + n])
+        pos.extend(range(a, a + n))
+        sl.extend(slots[i] if slots is not None else [-1] * n)
+    dev = model.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    cu = ctx.cu(rank_in_group, dev)
+    last = rank_in_group == cp - 1
+    logits_idx = (cu[1:] - 1).to(torch.int64) if last else torch.zeros(0, dtype=torch.int64, device=dev)
+    fb = ForwardBatch(input_ids=torch.tensor(ids, **i32), positions=torch.tensor(pos, **i32),
+                      slots=torch.tensor(sl, **i32), is_prefill=True, cu_seqlens=cu,
+                      max_seqlen=ctx.max_len(rank_in_group), logits_idx=logits_idx, cp=ctx)
+    logits = model.forward(fb, kv_caches)
+    if cp == 1:
+        return logits
+    V = model.dims.vocab
+    buf = logits.contiguous() if last else torch.empty(len(prompts), V, dtype=model.dtype, device=dev)
+    if _nccl(pg):
+        dist.broadcast(buf, ctx_ranks[-1], group=pg)
+    else:
+        host = buf.detach().cpu()
+        dist.broadcast(host, ctx_ranks[-1], group=pg)
+        buf = host.to(dev)
+    return buf

@@ -381,7 +381,8 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& cu_seqlens,
-                  int64_t max_seqlen, double scale, bool causal, Tensor& out) {
+                  int64_t max_seqlen, double scale, bool causal, Tensor& out,
+                  const c10::optional<Tensor>& cu_seqlens_k, const c10::optional<Tensor>& lse) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_BF16(out);
   for (const Tensor* t : {&q, &k, &v, (const Tensor*)&out})
     TORCH_CHECK(t->dim() == 3 && t->stride(2) == 1 && t->stride(1) == t->size(2) && t->stride(0) % 8 == 0,
@@ -391,11 +392,43 @@ void attn_prefill(const Tensor& q, const Tensor& k, const Tensor& v, const Tenso
   TORCH_CHECK(out.size(1) == Hq && out.size(2) == D && out.size(0) == q.size(0), "attn_prefill: out");
   CHECK_I32(cu_seqlens);
   const int nseq = cu_seqlens.numel() - 1;
+  const int* cuk = nullptr;
+  if (cu_seqlens_k.has_value()) {   // keys from another chunk (context-parallel ring step)
+    CHECK_I32(*cu_seqlens_k);
+    TORCH_CHECK(cu_seqlens_k->numel() == nseq + 1 && cu_seqlens_k->is_contiguous(), "attn_prefill: cu_seqlens_k");
+    TORCH_CHECK(!causal, "attn_prefill: separate key offsets are only defined for non-causal attention");
+    cuk = cu_seqlens_k->data_ptr<int>();
+  }
+  float* lp = nullptr;
+  if (lse.has_value()) {
+    CHECK_GPU(*lse);
+    TORCH_CHECK(lse->scalar_type() == at::kFloat && lse->is_contiguous() && lse->numel() == q.size(0) * Hq,
+                "attn_prefill: lse [T, Hq] f32");
+    lp = lse->data_ptr<float>();
+  }
   c10::DeviceGuard g(q.device());
   const int rc = bfly::launch_attn_prefill(bf(q), q.stride(0), bf(k), k.stride(0), bf(v), v.stride(0),
                                            cu_seqlens.data_ptr<int>(), nseq, max_seqlen, Hq, Hkv, D,
-                                           (float)scale, causal, bf(out), out.stride(0), cur_stream());
+                                           (float)scale, causal, bf(out), out.stride(0), cur_stream(),
+                                           cuk, lp);
   TORCH_CHECK(rc == 0, "attn_prefill: unsupported configuration (rc=", rc, ")");
+}
+
+void attn_lse_merge(Tensor& acc_o, Tensor& acc_lse, const Tensor& o, const Tensor& lse) {
+  CHECK_GPU(acc_o); CHECK_BF16(o);
+  TORCH_CHECK(acc_o.scalar_type() == at::kFloat && acc_o.dim() == 3 && acc_o.is_contiguous() && acc_o.size(2) == 128,
+              "attn_lse_merge: acc_o [T, H, 128] f32");
+  const int T = acc_o.size(0), H = acc_o.size(1);
+  TORCH_CHECK(acc_lse.scalar_type() == at::kFloat && acc_lse.is_contiguous() && acc_lse.numel() == (int64_t)T * H,
+              "attn_lse_merge: acc_lse [T, H] f32");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == (int64_t)T * H,
+              "attn_lse_merge: lse [T, H] f32");
+  TORCH_CHECK(o.dim() == 3 && o.size(0) == T && o.size(1) == H && o.size(2) == 128 && o.stride(2) == 1 &&
+                  o.stride(1) == 128, "attn_lse_merge: o [T, H, 128] bf16 with dense heads");
+  c10::DeviceGuard g(acc_o.device());
+  const int rc = bfly::launch_attn_lse_merge(acc_o.data_ptr<float>(), acc_lse.data_ptr<float>(), bf(o), o.stride(0),
+                                             lse.data_ptr<float>(), T, H, 128, cur_stream());
+  TORCH_CHECK(rc == 0, "attn_lse_merge: rejected (", rc, ")");
 }
 
 void moe_route(const Tensor& x, const Tensor& wr, int64_t top_k, Tensor& gates, Tensor& topk_ids,
@@ -617,7 +650,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, Tensor(b!)? residual, Tensor? w, float eps, "
         "int[] bases, int rank, int cap, Tensor? slabs=None) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
-        "bool causal, Tensor(a!) out) -> ()");
+        "bool causal, Tensor(a!) out, Tensor? cu_seqlens_k=None, Tensor(b!)? lse=None) -> ()");
+  m.def("attn_lse_merge(Tensor(a!) acc_o, Tensor(b!) acc_lse, Tensor o, Tensor lse) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
@@ -638,6 +672,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("rms_norm_partial", &rms_norm_partial);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
+  m.impl("attn_lse_merge", &attn_lse_merge);
   m.impl("probe", &probe);
   m.impl("custom_all_reduce", &custom_all_reduce);
   m.impl("moe_route", &moe_route);

@@ -86,7 +86,11 @@ int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const 
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
-                        hipStream_t stream);
+                        hipStream_t stream, const int* cu_k = nullptr,
+                        float* lse = nullptr);
+// K16 (context parallel): acc_o [T, H, 128] f32 / acc_lse [T, H] f32 absorb (o, lse).
+int launch_attn_lse_merge(float* acc_o, float* acc_lse, const bf16* o, long o_stride,
+                          const float* lse, int T, int H, int D, hipStream_t stream);
 
 // allreduce.hip — one-shot IPC all-reduce (+ fused residual add / RMSNorm)
 constexpr int kArBlocks = 128;

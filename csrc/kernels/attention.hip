@@ -333,8 +333,9 @@ template <int D>
 __global__ void __launch_bounds__(kPfThreads)
 attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
                     long k_stride, const bf16* __restrict__ v, long v_stride,
-                    const int* __restrict__ cu_seqlens, int Hq, int Hkv, float scale_log2,
-                    int causal, bf16* __restrict__ out, long o_stride) {
+                    const int* __restrict__ cu_seqlens, const int* __restrict__ cu_k, int Hq,
+                    int Hkv, float scale_log2, int causal, bf16* __restrict__ out, long o_stride,
+                    float* __restrict__ lse) {
   static_assert(D == 128, "prefill kernel is specialised for D=128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = 2 * kPfBKV * D * 2;  // K | V, 32 KiB
@@ -342,7 +343,11 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int seq = blockIdx.y, h = blockIdx.z;
   const int s0 = cu_seqlens[seq];
-  const int L = cu_seqlens[seq + 1] - s0;
+  const int L = cu_seqlens[seq + 1] - s0;            // query rows of this sequence
+  // keys: the same rows (self-attention), or another chunk of the sequence (context-parallel
+  // ring steps: non-causal, a different length and offset)
+  const int sk0 = cu_k[seq];
+  const int Lk = cu_k[seq + 1] - sk0;
   const int q0 = blockIdx.x * kPfBQ;
   if (q0 >= L) return;
   const int kh = h / (Hq / Hkv);
@@ -363,13 +368,13 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
   float m = kNegInf, lsum = 0.f;
 
-  const int kv_end = causal ? min(L, q0 + kPfBQ) : L;
+  const int kv_end = causal ? min(Lk, q0 + kPfBQ) : Lk;
   const int ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
   const int wave_qmax = q0 + 32 * wid + 31;
 
 #pragma unroll
   for (int st = 0; st < kPfStages - 1; ++st)
-    if (st < ntiles) pf_stage(k, k_stride, v, v_stride, s0, L, kh, st, smem + st * STAGE_BYTES, wid, lane);
+    if (st < ntiles) pf_stage(k, k_stride, v, v_stride, sk0, Lk, kh, st, smem + st * STAGE_BYTES, wid, lane);
   int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) pf_vm_wait<LPW>();   // tile t landed; tile t+1 may still fly
@@ -379,7 +384,7 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
     if (t + kPfStages - 1 < ntiles) {
       int nb = buf + kPfStages - 1;
       if (nb >= kPfStages) nb -= kPfStages;
-      pf_stage(k, k_stride, v, v_stride, s0, L, kh, t + kPfStages - 1, smem + nb * STAGE_BYTES, wid, lane);
+      pf_stage(k, k_stride, v, v_stride, sk0, Lk, kh, t + kPfStages - 1, smem + nb * STAGE_BYTES, wid, lane);
     }
     const int kv0 = t * kPfBKV;
     const char* kb = smem + buf * STAGE_BYTES;
@@ -404,9 +409,9 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float xv = sc[kt][r] * scale_log2;
-          if (!full || kv0 + kPfBKV > L) {
+          if (!full || kv0 + kPfBKV > Lk) {
             const int key = kv0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            const bool ok = key < L && (!causal || key <= qrow);
+            const bool ok = key < Lk && (!causal || key <= qrow);
             xv = ok ? xv : kNegInf;
           }
           sc[kt][r] = xv;
@@ -459,6 +464,10 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   }
   lsum += __shfl_xor(lsum, 32, 64);
   if (qrow >= L) return;
+  // natural-log sum of exp(score * scale) over the visible keys (-inf: none), for merging
+  // partial attention over key chunks (attn_lse_merge_kernel)
+  if (lse != nullptr && hi == 0)
+    lse[(long)(s0 + qrow) * Hq + h] = lsum > 0.f ? (m + __log2f(lsum)) * 0.69314718055994531f : kNegInf;
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
   bf16* op = out + (long)(s0 + qrow) * o_stride + (long)h * D;
   // o[dt][r] = O[query c][d = 32dt + (r&3) + 8(r>>2) + 4hi]
@@ -523,7 +532,7 @@ int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const 
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
-                        hipStream_t stream) {
+                        hipStream_t stream, const int* cu_k, float* lse) {
   if (nseq <= 0 || max_seqlen <= 0) return 0;
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -536,8 +545,40 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
     attr_set = true;
   }
   attn_prefill_kernel<128><<<grid, kPfThreads, lds, stream>>>(
-      q, q_stride, k, k_stride, v, v_stride, cu_seqlens, Hq, Hkv, scale_log2, causal ? 1 : 0,
-      out, o_stride);
+      q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cu_k != nullptr ? cu_k : cu_seqlens, Hq, Hkv,
+      scale_log2, causal ? 1 : 0, out, o_stride, lse);
+  return 0;
+}
+
+// K16: merge a partial attention result over another key chunk into running accumulators
+// (context-parallel ring attention): acc_lse' = log(e^acc_lse + e^lse),
+// acc_o' = acc_o * e^(acc_lse - acc_lse') + o * e^(lse - acc_lse'). One workgroup of 128
+// threads per (token, head) row; rows where both sides are empty (-inf) stay untouched.
+__global__ void __launch_bounds__(128)
+attn_lse_merge_kernel(float* __restrict__ acc_o, float* __restrict__ acc_lse,
+                      const bf16* __restrict__ o, long o_stride, const float* __restrict__ lse,
+                      int H) {
+  const long row = blockIdx.x;
+  const long t = row / H;
+  const int h = (int)(row % H), d = threadIdx.x;
+  const float a = acc_lse[row], b = lse[row];
+  const float mx = fmaxf(a, b);
+  if (mx == kNegInf) return;
+  const float wa = a == kNegInf ? 0.f : __expf(a - mx);
+  const float wb = b == kNegInf ? 0.f : __expf(b - mx);
+  const float inv = 1.f / (wa + wb);
+  const float ov = bf2f(o[t * o_stride + (long)h * 128 + d]);
+  float* ap = acc_o + row * 128 + d;
+  *ap = (*ap * wa + ov * wb) * inv;
+  __syncthreads();   // every thread read acc_lse[row] before it changes
+  if (d == 0) acc_lse[row] = mx + __logf(wa + wb);
+}
+
+int launch_attn_lse_merge(float* acc_o, float* acc_lse, const bf16* o, long o_stride,
+                          const float* lse, int T, int H, int D, hipStream_t stream) {
+  if (D != 128) return -1;
+  if ((long)T * H == 0) return 0;
+  attn_lse_merge_kernel<<<(unsigned)((long)T * H), 128, 0, stream>>>(acc_o, acc_lse, o, o_stride, lse, H);
   return 0;
 }
 

@@ -39,3 +39,13 @@ def test_bench_two_ranks_on_one_gpu(plan):
     assert len(lines) == 1, r.stdout[-3000:]
     res = json.loads(lines[0])
     assert res["config"]["parallelism"] == plan and res["value"] > 0 and res["dtype"] == "bf16"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_context_parallel_prefill_on_one_gpu(n):
+    r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", str(n), "--",
+                        sys.executable, os.path.join(ROOT, "tools", "gpu_cp_check.py")],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert r.stdout.count("PASS") == n, r.stdout[-4000:]

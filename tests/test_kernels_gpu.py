@@ -375,3 +375,41 @@ def test_moe_sparse_ffn(T, E, El, e0, k, H, F):
     ops.moe_gate_scale_(h, gates, e0, El)
     dense = ops.linear(h, dn)
     _close(got, dense, 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_attn_prefill_lse_and_key_offsets(causal):
+    """K3 with LSE output, and (non-causal) keys taken from other rows than the queries — the
+    ring-attention step of context parallelism."""
+    D, Hq, Hkv = 128, 8, 2
+    lq, lk = [1, 70, 300], ([1, 70, 300] if causal else [5, 0, 129])
+    cu = torch.tensor([0] + list(torch.tensor(lq).cumsum(0)), dtype=torch.int32, device=DEV)
+    cuk = torch.tensor([0] + list(torch.tensor(lk).cumsum(0)), dtype=torch.int32, device=DEV)
+    q = _bf(sum(lq), Hq, D, seed=80)
+    k, v = _bf(sum(lk), Hkv, D, seed=81), _bf(sum(lk), Hkv, D, seed=82)
+    kw = {} if causal else {"cu_seqlens_k": cuk}
+    o, lse = ops.attn_prefill(q, k, v, cu, max(lq), 0.088, causal, return_lse=True, **kw)
+    ro, rl = ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), cu.cpu(), max(lq), 0.088, causal, return_lse=True,
+                              **({} if causal else {"cu_seqlens_k": cuk.cpu()}))
+    _close(o, ro, 2e-2, 2e-2)
+    fin = torch.isfinite(rl)
+    assert torch.equal(torch.isfinite(lse.cpu()), fin)
+    _close(lse.cpu()[fin], rl[fin], 2e-3, 1e-3)
+
+
+def test_attn_lse_merge():
+    T, H, D = 37, 8, 128
+    acc = torch.randn(T, H, D, device=DEV)
+    al = torch.randn(T, H, device=DEV) * 3
+    al[3, :] = float("-inf")
+    o = _bf(T, H, D, seed=83)
+    lse = torch.randn(T, H, device=DEV) * 3
+    lse[5, 2] = float("-inf")
+    lse[3, 1] = float("-inf")
+    a2, l2 = acc.cpu().clone(), al.cpu().clone()
+    ops.attn_lse_merge_(acc, al, o, lse)
+    ref.attn_lse_merge_(a2, l2, o.cpu(), lse.cpu())
+    _close(acc, a2, 1e-3, 1e-3)
+    fin = torch.isfinite(l2)
+    assert torch.equal(torch.isfinite(al.cpu()), fin)
+    _close(al.cpu()[fin], l2[fin], 1e-4, 1e-4)
