@@ -329,10 +329,11 @@ class TransformerLM:
             if fb.is_prefill:
                 k = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
                 v = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
-                if fb.cp is not None:   # context parallel: K/V chunks circulate over the group
-                    from ..parallel.context_parallel import ring_attention
+                if fb.cp is not None:   # context parallel: ring (K/V circulate) or Ulysses
+                    from ..parallel import context_parallel as cpx
 
-                    attn = ring_attention(q, k, v, fb.cp, self.scale)
+                    fn = cpx.ulysses_attention if fb.cp.attn == "ulysses" else cpx.ring_attention
+                    attn = fn(q, k, v, fb.cp, self.scale)
                 else:
                     attn = ops.attn_prefill(q, k, v, fb.cu_seqlens, fb.max_seqlen, self.scale, True)
             else:

@@ -15,6 +15,12 @@ the LSE-merge kernel; chunks from later positions are masked entirely and only r
 transfer of step j+1 is posted before step j's attention runs, so on RCCL the K/V hop over
 xGMI overlaps the flash-attention kernel. The result equals single-device causal attention up to
 floating-point reassociation (tests/test_context_parallel.py).
+
+Ulysses (`ulysses_attention`, CPContext.attn = "ulysses"): instead of moving K/V around the
+ring, two all-to-alls re-shard the attention from "all heads of 1/cp of the tokens" to "1/cp
+of the heads of all tokens" and back; attention then runs as ordinary causal flash attention
+over whole sequences. It needs Hkv % cp == 0 (GQA: at most 8-way for Llama-3) and moves
+q/k/v/o once each, where the ring moves K/V cp-1 times; the ring has no head constraint.
 """
 from __future__ import annotations
 
@@ -40,6 +46,7 @@ class CPContext:
     rank: int                    # this rank's index in the group (= its chunk)
     pg: Optional[object]         # torch process group of `ranks` (None when cp == 1)
     lens: list                   # lens[r][i] = tokens of sequence i held by cp rank r
+    attn: str = "ring"           # "ring" | "ulysses"
 
     @property
     def size(self) -> int:
@@ -119,18 +126,67 @@ def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CPCon
     return acc_o.to(q.dtype)
 
 
+def _a2a(send: torch.Tensor, send_rows: list, recv_rows: list, ctx: CPContext) -> torch.Tensor:
+    """all-to-all along dim 0: rows [sum(send_rows[:j]), +send_rows[j]) go to rank j; the
+    blocks received from every rank (recv_rows[j] from rank j) come back concatenated."""
+    out = torch.empty((sum(recv_rows),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+    if _nccl(ctx.pg):
+        dist.all_to_all_single(out, send.contiguous(), output_split_sizes=list(recv_rows),
+                               input_split_sizes=list(send_rows), group=ctx.pg)
+        return out
+    host = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(host, send.detach().cpu().contiguous(), output_split_sizes=list(recv_rows),
+                           input_split_sizes=list(send_rows), group=ctx.pg)
+    return out.copy_(host)
+
+
+def ulysses_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CPContext,
+                      scale: float) -> torch.Tensor:
+    """Same contract as ring_attention, by sequence<->head all-to-alls (Hkv % cp == 0)."""
+    n, r = ctx.size, ctx.rank
+    T, Hq, D = q.shape
+    Hkv = k.shape[1]
+    if Hkv % n or Hq % n:
+        raise ValueError(f"Ulysses attention needs the head counts ({Hq}/{Hkv}) divisible by cp={n}")
+    hq, hk = Hq // n, Hkv // n
+    dev = q.device
+    # send: block j = heads of rank j for all local tokens, [n, T, heads/n, D]
+    qkv = torch.cat([q.view(T, n, hq, D), k.view(T, n, hk, D), v.view(T, n, hk, D)], 2)   # [T, n, hq+2hk, D]
+    recv_rows = [ctx.tokens(j) for j in range(n)]
+    got = _a2a(qkv.transpose(0, 1).reshape(n * T, hq + 2 * hk, D), [T] * n, recv_rows, ctx)   # [sum T_j, ...]
+    # reorder (source rank, sequence, chunk token) -> (sequence, position)
+    nseq = len(ctx.lens[0])
+    src_off = [sum(recv_rows[:j]) for j in range(n)]
+    perm = []
+    for i in range(nseq):
+        for j in range(n):
+            a = src_off[j] + sum(ctx.lens[j][:i])
+            perm.extend(range(a, a + ctx.lens[j][i]))
+    perm_t = torch.tensor(perm, dtype=torch.long, device=dev)
+    full = got.index_select(0, perm_t)
+    L = [sum(ctx.lens[j][i] for j in range(n)) for i in range(nseq)]
+    cu = torch.tensor([0] + [sum(L[:i + 1]) for i in range(nseq)], dtype=torch.int32, device=dev)
+    o = ops.attn_prefill(full[:, :hq], full[:, hq:hq + hk], full[:, hq + hk:], cu, max(L) if L else 0, scale, True)
+    back = torch.empty_like(o)
+    back[perm_t] = o                                                   # (source rank, seq, token) order
+    ret = _a2a(back, recv_rows, [T] * n, ctx)                          # [n * T, hq, D]: head block j
+    return ret.view(n, T, hq, D).transpose(0, 1).reshape(T, Hq, D)
+
+
 def cp_prefill(model, prompts: list, ctx_ranks: list, rank_in_group: int, pg=None,
-               kv_caches: Optional[list] = None, slots: Optional[list] = None) -> torch.Tensor:
+               kv_caches: Optional[list] = None, slots: Optional[list] = None,
+               attn: str = "ring") -> torch.Tensor:
     """Context-parallel prefill of `prompts` (token lists) by the CP group `ctx_ranks`; this
     rank processes its chunk of every prompt. `slots[i]` (optional) are the paged-cache slots of
-    THIS rank's chunk of prompt i in `kv_caches` (its local KV shard). Returns the last-token
+    THIS rank's chunk of prompt i in `kv_caches` (its local KV shard). `attn`: "ring" or
+    "ulysses" (all-to-all; head counts divisible by cp). Returns the last-token
     logits [nseq, vocab_local] on every rank of the group (broadcast from the last rank)."""
     from ..engine.batch import ForwardBatch
 
     cp = len(ctx_ranks)
     per_seq = [split_lengths(len(p), cp) for p in prompts]
     lens = [[per_seq[i][r] for i in range(len(prompts))] for r in range(cp)]
-    ctx = CPContext(list(ctx_ranks), rank_in_group, pg, lens)
+    ctx = CPContext(list(ctx_ranks), rank_in_group, pg, lens, attn)
     ids, pos, sl = [], [], []
     for i, p in enumerate(prompts):
         a = sum(per_seq[i][:rank_in_group])

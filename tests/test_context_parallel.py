@@ -34,7 +34,7 @@ def _single():
     return logits, kv, slots
 
 
-def _cp_rank(rank, world):
+def _cp_rank(rank, world, attn="ring"):
     import torch.distributed as dist
 
     from butterfly_amd.parallel.context_parallel import cp_prefill
@@ -47,15 +47,15 @@ def _cp_rank(rank, world):
         lens = split_lengths(len(p), world)
         a = sum(lens[:rank])
         slots.append([i * 64 + a + j for j in range(lens[rank])])
-    logits = cp_prefill(m, PROMPTS, list(range(world)), rank, dist.group.WORLD, kv, slots)
+    logits = cp_prefill(m, PROMPTS, list(range(world)), rank, dist.group.WORLD, kv, slots, attn=attn)
     # numpy: pickled by value through the result queue (tensors would go by shared memory)
     return logits.numpy(), [(k.numpy(), v.numpy()) for k, v in kv], slots
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_cp_prefill_matches_single(world):
+@pytest.mark.parametrize("world,attn", [(2, "ring"), (3, "ring"), (2, "ulysses")])
+def test_cp_prefill_matches_single(world, attn):
     want, kv_ref, slots_ref = _single()
-    outs = run_world(_cp_rank, world)
+    outs = run_world(_cp_rank, world, attn)
     for logits, kv, slots in outs:
         logits = torch.from_numpy(logits)
         kv = [(torch.from_numpy(k), torch.from_numpy(v)) for k, v in kv]

@@ -42,10 +42,10 @@ def test_bench_two_ranks_on_one_gpu(plan):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 3])
-def test_context_parallel_prefill_on_one_gpu(n):
+@pytest.mark.parametrize("n,attn", [(2, "ring"), (3, "ring"), (2, "ulysses")])
+def test_context_parallel_prefill_on_one_gpu(n, attn):
     r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", str(n), "--",
-                        sys.executable, os.path.join(ROOT, "tools", "gpu_cp_check.py")],
+                        sys.executable, os.path.join(ROOT, "tools", "gpu_cp_check.py"), "-", attn],
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert r.stdout.count("PASS") == n, r.stdout[-4000:]
