@@ -86,10 +86,14 @@ def main():
     log(f"model={cfg.name} gpus={a.gpus} plan={plan.name} stages={plan.stages}", rank)
 
     replica_batch = a.batch_per_gpu * a.gpus // mesh.dp
-    gen = a.warmup + a.steps + 2
+    prefill_budget = max(a.prompt_len, min(16384, replica_batch * a.prompt_len // 4))
+    # with mixed steps the first-admitted requests already decode while later prompts prefill:
+    # leave them enough tokens that the whole batch is still decoding through the timed steps
+    prefill_steps = -(-replica_batch * a.prompt_len // prefill_budget) + 2
+    gen = a.warmup + a.steps + 2 + prefill_steps
     max_seq = a.prompt_len + gen + 8
     ecfg = EngineConfig(max_batch=replica_batch, max_seq_len=max_seq,
-                        max_prefill_tokens=max(a.prompt_len, min(16384, replica_batch * a.prompt_len // 4)),
+                        max_prefill_tokens=prefill_budget,
                         kv_cache_tokens=replica_batch * (max_seq + 32),
                         use_graphs=not a.no_graphs,
                         graph_batch_sizes=[replica_batch])
@@ -114,7 +118,7 @@ def main():
     decode_streak = 0
     while eng.scheduler.num_waiting > 0 or decode_streak < groups:
         out = eng.step()
-        prefill_tokens += sum(len(eng.requests[r].prompt) for r in out.rids) if out.kind == "prefill" else 0
+        prefill_tokens += out.prefill_tokens
         decode_streak = decode_streak + 1 if out.kind == "decode" else 0
     sync()
     prefill_s = time.perf_counter() - tp0

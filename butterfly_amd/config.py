@@ -207,6 +207,9 @@ class EngineConfig:
     seed: int = 0
     dtype: str = "bf16"
     custom_allreduce: bool = True     # one-shot IPC all-reduce for small TP messages
+    # chunked prefill mixed into decode steps (pp == 1, no EP): every step decodes all running
+    # sequences and fills the rest of max_prefill_tokens with prompt chunks
+    mixed_prefill: bool = True
 
 
 def load_config_file(path: str | Path) -> dict:

@@ -24,6 +24,14 @@ class ForwardBatch:
     ep_tokens: int = 0                           # EP: token rows every rank pads to (0 = no pad)
     ep_alltoall: bool = False                    # EP: this step dispatches tokens by all-to-all
     cp: Optional[object] = None                  # prefill over a context-parallel group (CPContext)
+    # mixed steps (chunked prefill + decode): the first num_decode rows are decode rows
+    # (block_tables / ctx_lens / max_ctx describe them); the remaining rows are prompt chunks
+    # (cu_seqlens over them). A chunk starting at position p > 0 also attends to the p tokens
+    # already cached: prefix_lens (host list), prefix_cu (device cumsum), prefix_tables.
+    num_decode: int = 0
+    prefix_lens: Optional[list] = None
+    prefix_cu: Optional[torch.Tensor] = None
+    prefix_tables: Optional[torch.Tensor] = None
 
     @property
     def num_tokens(self) -> int:
@@ -40,7 +48,8 @@ class ForwardBatch:
         return ForwardBatch(mv(self.input_ids), mv(self.positions), mv(self.slots), self.is_prefill,
                             mv(self.cu_seqlens), self.max_seqlen, mv(self.block_tables),
                             mv(self.ctx_lens), self.max_ctx, mv(self.logits_idx), self.ep_tokens,
-                            self.ep_alltoall, self.cp)
+                            self.ep_alltoall, self.cp, self.num_decode, self.prefix_lens,
+                            mv(self.prefix_cu), mv(self.prefix_tables))
 
 
 def make_prefill_batch(prompts: list[list[int]], slots: list[list[int]], device="cpu",

@@ -65,6 +65,7 @@ class StepOutput:
     new_tokens: list
     finished: list
     seconds: float
+    prefill_tokens: int = 0       # prompt tokens this step put through the model
 
 
 class LLMEngine:
@@ -109,11 +110,16 @@ class LLMEngine:
         # pipeline parallelism without per-step fill/drain: pp request groups in flight
         # (engine/pipeline.py); EP layouts keep the synchronous path (EP collectives span DP ranks)
         self.async_pp = mesh.pp > 1 and mesh.ep == 1 and flags.get("BFLY_PP_ASYNC")
+        self.mixed = False
         if self.async_pp:
             self.scheduler = GroupedScheduler(native, self.kv.manager, mesh.pp, engine_cfg.max_batch,
                                               engine_cfg.max_prefill_tokens)
         else:
-            self.scheduler = native.Scheduler(self.kv.manager, engine_cfg.max_batch, engine_cfg.max_prefill_tokens)
+            # mixed steps (chunked prefill riding along decode) need one forward per step over
+            # every row: single-stage, non-EP layouts
+            self.mixed = bool(engine_cfg.mixed_prefill) and mesh.pp == 1 and mesh.ep == 1
+            self.scheduler = native.Scheduler(self.kv.manager, engine_cfg.max_batch, engine_cfg.max_prefill_tokens,
+                                              self.mixed)
         self._tick = 0
         self._inflight: list = []        # PipePlans entered at ticks k-pp+1 .. k
         self._pending: Optional[PipePlan] = None   # left the last stage; ids not yet applied
@@ -218,12 +224,25 @@ class LLMEngine:
         rids = list(plan.seq_ids)
         if plan.cow:
             self.kv.copy_blocks(list(plan.cow))
+        if self.mixed and plan.kind in (1, 3):
+            # chunked prefill (+ decode rows): sample the decode rows and completed prompts
+            fb, sample = self.runner.mixed_batch(plan, lambda r: self.requests[r].tokens)
+            logits = self.runner.run(fb)
+            new = []
+            if sample:
+                temps, seeds, params = self._sample_params(sample)
+                new = self.sampler.sample(logits, temps, seeds, params).tolist()
+            out = self._apply_tokens("prefill" if plan.kind == 1 else "mixed", sample, new, t0)
+            out.prefill_tokens = int(sum(plan.prefill_lens))
+            return out
         if plan.kind == 1:
             fb = self.runner.prefill_batch(plan, lambda r: self.requests[r].tokens)
             fb.ep_tokens = ep_pad
             fb.ep_alltoall = self.mesh.ep > 1
             tokens = self._run_stages(lambda h: self.runner.run(fb, h), fb.num_tokens, len(rids), rids)
-            kind = "prefill"
+            out = self._apply_tokens("prefill", rids, tokens.tolist(), t0)
+            out.prefill_tokens = fb.num_tokens
+            return out
         else:
             last = [self.requests[r].tokens[-1] for r in rids]
             inp = self.runner.decode_inputs(plan, last)
@@ -340,6 +359,7 @@ class LLMEngine:
         if self._pending is not None:
             p, self._pending = self._pending, None
             out = self._apply_tokens(p.kind, p.rids, p.ids.tolist(), t0)
+            out.prefill_tokens = p.tokens if p.plan.kind == 1 else 0
         # schedule the group entering stage 0 (every rank: replicated deterministic state)
         g = k % pp
         plan = self.scheduler.groups[g].schedule()

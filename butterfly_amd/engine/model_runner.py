@@ -78,6 +78,54 @@ class ModelRunner:
             max_seqlen=max(cu[i + 1] - cu[i] for i in range(len(cu) - 1)),
             logits_idx=torch.tensor(last, dtype=torch.int64).to(dev, non_blocking=True))
 
+    def mixed_batch(self, plan, tokens_of) -> tuple:
+        """Batch of a mixed / chunked-prefill step (runtime/scheduler.cpp mixed mode): decode
+        rows first, then each scheduled prompt chunk. Returns (batch, rids whose row is
+        sampled: every decode row and the last row of every chunk that completes its prompt)."""
+        nd = plan.num_decode
+        sids = list(plan.seq_ids)
+        dec = sids[:nd]
+        ids = [tokens_of(s)[-1] for s in dec]
+        pos = list(plan.decode_positions)
+        slots = list(plan.decode_slots)
+        rows, sample = list(range(nd)), list(dec)
+        cu, prefix, chunk_sids = [0], [], sids[nd:]
+        for j, sid in enumerate(chunk_sids):
+            st, n = int(plan.prefill_starts[j]), int(plan.prefill_lens[j])
+            ids.extend(tokens_of(sid)[st:st + n])
+            pos.extend(range(st, st + n))
+            slots.extend(plan.prefill_slots[j])
+            cu.append(cu[-1] + n)
+            prefix.append(st)
+            if plan.prefill_final[j]:
+                rows.append(nd + cu[-1] - 1)
+                sample.append(sid)
+        dev = self.device
+        t32 = lambda a: torch.tensor(a, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
+        bt = ctx = pre_cu = pre_tab = None
+        if nd:
+            self.kv.manager.fill_decode_tables(dec, self._tables_host[:nd], self._ctx_host[:nd])
+            bt = torch.from_numpy(self._tables_host[:nd].copy()).to(dev, non_blocking=True)
+            ctx = torch.from_numpy(self._ctx_host[:nd].copy()).to(dev, non_blocking=True)
+        if any(prefix):
+            pc = [0]
+            for p in prefix:
+                pc.append(pc[-1] + p)
+            pre_cu = t32(pc)
+            tab = np.zeros((len(chunk_sids), self.max_blocks), dtype=np.int32)
+            for j, sid in enumerate(chunk_sids):
+                if prefix[j]:
+                    b = self.kv.manager.block_table(sid)
+                    tab[j, : len(b)] = b
+            pre_tab = torch.from_numpy(tab).to(dev, non_blocking=True)
+        fb = ForwardBatch(input_ids=t32(ids), positions=t32(pos), slots=t32(slots), is_prefill=True,
+                          cu_seqlens=t32(cu), max_seqlen=max((cu[i + 1] - cu[i] for i in range(len(cu) - 1)), default=0),
+                          block_tables=bt, ctx_lens=ctx, max_ctx=self.max_seq_len,
+                          logits_idx=torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True),
+                          num_decode=nd, prefix_lens=prefix if any(prefix) else None, prefix_cu=pre_cu,
+                          prefix_tables=pre_tab)
+        return fb, sample
+
     def decode_inputs(self, plan, last_tokens: list) -> dict:
         B = len(plan.seq_ids)
         self.kv.manager.fill_decode_tables(list(plan.seq_ids), self._tables_host[:B], self._ctx_host[:B])

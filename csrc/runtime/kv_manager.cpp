@@ -27,6 +27,8 @@ void register_kv_manager(py::module_& m) {
       .def("can_allocate", &KVBlockManager::can_allocate)
       .def("allocate", &KVBlockManager::allocate)
       .def("append_slot", &KVBlockManager::append_slot)
+      .def("extend", &KVBlockManager::extend)
+      .def("extend_blocks", &KVBlockManager::extend_blocks)
       .def("can_append", &KVBlockManager::can_append)
       .def("fork", &KVBlockManager::fork)
       .def("free", &KVBlockManager::free)

@@ -46,6 +46,24 @@ class KVBlockManager {
     return slots;
   }
 
+  // Slots for `tokens` more tokens of an existing sequence (chunked prefill: the next chunk of
+  // a prompt whose earlier chunks are cached). Its pages are private (a sequence is forked only
+  // after its prefill), so no copy-on-write is needed.
+  std::vector<int32_t> extend(int64_t sid, int64_t tokens) {
+    Seq& s = get(sid);
+    if (extend_blocks(sid, tokens) > num_free()) throw std::runtime_error("KV cache out of blocks");
+    while ((int64_t)s.blocks.size() * block_size_ < s.len + tokens) s.blocks.push_back(take());
+    std::vector<int32_t> slots(tokens);
+    for (int64_t t = 0; t < tokens; ++t) slots[t] = slot_of(s, s.len + t);
+    s.len += tokens;
+    return slots;
+  }
+  // Fresh pages extend(sid, tokens) would take.
+  int extend_blocks(int64_t sid, int64_t tokens) const {
+    const Seq& s = cget(sid);
+    return blocks_needed(s.len + tokens) - (int)s.blocks.size();
+  }
+
   // Reserve the slot for one more token. Returns (slot, cow_src, cow_dst): when the last page
   // is shared, a fresh page is taken and the caller must copy cow_src -> cow_dst first.
   std::tuple<int32_t, int32_t, int32_t> append_slot(int64_t sid) {

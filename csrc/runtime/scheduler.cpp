@@ -10,6 +10,12 @@
 //   2. otherwise decode every running sequence; if the KV cache cannot hold one more token
 //      for each of them, preempt the most recently admitted ones (free their pages, requeue
 //      them at the FRONT of the waiting queue for recompute) until it can.
+// Mixed mode (`mixed`, chunked prefill + decode in one step): every step decodes all
+// decode-ready sequences AND spends the rest of the token budget on prompt chunks — first the
+// sequences already being prefilled (in admission order), then new admissions. A prompt longer
+// than the budget is prefilled over several steps (its later chunks attend to the cached
+// earlier ones), and decoding never stalls behind a long prefill: the prefill rows ride along
+// the decode step's weight streaming. kind 3 = mixed step.
 // The scheduler owns page allocation (through KVBlockManager) and returns the cache slots
 // of every token it schedules.
 #include <pybind11/pybind11.h>
@@ -28,10 +34,13 @@ namespace py = pybind11;
 namespace bfly_rt {
 
 struct StepPlan {
-  int kind = 0;  // 0 idle, 1 prefill, 2 decode
-  std::vector<int64_t> seq_ids;
-  std::vector<std::vector<int32_t>> prefill_slots;  // per sequence, every token
-  std::vector<int64_t> prefill_lens;
+  int kind = 0;  // 0 idle, 1 prefill, 2 decode, 3 mixed (decode rows first, then prompt chunks)
+  std::vector<int64_t> seq_ids;                     // decode sequences, then prefill sequences
+  int num_decode = 0;                               // leading decode rows of seq_ids
+  std::vector<std::vector<int32_t>> prefill_slots;  // per prefill sequence, every chunk token
+  std::vector<int64_t> prefill_lens;                // chunk lengths
+  std::vector<int64_t> prefill_starts;              // position of each chunk's first token
+  std::vector<bool> prefill_final;                  // chunk completes the (re)prompt: sample
   std::vector<int32_t> decode_slots;                // per sequence, the new token
   std::vector<int32_t> decode_positions;
   std::vector<std::pair<int32_t, int32_t>> cow;     // page copies to do before the step
@@ -40,12 +49,12 @@ struct StepPlan {
 
 class Scheduler {
  public:
-  Scheduler(KVBlockManager& kv, int max_batch, int64_t max_prefill_tokens)
-      : kv_(kv), max_batch_(max_batch), max_prefill_tokens_(max_prefill_tokens) {}
+  Scheduler(KVBlockManager& kv, int max_batch, int64_t max_prefill_tokens, bool mixed = false)
+      : kv_(kv), max_batch_(max_batch), max_prefill_tokens_(max_prefill_tokens), mixed_(mixed) {}
 
   void add(int64_t sid, int64_t prompt_len, int64_t max_new_tokens) {
     if (info_.count(sid)) throw std::invalid_argument("duplicate sequence id");
-    info_[sid] = Info{prompt_len, 0, max_new_tokens};
+    info_[sid] = Info{prompt_len, 0, max_new_tokens, false};
     waiting_.push_back(sid);
   }
 
@@ -67,6 +76,7 @@ class Scheduler {
   std::vector<int64_t> waiting() const { return std::vector<int64_t>(waiting_.begin(), waiting_.end()); }
 
   StepPlan schedule() {
+    if (mixed_) return schedule_mixed();
     StepPlan plan;
     // --- 1. prefill admission --------------------------------------------------------------
     int64_t budget = max_prefill_tokens_;
@@ -81,6 +91,8 @@ class Scheduler {
       waiting_.pop_front();
       plan.seq_ids.push_back(sid);
       plan.prefill_lens.push_back(len);
+      plan.prefill_starts.push_back(0);
+      plan.prefill_final.push_back(true);
       plan.prefill_slots.push_back(kv_.allocate(sid, len));
       free_pages = kv_.num_free();
       budget -= len;
@@ -103,6 +115,7 @@ class Scheduler {
     if (running_.empty()) return plan;
     plan.kind = 2;
     plan.seq_ids = running_;
+    plan.num_decode = (int)running_.size();
     for (int64_t sid : running_) {
       auto [slot, src, dst] = kv_.append_slot(sid);
       plan.decode_slots.push_back(slot);
@@ -116,10 +129,81 @@ class Scheduler {
  private:
   struct Info {
     int64_t prompt_len, generated, max_new;
+    bool in_prefill;   // mixed mode: admitted, its (re)prompt not yet fully scheduled
   };
+
+  StepPlan schedule_mixed() {
+    StepPlan plan;
+    // --- 1. decode rows: every running sequence whose prompt is fully cached --------------------
+    auto decode_ready = [&]() {
+      std::vector<int64_t> d;
+      for (int64_t sid : running_)
+        if (!info_.at(sid).in_prefill) d.push_back(sid);
+      return d;
+    };
+    std::vector<int64_t> dec = decode_ready();
+    while (!dec.empty() && !kv_.can_append(dec)) {   // preempt the newest running sequence
+      const int64_t victim = running_.back();
+      running_.pop_back();
+      kv_.free(victim);
+      info_.at(victim).in_prefill = false;
+      waiting_.push_front(victim);
+      plan.preempted.push_back(victim);
+      dec = decode_ready();
+    }
+    for (int64_t sid : dec) {
+      auto [slot, src, dst] = kv_.append_slot(sid);
+      plan.seq_ids.push_back(sid);
+      plan.decode_slots.push_back(slot);
+      const Info& in = info_.at(sid);
+      plan.decode_positions.push_back((int32_t)(in.prompt_len + in.generated - 1));
+      if (src >= 0) plan.cow.emplace_back(src, dst);
+    }
+    plan.num_decode = (int)dec.size();
+    int64_t budget = max_prefill_tokens_ - plan.num_decode;
+    // --- 2. next chunks of the prompts being prefilled (admission order) ------------------------
+    for (int64_t sid : running_) {
+      if (budget <= 0) break;
+      Info& in = info_.at(sid);
+      if (!in.in_prefill) continue;
+      const int64_t target = in.prompt_len + in.generated, cached = kv_.length(sid);
+      const int64_t n = std::min(target - cached, budget);
+      if (kv_.extend_blocks(sid, n + (n == target - cached ? 1 : 0)) > kv_.num_free()) break;
+      plan.seq_ids.push_back(sid);
+      plan.prefill_starts.push_back(cached);
+      plan.prefill_lens.push_back(n);
+      plan.prefill_slots.push_back(kv_.extend(sid, n));
+      plan.prefill_final.push_back(cached + n == target);
+      if (cached + n == target) in.in_prefill = false;
+      budget -= n;
+    }
+    // --- 3. admit waiting sequences (FIFO) into the remaining budget ----------------------------
+    while (budget > 0 && !waiting_.empty() && (int)running_.size() < max_batch_) {
+      const int64_t sid = waiting_.front();
+      Info& in = info_.at(sid);
+      const int64_t target = in.prompt_len + in.generated;   // recompute after preemption
+      const int64_t n = std::min(target, budget);
+      // the first chunk's pages (+ one decode page when it is the whole prompt)
+      if (kv_.blocks_needed(n + (n == target ? 1 : 0)) > kv_.num_free()) break;
+      waiting_.pop_front();
+      running_.push_back(sid);
+      plan.seq_ids.push_back(sid);
+      plan.prefill_starts.push_back(0);
+      plan.prefill_lens.push_back(n);
+      plan.prefill_slots.push_back(kv_.allocate(sid, n));
+      plan.prefill_final.push_back(n == target);
+      in.in_prefill = n < target;
+      budget -= n;
+    }
+    const bool has_prefill = (int)plan.seq_ids.size() > plan.num_decode;
+    plan.kind = plan.num_decode > 0 ? (has_prefill ? 3 : 2) : (has_prefill ? 1 : 0);
+    return plan;
+  }
+
   KVBlockManager& kv_;
   int max_batch_;
   int64_t max_prefill_tokens_;
+  bool mixed_;
   std::deque<int64_t> waiting_;
   std::vector<int64_t> running_;
   std::unordered_map<int64_t, Info> info_;
@@ -129,15 +213,18 @@ void register_scheduler(py::module_& m) {
   py::class_<StepPlan>(m, "StepPlan")
       .def_readonly("kind", &StepPlan::kind)
       .def_readonly("seq_ids", &StepPlan::seq_ids)
+      .def_readonly("num_decode", &StepPlan::num_decode)
       .def_readonly("prefill_slots", &StepPlan::prefill_slots)
       .def_readonly("prefill_lens", &StepPlan::prefill_lens)
+      .def_readonly("prefill_starts", &StepPlan::prefill_starts)
+      .def_readonly("prefill_final", &StepPlan::prefill_final)
       .def_readonly("decode_slots", &StepPlan::decode_slots)
       .def_readonly("decode_positions", &StepPlan::decode_positions)
       .def_readonly("cow", &StepPlan::cow)
       .def_readonly("preempted", &StepPlan::preempted);
   py::class_<Scheduler>(m, "Scheduler")
-      .def(py::init<KVBlockManager&, int, int64_t>(), py::arg("kv"), py::arg("max_batch"),
-           py::arg("max_prefill_tokens"), py::keep_alive<1, 2>())
+      .def(py::init<KVBlockManager&, int, int64_t, bool>(), py::arg("kv"), py::arg("max_batch"),
+           py::arg("max_prefill_tokens"), py::arg("mixed") = false, py::keep_alive<1, 2>())
       .def("add", &Scheduler::add)
       .def("on_token", &Scheduler::on_token)
       .def("finish", &Scheduler::finish)

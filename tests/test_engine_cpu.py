@@ -1,5 +1,6 @@
 """Engine on CPU: continuous batching + paged KV + scheduler produce the same greedy tokens as
 step-by-step full recompute."""
+import pytest
 import torch
 
 from butterfly_amd.config import EngineConfig, ModelConfig
@@ -36,3 +37,31 @@ def test_engine_preemption_recovers():
     outs = eng.generate(prompts, SamplingParams(max_tokens=20))
     for p, o in zip(prompts, outs):
         assert o == _greedy_reference(eng.model, p, 20)
+
+
+@pytest.mark.parametrize("budget", [7, 16, 64])
+def test_mixed_chunked_prefill_matches_unmixed(budget):
+    """Chunked prefill mixed into decode steps (scheduler mixed mode): prompts longer than the
+    per-step token budget are prefilled over several steps while earlier requests decode; the
+    generated tokens must equal the plain prefill-then-decode engine's."""
+    from butterfly_amd.config import EngineConfig, ModelConfig
+    from butterfly_amd.engine.engine import LLMEngine
+    from butterfly_amd.engine.sampler import SamplingParams
+
+    cfg = ModelConfig.from_preset("llama-tiny")
+    prompts = [[(5 * i + 3 * j) % 1000 + 1 for j in range(n)] for i, n in enumerate((45, 3, 20, 33, 1, 9))]
+
+    def run(mixed):
+        e = LLMEngine(cfg, engine_cfg=EngineConfig(max_batch=4, max_seq_len=128, max_prefill_tokens=budget,
+                                                   kv_cache_tokens=1024, use_graphs=False, seed=2,
+                                                   mixed_prefill=mixed), device="cpu")
+        kinds = set()
+        rids = [e.add_request(p, SamplingParams(max_tokens=6 + i, ignore_eos=True)) for i, p in enumerate(prompts)]
+        while e.has_unfinished():
+            kinds.add(e.step().kind)
+        return [e.requests[r].output for r in rids], kinds
+
+    ref, _ = run(False)
+    got, kinds = run(True)
+    assert got == ref
+    assert "mixed" in kinds

@@ -73,3 +73,39 @@ def test_engine_temperature_sampling_runs():
     out = eng.generate([[1, 2, 3], [4, 5]], SamplingParams(max_tokens=8, temperature=0.8, seed=3))
     assert all(len(o) == 8 for o in out)
     assert all(0 <= t < cfg.vocab_size for o in out for t in o)
+
+
+def test_mixed_chunked_step_matches_reference():
+    """A mixed step (decode row + a prompt chunk attending to its cached prefix through the
+    LSE-merged flash prefill) on the HIP kernels vs the fp32 reference ops."""
+    from butterfly_amd.engine.batch import ForwardBatch
+
+    cfg, g, c = _pair("llama-small")
+    bs, V = 32, cfg.vocab_size
+    A = [(7 * j) % 3000 + 1 for j in range(90)]
+    B = [(11 * j) % 3000 + 2 for j in range(20)]
+    # cache: A in blocks 0..2, B in blocks 4..5
+    sa = [j for j in range(90)]
+    sb = [4 * bs + j for j in range(21)]
+    kg, kc = g.allocate_kv_cache(8, bs), c.allocate_kv_cache(8, bs)
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32)  # noqa: E731
+    # step 1: A[0:40) (not final) + B (final) as plain prefill
+    fb1 = ForwardBatch(input_ids=i32(A[:40] + B), positions=i32(list(range(40)) + list(range(20))),
+                       slots=i32(sa[:40] + sb[:20]), is_prefill=True, cu_seqlens=i32([0, 40, 60]), max_seqlen=40,
+                       logits_idx=torch.tensor([59]))
+    l1g, l1c = g.forward(fb1.to("cuda"), kg), c.forward(fb1, kc)
+    assert _rel(l1g[:, :V], l1c[:, :V]) < 2e-2
+    tok = int(l1c[0, :V].argmax())
+    # step 2: decode row for B + chunk A[40:90) with a 40-token cached prefix
+    fb2 = ForwardBatch(input_ids=i32([tok] + A[40:]), positions=i32([20] + list(range(40, 90))),
+                       slots=i32([sb[20]] + sa[40:]), is_prefill=True, cu_seqlens=i32([0, 50]), max_seqlen=50,
+                       block_tables=i32([[4, 5, 0]]), ctx_lens=i32([21]), max_ctx=96,
+                       logits_idx=torch.tensor([0, 50]), num_decode=1, prefix_lens=[40], prefix_cu=i32([0, 40]),
+                       prefix_tables=i32([[0, 1, 2]]))
+    l2g, l2c = g.forward(fb2.to("cuda"), kg), c.forward(fb2, kc)
+    assert _rel(l2g[:, :V], l2c[:, :V]) < 3e-2
+    # and the chunked prompt's last-token logits equal a whole-prompt prefill's
+    kw = c.allocate_kv_cache(8, bs)
+    whole = c.forward(ForwardBatch(input_ids=i32(A), positions=i32(list(range(90))), slots=i32(sa), is_prefill=True,
+                                   cu_seqlens=i32([0, 90]), max_seqlen=90, logits_idx=torch.tensor([89])), kw)
+    assert _rel(l2c[1:2, :V], whole[:, :V]) < 1e-4
