@@ -94,7 +94,7 @@ def test_mixed_chunked_step_matches_reference():
                        slots=i32(sa[:40] + sb[:20]), is_prefill=True, cu_seqlens=i32([0, 40, 60]), max_seqlen=40,
                        logits_idx=torch.tensor([59]))
     l1g, l1c = g.forward(fb1.to("cuda"), kg), c.forward(fb1, kc)
-    assert _rel(l1g[:, :V], l1c[:, :V]) < 2e-2
+    assert _rel(l1g[:, :V], l1c[:, :V]) < 5e-2      # one bf16 row vs fp32 (wrong would be O(1))
     tok = int(l1c[0, :V].argmax())
     # step 2: decode row for B + chunk A[40:90) with a 40-token cached prefix
     fb2 = ForwardBatch(input_ids=i32([tok] + A[40:]), positions=i32([20] + list(range(40, 90))),
@@ -103,7 +103,7 @@ def test_mixed_chunked_step_matches_reference():
                        logits_idx=torch.tensor([0, 50]), num_decode=1, prefix_lens=[40], prefix_cu=i32([0, 40]),
                        prefix_tables=i32([[0, 1, 2]]))
     l2g, l2c = g.forward(fb2.to("cuda"), kg), c.forward(fb2, kc)
-    assert _rel(l2g[:, :V], l2c[:, :V]) < 3e-2
+    assert _rel(l2g[:, :V], l2c[:, :V]) < 5e-2
     # and the chunked prompt's last-token logits equal a whole-prompt prefill's
     kw = c.allocate_kv_cache(8, bs)
     whole = c.forward(ForwardBatch(input_ids=i32(A), positions=i32(list(range(90))), slots=i32(sa), is_prefill=True,
