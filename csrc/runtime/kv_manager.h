@@ -1,7 +1,9 @@
 // Paged KV-cache block manager (see kv_manager.cpp for the design notes).
 #pragma once
+#ifndef BFLY_RT_NO_PYTHON   // the sanitizer self-test builds the runtime without Python
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#endif
 
 #include <cstdint>
 #include <stdexcept>
@@ -9,7 +11,9 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef BFLY_RT_NO_PYTHON
 namespace py = pybind11;
+#endif
 
 namespace bfly_rt {
 
@@ -115,6 +119,7 @@ class KVBlockManager {
   }
   int64_t length(int64_t sid) const { return cget(sid).len; }
 
+#ifndef BFLY_RT_NO_PYTHON
   // Decode-step arrays for a batch, written into caller buffers:
   //   tables [B, max_blocks] (row-major, zero padded), ctx_lens [B] = len after append.
   // Call after append_slot for this step.
@@ -135,6 +140,7 @@ class KVBlockManager {
       C(i) = (int32_t)s.len;
     }
   }
+#endif
 
  private:
   struct Seq {

@@ -1,0 +1,128 @@
+// Host-runtime self-test for sanitizer builds ("host ASan/UBSan builds of
+// csrc/runtime for the CPU-testable parts"). Built by tests/test_runtime_sanitizers.py with
+//   g++ -fsanitize=address,undefined -fno-omit-frame-pointer selftest.cpp  (no Python headers)
+// and run as a plain executable (no Python). It drives the paged-KV block manager and the
+// continuous-batching scheduler (legacy and mixed/chunked modes) through long randomized
+// request streams and checks the invariants the engine relies on:
+//   * a cache slot is owned by at most one live (non-forked) sequence at any time;
+//   * pages are conserved: free + referenced == total, and everything is free at the end;
+//   * every request finishes with exactly max_new tokens, whatever preemption happened;
+//   * chunk starts/lengths tile each (re)prompt exactly once.
+// Exit code 0 = pass; a failed check prints and aborts (and ASan/UBSan abort on memory / UB).
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <set>
+#include <unordered_map>
+#include <vector>
+
+#define BFLY_RT_NO_PYTHON
+#include "../scheduler.h"
+
+using namespace bfly_rt;
+
+#define CHECK(c)                                                               \
+  do {                                                                         \
+    if (!(c)) {                                                                \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      std::abort();                                                            \
+    }                                                                          \
+  } while (0)
+
+static void test_kv_manager() {
+  KVBlockManager kv(16, 4);
+  auto a = kv.allocate(1, 6);                // 2 pages
+  CHECK(a.size() == 6 && kv.num_free() == 14);
+  auto b = kv.extend(1, 3);                  // 9 tokens -> 3 pages
+  CHECK(b.size() == 3 && kv.num_free() == 13 && kv.length(1) == 9);
+  kv.fork(1, 2);                             // shares 3 pages
+  CHECK(kv.num_free() == 13);
+  auto [s1, src, dst] = kv.append_slot(2);   // last page shared -> copy-on-write
+  CHECK(src >= 0 && dst >= 0 && src != dst && kv.num_free() == 12);
+  (void)s1;
+  for (int i = 0; i < 3; ++i) kv.append_slot(1);   // 12 tokens: fills page 3 of seq 1
+  kv.free(1);
+  kv.free(2);
+  CHECK(kv.num_free() == 16 && kv.num_seqs() == 0);
+  bool threw = false;
+  try {
+    kv.allocate(3, 100);
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  CHECK(threw && kv.num_free() == 16);
+}
+
+static void run_stream(bool mixed, unsigned seed) {
+  std::mt19937 rng(seed);
+  const int kPages = 48, kBS = 8, kMaxBatch = 6;
+  KVBlockManager kv(kPages, kBS);
+  Scheduler sch(kv, kMaxBatch, /*max_prefill_tokens=*/mixed ? 24 : 64, mixed);
+  struct Req {
+    int64_t prompt, max_new, gen = 0;
+    int64_t cached = 0;      // tokens of (prompt + generated) scheduled into the cache
+    bool done = false;
+  };
+  std::unordered_map<int64_t, Req> reqs;
+  int64_t next_id = 0;
+  int steps = 0;
+  auto add = [&]() {
+    Req r{(int64_t)(rng() % 40) + 1, (int64_t)(rng() % 12) + 1};
+    sch.add(next_id, r.prompt, r.max_new);
+    reqs[next_id++] = r;
+  };
+  for (int i = 0; i < 8; ++i) add();
+  while (sch.num_waiting() + sch.num_running() > 0 || next_id < 60) {
+    if (next_id < 60 && rng() % 3 == 0) add();
+    StepPlan p = sch.schedule();
+    ++steps;
+    CHECK(steps < 100000);
+    for (int64_t v : p.preempted) reqs[v].cached = 0;   // pages freed: recompute later
+    std::set<int32_t> used;                            // slots written this step
+    const int nd = p.num_decode;
+    for (int i = 0; i < nd; ++i) {
+      Req& r = reqs.at(p.seq_ids[i]);
+      CHECK(!r.done && r.gen >= 1);
+      CHECK(p.decode_positions[i] == r.prompt + r.gen - 1);
+      CHECK(used.insert(p.decode_slots[i]).second);
+      r.cached = r.prompt + r.gen;
+    }
+    std::vector<int64_t> sampled(p.seq_ids.begin(), p.seq_ids.begin() + nd);
+    for (size_t j = 0; j + nd < p.seq_ids.size(); ++j) {
+      const int64_t sid = p.seq_ids[nd + j];
+      Req& r = reqs.at(sid);
+      CHECK(p.prefill_starts[j] == r.cached);          // chunks tile the (re)prompt in order
+      CHECK((int64_t)p.prefill_slots[j].size() == p.prefill_lens[j] && p.prefill_lens[j] > 0);
+      for (int32_t s : p.prefill_slots[j]) CHECK(used.insert(s).second);
+      r.cached += p.prefill_lens[j];
+      CHECK(r.cached <= r.prompt + r.gen);
+      CHECK(bool(p.prefill_final[j]) == (r.cached == r.prompt + r.gen));
+      if (p.prefill_final[j]) sampled.push_back(sid);
+    }
+    for (int32_t s : used) CHECK(s >= 0 && s < kPages * kBS);
+    // the engine: one token per sampled row, finish at max_new
+    for (int64_t sid : sampled) {
+      Req& r = reqs.at(sid);
+      sch.on_token(sid);
+      ++r.gen;
+      if (r.gen >= r.max_new) {
+        r.done = true;
+        sch.finish(sid);
+      }
+    }
+    CHECK(kv.num_free() <= kPages);
+  }
+  for (auto& kvp : reqs) CHECK(kvp.second.done && kvp.second.gen == kvp.second.max_new);
+  CHECK(kv.num_free() == kPages && kv.num_seqs() == 0);
+  std::printf("stream mixed=%d seed=%u: %zu requests in %d steps\n", (int)mixed, seed, reqs.size(), steps);
+}
+
+int main() {
+  test_kv_manager();
+  for (unsigned seed = 1; seed <= 20; ++seed) {
+    run_stream(false, seed);
+    run_stream(true, seed);
+  }
+  std::printf("runtime selftest: PASS\n");
+  return 0;
+}
