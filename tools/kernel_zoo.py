@@ -34,6 +34,12 @@ wd = rnd(8192, 28672, scale=0.01)
 hd = rnd(64, 28672)
 for _ in range(R):
     ops.linear(hd, wd)
+# TP2 replica decode (B = 128): gate/up shard -> decode ring GEMM
+w2 = rnd(28672, 8192, scale=0.01)
+x2 = rnd(128, 8192)
+for _ in range(R):
+    ops.linear(x2, w2, epilogue="silu")
+del w2
 del w, x
 torch.cuda.empty_cache()
 # decode attention: B=64, ctx 1024, 64 q / 8 kv heads
