@@ -210,6 +210,9 @@ class EngineConfig:
     # chunked prefill mixed into decode steps (pp == 1, no EP): every step decodes all running
     # sequences and fills the rest of max_prefill_tokens with prompt chunks
     mixed_prefill: bool = True
+    # automatic prefix caching (with mixed_prefill): full prompt pages are registered under a
+    # hash of their token prefix and reused by later requests that start with the same tokens
+    prefix_caching: bool = True
 
 
 def load_config_file(path: str | Path) -> dict:

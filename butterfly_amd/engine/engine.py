@@ -110,7 +110,7 @@ class LLMEngine:
         # pipeline parallelism without per-step fill/drain: pp request groups in flight
         # (engine/pipeline.py); EP layouts keep the synchronous path (EP collectives span DP ranks)
         self.async_pp = mesh.pp > 1 and mesh.ep == 1 and flags.get("BFLY_PP_ASYNC")
-        self.mixed = False
+        self.mixed = self.prefix_cache = False
         if self.async_pp:
             self.scheduler = GroupedScheduler(native, self.kv.manager, mesh.pp, engine_cfg.max_batch,
                                               engine_cfg.max_prefill_tokens)
@@ -118,8 +118,9 @@ class LLMEngine:
             # mixed steps (chunked prefill riding along decode) need one forward per step over
             # every row: single-stage, non-EP layouts
             self.mixed = bool(engine_cfg.mixed_prefill) and mesh.pp == 1 and mesh.ep == 1
+            self.prefix_cache = self.mixed and bool(engine_cfg.prefix_caching)
             self.scheduler = native.Scheduler(self.kv.manager, engine_cfg.max_batch, engine_cfg.max_prefill_tokens,
-                                              self.mixed)
+                                              self.mixed, self.prefix_cache)
         self._tick = 0
         self._inflight: list = []        # PipePlans entered at ticks k-pp+1 .. k
         self._pending: Optional[PipePlan] = None   # left the last stage; ids not yet applied
@@ -172,7 +173,10 @@ class LLMEngine:
         if len(prompt) + params.max_tokens > self.ecfg.max_seq_len:
             raise ValueError(f"prompt ({len(prompt)}) + max_tokens ({params.max_tokens}) exceeds max_seq_len")
         self.requests[rid] = Request(rid, list(prompt), params, arrival=time.perf_counter())
-        self.scheduler.add(rid, len(prompt), params.max_tokens)
+        if self.prefix_cache:
+            self.scheduler.add(rid, len(prompt), params.max_tokens, list(prompt))
+        else:
+            self.scheduler.add(rid, len(prompt), params.max_tokens)
         return rid
 
     def has_unfinished(self) -> bool:

@@ -34,7 +34,12 @@ void register_kv_manager(py::module_& m) {
       .def("free", &KVBlockManager::free)
       .def("block_table", &KVBlockManager::block_table)
       .def("length", &KVBlockManager::length)
-      .def("fill_decode_tables", &KVBlockManager::fill_decode_tables);
+      .def("fill_decode_tables", &KVBlockManager::fill_decode_tables)
+      .def_property_readonly("num_cached_blocks", &KVBlockManager::num_cached_blocks)
+      .def("block_hashes", &KVBlockManager::block_hashes)
+      .def("match_prefix", &KVBlockManager::match_prefix)
+      .def("allocate_prefixed", &KVBlockManager::allocate_prefixed)
+      .def("register_blocks", &KVBlockManager::register_blocks);
 }
 
 }  // namespace bfly_rt

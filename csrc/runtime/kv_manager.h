@@ -5,7 +5,10 @@
 #include <pybind11/pybind11.h>
 #endif
 
+#include <algorithm>
 #include <cstdint>
+#include <iterator>
+#include <list>
 #include <stdexcept>
 #include <tuple>
 #include <unordered_map>
@@ -17,10 +20,28 @@ namespace py = pybind11;
 
 namespace bfly_rt {
 
+// Prefix caching: a FULL page whose tokens are known (a prompt block) is registered under a
+// chained 64-bit hash of every token up to its end. When its last owner frees it, the page is
+// not returned to the free list but parked in an LRU of cached pages, still counted as free
+// capacity; a later request whose prompt starts with the same blocks takes those pages back
+// (match_prefix / allocate_prefixed) and only prefills the rest. Pages are evicted from the
+// LRU (and unregistered) only when the free list is empty.
+inline uint64_t kv_block_hash(uint64_t prev, const int32_t* tok, int n) {
+  uint64_t h = prev ^ 0x9E3779B97F4A7C15ull;
+  for (int i = 0; i < n; ++i) {
+    uint64_t z = h + (uint64_t)(uint32_t)tok[i] + 0x9E3779B97F4A7C15ull;   // splitmix64 step
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    h = z ^ (z >> 31);
+  }
+  return h | 1ull;   // 0 = "no hash"
+}
+
 class KVBlockManager {
  public:
   KVBlockManager(int num_blocks, int block_size)
-      : num_blocks_(num_blocks), block_size_(block_size), refcnt_(num_blocks, 0) {
+      : num_blocks_(num_blocks), block_size_(block_size), refcnt_(num_blocks, 0),
+        hash_(num_blocks, 0), lru_pos_(num_blocks) {
     if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("bad KV geometry");
     free_.reserve(num_blocks);
     for (int b = num_blocks - 1; b >= 0; --b) free_.push_back(b);
@@ -28,7 +49,52 @@ class KVBlockManager {
 
   int num_blocks() const { return num_blocks_; }
   int block_size() const { return block_size_; }
-  int num_free() const { return (int)free_.size(); }
+  int num_free() const { return (int)(free_.size() + lru_.size()); }
+  int num_cached_blocks() const { return (int)cached_.size(); }
+
+  // Hashes of the full blocks of `tokens` (block i covers tokens [i*bs, (i+1)*bs)).
+  std::vector<uint64_t> block_hashes(const std::vector<int32_t>& tokens) const {
+    std::vector<uint64_t> hs;
+    uint64_t h = 0;
+    for (size_t i = 0; (i + 1) * block_size_ <= tokens.size(); ++i) {
+      h = kv_block_hash(h, tokens.data() + i * block_size_, block_size_);
+      hs.push_back(h);
+    }
+    return hs;
+  }
+  // Leading blocks of `hashes` whose pages are cached (live or parked in the LRU).
+  int match_prefix(const std::vector<uint64_t>& hashes, int max_blocks) const {
+    int n = 0;
+    while (n < max_blocks && n < (int)hashes.size() && cached_.count(hashes[n])) ++n;
+    return n;
+  }
+  // Register a sequence that starts with the cached pages of hashes[0..nblocks) and has
+  // `tokens` more tokens to cache; returns the slots of those tokens.
+  std::vector<int32_t> allocate_prefixed(int64_t sid, const std::vector<uint64_t>& hashes, int nblocks,
+                                         int64_t tokens) {
+    if (seqs_.count(sid)) throw std::invalid_argument("sequence already allocated");
+    Seq s;
+    for (int i = 0; i < nblocks; ++i) {
+      const int b = cached_.at(hashes[i]);
+      if (refcnt_[b] == 0) lru_.erase(lru_pos_[b]);   // parked page comes back to life
+      ++refcnt_[b];
+      s.blocks.push_back(b);
+    }
+    s.len = (int64_t)nblocks * block_size_;
+    seqs_.emplace(sid, std::move(s));
+    return tokens > 0 ? extend(sid, tokens) : std::vector<int32_t>{};
+  }
+  // Register the sequence's pages that are now full and whose content is hashes[i].
+  void register_blocks(int64_t sid, const std::vector<uint64_t>& hashes) {
+    const Seq& s = cget(sid);
+    const int full = (int)std::min<int64_t>((int64_t)hashes.size(), s.len / block_size_);
+    for (int i = 0; i < full; ++i) {
+      const int b = s.blocks[i];
+      if (hash_[b] != 0 || cached_.count(hashes[i])) continue;
+      hash_[b] = hashes[i];
+      cached_[hashes[i]] = b;
+    }
+  }
   int num_seqs() const { return (int)seqs_.size(); }
   bool has(int64_t sid) const { return seqs_.count(sid) != 0; }
 
@@ -74,10 +140,10 @@ class KVBlockManager {
     Seq& s = get(sid);
     int cow_src = -1, cow_dst = -1;
     if (s.len % block_size_ == 0) {
-      if (free_.empty()) throw std::runtime_error("KV cache out of blocks");
+      if (num_free() == 0) throw std::runtime_error("KV cache out of blocks");
       s.blocks.push_back(take());
     } else if (refcnt_[s.blocks.back()] > 1) {
-      if (free_.empty()) throw std::runtime_error("KV cache out of blocks");
+      if (num_free() == 0) throw std::runtime_error("KV cache out of blocks");
       cow_src = s.blocks.back();
       cow_dst = take();
       --refcnt_[cow_src];
@@ -148,13 +214,27 @@ class KVBlockManager {
     int64_t len = 0;
   };
   int take() {
-    const int b = free_.back();
-    free_.pop_back();
+    int b;
+    if (!free_.empty()) {
+      b = free_.back();
+      free_.pop_back();
+    } else {   // evict the least recently parked cached page
+      b = lru_.front();
+      lru_.pop_front();
+      cached_.erase(hash_[b]);
+      hash_[b] = 0;
+    }
     refcnt_[b] = 1;
     return b;
   }
   void release(int b) {
-    if (--refcnt_[b] == 0) free_.push_back(b);
+    if (--refcnt_[b] != 0) return;
+    if (hash_[b] != 0) {
+      lru_.push_back(b);
+      lru_pos_[b] = std::prev(lru_.end());
+    } else {
+      free_.push_back(b);
+    }
   }
   int32_t slot_of(const Seq& s, int64_t t) const {
     return (int32_t)(s.blocks[t / block_size_] * block_size_ + t % block_size_);
@@ -173,6 +253,10 @@ class KVBlockManager {
   int num_blocks_, block_size_;
   std::vector<int> free_;
   std::vector<int> refcnt_;
+  std::vector<uint64_t> hash_;                        // per page: registered hash (0 = none)
+  std::list<int> lru_;                                // parked cached pages, oldest first
+  std::vector<std::list<int>::iterator> lru_pos_;
+  std::unordered_map<uint64_t, int> cached_;          // hash -> page
   std::unordered_map<int64_t, Seq> seqs_;
 };
 

@@ -22,9 +22,12 @@ void register_scheduler(py::module_& m) {
       .def_readonly("cow", &StepPlan::cow)
       .def_readonly("preempted", &StepPlan::preempted);
   py::class_<Scheduler>(m, "Scheduler")
-      .def(py::init<KVBlockManager&, int, int64_t, bool>(), py::arg("kv"), py::arg("max_batch"),
-           py::arg("max_prefill_tokens"), py::arg("mixed") = false, py::keep_alive<1, 2>())
-      .def("add", &Scheduler::add)
+      .def(py::init<KVBlockManager&, int, int64_t, bool, bool>(), py::arg("kv"), py::arg("max_batch"),
+           py::arg("max_prefill_tokens"), py::arg("mixed") = false, py::arg("prefix_cache") = false,
+           py::keep_alive<1, 2>())
+      .def("add", &Scheduler::add, py::arg("sid"), py::arg("prompt_len"), py::arg("max_new_tokens"),
+           py::arg("tokens") = std::vector<int32_t>{})
+      .def_property_readonly("prefix_hit_tokens", &Scheduler::prefix_hit_tokens)
       .def("on_token", &Scheduler::on_token)
       .def("finish", &Scheduler::finish)
       .def("schedule", &Scheduler::schedule)

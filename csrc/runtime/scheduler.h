@@ -46,14 +46,23 @@ struct StepPlan {
 
 class Scheduler {
  public:
-  Scheduler(KVBlockManager& kv, int max_batch, int64_t max_prefill_tokens, bool mixed = false)
-      : kv_(kv), max_batch_(max_batch), max_prefill_tokens_(max_prefill_tokens), mixed_(mixed) {}
+  Scheduler(KVBlockManager& kv, int max_batch, int64_t max_prefill_tokens, bool mixed = false,
+            bool prefix_cache = false)
+      : kv_(kv), max_batch_(max_batch), max_prefill_tokens_(max_prefill_tokens), mixed_(mixed),
+        prefix_cache_(mixed && prefix_cache) {}
 
-  void add(int64_t sid, int64_t prompt_len, int64_t max_new_tokens) {
+  // `tokens` (optional): the prompt, for prefix caching (mixed mode: a later chunk, or a
+  // request admitted with a cached prefix, attends to the cached pages of earlier tokens).
+  void add(int64_t sid, int64_t prompt_len, int64_t max_new_tokens,
+           const std::vector<int32_t>& tokens = {}) {
     if (info_.count(sid)) throw std::invalid_argument("duplicate sequence id");
-    info_[sid] = Info{prompt_len, 0, max_new_tokens, false};
+    Info in{prompt_len, 0, max_new_tokens, false, {}};
+    if (prefix_cache_ && (int64_t)tokens.size() == prompt_len) in.hashes = kv_.block_hashes(tokens);
+    info_[sid] = std::move(in);
     waiting_.push_back(sid);
   }
+
+  int64_t prefix_hit_tokens() const { return prefix_hit_tokens_; }
 
   // Record one generated token (after a prefill or decode step produced it).
   void on_token(int64_t sid) { info_.at(sid).generated++; }
@@ -127,6 +136,7 @@ class Scheduler {
   struct Info {
     int64_t prompt_len, generated, max_new;
     bool in_prefill;   // mixed mode: admitted, its (re)prompt not yet fully scheduled
+    std::vector<uint64_t> hashes;   // prefix cache: chained hashes of the prompt's full blocks
   };
 
   StepPlan schedule_mixed() {
@@ -175,23 +185,33 @@ class Scheduler {
       budget -= n;
     }
     // --- 3. admit waiting sequences (FIFO) into the remaining budget ----------------------------
+    const int bs = kv_.block_size();
     while (budget > 0 && !waiting_.empty() && (int)running_.size() < max_batch_) {
       const int64_t sid = waiting_.front();
       Info& in = info_.at(sid);
       const int64_t target = in.prompt_len + in.generated;   // recompute after preemption
-      const int64_t n = std::min(target, budget);
-      // the first chunk's pages (+ one decode page when it is the whole prompt)
-      if (kv_.blocks_needed(n + (n == target ? 1 : 0)) > kv_.num_free()) break;
+      // cached prefix: whole blocks, and at least one token left to compute (it yields logits)
+      const int P = prefix_cache_ ? kv_.match_prefix(in.hashes, (int)((target - 1) / bs)) : 0;
+      const int64_t start = (int64_t)P * bs;
+      const int64_t n = std::min(target - start, budget);
+      const bool fin = start + n == target;
+      // fresh pages for the chunk (+ one decode page when it completes the prompt); the
+      // matched pages may be parked ones, which also count as free: reserve them too
+      if (kv_.blocks_needed(start + n + (fin ? 1 : 0)) > kv_.num_free()) break;
       waiting_.pop_front();
       running_.push_back(sid);
       plan.seq_ids.push_back(sid);
-      plan.prefill_starts.push_back(0);
+      plan.prefill_starts.push_back(start);
       plan.prefill_lens.push_back(n);
-      plan.prefill_slots.push_back(kv_.allocate(sid, n));
-      plan.prefill_final.push_back(n == target);
-      in.in_prefill = n < target;
+      plan.prefill_slots.push_back(P > 0 ? kv_.allocate_prefixed(sid, in.hashes, P, n) : kv_.allocate(sid, n));
+      plan.prefill_final.push_back(fin);
+      in.in_prefill = !fin;
+      prefix_hit_tokens_ += start;
       budget -= n;
     }
+    if (prefix_cache_)   // pages completed by this step's chunks become reusable next step
+      for (size_t j = plan.num_decode; j < plan.seq_ids.size(); ++j)
+        kv_.register_blocks(plan.seq_ids[j], info_.at(plan.seq_ids[j]).hashes);
     const bool has_prefill = (int)plan.seq_ids.size() > plan.num_decode;
     plan.kind = plan.num_decode > 0 ? (has_prefill ? 3 : 2) : (has_prefill ? 1 : 0);
     return plan;
@@ -201,6 +221,8 @@ class Scheduler {
   int max_batch_;
   int64_t max_prefill_tokens_;
   bool mixed_;
+  bool prefix_cache_;
+  int64_t prefix_hit_tokens_ = 0;
   std::deque<int64_t> waiting_;
   std::vector<int64_t> running_;
   std::unordered_map<int64_t, Info> info_;

@@ -29,6 +29,26 @@ using namespace bfly_rt;
     }                                                                          \
   } while (0)
 
+static void test_prefix_cache_pages() {
+  KVBlockManager kv(8, 4);
+  std::vector<int32_t> t = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10};
+  auto hs = kv.block_hashes(t);                  // 2 full blocks
+  CHECK(hs.size() == 2 && hs[0] != hs[1]);
+  kv.allocate(1, 10);
+  kv.register_blocks(1, hs);
+  CHECK(kv.num_cached_blocks() == 2 && kv.match_prefix(hs, 2) == 2);
+  kv.free(1);                                    // pages parked, still free capacity
+  CHECK(kv.num_free() == 8 && kv.match_prefix(hs, 2) == 2);
+  auto slots = kv.allocate_prefixed(2, hs, 2, 3);   // reuse both pages, 3 new tokens
+  CHECK(slots.size() == 3 && kv.length(2) == 11 && kv.num_free() == 5);
+  kv.free(2);
+  // exhaust the free list: parked pages are evicted (and unregistered) last
+  kv.allocate(3, 32);
+  CHECK(kv.num_free() == 0 && kv.num_cached_blocks() == 0 && kv.match_prefix(hs, 2) == 0);
+  kv.free(3);
+  CHECK(kv.num_free() == 8);
+}
+
 static void test_kv_manager() {
   KVBlockManager kv(16, 4);
   auto a = kv.allocate(1, 6);                // 2 pages
@@ -53,11 +73,11 @@ static void test_kv_manager() {
   CHECK(threw && kv.num_free() == 16);
 }
 
-static void run_stream(bool mixed, unsigned seed) {
+static void run_stream(bool mixed, unsigned seed, bool prefix_cache = false) {
   std::mt19937 rng(seed);
   const int kPages = 48, kBS = 8, kMaxBatch = 6;
   KVBlockManager kv(kPages, kBS);
-  Scheduler sch(kv, kMaxBatch, /*max_prefill_tokens=*/mixed ? 24 : 64, mixed);
+  Scheduler sch(kv, kMaxBatch, /*max_prefill_tokens=*/mixed ? 24 : 64, mixed, prefix_cache);
   struct Req {
     int64_t prompt, max_new, gen = 0;
     int64_t cached = 0;      // tokens of (prompt + generated) scheduled into the cache
@@ -66,9 +86,16 @@ static void run_stream(bool mixed, unsigned seed) {
   std::unordered_map<int64_t, Req> reqs;
   int64_t next_id = 0;
   int steps = 0;
+  // prompts drawn from 3 shared prefixes + a random tail (prefix-cache hits and evictions)
+  std::vector<std::vector<int32_t>> heads(3);
+  for (auto& h : heads)
+    for (int i = 0; i < 24; ++i) h.push_back((int32_t)(rng() % 1000));
   auto add = [&]() {
     Req r{(int64_t)(rng() % 40) + 1, (int64_t)(rng() % 12) + 1};
-    sch.add(next_id, r.prompt, r.max_new);
+    std::vector<int32_t> toks;
+    const auto& h = heads[rng() % 3];
+    for (int64_t i = 0; i < r.prompt; ++i) toks.push_back(i < 24 && rng() % 8 ? h[i] : (int32_t)(rng() % 1000));
+    sch.add(next_id, r.prompt, r.max_new, toks);
     reqs[next_id++] = r;
   };
   for (int i = 0; i < 8; ++i) add();
@@ -91,6 +118,10 @@ static void run_stream(bool mixed, unsigned seed) {
     for (size_t j = 0; j + nd < p.seq_ids.size(); ++j) {
       const int64_t sid = p.seq_ids[nd + j];
       Req& r = reqs.at(sid);
+      if (r.cached == 0 && p.prefill_starts[j] > 0) {   // admitted with a cached prefix
+        CHECK(prefix_cache && p.prefill_starts[j] % kBS == 0 && p.prefill_starts[j] < r.prompt + r.gen);
+        r.cached = p.prefill_starts[j];
+      }
       CHECK(p.prefill_starts[j] == r.cached);          // chunks tile the (re)prompt in order
       CHECK((int64_t)p.prefill_slots[j].size() == p.prefill_lens[j] && p.prefill_lens[j] > 0);
       for (int32_t s : p.prefill_slots[j]) CHECK(used.insert(s).second);
@@ -114,14 +145,17 @@ static void run_stream(bool mixed, unsigned seed) {
   }
   for (auto& kvp : reqs) CHECK(kvp.second.done && kvp.second.gen == kvp.second.max_new);
   CHECK(kv.num_free() == kPages && kv.num_seqs() == 0);
-  std::printf("stream mixed=%d seed=%u: %zu requests in %d steps\n", (int)mixed, seed, reqs.size(), steps);
+  std::printf("stream mixed=%d prefix_cache=%d seed=%u: %zu requests in %d steps, %lld prefix-hit tokens\n",
+              (int)mixed, (int)prefix_cache, seed, reqs.size(), steps, (long long)sch.prefix_hit_tokens());
 }
 
 int main() {
   test_kv_manager();
+  test_prefix_cache_pages();
   for (unsigned seed = 1; seed <= 20; ++seed) {
     run_stream(false, seed);
     run_stream(true, seed);
+    run_stream(true, seed, /*prefix_cache=*/true);
   }
   std::printf("runtime selftest: PASS\n");
   return 0;

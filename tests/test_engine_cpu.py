@@ -65,3 +65,29 @@ def test_mixed_chunked_prefill_matches_unmixed(budget):
     got, kinds = run(True)
     assert got == ref
     assert "mixed" in kinds
+
+
+def test_prefix_caching_reuses_pages_and_matches():
+    """Requests sharing a long prompt prefix: later ones take the cached pages (prefill starts
+    after the shared blocks) and generate exactly what an engine without the cache does —
+    also after the first owner finished (its pages parked in the LRU, not freed)."""
+    cfg = ModelConfig.from_preset("llama-tiny")
+    shared = [(13 * j) % 1000 + 1 for j in range(100)]
+    prompts = [shared + [5, 6, 7], shared + [9], shared[:64] + [1, 2, 3, 4], shared + [5, 6, 7, 8]]
+
+    def run(cache):
+        e = LLMEngine(cfg, engine_cfg=EngineConfig(max_batch=4, max_seq_len=256, max_prefill_tokens=64,
+                                                   kv_cache_tokens=2048, use_graphs=False, seed=4,
+                                                   prefix_caching=cache), device="cpu")
+        first = e.add_request(prompts[0], SamplingParams(max_tokens=5, ignore_eos=True))
+        while e.has_unfinished():
+            e.step()
+        rids = [e.add_request(p, SamplingParams(max_tokens=5, ignore_eos=True)) for p in prompts[1:]]
+        while e.has_unfinished():
+            e.step()
+        return [e.requests[r].output for r in [first] + rids], e.scheduler.prefix_hit_tokens
+
+    ref, hits0 = run(False)
+    got, hits = run(True)
+    assert got == ref
+    assert hits0 == 0 and hits >= 3 * 64      # three later prompts reuse >= 2 blocks of 32
