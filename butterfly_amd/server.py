@@ -7,6 +7,11 @@ group, every rank adds them to its engine in the same order, and all ranks take 
 together — identical scheduler inputs on every rank, so identical step plans (the engine's
 determinism contract, engine/engine.py). Data-parallel replicas: rank 0 assigns each request
 to a replica round-robin; replicas that get nothing simply step idle.
+
+Streaming (`"stream": true`, OpenAI server-sent events): the stream flag travels with the
+request broadcast, so each replica's leader also reports the tokens its streaming requests
+gained in the step; rank 0 pushes them into the request's queue and the HTTP handler emits one
+`data:` event per token, then a final event with the finish reason and `data: [DONE]`.
 """
 from __future__ import annotations
 
@@ -34,6 +39,8 @@ class ServingLoop:
         self.inbox: "queue.Queue" = queue.Queue()
         self.waiters: dict = {}
         self.results: dict = {}
+        self.streams: dict = {}          # rank 0: gid -> queue of ("token", id) / ("done", result)
+        self.streaming: set = set()      # every rank: gids whose tokens are reported per step
         self.idle_sleep = idle_sleep
         self.stop = False
         self._ids = itertools.count()
@@ -41,12 +48,28 @@ class ServingLoop:
         self.ctrl = dist.new_group(backend="gloo") if self.world > 1 else None
 
     # rank 0: called from HTTP handlers (any thread)
-    def submit(self, token_ids: list, params: SamplingParams) -> int:
+    def submit(self, token_ids: list, params: SamplingParams, stream: bool = False) -> int:
         gid = next(self._ids)
         ev = threading.Event()
         self.waiters[gid] = ev
-        self.inbox.put((gid, list(token_ids), params, next(self._dp_rr) % self.llm.plan.dp))
+        if stream:
+            self.streams[gid] = queue.Queue()
+        self.inbox.put((gid, list(token_ids), params, next(self._dp_rr) % self.llm.plan.dp, stream))
         return gid
+
+    def stream_events(self, gid: int, timeout: float = 600.0):
+        """Blocking iterator over ("token", id) ... ("done", result) for a streaming request."""
+        q = self.streams[gid]
+        try:
+            while True:
+                kind, val = q.get(timeout=timeout)
+                yield kind, val
+                if kind == "done":
+                    return
+        finally:
+            self.streams.pop(gid, None)
+            self.waiters.pop(gid, None)
+            self.results.pop(gid, None)
 
     def wait(self, gid: int, timeout: Optional[float] = None) -> dict:
         self.waiters[gid].wait(timeout)
@@ -76,15 +99,20 @@ class ServingLoop:
         leader = c.tp == 0 and c.pp == 0          # one reporter per data-parallel replica
         while True:
             new, stop = self._exchange()
-            for gid, ids, params, dp in new:
+            for gid, ids, params, dp, stream in new:
                 if dp == my_dp:
                     eng.add_request(ids, params, rid=gid)
+                    if stream:
+                        self.streaming.add(gid)
             if stop and self._all_idle():      # collective: every rank evaluates it
                 return
-            finished = []
+            finished, tokens = [], []
             if eng.has_unfinished() or self.llm.plan.ep > 1:
                 out = eng.step()
+                if self.streaming:
+                    tokens = [(r, t) for r, t in zip(out.rids, out.new_tokens) if r in self.streaming]
                 for rid in out.finished:
+                    self.streaming.discard(rid)
                     req = eng.requests.pop(rid)
                     finished.append((rid, {"token_ids": list(req.output), "finish_reason": req.finish_reason,
                                            "ttft_s": req.first_token_time - req.arrival if req.first_token_time else None,
@@ -93,10 +121,15 @@ class ServingLoop:
                 time.sleep(self.idle_sleep)
             if self.world > 1:
                 got = [None] * self.world if self.rank == 0 else None
-                dist.gather_object(finished if leader else [], got, dst=0, group=self.ctrl)
+                dist.gather_object((finished, tokens) if leader else ([], []), got, dst=0, group=self.ctrl)
                 if self.rank == 0:
-                    finished = [x for lst in got for x in lst]
+                    finished = [x for f, _ in got for x in f]
+                    tokens = [x for _, t in got for x in t]
             if self.rank == 0:
+                for rid, tok in tokens:
+                    q = self.streams.get(rid)
+                    if q is not None:
+                        q.put(("token", int(tok)))
                 for rid, res in finished:
                     self._publish(rid, res)
 
@@ -109,6 +142,10 @@ class ServingLoop:
         return not any(o[0] for o in out)
 
     def _publish(self, rid, res) -> None:
+        q = self.streams.get(rid)
+        if q is not None:
+            q.put(("done", res))
+            return
         self.results[rid] = res
         ev = self.waiters.get(rid)
         if ev:
@@ -118,15 +155,18 @@ class ServingLoop:
 def _request_model(BaseModel):
     # built at runtime (pydantic is imported lazily); annotations are real types, not strings
     ns = {"__annotations__": {"model": Optional[str], "prompt": object, "max_tokens": int, "temperature": float,
-                              "top_p": float, "top_k": int, "seed": Optional[int], "stop_token_ids": list},
+                              "top_p": float, "top_k": int, "seed": Optional[int], "stop_token_ids": list,
+                              "stream": bool},
           "model": None, "max_tokens": 16, "temperature": 0.0, "top_p": 1.0, "top_k": 0, "seed": None,
-          "stop_token_ids": []}
+          "stop_token_ids": [], "stream": False}
     return type("CompletionRequest", (BaseModel,), ns)
 
 
 def create_app(loop: ServingLoop):
+    import json
+
     from fastapi import FastAPI, HTTPException
-    from fastapi.responses import PlainTextResponse
+    from fastapi.responses import PlainTextResponse, StreamingResponse
     from pydantic import BaseModel
 
     app = FastAPI(title="butterfly_amd")
@@ -155,6 +195,23 @@ def create_app(loop: ServingLoop):
             raise HTTPException(400, "prompt must be a string or a list of token ids")
         params = SamplingParams(max_tokens=req.max_tokens, temperature=req.temperature, top_p=req.top_p,
                                 top_k=req.top_k, seed=req.seed, stop_token_ids=req.stop_token_ids)
+        if req.stream:
+            gid = loop.submit(ids, params, stream=True)
+
+            def sse():   # runs in Starlette's threadpool: the blocking queue reads are fine
+                for kind, val in loop.stream_events(gid):
+                    if kind == "token":
+                        chunk = {"index": 0, "token_ids": [val], "text": tok.decode([val]) if is_text else None,
+                                 "finish_reason": None}
+                    else:
+                        chunk = {"index": 0, "token_ids": [], "text": "" if is_text else None,
+                                 "finish_reason": val["finish_reason"]}
+                    ev = {"id": f"cmpl-{gid}", "object": "text_completion", "model": loop.llm.cfg.name,
+                          "choices": [chunk]}
+                    yield f"data: {json.dumps(ev)}\n\n"
+                yield "data: [DONE]\n\n"
+
+            return StreamingResponse(sse(), media_type="text/event-stream")
         gid = loop.submit(ids, params)
         res = await asyncio.get_running_loop().run_in_executor(None, loop.wait, gid, 600.0)
         text = tok.decode(res["token_ids"]) if is_text else None

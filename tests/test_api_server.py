@@ -41,6 +41,15 @@ def test_http_completions():
         r2 = c.post("/v1/completions", json={"prompt": "hi there", "max_tokens": 3}).json()
         assert isinstance(r2["choices"][0]["text"], str)
         assert "bfly_steps_decode" in c.get("/metrics").text
+        # server-sent events: one event per generated token, then the finish event and [DONE]
+        import json
+
+        with c.stream("POST", "/v1/completions", json={"prompt": [1, 2, 3], "max_tokens": 4, "stream": True}) as resp:
+            events = [ln[len("data: "):] for ln in resp.iter_lines() if ln.startswith("data: ")]
+        assert events[-1] == "[DONE]"
+        chunks = [json.loads(e)["choices"][0] for e in events[:-1]]
+        assert [t for ch in chunks for t in ch["token_ids"]] == r["choices"][0]["token_ids"]
+        assert chunks[-1]["finish_reason"] == "length"
     finally:
         loop.stop = True
         th.join(timeout=30)
