@@ -228,6 +228,14 @@ class LLMEngine:
         rids = list(plan.seq_ids)
         if plan.cow:
             self.kv.copy_blocks(list(plan.cow))
+        m = self.kv.manager
+        self.metrics.set("kv_blocks_free", m.num_free)
+        self.metrics.set("kv_blocks_used_fraction", 1.0 - m.num_free / max(1, m.num_blocks))
+        if self.prefix_cache:
+            self.metrics.set("prefix_cache_hit_tokens", self.scheduler.prefix_hit_tokens)
+            self.metrics.set("prefix_cache_blocks", m.num_cached_blocks)
+        if plan.preempted:
+            self.metrics.inc("preempted_sequences", len(plan.preempted))
         if self.mixed and plan.kind in (1, 3):
             # chunked prefill (+ decode rows): sample the decode rows and completed prompts
             fb, sample = self.runner.mixed_batch(plan, lambda r: self.requests[r].tokens)
