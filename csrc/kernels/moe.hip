@@ -1,9 +1,9 @@
 // Mixture-of-experts kernels (K11 router, K12 gating) for the dense-dispatch MoE path.
 //
-// moe_route: one wave per token. logits[e] = x . Wr[e] (E <= 64 experts, 16-B loads of the
-// token row and of each router row), softmax over experts, top-k selection, renormalisation
-// over the selected experts (Mixtral semantics), and a dense gate row gates[t, e] (0 for
-// experts not selected) used by the fixed-shape expert GEMMs; topk ids/weights are also
+// moe_route: one workgroup per token. logits[e] = x . Wr[e] (E <= 64 experts, 16-B loads of
+// the token row and of each router row, 4-wave reduction), softmax over experts, top-k
+// selection, renormalisation over the selected experts (Mixtral semantics), and a dense gate
+// row gates[t, e] (0 for experts not selected) used by the fixed-shape expert GEMMs; topk ids/weights are also
 // emitted for the sparse (grouped) path and for routing statistics.
 //
 // moe_gate_scale: h[t, e*F + f] *= gates[t, e0 + e] for the local experts: the gate weight is
@@ -29,48 +29,53 @@ __global__ void __launch_bounds__(256)
 moe_route_kernel(const bf16* __restrict__ x, long x_stride, const bf16* __restrict__ wr, int T,
                  int H, int E, int K, float* __restrict__ gates, int* __restrict__ topk_ids,
                  float* __restrict__ topk_w) {
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= T) return;
+  // one workgroup per token: the 256 threads split the hidden dim (16-B chunks), every expert's
+  // partial dot is wave-reduced and the 4 wave partials summed through LDS; wave 0 then holds
+  // logit e in lane e (E <= 64) for the softmax / top-k, all in registers (no scratch arrays).
+  __shared__ float red[4][kMaxExperts];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int t = blockIdx.x;
   const bf16* xr = x + (long)t * x_stride;
-  float logit[kMaxExperts];
+#pragma unroll 2
   for (int e = 0; e < E; ++e) {
     float acc = 0.f;
-    for (int c = lane * 8; c < H; c += 64 * 8) {
+    for (int c = tid * 8; c < H; c += 256 * 8) {
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(xr + c);
       const bf16x8 w = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc += bf2f(a[j]) * bf2f(w[j]);
     }
-    logit[e] = wave_sum(acc);
+    acc = wave_sum(acc);
+    if (lane == 0) red[wv][e] = acc;
   }
-  if (lane != 0) return;
-  float mx = -INFINITY;
-  for (int e = 0; e < E; ++e) mx = fmaxf(mx, logit[e]);
-  float den = 0.f;
-  for (int e = 0; e < E; ++e) {
-    logit[e] = __expf(logit[e] - mx);
-    den += logit[e];
-  }
-  for (int e = 0; e < E; ++e) gates[(long)t * E + e] = 0.f;
-  float sel_sum = 0.f;
-  int ids[8];
-  float ws[8];
+  __syncthreads();
+  if (wv != 0) return;
+  const bool live = lane < E;
+  const float logit = live ? red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane] : -INFINITY;
+  const float mx = wave_max(logit);
+  float p = live ? __expf(logit - mx) : 0.f;
+  const float den = wave_sum(p);
+  float g = 0.f, sel_sum = 0.f;
+  int my_rank = -1;                     // this expert's position in the top-k (-1: not selected)
   for (int k = 0; k < K; ++k) {
-    int best = 0;
-    float bv = -1.f;
-    for (int e = 0; e < E; ++e)
-      if (logit[e] > bv) { bv = logit[e]; best = e; }
-    ids[k] = best;
-    ws[k] = bv / den;
-    sel_sum += ws[k];
-    logit[best] = -2.f;  // exclude from further selection
+    // arg-max over lanes, ties to the lowest expert id
+    float bv = live ? p : -1.f;
+    int bi = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    sel_sum += bv / den;
+    if (lane == bi) { my_rank = k; g = p / den; p = -1.f; }
   }
-  for (int k = 0; k < K; ++k) {
-    const float w = ws[k] / sel_sum;
-    topk_ids[(long)t * K + k] = ids[k];
-    topk_w[(long)t * K + k] = w;
-    gates[(long)t * E + ids[k]] = w;
+  if (!live) return;
+  const float w = my_rank >= 0 ? g / sel_sum : 0.f;
+  gates[(long)t * E + lane] = w;
+  if (my_rank >= 0) {
+    topk_ids[(long)t * K + my_rank] = lane;
+    topk_w[(long)t * K + my_rank] = w;
   }
 }
 
@@ -167,7 +172,7 @@ int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H,
                      float* gates, int* topk_ids, float* topk_w, hipStream_t stream) {
   if (T <= 0) return 0;
   if (E > kMaxExperts || K > 8 || K > E || H % 8 != 0) return -1;
-  moe_route_kernel<<<(T + 3) / 4, 256, 0, stream>>>(x, x_stride, wr, T, H, E, K, gates, topk_ids, topk_w);
+  moe_route_kernel<<<T, 256, 0, stream>>>(x, x_stride, wr, T, H, E, K, gates, topk_ids, topk_w);
   return 0;
 }
 
