@@ -583,20 +583,28 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
 
 // ---------------------------------------------------------------------------------------
 // Big-tile GEMM (prefill / large M): 256x256 tile, 8 waves (2 along M x 4 along N, each
-// owning a 128x64 output block = 8x4 MFMA 16x16x32 accumulators), BK = 32, 4-stage ring of
-// glds-staged K-tiles (4 x 32 KiB = 128 KiB LDS, one workgroup per CU). Per K-step a wave
+// owning a 128x64 output block = 8x4 MFMA 16x16x32 accumulators), BK = 32, 5-stage ring of
+// glds-staged K-tiles (5 x 32 KiB = the whole 160 KiB LDS, one workgroup per CU). Per K-step a wave
 // issues 12 ds_read_b128 and 32 MFMAs (half the LDS bytes per MFMA of the 128x128 tile), waits
-// for its K-tile with a counted vmcnt (two K-tiles stay in flight across the raw barrier),
+// for its K-tile with a counted vmcnt (up to three K-tiles stay in flight across the raw barrier),
 // and runs the MFMA cluster at raised priority (cdna_hip_programming.md T3/T4 + setprio).
-// LDS rows are 64 B; slot = chunk ^ ((row >> 2) & 3) makes every 16-lane ds_read_b128 group
-// hit 16 distinct 16-B slots of the bank row (the DMA writes lane-linearly, so the swizzle is
+// LDS rows are 64 B; the big_swz permutation makes every 16-lane ds_read_b128 group hit 16
+// distinct 16-B slots of the bank line (the DMA writes lane-linearly, so the swizzle is
 // applied on the per-lane SOURCE address). Tiles are walked in GROUP_M super-rows inside each
 // XCD's contiguous range, so the 32 CUs of an XCD share X and W panels in their L2.
 // ---------------------------------------------------------------------------------------
 constexpr int kBigThreads = 512;
 constexpr int kBigBK = 32;
-constexpr int kBigStages = 4;
+constexpr int kBigStages = 5;   // 5 x 32 KiB = the whole 160 KiB LDS (1-2 % over 4 stages)
 constexpr int kBigGroupM = 8;
+
+// 64-B rows put 4 rows on one 256-B bank line; the 16-B slot of (row, chunk) is
+// (row % 4) * 4 + (chunk ^ big_swz(row)). ds_read_b128 serves a wave in the lane groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): for a fragment read (row = lane & 15,
+// chunk = lane >> 4) each group holds rows {q, q+4, q+8, q+12} of one q = row % 4 with chunks
+// {c, c^1, c^1, c}, and the permutation 0,2,3,1 over (row >> 2) & 3 sends those to 4 distinct
+// slots: conflict-free (a plain XOR with (row >> 2) & 3 is 2-way in every group).
+__device__ __forceinline__ int big_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
 
 __device__ __forceinline__ void big_stage(const bf16* __restrict__ src, long ld, int row0,
                                           int row_max, int k0, char* lds, int wid, int lane) {
@@ -606,7 +614,7 @@ __device__ __forceinline__ void big_stage(const bf16* __restrict__ src, long ld,
     const int blk = i * 8 + wid;
     const int row = blk * 16 + (lane >> 2);
     const int slot = lane & 3;
-    const int chunk = slot ^ ((row >> 2) & 3);
+    const int chunk = slot ^ big_swz(row);
     int gr = row0 + row;
     gr = gr < row_max ? gr : row_max - 1;
     const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
@@ -615,9 +623,19 @@ __device__ __forceinline__ void big_stage(const bf16* __restrict__ src, long ld,
 }
 
 __device__ __forceinline__ bf16x8 big_frag(const char* lds, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(lds + row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4));
+  return *reinterpret_cast<const bf16x8*>(lds + row * 64 + ((chunk ^ big_swz(row)) << 4));
 }
 
+// s_waitcnt vmcnt(n * LPW) for a runtime n in [0, S-2] (vmcnt takes an immediate).
+template <int S, int LPW>
+__device__ __forceinline__ void big_wait(int n) {
+  if (S > 4 && n >= 3) vm_wait<3 * LPW>();
+  else if (n >= 2) vm_wait<2 * LPW>();
+  else if (n == 1) vm_wait<LPW>();
+  else vm_wait<0>();
+}
+
+template <int S>
 __global__ void __launch_bounds__(kBigThreads)
 gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -659,19 +677,15 @@ gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
   // they passed, lgkmcnt(0) retired) with stage k+3, and retires its ds_reads before the
   // barrier that ends the phase.
 #pragma unroll
-  for (int s = 0; s < kBigStages - 1; ++s) {
+  for (int s = 0; s < S - 1; ++s) {
     if (kt0 + s < kt1) {
       char* b = smem + s * STAGE_BYTES;
       big_stage(X, ldx, m0, M, (kt0 + s) * kBigBK, b, wid, lane);
       big_stage(W, ldw, n0, N, (kt0 + s) * kBigBK, b + A_BYTES, wid, lane);
     }
   }
-  {
-    const int issued = min(kBigStages - 1, kt1 - kt0);   // stages in flight; stage 0 must land
-    if (issued >= 3) vm_wait<2 * LPW>();
-    else if (issued == 2) vm_wait<LPW>();
-    else vm_wait<0>();
-  }
+  // stage 0 must land; the (issued - 1) later stages may still fly
+  big_wait<S, LPW>(min(S - 1, kt1 - kt0) - 1);
   __builtin_amdgcn_s_barrier();
   if (wm == 1) __builtin_amdgcn_s_barrier();
   int buf = 0;
@@ -684,17 +698,15 @@ gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
     for (int j = 0; j < TJ; ++j) bfr[j] = big_frag(Bs, wn * 64 + 16 * j + (lane & 15), lane >> 4);
 #pragma unroll
     for (int i = 0; i < TI; ++i) af[i] = big_frag(As, wm * 128 + 16 * i + (lane & 15), lane >> 4);
-    if (kt + kBigStages - 1 < kt1) {
-      int nbuf = buf + kBigStages - 1;
-      if (nbuf >= kBigStages) nbuf -= kBigStages;
+    if (kt + S - 1 < kt1) {
+      int nbuf = buf + S - 1;
+      if (nbuf >= S) nbuf -= S;
       char* nb = smem + nbuf * STAGE_BYTES;
-      big_stage(X, ldx, m0, M, (kt + kBigStages - 1) * kBigBK, nb, wid, lane);
-      big_stage(W, ldw, n0, N, (kt + kBigStages - 1) * kBigBK, nb + A_BYTES, wid, lane);
+      big_stage(X, ldx, m0, M, (kt + S - 1) * kBigBK, nb, wid, lane);
+      big_stage(W, ldw, n0, N, (kt + S - 1) * kBigBK, nb + A_BYTES, wid, lane);
     }
-    // stage kt+1 must have landed; stages kt+2 / kt+3 (just issued) may still fly
-    if (kt + 3 < kt1) vm_wait<2 * LPW>();
-    else if (kt + 2 < kt1) vm_wait<LPW>();
-    else vm_wait<0>();
+    // stage kt+1 must have landed; stages kt+2 .. kt+S-1 (issued) may still fly
+    big_wait<S, LPW>(min(kt1 - 1, kt + S - 1) - (kt + 1));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // MFMA phase
@@ -705,7 +717,7 @@ gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
       for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
-    if (++buf == kBigStages) buf = 0;
+    if (++buf == S) buf = 0;
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
 
@@ -819,16 +831,22 @@ static void run_big(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                     hipStream_t stream) {
   const int tiles = ((M + 255) / 256) * (N / 256);
-  const size_t lds = (size_t)kBigStages * 2 * 256 * kBigBK * 2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
+  static int stages = 0;
+  if (!stages) {
+    const char* e = getenv("BFLY_BIG_STAGES");
+    stages = e && atoi(e) == 4 ? 4 : kBigStages;   // BFLY_BIG_STAGES=4: A/B against the 128 KiB ring
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<4>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 256 * kBigBK * 2);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<5>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 256 * kBigBK * 2);
   }
+  const size_t lds = (size_t)stages * 2 * 256 * kBigBK * 2;
   dim3 grid(tiles, sk);
-  gemm_big_kernel<<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo,
-                                                      sk > 1 ? splitk_part(ws) : nullptr);
+  float* part = sk > 1 ? splitk_part(ws) : nullptr;
+  if (stages == 5)
+    gemm_big_kernel<5><<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  else
+    gemm_big_kernel<4><<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
 
