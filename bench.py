@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=1024)
     ap.add_argument("--plan", default="auto", help="auto | e.g. tp8, tp2xpp4, dp2xtp4")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kv-dtype", default="auto", help="KV-cache elements: auto (= bf16) | fp8")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     a = ap.parse_args()
 
@@ -96,7 +97,8 @@ def main():
                         max_prefill_tokens=prefill_budget,
                         kv_cache_tokens=replica_batch * (max_seq + 32),
                         use_graphs=not a.no_graphs,
-                        graph_batch_sizes=[replica_batch])
+                        graph_batch_sizes=[replica_batch],
+                        kv_cache_dtype=a.kv_dtype)
     t0 = time.perf_counter()
     eng = LLMEngine(cfg, mesh, ecfg, comm=comm, stage_layers=plan.stages)
     sync()
@@ -177,7 +179,7 @@ def main():
         "config": {"model": "Llama-3-70B" if a.model == "llama3-70b" else a.model,
                    "global_batch": a.batch_per_gpu * a.gpus, "seq_len": a.prompt_len,
                    "parallelism": plan.name, "stages": [list(s) for s in plan.stages],
-                   "hipgraph": eng.runner.use_graphs, "pp_async_groups": groups if groups > 1 else None},
+                   "hipgraph": eng.runner.use_graphs, "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""), "pp_async_groups": groups if groups > 1 else None},
     }
     if rank == 0:
         line = json.dumps(res)

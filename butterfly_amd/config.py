@@ -213,6 +213,10 @@ class EngineConfig:
     # automatic prefix caching (with mixed_prefill): full prompt pages are registered under a
     # hash of their token prefix and reused by later requests that start with the same tokens
     prefix_caching: bool = True
+    # KV-cache element type: "auto" (= the model dtype, bf16 on GPU) or "fp8" (e4m3, unscaled,
+    # |x| <= 448): half the KV bytes per token, so twice the cached tokens and half the KV
+    # traffic of a decode step; attention math stays bf16 (csrc/include/bfly_kv.h)
+    kv_cache_dtype: str = "auto"
 
 
 def load_config_file(path: str | Path) -> dict:

@@ -94,7 +94,8 @@ class LLMEngine:
         self.eos = eos_token_id
         # ---- KV cache sizing ------------------------------------------------------------
         bs = engine_cfg.block_size
-        per_tok = self.model.kv_bytes_per_token()
+        self.kv_dtype = kv_cache_dtype(engine_cfg.kv_cache_dtype, self.model.dtype)
+        per_tok = self.model.kv_bytes_per_token(self.kv_dtype)
         if engine_cfg.kv_cache_tokens:
             nblocks = (engine_cfg.kv_cache_tokens + bs - 1) // bs
         else:
@@ -105,7 +106,7 @@ class LLMEngine:
             nblocks = min(nblocks, max(need, 1))
         if nblocks <= 0:
             raise RuntimeError("no HBM left for the KV cache")
-        self.kv = KVCache(self.model, nblocks, bs)
+        self.kv = KVCache(self.model, nblocks, bs, self.kv_dtype)
         native = __import__("butterfly_amd._native_loader", fromlist=["native"]).native()
         # pipeline parallelism without per-step fill/drain: pp request groups in flight
         # (engine/pipeline.py); EP layouts keep the synchronous path (EP collectives span DP ranks)
@@ -419,6 +420,18 @@ class LLMEngine:
         while self.has_unfinished():
             self.step()
         return [self.requests[r].output for r in rids]
+
+
+def kv_cache_dtype(name: str, model_dtype: torch.dtype) -> torch.dtype:
+    """EngineConfig.kv_cache_dtype -> torch dtype ("auto": the model's own dtype)."""
+    name = (name or "auto").lower()
+    if name in ("auto", "model"):
+        return model_dtype
+    if name in ("fp8", "fp8_e4m3", "float8_e4m3fn"):
+        return torch.float8_e4m3fn
+    if name in ("bf16", "bfloat16"):
+        return torch.bfloat16
+    raise ValueError(f"unknown kv_cache_dtype {name!r} (auto | bf16 | fp8)")
 
 
 def balanced_stages(num_layers: int, pp: int) -> list:

@@ -374,7 +374,7 @@ class TransformerLM:
             qp, kp, vp = q[nd:], k[nd:], v[nd:]
             if fb.prefix_lens is not None and any(fb.prefix_lens):
                 o, lse = ops.attn_prefill(qp, kp, vp, fb.cu_seqlens, fb.max_seqlen, self.scale, True, return_lse=True)
-                kpre, vpre = self._gather_prefix(kc, vc, fb.prefix_tables, fb.prefix_lens)
+                kpre, vpre = self._gather_prefix(kc, vc, fb.prefix_tables, fb.prefix_lens, q.dtype)
                 o2, l2 = ops.attn_prefill(qp, kpre, vpre, fb.cu_seqlens, fb.max_seqlen, self.scale, False,
                                           cu_seqlens_k=fb.prefix_cu, return_lse=True)
                 acc = o.float()
@@ -385,7 +385,7 @@ class TransformerLM:
         return parts[0] if len(parts) == 1 else torch.cat(parts)
 
     @staticmethod
-    def _gather_prefix(kc, vc, tables, lens: list) -> tuple:
+    def _gather_prefix(kc, vc, tables, lens: list, dtype: Optional[torch.dtype] = None) -> tuple:
         """Contiguous [sum(lens), Hkv, D] K and V of each sequence's first lens[i] cached tokens
         (paged layouts: K [blocks, Hkv, BS, D], V [blocks, Hkv, D, BS])."""
         BS = kc.shape[2]
@@ -396,7 +396,10 @@ class TransformerLM:
             blk = tables[i, : (n + BS - 1) // BS].long()
             ks.append(kc.index_select(0, blk).permute(0, 2, 1, 3).reshape(-1, kc.shape[1], kc.shape[3])[:n])
             vs.append(vc.index_select(0, blk).permute(0, 3, 1, 2).reshape(-1, vc.shape[1], vc.shape[2])[:n])
-        return torch.cat(ks).contiguous(), torch.cat(vs).contiguous()
+        k, v = torch.cat(ks), torch.cat(vs)
+        if dtype is not None and k.dtype != dtype:     # FP8 cache: widen for flash attention
+            k, v = k.to(dtype), v.to(dtype)
+        return k.contiguous(), v.contiguous()
 
     def _add_norm(self, t: torch.Tensor, prefix: str, residual: torch.Tensor, partial: bool) -> torch.Tensor:
         """residual += (all_reduce(t) if partial else t); return norm(residual). With TP the
@@ -488,15 +491,17 @@ class TransformerLM:
     # ------------------------------------------------------------------------------------
     # KV cache layout helpers
     # ------------------------------------------------------------------------------------
-    def kv_bytes_per_token(self) -> int:
+    def kv_bytes_per_token(self, dtype: Optional[torch.dtype] = None) -> int:
         """Local KV bytes per cached token (local layers x local kv heads x K,V)."""
-        return 2 * len(self.layer_ids) * self.dims.hkv * self.cfg.head_dim * torch.finfo(self.dtype).bits // 8
+        bits = torch.finfo(dtype or self.dtype).bits
+        return 2 * len(self.layer_ids) * self.dims.hkv * self.cfg.head_dim * bits // 8
 
-    def allocate_kv_cache(self, num_blocks: int, block_size: int) -> list:
+    def allocate_kv_cache(self, num_blocks: int, block_size: int, dtype: Optional[torch.dtype] = None) -> list:
         D, hk = self.cfg.head_dim, self.dims.hkv
+        dt = dtype or self.dtype
         caches = []
         for _ in self.layer_ids:
-            k = torch.zeros(num_blocks, hk, block_size, D, dtype=self.dtype, device=self.device)
-            v = torch.zeros(num_blocks, hk, D, block_size, dtype=self.dtype, device=self.device)
+            k = torch.zeros(num_blocks, hk, block_size, D, dtype=dt, device=self.device)
+            v = torch.zeros(num_blocks, hk, D, block_size, dtype=dt, device=self.device)
             caches.append((k, v))
         return caches

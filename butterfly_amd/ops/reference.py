@@ -97,8 +97,11 @@ def kv_append(k, v, slots, k_cache, v_cache):
     keep = sl >= 0
     sl = sl[keep]
     blk, off = sl // BS, sl % BS
-    k_cache[blk, :, off, :] = k[keep].to(k_cache.dtype)
-    v_cache[blk, :, :, off] = v[keep].to(v_cache.dtype)
+    k, v = k[keep], v[keep]
+    if k_cache.dtype == torch.float8_e4m3fn:   # the kernels clamp to the e4m3 range
+        k, v = k.float().clamp(-448, 448), v.float().clamp(-448, 448)
+    k_cache[blk, :, off, :] = k.to(k_cache.dtype)
+    v_cache[blk, :, :, off] = v.to(v_cache.dtype)
 
 
 def silu_mul(gu, out=None, interleave=0):

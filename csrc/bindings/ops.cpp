@@ -27,6 +27,11 @@ inline bfly::bf16* bf(const Tensor& t) { return reinterpret_cast<bfly::bf16*>(t.
 #define CHECK_INNER(t) TORCH_CHECK((t).stride(-1) == 1, #t " must have unit inner stride")
 #define CHECK_ALIGN16(t) \
   TORCH_CHECK(reinterpret_cast<uintptr_t>((t).data_ptr()) % 16 == 0, #t " must be 16-B aligned")
+// paged KV caches: bf16, or FP8 e4m3 (torch.float8_e4m3fn) for the optional FP8 KV cache
+#define CHECK_KV(k, v)                                                                          \
+  TORCH_CHECK(((k).scalar_type() == at::kBFloat16 || (k).scalar_type() == at::kFloat8_e4m3fn) && \
+                  (v).scalar_type() == (k).scalar_type(),                                       \
+              "KV caches must both be bf16 or both float8_e4m3fn")
 #define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
 
 void rms_norm(const Tensor& x, const Tensor& w, double eps, Tensor& out,
@@ -85,24 +90,25 @@ void rope_kv(Tensor& qkv, const Tensor& positions, const Tensor& cos_t, const Te
   TORCH_CHECK(cos_t.is_contiguous() && sin_t.is_contiguous() && cos_t.size(-1) == D / 2 &&
                   sin_t.sizes() == cos_t.sizes(), "rope_kv: table shape [max_pos, D/2]");
   const int* sl = nullptr;
-  bfly::bf16 *kc = nullptr, *vc = nullptr;
-  int BS = 1;
+  void *kc = nullptr, *vc = nullptr;
+  int BS = 1, fp8 = 0;
   if (slots.has_value()) {
     CHECK_I32(*slots);
     TORCH_CHECK(slots->numel() == T, "rope_kv: slots");
     TORCH_CHECK(k_cache.has_value() && v_cache.has_value(), "rope_kv: caches required with slots");
     const Tensor& K = *k_cache;
     const Tensor& V = *v_cache;
-    CHECK_BF16(K); CHECK_BF16(V);
+    CHECK_KV(K, V);
     TORCH_CHECK(K.dim() == 4 && K.is_contiguous() && K.size(1) == num_kv_heads && K.size(3) == D,
                 "rope_kv: k_cache must be [blocks, Hkv, BS, D]");
     TORCH_CHECK(V.dim() == 4 && V.is_contiguous() && V.size(1) == num_kv_heads && V.size(2) == D &&
                     V.size(3) == K.size(2) && V.size(0) == K.size(0),
                 "rope_kv: v_cache must be [blocks, Hkv, D, BS]");
     sl = slots->data_ptr<int>();
-    kc = bf(K);
-    vc = bf(V);
+    kc = K.data_ptr();
+    vc = V.data_ptr();
     BS = K.size(2);
+    fp8 = K.scalar_type() == at::kFloat8_e4m3fn;
   }
   const float* part = nullptr;
   int sk = 0;
@@ -116,7 +122,7 @@ void rope_kv(Tensor& qkv, const Tensor& positions, const Tensor& cos_t, const Te
   c10::DeviceGuard g(qkv.device());
   bfly::launch_rope_kv(bf(qkv), T, num_q_heads, num_kv_heads, D, positions.data_ptr<int>(),
                        cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), sl, kc, vc, BS,
-                       cur_stream(), part, sk);
+                       cur_stream(), part, sk, fp8);
 }
 
 void kv_append(const Tensor& k, const Tensor& v, const Tensor& slots, Tensor& k_cache,
@@ -130,9 +136,12 @@ void kv_append(const Tensor& k, const Tensor& v, const Tensor& slots, Tensor& k_
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "kv_append: k_cache");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == D, "kv_append: v_cache");
   TORCH_CHECK(slots.numel() == T, "kv_append: slots");
+  CHECK_KV(k_cache, v_cache);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "kv_append: caches must be contiguous");
   c10::DeviceGuard g(k.device());
   bfly::launch_kv_append(bf(k), k.stride(0), bf(v), v.stride(0), slots.data_ptr<int>(),
-                         bf(k_cache), bf(v_cache), T, Hkv, D, k_cache.size(2), cur_stream());
+                         k_cache.data_ptr(), v_cache.data_ptr(), T, Hkv, D, k_cache.size(2), cur_stream(),
+                         k_cache.scalar_type() == at::kFloat8_e4m3fn);
 }
 
 void silu_mul(const Tensor& gu, Tensor& out, int64_t interleave) {
@@ -344,7 +353,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  int64_t max_ctx, int64_t part_tokens, Tensor& out,
                  const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml,
                  const c10::optional<Tensor>& counters) {
-  CHECK_GPU(q); CHECK_BF16(q); CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_BF16(out);
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_KV(k_cache, v_cache); CHECK_BF16(out);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "attn_decode: q [B, Hq, D]");
   const int B = q.size(0), Hq = q.size(1), D = q.size(2);
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "attn_decode: caches");
@@ -373,10 +382,11 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
     cnt = counters->data_ptr<int>();
   }
   c10::DeviceGuard g(q.device());
-  const int rc = bfly::launch_attn_decode(bf(q), q.stride(0), bf(k_cache), bf(v_cache),
+  const int rc = bfly::launch_attn_decode(bf(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                           block_tables.data_ptr<int>(), block_tables.stride(0),
                                           ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale,
-                                          max_ctx, part_tokens, bf(out), po, pml, cur_stream(), cnt);
+                                          max_ctx, part_tokens, bf(out), po, pml, cur_stream(), cnt,
+                                          k_cache.scalar_type() == at::kFloat8_e4m3fn);
   TORCH_CHECK(rc == 0, "attn_decode: unsupported configuration (rc=", rc, ")");
 }
 

@@ -31,13 +31,14 @@ void launch_layernorm(const bf16* x, bf16* residual, const bf16* w, const bf16* 
 // rope.hip
 // `part` (optional): the QKV row is the sum of `sk` f32 split-K slabs [sk][T][row] of the
 // GEMM (deferred reduce fused here); the bf16 row is written to `qkv` as well
+// Caches hold bf16, or FP8 e4m3 when `kv_fp8` (bfly_kv.h).
 void launch_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* positions,
-                    const float* cos_t, const float* sin_t, const int* slots, bf16* k_cache,
-                    bf16* v_cache, int block_size, hipStream_t stream,
-                    const float* part = nullptr, int sk = 0);
+                    const float* cos_t, const float* sin_t, const int* slots, void* k_cache,
+                    void* v_cache, int block_size, hipStream_t stream,
+                    const float* part = nullptr, int sk = 0, int kv_fp8 = 0);
 void launch_kv_append(const bf16* k, long k_stride, const bf16* v, long v_stride,
-                      const int* slots, bf16* k_cache, bf16* v_cache, int T, int Hkv, int D,
-                      int block_size, hipStream_t stream);
+                      const int* slots, void* k_cache, void* v_cache, int T, int Hkv, int D,
+                      int block_size, hipStream_t stream, int kv_fp8 = 0);
 
 // elementwise.hip
 void launch_silu_mul(const bf16* gu, bf16* out, long rows, int ffn, int interleave,
@@ -78,11 +79,12 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 // attention.hip
 int attn_decode_splits(int max_ctx, int part_tokens);
 int attn_decode_part_tokens(int B, int Hkv, int max_ctx);
-int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
+int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
                        bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                       int* counters = nullptr);   // zeroed [B*Hkv]: fused split combine
+                       int* counters = nullptr,    // zeroed [B*Hkv]: fused split combine
+                       int kv_fp8 = 0);            // caches hold FP8 e4m3 (bfly_kv.h)
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,

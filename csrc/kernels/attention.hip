@@ -12,6 +12,8 @@
 //   CONSECUTIVE keys: with V^T pages ([D][BS], written transposed by rope_kv) the PV A
 //   operand is then one 16-B load.
 //   Split-K over the context (flash-decoding) with an f32 partial combine kernel.
+//   The cache may hold FP8 e4m3 instead of bf16 (bfly_kv.h): half the bytes per page, widened
+//   to bf16 in registers before the same MFMAs.
 //
 // Prefill (attn_prefill_kernel): causal varlen flash attention. Workgroup = 256 query rows
 // of one head (8 waves x 32 rows, 2 waves per SIMD), KV tiles of 64 keys staged by LDS-DMA
@@ -21,6 +23,7 @@
 // P^T B operand (§3 "An accumulator tile as the next MFMA's operand").
 #include "bfly_common.h"
 #include "bfly_kernels.h"
+#include "bfly_kv.h"
 
 namespace bfly {
 
@@ -82,10 +85,10 @@ __device__ __forceinline__ void decode_split_done(const float* __restrict__ part
   }
 }
 
-template <int D, int BS>
+template <int D, int BS, typename CT>
 __global__ void __launch_bounds__(kAttnThreads)
-attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k_cache,
-                   const bf16* __restrict__ v_cache, const int* __restrict__ block_tables,
+attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restrict__ k_cache,
+                   const CT* __restrict__ v_cache, const int* __restrict__ block_tables,
                    int bt_stride, const int* __restrict__ ctx_lens, int Hq, int Hkv,
                    float scale_log2, int part_tokens, bf16* __restrict__ out,
                    float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -116,14 +119,19 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
   const int g = lane >> 4, r = lane & 15;
   // d permutation: sub-step ds, lane group g, element j hold d = 32 ds + 8 g + j, so each K
   // load instruction reads 64 contiguous bytes of every key row (full cache-line pairs).
+  // FP8 rows are 128 B: there a lane loads 16 B covering TWO sub-steps,
+  // d = 64 (ds >> 1) + 16 g + 8 (ds & 1) + j, again 64 contiguous bytes per row and load.
+  // (Any d order works as long as Q uses the same one: QK^T sums over d.)
+  constexpr bool kF8 = sizeof(CT) == 1;
+  auto d_off = [&](int ds) { return kF8 ? 64 * (ds >> 1) + 16 * g + 8 * (ds & 1) : 32 * ds + 8 * g; };
   // Q^T fragment (B operand): lane holds Q[row r][d]; rows >= G are zero.
   bf16x8 qf[4];
   {
     const int qr = r < G ? r : 0;
-    const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D + 8 * g;
+    const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D;
 #pragma unroll
     for (int ds = 0; ds < 4; ++ds) {
-      qf[ds] = *reinterpret_cast<const bf16x8*>(qp + 32 * ds);
+      qf[ds] = *reinterpret_cast<const bf16x8*>(qp + d_off(ds));
       if (r >= G) qf[ds] = bf16x8{};
     }
   }
@@ -137,29 +145,39 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
   const int* bt = block_tables + (long)b * bt_stride;
 
   // K rows: tile kt, lane row r -> key sigma(kt, r) = 8*(r>>2) + 4*kt + (r&3)
-  auto load_page = [&](int p, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
+  // K/V are loaded raw (bf16, or FP8 at half the bytes) and widened to bf16 right before
+  // their MFMA, so the prefetched page costs half the VGPRs with an FP8 cache
+  typedef typename KV<CT>::raw_t raw_t;
+  auto load_page = [&](int p, raw_t (&kf)[2][4], raw_t (&vf)[8]) {
     const long blk = bt[p];
-    const bf16* kb = k_cache + ((blk * Hkv + h) * BS) * D + 8 * g;
-    const bf16* vb = v_cache + (blk * Hkv + h) * (long)D * BS;
+    const CT* kb = k_cache + ((blk * Hkv + h) * BS) * D;
+    const CT* vb = v_cache + (blk * Hkv + h) * (long)D * BS;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       const int key = 8 * (r >> 2) + 4 * kt + (r & 3);
 #pragma unroll
       for (int ds = 0; ds < 4; ++ds)
-        kf[kt][ds] = ld_nt(reinterpret_cast<const bf16x8*>(kb + key * D + 32 * ds));
+        if constexpr (kF8) {
+          if (ds & 1) continue;
+          const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(kb + key * D + d_off(ds)));
+          kf[kt][ds] = raw_t{w[0], w[1]};
+          kf[kt][ds + 1] = raw_t{w[2], w[3]};
+        } else {
+          kf[kt][ds] = KV<CT>::ld(kb + key * D + d_off(ds));
+        }
     }
     // V^T rows: d = 16dt + r, keys 8g .. 8g+7
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
-      vf[dt] = ld_nt(reinterpret_cast<const bf16x8*>(vb + (16 * dt + r) * BS + 8 * g));
+      vf[dt] = KV<CT>::ld(vb + (16 * dt + r) * BS + 8 * g);
   };
-  auto compute_page = [&](int p, const bf16x8 (&kf)[2][4], const bf16x8 (&vf)[8]) {
+  auto compute_page = [&](int p, const raw_t (&kf)[2][4], const raw_t (&vf)[8]) {
     f32x4 st[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       st[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) st[kt] = mfma16(kf[kt][ds], qf[ds], st[kt]);
+      for (int ds = 0; ds < 4; ++ds) st[kt] = mfma16(KV<CT>::widen(kf[kt][ds]), qf[ds], st[kt]);
     }
     // st[kt][i] = S[key = p*BS + 8g + 4kt + i][query r]
     float x[8];
@@ -191,23 +209,44 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __rest
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       o[dt] *= alpha;
-      o[dt] = mfma16(vf[dt], pb, o[dt]);
+      o[dt] = mfma16(KV<CT>::widen(vf[dt]), pb, o[dt]);
     }
   };
 
   // software pipeline over this wave's pages (p0 + wid, +4, ...): the next page's K/V loads
   // are in flight while the current page is computed; two named register sets (rule 20).
-  bf16x8 kA[2][4], vA[8], kB[2][4], vB[8];
+  raw_t kA[2][4], vA[8], kB[2][4], vB[8];
   int p = p0 + wid;
   if (p < p1) load_page(p, kA, vA);
-  while (p < p1) {
+  if constexpr (sizeof(CT) == 2) {
+    while (p < p1) {
+      if (p + 4 < p1) load_page(p + 4, kB, vB);
+      compute_page(p, kA, vA);
+      p += 4;
+      if (p >= p1) break;
+      if (p + 4 < p1) load_page(p + 4, kA, vA);
+      compute_page(p, kB, vB);
+      p += 4;
+    }
+  } else {
+    // FP8 pages are half the bytes: keep TWO pages in flight (three register sets in
+    // rotation, the VGPRs of 1.5 bf16 sets) so the bytes in flight per wave, which bound a
+    // latency-limited stream, match the bf16 kernel's
+    raw_t kC[2][4], vC[8];
     if (p + 4 < p1) load_page(p + 4, kB, vB);
-    compute_page(p, kA, vA);
-    p += 4;
-    if (p >= p1) break;
-    if (p + 4 < p1) load_page(p + 4, kA, vA);
-    compute_page(p, kB, vB);
-    p += 4;
+    while (p < p1) {
+      if (p + 8 < p1) load_page(p + 8, kC, vC);
+      compute_page(p, kA, vA);
+      p += 4;
+      if (p >= p1) break;
+      if (p + 8 < p1) load_page(p + 8, kA, vA);
+      compute_page(p, kB, vB);
+      p += 4;
+      if (p >= p1) break;
+      if (p + 8 < p1) load_page(p + 8, kB, vB);
+      compute_page(p, kC, vC);
+      p += 4;
+    }
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -505,11 +544,11 @@ int attn_decode_part_tokens(int B, int Hkv, int max_ctx) {
   return part;
 }
 
-int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const bf16* v_cache,
+int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
                        bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                       int* counters) {
+                       int* counters, int kv_fp8) {
   if (B <= 0) return 0;
   if (D != 128 || block_size != 32 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
   if (part_tokens <= 0) part_tokens = attn_decode_part_tokens(B, Hkv, max_ctx);
@@ -519,9 +558,15 @@ int launch_attn_decode(const bf16* q, long q_stride, const bf16* k_cache, const 
   if (nsplit > 1 && (part_o == nullptr || part_ml == nullptr)) return -3;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(nsplit, Hkv, B);
-  attn_decode_kernel<128, 32><<<grid, kAttnThreads, 0, stream>>>(
-      q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, Hq, Hkv, scale_log2,
-      part_tokens, out, part_o, part_ml, nsplit > 1 ? counters : nullptr);
+  int* cnt = nsplit > 1 ? counters : nullptr;
+  if (kv_fp8)
+    attn_decode_kernel<128, 32, fp8_t><<<grid, kAttnThreads, 0, stream>>>(
+        q, q_stride, static_cast<const fp8_t*>(k_cache), static_cast<const fp8_t*>(v_cache), block_tables,
+        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, cnt);
+  else
+    attn_decode_kernel<128, 32, bf16><<<grid, kAttnThreads, 0, stream>>>(
+        q, q_stride, static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), block_tables,
+        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, cnt);
   if (nsplit > 1 && counters == nullptr) {
     dim3 g2(Hq / Hkv, Hkv, B);
     attn_decode_combine_kernel<128><<<g2, 128, 0, stream>>>(part_o, part_ml, nsplit, Hq, Hkv, out);

@@ -25,6 +25,7 @@ namespace bfly {
 
 constexpr int kMaxExperts = 64;
 
+template <int EC>   // EC > 0: compile-time expert count (E == EC); 0: runtime E
 __global__ void __launch_bounds__(256)
 moe_route_kernel(const bf16* __restrict__ x, long x_stride, const bf16* __restrict__ wr, int T,
                  int H, int E, int K, float* __restrict__ gates, int* __restrict__ topk_ids,
@@ -36,17 +37,40 @@ moe_route_kernel(const bf16* __restrict__ x, long x_stride, const bf16* __restri
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int t = blockIdx.x;
   const bf16* xr = x + (long)t * x_stride;
-#pragma unroll 2
-  for (int e = 0; e < E; ++e) {
-    float acc = 0.f;
+  if constexpr (EC > 0) {
+    // compile-time expert count: every router-row load of a chunk is independent and in
+    // flight together; E accumulators in registers
+    float acc[EC];
+#pragma unroll
+    for (int e = 0; e < EC; ++e) acc[e] = 0.f;
     for (int c = tid * 8; c < H; c += 256 * 8) {
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(xr + c);
-      const bf16x8 w = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
+      bf16x8 w[EC];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc += bf2f(a[j]) * bf2f(w[j]);
+      for (int e = 0; e < EC; ++e) w[e] = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
+#pragma unroll
+      for (int e = 0; e < EC; ++e)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[e] += bf2f(a[j]) * bf2f(w[e][j]);
     }
-    acc = wave_sum(acc);
-    if (lane == 0) red[wv][e] = acc;
+#pragma unroll
+    for (int e = 0; e < EC; ++e) {
+      const float s = wave_sum(acc[e]);
+      if (lane == 0) red[wv][e] = s;
+    }
+  } else {
+#pragma unroll 2
+    for (int e = 0; e < E; ++e) {
+      float acc = 0.f;
+      for (int c = tid * 8; c < H; c += 256 * 8) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(xr + c);
+        const bf16x8 w = *reinterpret_cast<const bf16x8*>(wr + (long)e * H + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += bf2f(a[j]) * bf2f(w[j]);
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) red[wv][e] = acc;
+    }
   }
   __syncthreads();
   if (wv != 0) return;
@@ -172,7 +196,10 @@ int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H,
                      float* gates, int* topk_ids, float* topk_w, hipStream_t stream) {
   if (T <= 0) return 0;
   if (E > kMaxExperts || K > 8 || K > E || H % 8 != 0) return -1;
-  moe_route_kernel<<<T, 256, 0, stream>>>(x, x_stride, wr, T, H, E, K, gates, topk_ids, topk_w);
+  if (E == 8)
+    moe_route_kernel<8><<<T, 256, 0, stream>>>(x, x_stride, wr, T, H, E, K, gates, topk_ids, topk_w);
+  else
+    moe_route_kernel<0><<<T, 256, 0, stream>>>(x, x_stride, wr, T, H, E, K, gates, topk_ids, topk_w);
   return 0;
 }
 

@@ -7,9 +7,12 @@
 // slots     [T] int32: cache slot = block * BS + offset, < 0 = do not cache
 // k_cache   [num_blocks, Hkv, BS, D]      (K rows contiguous: decode QK^T operand)
 // v_cache   [num_blocks, Hkv, D, BS]      (V stored transposed: decode PV operand reads
-//                                          8 consecutive keys of one d as one 16-B load)
+//                                          8 consecutive keys of one d as one load)
+// Cache elements are bf16 or FP8 e4m3 (bfly_kv.h); the rotated bf16 values are what is
+// cached, so an FP8 cache holds exactly torch's bf16 -> float8_e4m3fn conversion of them.
 #include "bfly_common.h"
 #include "bfly_kernels.h"
+#include "bfly_kv.h"
 
 namespace bfly {
 
@@ -34,12 +37,12 @@ __device__ __forceinline__ bf16x8 rope_load(const bf16* __restrict__ row, const 
   return a;
 }
 
-template <int D>
+template <int D, typename CT>
 __global__ void __launch_bounds__(kRopeThreads)
 rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
                const float* __restrict__ cos_t, const float* __restrict__ sin_t,
-               const int* __restrict__ slots, bf16* __restrict__ k_cache,
-               bf16* __restrict__ v_cache, int Hq, int Hkv, int BS,
+               const int* __restrict__ slots, CT* __restrict__ k_cache,
+               CT* __restrict__ v_cache, int Hq, int Hkv, int BS,
                const float* __restrict__ part, int sk, long slab) {
   constexpr int H2 = D / 2;        // rotation pairs per head
   constexpr int LPH = H2 / 8;      // lanes per head (each lane: 8 pairs)
@@ -79,31 +82,31 @@ rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
     *reinterpret_cast<bf16x8*>(hp + p0 + H2) = ob;
     if (h >= Hq && slot >= 0 && k_cache) {
       const int kh = h - Hq;
-      bf16* kp = k_cache + (((long)blk * Hkv + kh) * BS + off) * D;
-      *reinterpret_cast<bf16x8*>(kp + p0) = oa;
-      *reinterpret_cast<bf16x8*>(kp + p0 + H2) = ob;
+      CT* kp = k_cache + (((long)blk * Hkv + kh) * BS + off) * D;
+      KV<CT>::store8(kp + p0, oa);
+      KV<CT>::store8(kp + p0 + H2, ob);
     }
     return;
   }
-  // V heads: (materialise and) copy into the transposed cache page (8 scattered 2-B stores)
+  // V heads: (materialise and) copy into the transposed cache page (8 scattered stores)
   const int iv = i - nrot;
   const int kh = iv / LPV, d0 = (iv % LPV) * 8;
   const int col = (Hq + Hkv + kh) * D + d0;
   const bf16x8 v = rope_load<D>(row, prow, sk, slab, col);
   if (prow) *reinterpret_cast<bf16x8*>(row + col) = v;
   if (slot < 0 || !v_cache) return;
-  bf16* vp = v_cache + ((long)blk * Hkv + kh) * D * BS + off;
+  CT* vp = v_cache + ((long)blk * Hkv + kh) * D * BS + off;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) vp[(long)(d0 + j) * BS] = v[j];
+  for (int j = 0; j < 8; ++j) KV<CT>::store1(vp + (long)(d0 + j) * BS, v[j]);
 }
 
 // Standalone paged-cache append for already-rotated K and V ([T, Hkv, D] each, any row
 // stride): used by the prefill path when K/V come from somewhere other than a fused QKV row.
-template <int D>
+template <int D, typename CT>
 __global__ void __launch_bounds__(kRopeThreads)
 kv_append_kernel(const bf16* __restrict__ k, long k_stride, const bf16* __restrict__ v,
-                 long v_stride, const int* __restrict__ slots, bf16* __restrict__ k_cache,
-                 bf16* __restrict__ v_cache, int Hkv, int BS) {
+                 long v_stride, const int* __restrict__ slots, CT* __restrict__ k_cache,
+                 CT* __restrict__ v_cache, int Hkv, int BS) {
   const int t = blockIdx.x;
   const int slot = slots[t];
   if (slot < 0) return;
@@ -113,40 +116,67 @@ kv_append_kernel(const bf16* __restrict__ k, long k_stride, const bf16* __restri
     const int h = i / LPV, d0 = (i % LPV) * 8;
     const bf16x8 kv = *reinterpret_cast<const bf16x8*>(k + (long)t * k_stride + (long)h * D + d0);
     const bf16x8 vv = *reinterpret_cast<const bf16x8*>(v + (long)t * v_stride + (long)h * D + d0);
-    *reinterpret_cast<bf16x8*>(k_cache + (((long)blk * Hkv + h) * BS + off) * D + d0) = kv;
-    bf16* vp = v_cache + ((long)blk * Hkv + h) * D * BS + off;
+    KV<CT>::store8(k_cache + (((long)blk * Hkv + h) * BS + off) * D + d0, kv);
+    CT* vp = v_cache + ((long)blk * Hkv + h) * D * BS + off;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vp[(long)(d0 + j) * BS] = vv[j];
+    for (int j = 0; j < 8; ++j) KV<CT>::store1(vp + (long)(d0 + j) * BS, vv[j]);
+  }
+}
+
+template <typename CT>
+static void run_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* positions,
+                        const float* cos_t, const float* sin_t, const int* slots, void* k_cache,
+                        void* v_cache, int block_size, hipStream_t stream, const float* part, int sk) {
+  const long slab = (long)T * (Hq + 2 * Hkv) * D;
+  const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+  const dim3 grid(T, (items + kRopeThreads - 1) / kRopeThreads);
+  CT* kc = static_cast<CT*>(k_cache);
+  CT* vc = static_cast<CT*>(v_cache);
+  if (D == 128) {
+    rope_kv_kernel<128, CT><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, kc, vc,
+                                                              Hq, Hkv, block_size, part, sk, slab);
+  } else if (D == 64) {
+    rope_kv_kernel<64, CT><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, kc, vc,
+                                                             Hq, Hkv, block_size, part, sk, slab);
   }
 }
 
 void launch_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* positions,
-                    const float* cos_t, const float* sin_t, const int* slots, bf16* k_cache,
-                    bf16* v_cache, int block_size, hipStream_t stream, const float* part, int sk) {
+                    const float* cos_t, const float* sin_t, const int* slots, void* k_cache,
+                    void* v_cache, int block_size, hipStream_t stream, const float* part, int sk,
+                    int kv_fp8) {
   if (T <= 0) return;
-  const long slab = (long)T * (Hq + 2 * Hkv) * D;
-  const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
-  const dim3 grid(T, (items + kRopeThreads - 1) / kRopeThreads);
+  if (kv_fp8)
+    run_rope_kv<fp8_t>(qkv, T, Hq, Hkv, D, positions, cos_t, sin_t, slots, k_cache, v_cache, block_size,
+                       stream, part, sk);
+  else
+    run_rope_kv<bf16>(qkv, T, Hq, Hkv, D, positions, cos_t, sin_t, slots, k_cache, v_cache, block_size,
+                      stream, part, sk);
+}
+
+template <typename CT>
+static void run_kv_append(const bf16* k, long k_stride, const bf16* v, long v_stride, const int* slots,
+                          void* k_cache, void* v_cache, int T, int Hkv, int D, int block_size,
+                          hipStream_t stream) {
+  CT* kc = static_cast<CT*>(k_cache);
+  CT* vc = static_cast<CT*>(v_cache);
   if (D == 128) {
-    rope_kv_kernel<128><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, k_cache,
-                                                          v_cache, Hq, Hkv, block_size, part, sk, slab);
+    kv_append_kernel<128, CT><<<T, kRopeThreads, 0, stream>>>(k, k_stride, v, v_stride, slots, kc, vc, Hkv,
+                                                             block_size);
   } else if (D == 64) {
-    rope_kv_kernel<64><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, k_cache,
-                                                         v_cache, Hq, Hkv, block_size, part, sk, slab);
+    kv_append_kernel<64, CT><<<T, kRopeThreads, 0, stream>>>(k, k_stride, v, v_stride, slots, kc, vc, Hkv,
+                                                            block_size);
   }
 }
 
 void launch_kv_append(const bf16* k, long k_stride, const bf16* v, long v_stride,
-                      const int* slots, bf16* k_cache, bf16* v_cache, int T, int Hkv, int D,
-                      int block_size, hipStream_t stream) {
+                      const int* slots, void* k_cache, void* v_cache, int T, int Hkv, int D,
+                      int block_size, hipStream_t stream, int kv_fp8) {
   if (T <= 0) return;
-  if (D == 128) {
-    kv_append_kernel<128><<<T, kRopeThreads, 0, stream>>>(k, k_stride, v, v_stride, slots,
-                                                         k_cache, v_cache, Hkv, block_size);
-  } else if (D == 64) {
-    kv_append_kernel<64><<<T, kRopeThreads, 0, stream>>>(k, k_stride, v, v_stride, slots,
-                                                        k_cache, v_cache, Hkv, block_size);
-  }
+  if (kv_fp8)
+    run_kv_append<fp8_t>(k, k_stride, v, v_stride, slots, k_cache, v_cache, T, Hkv, D, block_size, stream);
+  else
+    run_kv_append<bf16>(k, k_stride, v, v_stride, slots, k_cache, v_cache, T, Hkv, D, block_size, stream);
 }
 
 }  // namespace bfly

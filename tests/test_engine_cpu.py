@@ -91,3 +91,20 @@ def test_prefix_caching_reuses_pages_and_matches():
     got, hits = run(True)
     assert got == ref
     assert hits0 == 0 and hits >= 3 * 64      # three later prompts reuse >= 2 blocks of 32
+
+
+def test_fp8_kv_cache_engine_cpu():
+    """kv_cache_dtype="fp8": float8_e4m3fn pages (a quarter of the fp32 CPU bytes), the engine
+    runs prefill, mixed steps and decode through them."""
+
+    cfg = ModelConfig.from_preset("llama-tiny")
+    base = dict(max_batch=4, max_seq_len=96, kv_cache_tokens=512, use_graphs=False)
+    e8 = LLMEngine(cfg, engine_cfg=EngineConfig(kv_cache_dtype="fp8", **base), device="cpu")
+    e32 = LLMEngine(cfg, engine_cfg=EngineConfig(**base), device="cpu")
+    assert e8.kv.layers[0][0].dtype == torch.float8_e4m3fn
+    assert e8.kv.bytes() * 4 == e32.kv.bytes()
+    prompts = [[3, 1, 4, 1, 5, 9, 2, 6] * 3, [7, 7, 2]]
+    out = e8.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    assert [len(o) for o in out] == [6, 6]
+    with pytest.raises(ValueError):
+        LLMEngine(cfg, engine_cfg=EngineConfig(kv_cache_dtype="int4", **base), device="cpu")

@@ -109,3 +109,45 @@ def test_mixed_chunked_step_matches_reference():
     whole = c.forward(ForwardBatch(input_ids=i32(A), positions=i32(list(range(90))), slots=i32(sa), is_prefill=True,
                                    cu_seqlens=i32([0, 90]), max_seqlen=90, logits_idx=torch.tensor([89])), kw)
     assert _rel(l2c[1:2, :V], whole[:, :V]) < 1e-4
+
+
+def test_engine_fp8_kv_cache():
+    """FP8 KV cache end to end (HIP rope/append + decode attention, hipGraphs, mixed prefill):
+    the engine runs, and the first token (from the prefill, which reads no cache) matches
+    the bf16-cache engine's. Decode logits are compared at model level below."""
+    cfg = ModelConfig.from_preset("llama-small")
+    prompts = [[i + 1, 2 * i + 3, 5] * 9 for i in range(5)]
+    outs = {}
+    for kvd in ("auto", "fp8"):
+        eng = LLMEngine(cfg, engine_cfg=EngineConfig(max_batch=8, max_seq_len=128, kv_cache_tokens=2048,
+                                                     kv_cache_dtype=kvd, graph_batch_sizes=[8]))
+        assert eng.kv.layers[0][0].dtype == (torch.float8_e4m3fn if kvd == "fp8" else torch.bfloat16)
+        outs[kvd] = eng.generate(prompts, SamplingParams(max_tokens=12, ignore_eos=True))
+    assert all(len(o) == 12 for o in outs["fp8"])
+    assert [o[0] for o in outs["fp8"]] == [o[0] for o in outs["auto"]]
+
+
+def test_fp8_kv_decode_logits_close_to_bf16():
+    cfg = ModelConfig.from_preset("llama-small")
+    g = build_model(cfg, device="cuda", dtype=torch.bfloat16)
+    g.init_random(seed=7)
+    bs = 32
+    prompts = [list(range(1, 70)), [3, 1, 4, 1, 5] * 20, [9]]
+    tables, slots, nxt = [], [], 0
+    for p in prompts:
+        nb = (len(p) + 8 + bs - 1) // bs
+        tables.append(list(range(nxt, nxt + nb)))
+        nxt += nb
+        slots.append([tables[-1][j // bs] * bs + j % bs for j in range(len(p))])
+    logits = {}
+    for dt in (torch.bfloat16, torch.float8_e4m3fn):
+        kv = g.allocate_kv_cache(nxt + 1, bs, dt)
+        fb = make_prefill_batch(prompts, slots)
+        lp = g.forward(fb.to("cuda"), kv)
+        toks = [int(t) for t in lp[:, :cfg.vocab_size].argmax(-1)]
+        pos = [len(p) for p in prompts]
+        sl = [tables[i][pos[i] // bs] * bs + pos[i] % bs for i in range(len(prompts))]
+        mb = max(len(t) for t in tables)
+        db = make_decode_batch(toks, pos, sl, tables, mb, mb * bs)
+        logits[dt] = g.forward(db.to("cuda"), kv)[:, :cfg.vocab_size]
+    assert _rel(logits[torch.float8_e4m3fn], logits[torch.bfloat16]) < 0.1

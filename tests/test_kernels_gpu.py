@@ -413,3 +413,57 @@ def test_attn_lse_merge():
     fin = torch.isfinite(l2)
     assert torch.equal(torch.isfinite(al.cpu()), fin)
     _close(al.cpu()[fin], l2[fin], 1e-4, 1e-4)
+
+
+# ---- FP8 (e4m3) KV cache ----------------------------------------------------------------
+F8 = torch.float8_e4m3fn
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(8, 1), (32, 8)])
+def test_attn_decode_fp8_cache(Hq, Hkv):
+    """Decode attention over an FP8 cache == the fp32 reference over the same FP8 values."""
+    D, BS = 128, 32
+    lens = [1, 33, 300, 900]
+    B = len(lens)
+    mb = (max(lens) + BS - 1) // BS
+    nblk = B * mb + 2
+    kc = (_bf(nblk, Hkv, BS, D, seed=60) * 3).to(F8)
+    vc = (_bf(nblk, Hkv, D, BS, seed=61) * 3).to(F8)
+    bt = torch.randperm(nblk)[: B * mb].view(B, mb).to(torch.int32).to(DEV)
+    ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    q = _bf(B, Hq, D, seed=62)
+    scale = 1.0 / math.sqrt(D)
+    want = ref.attn_decode(q, kc, vc, bt, ctx, scale)
+    o = ops.attn_decode(q, kc, vc, bt, ctx, scale, max(lens))
+    _close(o, want, 2e-2, 2e-2)
+    # and close to attention over the unquantized values (e4m3: ~3 significant bits)
+    o16 = ops.attn_decode(q, kc.to(torch.bfloat16), vc.to(torch.bfloat16), bt, ctx, scale, max(lens))
+    _close(o, o16, 2e-2, 2e-2)
+
+
+def test_rope_kv_and_kv_append_fp8_cache():
+    """The kernels store torch's bf16 -> float8_e4m3fn conversion (RNE, clamped to +-448) of
+    the rotated K and of V, at the paged (K row / transposed V) positions."""
+    D, BS, Hq, Hkv, T = 128, 32, 8, 2, 37
+    qkv = _bf(T, (Hq + 2 * Hkv) * D, seed=63) * 40          # some values past the e4m3 range
+    pos = torch.randint(0, 500, (T,), dtype=torch.int32).to(DEV)
+    inv = 1.0 / (500000 ** (torch.arange(0, D, 2).float() / D))
+    ang = torch.arange(1024).float()[:, None] * inv[None]
+    cos, sin = ang.cos().to(DEV), ang.sin().to(DEV)
+    nblk = 4
+    slots = torch.randperm(nblk * BS)[:T].to(torch.int32).to(DEV)
+    kc = torch.zeros(nblk, Hkv, BS, D, dtype=F8, device=DEV)
+    vc = torch.zeros(nblk, Hkv, D, BS, dtype=F8, device=DEV)
+    out = ops.rope_kv(qkv.clone(), pos, cos, sin, Hq, Hkv, slots, kc, vc)
+    k = out[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D).float().clamp(-448, 448).to(F8)
+    v = out[:, (Hq + Hkv) * D:].view(T, Hkv, D).float().clamp(-448, 448).to(F8)
+    sl = slots.long()
+    blk, off = sl // BS, sl % BS
+    assert torch.equal(kc[blk, :, off, :].view(torch.uint8), k.view(torch.uint8))
+    assert torch.equal(vc[blk, :, :, off].view(torch.uint8), v.view(torch.uint8))
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    kk = out[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D)
+    vv = out[:, (Hq + Hkv) * D:].view(T, Hkv, D)
+    ops.kv_append(kk, vv, slots, kc2, vc2)
+    assert torch.equal(kc2.view(torch.uint8), kc.view(torch.uint8))
+    assert torch.equal(vc2.view(torch.uint8), vc.view(torch.uint8))

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--prefill", default="16:1024:64:8,4:4096:64:8,1:16384:64:8",
                     help="prefill cases seqs:len:Hq:Hkv ('' to skip)")
     ap.add_argument("--parts", default="0", help="decode split sizes to try (0 = auto)")
+    ap.add_argument("--kv-dtype", default="bf16,fp8", help="decode cache element types to time")
     a = ap.parse_args()
     ops.load_library()
     for case in filter(None, a.prefill.split(",")):
@@ -41,12 +42,13 @@ def main():
         us = st.elapsed_time(en) / it * 1e3
         flops = 4.0 * n * Ls * Ls / 2 * Hq * D          # causal useful FLOPs
         print(json.dumps({"prefill": case, "us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}), flush=True)
-    for case in a.cases.split(","):
+    for case, kvd in [(c, k) for c in a.cases.split(",") for k in a.kv_dtype.split(",")]:
         B, ctx, Hq, Hkv = map(int, case.split(":"))
+        cdt = torch.float8_e4m3fn if kvd == "fp8" else torch.bfloat16
         D, BS = 128, 32
         nb = (ctx + BS - 1) // BS
-        kc = torch.randn(B * nb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
-        vc = torch.randn(B * nb, Hkv, D, BS, device="cuda", dtype=torch.bfloat16)
+        kc = torch.randn(B * nb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16).to(cdt)
+        vc = torch.randn(B * nb, Hkv, D, BS, device="cuda", dtype=torch.bfloat16).to(cdt)
         bt = torch.randperm(B * nb, device="cuda").to(torch.int32).view(B, nb)
         cl = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
         q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
@@ -64,9 +66,9 @@ def main():
             en.record()
             torch.cuda.synchronize()
             us = st.elapsed_time(en) / it * 1e3
-            byts = 2 * B * ctx * Hkv * D * 2
+            byts = 2 * B * ctx * Hkv * D * kc.element_size()
             used = pt if pt > 0 else torch.ops.bfly.attn_decode_part_tokens(B, Hkv, ctx)
-            print(json.dumps({"B": B, "ctx": ctx, "Hq": Hq, "Hkv": Hkv, "us": round(us, 2),
+            print(json.dumps({"B": B, "ctx": ctx, "Hq": Hq, "Hkv": Hkv, "kv": kvd, "us": round(us, 2),
                               "TBps": round(byts / us / 1e6, 3), "part_tokens": used}), flush=True)
 
 if __name__ == "__main__":
