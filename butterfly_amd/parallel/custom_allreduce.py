@@ -47,9 +47,22 @@ class CustomAllReduce:
             handle = bytes(L.car_ipc_handle(self._ptr).tolist())
         except Exception as e:  # noqa: BLE001
             log.warning("custom all-reduce: buffer export failed (%r)", e)
+        # the kernel loads peer rows directly: every peer GPU must be reachable over P2P
+        # (xGMI). Ranks sharing one device (the 1-GPU test setup) need no peer mapping.
+        me = self.device.index if self.device.index is not None else torch.cuda.current_device()
         handles: list = [None] * self.world
-        dist.all_gather_object(handles, handle, group=pg)
+        dist.all_gather_object(handles, (handle, me), group=pg)
+        devs = [d for _, d in handles]
+        handles = [h for h, _ in handles]
         local_ok = all(h is not None for h in handles)
+        try:
+            unreachable = [d for d in devs if d != me and not torch.cuda.can_device_access_peer(me, d)]
+        except Exception as e:  # noqa: BLE001
+            unreachable = [repr(e)]
+        if unreachable:
+            log.warning("custom all-reduce: no P2P access from device %d to %s; using RCCL",
+                        me, unreachable)
+            local_ok = False
         if local_ok:
             try:
                 for r, h in enumerate(handles):
