@@ -387,7 +387,8 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   // ring steps: non-causal, a different length and offset)
   const int sk0 = cu_k[seq];
   const int Lk = cu_k[seq + 1] - sk0;
-  const int q0 = blockIdx.x * kPfBQ;
+  // heaviest (last, under the causal mask) query blocks first: the grid's tail is light work
+  const int q0 = (causal ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * kPfBQ;
   if (q0 >= L) return;
   const int kh = h / (Hq / Hkv);
   const int hi = lane >> 5, c = lane & 31;
@@ -441,25 +442,30 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
           sc[kt] = mfma32(kf, qf[ks], sc[kt]);
         }
       }
-      const bool full = !causal || kv0 + kPfBKV - 1 <= q0 + 32 * wid;   // no masking needed
+      // Masking only on the diagonal / ragged-end tiles (wave-uniform branch); the softmax
+      // works on raw scores: max first, then one FMA (score * scale - max) per element and a
+      // bare v_exp_f32 (no denormal range fix-up: p underflowing to 0 is what softmax wants).
+      // This trims the VALU work per tile, which bounds this kernel next to the MFMAs.
+      const bool need_mask = (causal && kv0 + kPfBKV - 1 > q0 + 32 * wid) || kv0 + kPfBKV > Lk;
+      if (need_mask) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            const bool ok = key < Lk && (!causal || key <= qrow);
+            sc[kt][r] = ok ? sc[kt][r] : kNegInf;
+          }
+      }
       float tmax = kNegInf;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float xv = sc[kt][r] * scale_log2;
-          if (!full || kv0 + kPfBKV > Lk) {
-            const int key = kv0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            const bool ok = key < Lk && (!causal || key <= qrow);
-            xv = ok ? xv : kNegInf;
-          }
-          sc[kt][r] = xv;
-          tmax = fmaxf(tmax, xv);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        for (int r = 0; r < 16; r += 2) tmax = fmaxf(tmax, fmaxf(sc[kt][r], sc[kt][r + 1]));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;   // scale > 0
       const float mn = fmaxf(m, tmax);
       const float mb = mn == kNegInf ? 0.f : mn;
-      const float alpha = exp2f(m - mb);
+      const float alpha = __builtin_amdgcn_exp2f(m - mb);
       m = mn;
       bf16x8 pb[2][2];
       float ps = 0.f;
@@ -469,7 +475,7 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
         for (int s = 0; s < 2; ++s)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float pv = exp2f(sc[kt][8 * s + j] - mb);
+            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kt][8 * s + j], scale_log2, -mb));
             ps += pv;
             pb[kt][s][j] = f2bf(pv);
           }
