@@ -334,6 +334,12 @@ constexpr int kPfThreads = kPfWaves * 64;
 __device__ __forceinline__ int pf_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 __device__ __forceinline__ int pf_off(int row, int ch) { return row * 256 + 16 * (ch ^ pf_swz(row)); }
 
+__device__ __forceinline__ float pf_max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 typedef __attribute__((address_space(3))) void* pf_lds_t;
 typedef __attribute__((address_space(1))) void* pf_gbl_t;
 
@@ -457,11 +463,18 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
             sc[kt][r] = ok ? sc[kt][r] : kNegInf;
           }
       }
-      float tmax = kNegInf;
+      // row max: 4 independent v_max3 chains (fmaxf on MFMA results would add canonicalising
+      // v_max_f32 per element under this build's float flags)
+      float tc[4];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) tmax = fmaxf(tmax, fmaxf(sc[kt][r], sc[kt][r + 1]));
+      for (int c = 0; c < 4; ++c) {
+        const int kt = c >> 1, r0 = 8 * (c & 1);
+        tc[c] = pf_max3(sc[kt][r0], sc[kt][r0 + 1], sc[kt][r0 + 2]);
+        tc[c] = pf_max3(tc[c], sc[kt][r0 + 3], sc[kt][r0 + 4]);
+        tc[c] = pf_max3(tc[c], sc[kt][r0 + 5], sc[kt][r0 + 6]);
+        tc[c] = pf_max3(tc[c], sc[kt][r0 + 7], tc[c]);
+      }
+      float tmax = pf_max3(pf_max3(tc[0], tc[1], tc[2]), tc[3], tc[3]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;   // scale > 0
       const float mn = fmaxf(m, tmax);
       const float mb = mn == kNegInf ? 0.f : mn;
