@@ -17,7 +17,7 @@
 //
 // Prefill (attn_prefill_kernel): causal varlen flash attention. Workgroup = 256 query rows
 // of one head (8 waves x 32 rows, 2 waves per SIMD), KV tiles of 64 keys staged by LDS-DMA
-// into a 3-deep ring of XOR-swizzled LDS images (cdna_hip_programming.md T10 image (b)): K is
+// into a 4-deep ring of XOR-swizzled LDS images (cdna_hip_programming.md T10 image (b)): K is
 // read by ds_read_b128 as the 32x32x16 A operand of S^T = K . Q^T, V by ds_read_b64_tr_b16 as
 // the A operand of O^T = V^T . P^T; the S^T accumulator is converted in registers into the
 // P^T B operand (§3 "An accumulator tile as the next MFMA's operand").
@@ -326,7 +326,12 @@ attn_decode_combine_kernel(const float* __restrict__ part_o, const float* __rest
 // ---------------------------------------------------------------------------------------
 // Prefill
 // ---------------------------------------------------------------------------------------
-constexpr int kPfBQ = 256, kPfBKV = 64, kPfWaves = 8, kPfStages = 3;
+// 256 query rows (8 waves x 32) and a 4-deep 128 KiB K/V ring (3 deep: 0-2 % slower). Measured
+// alternative: 128 rows /
+// 2 stages (two workgroups per CU, uncoupled barriers) is 6-15 % slower: one tile of compute
+// does not hide the K/V fetch (profiles/r1_attn_prefill_valu_trim.log).
+constexpr int kPfBQ = 256, kPfBKV = 64, kPfWaves = kPfBQ / 32, kPfStages = 4;
+constexpr int kPfIters = 16 / kPfWaves;   // 16 pieces of 4 key rows per K (and V) tile
 constexpr int kPfThreads = kPfWaves * 64;
 
 // Byte offset of 16-B chunk `ch` (0..15) of row `row` in a [rows][128 x bf16] LDS image
@@ -354,7 +359,7 @@ __device__ __forceinline__ void pf_stage(const bf16* __restrict__ k, long k_stri
                                          const bf16* __restrict__ v, long v_stride, int s0, int L,
                                          int kh, int t, char* kb, int wid, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kPfIters; ++i) {
     const int piece = i * kPfWaves + wid;          // 16 pieces of 4 rows
     const int row = piece * 4 + (lane >> 4);
     const int ch = (lane & 15) ^ pf_swz(row);
@@ -368,9 +373,9 @@ __device__ __forceinline__ void pf_stage(const bf16* __restrict__ k, long k_stri
   }
 }
 
-// Causal varlen flash attention. Workgroup = 256 query rows of one head (8 waves x 32 rows,
+// Causal varlen flash attention. Workgroup = kPfBQ query rows of one head (32 rows per wave;
 // two waves per SIMD so one wave's softmax overlaps the other's MFMAs); 64-key K/V tiles in a
-// 3-deep LDS-DMA ring (counted vmcnt, one raw barrier per tile). Per wave: S^T = K Q^T on
+// kPfStages-deep LDS-DMA ring (counted vmcnt, one raw barrier per tile). Per wave: S^T = K Q^T on
 // 32x32x16 MFMAs (the lane owns one query column: row max/sum are lane-local plus one swap),
 // P^T built in registers from the accumulator, O^T += V^T P^T with V fed by transposed LDS
 // reads (ds_read_b64_tr_b16).
@@ -384,7 +389,7 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   static_assert(D == 128, "prefill kernel is specialised for D=128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = 2 * kPfBKV * D * 2;  // K | V, 32 KiB
-  constexpr int LPW = 4;                            // glds per wave per stage
+  constexpr int LPW = 2 * kPfIters;                 // glds per wave per stage
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int seq = blockIdx.y, h = blockIdx.z;
   const int s0 = cu_seqlens[seq];
@@ -423,7 +428,9 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
     if (st < ntiles) pf_stage(k, k_stride, v, v_stride, sk0, Lk, kh, st, smem + st * STAGE_BYTES, wid, lane);
   int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) pf_vm_wait<LPW>();   // tile t landed; tile t+1 may still fly
+    // tile t landed; the (up to kPfStages - 2) tiles issued after it may still fly
+    if (kPfStages > 3 && t + 2 < ntiles) pf_vm_wait<LPW * (kPfStages > 3 ? 2 : 0)>();
+    else if (kPfStages > 2 && t + 1 < ntiles) pf_vm_wait<LPW * (kPfStages > 2 ? 1 : 0)>();
     else pf_vm_wait<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -475,7 +482,10 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
         tc[c] = pf_max3(tc[c], sc[kt][r0 + 7], tc[c]);
       }
       float tmax = pf_max3(pf_max3(tc[0], tc[1], tc[2]), tc[3], tc[3]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;   // scale > 0
+      {  // the other half-wave's keys: v_permlane32_swap instead of an LDS bpermute round trip
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = pf_max3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), __uint_as_float(sw[1])) * scale_log2;  // scale > 0
+      }
       const float mn = fmaxf(m, tmax);
       const float mb = mn == kNegInf ? 0.f : mn;
       const float alpha = __builtin_amdgcn_exp2f(m - mb);
@@ -601,7 +611,7 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid((max_seqlen + kPfBQ - 1) / kPfBQ, nseq, Hq);
-  const size_t lds = (size_t)kPfStages * 2 * kPfBKV * D * 2;  // 96 KiB: 3 x (K | V)
+  const size_t lds = (size_t)kPfStages * 2 * kPfBKV * D * 2;  // stages x (K | V) 32 KiB
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_kernel<128>),
