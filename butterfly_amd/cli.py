@@ -1,6 +1,7 @@
 """Command line: `python -m butterfly_amd <command>`.
 
   partition  --model llama3-70b --gpus 8 [--strategy tp2xpp4] [--objective latency] [--out plan.json]
+             [--schedule RANK]   (that rank's decode-step communication program)
   generate   --model llama-tiny|CKPT_DIR --prompt "..." [--max-tokens N] [--plan auto|tp2]
   serve      --model ... [--host 127.0.0.1 --port 8000]         (run under `launch` for N GPUs)
   bench      ...                                                  (forwards to bench.py)
@@ -36,6 +37,17 @@ def cmd_partition(a) -> int:
     est = plan.estimate
     print(f"plan {plan.name}: stages={plan.stages} est {est['tokens_per_second']:.0f} tok/s, "
           f"step {est['step_seconds'] * 1e3:.2f} ms", file=sys.stderr)
+    if a.schedule is not None:
+        # the communication program of one decode step on the given rank (partition/schedule.py)
+        from .partition.schedule import check_programs, programs
+
+        B = a.batch_per_gpu * a.gpus // plan.mesh.dp
+        m = plan.mesh
+        # default asynchronous pipeline: one step (tick) carries one of pp request groups
+        progs = programs(plan, B // m.pp if m.pp > 1 and m.ep == 1 else B)
+        check_programs(progs)
+        print(progs[a.schedule].describe(), file=sys.stderr)
+        return 0
     if not a.out:
         print(text)
     return 0
@@ -131,6 +143,8 @@ def main(argv=None) -> int:
     p.add_argument("--batch-per-gpu", type=int, default=64)
     p.add_argument("--ctx", type=int, default=1024)
     p.add_argument("--out", default=None)
+    p.add_argument("--schedule", type=int, default=None, metavar="RANK",
+                   help="print RANK's decode-step communication program instead of the plan JSON")
     p.set_defaults(fn=cmd_partition)
     g = sub.add_parser("generate")
     g.add_argument("--model", default="llama-tiny")

@@ -1,0 +1,195 @@
+"""Communication schedule: the per-rank program of one engine step, derived from a PartitionPlan
+(SURVEY.md §2.7-A A11 "comm scheduler / rank program", §2.7-C collective call sites).
+
+`rank_program(plan, rank, tokens)` lists, in issue order, what rank `rank` does in one decode
+step (one request group of `tokens` sequences): compute blocks (stage layer ranges) and the
+communication instructions between them, with group, peer and payload. It is the program the
+engine runs — `engine/engine.py:_run_stages` / `_pipe_stage` (recv residual stream -> stage
+-> isend, or sample + broadcast ids) and `models/transformer.py` (vocab-parallel embedding
+all-reduce, two TP all-reduces per layer, EP all-gather / reduce-scatter, vocab-parallel
+sampling all-gather) — written down ahead of time so that it can be
+
+  * checked for cross-rank consistency without running anything (`check_programs`: every
+    group collective is issued by all members in the same order with the same payload, every
+    send has its recv at the same position of the pair's stream: no deadlock, no mismatch);
+  * priced per xGMI link (`link_bytes`: bytes each directed GPU pair carries per step, ring
+    all-reduce/all-gather/reduce-scatter and point-to-point hops), which is what the
+    partitioner's cut-point objective minimises (`search.link_traffic`);
+  * compared with what the engine actually issued (tests/test_schedule.py replays a decode
+    step through the loopback backend, parallel/fake.py, and diffs its log against this).
+
+Stream assignment follows the engine: TP all-reduces run on the compute stream (one-shot IPC
+kernel when BFLY_CUSTOM_AR is active, else RCCL, both stream-ordered), PP sends are `isend` on
+RCCL's stream (they overlap the next group's compute), the token broadcast ends the step.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+from ..config import ModelConfig
+from .plan import PartitionPlan
+
+BF16 = 2
+
+
+@dataclass(frozen=True)
+class Instr:
+    op: str                      # compute | all_reduce | all_gather | reduce_scatter | send | recv | broadcast
+    group: tuple = ()            # global ranks taking part (send/recv: (src, dst))
+    nbytes: int = 0              # payload this rank contributes (all_gather: its own slice)
+    stream: str = "compute"      # compute | comm
+    note: str = ""
+
+    def key(self) -> tuple:
+        """What must agree between the members of a collective (or a send/recv pair)."""
+        return (self.op if self.op not in ("send", "recv") else "p2p", self.group, self.nbytes)
+
+
+@dataclass
+class RankProgram:
+    rank: int
+    tokens: int
+    instrs: list = field(default_factory=list)
+
+    def comm(self) -> list:
+        return [i for i in self.instrs if i.op != "compute"]
+
+    def bytes_by_op(self) -> dict:
+        out: dict = {}
+        for i in self.comm():
+            out[i.op] = out.get(i.op, 0) + i.nbytes
+        return out
+
+    def describe(self) -> str:
+        lines = [f"rank {self.rank}: decode step, {self.tokens} tokens"]
+        for i in self.instrs:
+            if i.op == "compute":
+                lines.append(f"  [compute] {i.note}")
+            else:
+                lines.append(f"  [{i.stream:7s}] {i.op:14s} {str(i.group):24s} {i.nbytes:>12,d} B  {i.note}")
+        return "\n".join(lines)
+
+
+def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int = 1) -> RankProgram:
+    """The decode-step program of `rank` for `tokens` sequences. With the asynchronous pipeline
+    (default) a step is one tick carrying one request group (`tokens` = the group's size, one
+    microbatch); the synchronous pipeline (engine._pipeline_decode) cuts the step's batch into
+    `microbatches` parts that flow through the stages back to back, then broadcasts all ids."""
+    prog = RankProgram(rank, tokens)
+    M = max(1, min(microbatches, tokens))
+    bounds = [tokens * i // M for i in range(M + 1)]
+    for m in range(M):
+        _microbatch(plan, rank, bounds[m + 1] - bounds[m], prog.instrs.append, ep_sync=(m == 0))
+    if plan.mesh.pp > 1:
+        prog.instrs.append(Instr("broadcast", tuple(plan.mesh.pp_group(rank)), tokens * 4, "comm",
+                                 "sampled ids from the last stage"))
+    return prog
+
+
+def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool) -> None:
+    cfg: ModelConfig = plan.model
+    mesh = plan.mesh
+    c = mesh.coord(rank)
+    tp_g = tuple(mesh.tp_group(rank))
+    tp, pp, ep = mesh.tp, mesh.pp, mesh.ep
+    a, b = plan.stages[c.pp]
+    first, last = c.pp == 0, c.pp == pp - 1
+    h = cfg.hidden_size
+    act = tokens * h * BF16
+    R = tokens
+    moe = cfg.is_moe
+    ep_g = tuple(next(g for g in mesh.all_groups("ep") if rank in g)) if ep > 1 else ()
+    if ep > 1 and ep_sync:
+        # all EP ranks agree on the padded row count, on prefill vs decode and on idling
+        add(Instr("max_int", ep_g, 3 * 8, "compute", "EP step agreement (rows, prefill?, work?)"))
+    if first:
+        add(Instr("compute", note="embedding gather (vocab shard)"))
+        if tp > 1:
+            add(Instr("all_reduce", tp_g, act, "compute", "vocab-parallel embedding"))
+    else:
+        add(Instr("recv", (mesh.prev_stage(rank), rank), act, "comm", "residual stream from previous stage"))
+    for layer in range(a, b):
+        add(Instr("compute", note=f"layer {layer}: norm, QKV, RoPE+KV append, attention, O"))
+        if tp > 1:
+            add(Instr("all_reduce", tp_g, act, "compute", f"layer {layer} attention output (+ add, RMSNorm)"))
+        if moe and ep > 1:
+            add(Instr("compute", note=f"layer {layer}: router"))
+            add(Instr("all_gather", ep_g, act, "compute", f"layer {layer} EP: token rows"))
+            add(Instr("all_gather", ep_g, tokens * cfg.num_experts * 4, "compute",
+                      f"layer {layer} EP: router gates (f32)"))
+            add(Instr("compute", note=f"layer {layer}: local experts on all EP ranks' rows"))
+            add(Instr("reduce_scatter", ep_g, act * ep, "compute", f"layer {layer} EP: expert outputs"))
+        else:
+            add(Instr("compute", note=f"layer {layer}: " + ("router + experts" if moe else "gate/up, SiLU, down")))
+            if tp > 1:
+                # fused with the next layer's add+RMSNorm; after a stage's last layer it is a
+                # plain all-reduce (last stage: only the sampled rows are reduced)
+                nb = R * h * BF16 if (last and layer == b - 1) else act
+                add(Instr("all_reduce", tp_g, nb, "compute", f"layer {layer} FFN output"))
+    if last:
+        add(Instr("compute", note="final norm, LM head (vocab shard), sampling"))
+        if tp > 1:
+            add(Instr("all_gather", tp_g, R * 2 * 4, "compute", "vocab-parallel argmax: (score, id) pairs"))
+    else:
+        add(Instr("send", (rank, mesh.next_stage(rank)), act, "comm", "residual stream to next stage"))
+
+
+def check_programs(progs: dict) -> None:
+    """Raise ValueError unless the programs of all ranks are mutually consistent: for every group
+    the members issue the same sequence of collectives (op, payload), and every (src, dst) pair
+    sees its sends and recvs in the same order with the same payloads."""
+    by_group: dict = {}
+    for r, p in progs.items():
+        for i in p.comm():
+            if i.op in ("send", "recv"):
+                by_group.setdefault(("p2p",) + i.group, {}).setdefault(r, []).append(i.nbytes)
+            else:
+                by_group.setdefault(i.group, {}).setdefault(r, []).append((i.op, i.nbytes))
+    for g, seqs in by_group.items():
+        if g and g[0] == "p2p":
+            src, dst = g[1], g[2]
+            if seqs.get(src) != seqs.get(dst):
+                raise ValueError(f"p2p {src}->{dst}: sends {seqs.get(src)} vs recvs {seqs.get(dst)}")
+            continue
+        members = set(g)
+        if set(seqs) != members:
+            raise ValueError(f"group {g}: only ranks {sorted(seqs)} issue collectives")
+        ref = seqs[min(seqs)]
+        for r, s in seqs.items():
+            if s != ref:
+                raise ValueError(f"group {g}: rank {r} issues {s[:4]}... vs {ref[:4]}...")
+
+
+def link_bytes(plan: PartitionPlan, progs: dict) -> dict:
+    """Bytes per directed GPU pair for one step. Ring collectives over a group of n move
+    2(n-1)/n of the payload (all-reduce) or (n-1)/n of the gathered tensor (all-gather /
+    reduce-scatter) through each member's link to its ring successor; p2p goes direct."""
+    out: dict = {}
+    place = plan.placement
+
+    def put(src, dst, nb):
+        k = f"{place[src]}-{place[dst]}"
+        out[k] = out.get(k, 0.0) + nb
+
+    for r, p in progs.items():
+        for i in p.comm():
+            n = len(i.group)
+            if i.op == "send":
+                put(i.group[0], i.group[1], i.nbytes)
+            elif i.op in ("all_reduce", "all_gather", "reduce_scatter", "broadcast") and n > 1:
+                nxt = i.group[(i.group.index(r) + 1) % n]
+                if i.op == "all_reduce":
+                    put(r, nxt, 2.0 * (n - 1) / n * i.nbytes)
+                elif i.op == "all_gather":
+                    put(r, nxt, (n - 1) * i.nbytes)
+                elif i.op == "reduce_scatter":
+                    put(r, nxt, (n - 1) / n * i.nbytes)
+                elif i.group.index(r) == n - 1:   # broadcast from the last member: a chain
+                    put(r, nxt, i.nbytes)
+    return out
+
+
+def programs(plan: PartitionPlan, tokens: int, microbatches: int = 1) -> dict:
+    """rank_program for every rank (each DP replica decodes `tokens` sequences)."""
+    return {r: rank_program(plan, r, tokens, microbatches) for r in range(plan.n_gpus)}

@@ -109,26 +109,12 @@ def evaluate(cfg: ModelConfig, dp: int, tp: int, pp: int, ep: int, *, batch_per_
 
 
 def link_traffic(plan: PartitionPlan) -> dict:
-    """xGMI bytes per generated token on each directed GPU pair (ring all-reduce + PP)."""
-    cfg = plan.model
-    mesh = plan.mesh
-    h2 = 2.0 * cfg.hidden_size
-    out: dict[str, float] = {}
-    n_layers_ar = 2
-    for r in range(plan.n_gpus):
-        g = mesh.tp_group(r)
-        if len(g) > 1:
-            i = g.index(r)
-            nb = g[(i + 1) % len(g)]
-            a, b = plan.stages[mesh.coord(r).pp]
-            per_tok = n_layers_ar * (b - a) * 2.0 * (len(g) - 1) / len(g) * h2
-            key = f"{plan.placement[r]}-{plan.placement[nb]}"
-            out[key] = out.get(key, 0.0) + per_tok
-        nxt = mesh.next_stage(r)
-        if nxt is not None:
-            key = f"{plan.placement[r]}-{plan.placement[nxt]}"
-            out[key] = out.get(key, 0.0) + h2 / max(1, plan.tp)
-    return out
+    """xGMI bytes per generated token on each directed GPU pair, from the plan's communication
+    schedule (schedule.py: ring TP all-reduces incl. the embedding one, PP hops of the full
+    residual stream between same-TP-index ranks, the sampling all-gather, the token broadcast)."""
+    from .schedule import link_bytes, programs
+
+    return link_bytes(plan, programs(plan, 1))
 
 
 def partition(cfg: Union[ModelConfig, str], n_gpus: int, strategy: Union[str, dict] = "auto",

@@ -1,0 +1,111 @@
+"""Communication schedule (partition/schedule.py): the per-rank decode-step programs derived from
+a plan are mutually consistent for every factorisation, a broken program is caught, and the
+program matches what the engine actually issues (replayed through the loopback backend)."""
+import pytest
+import torch
+
+from butterfly_amd.config import EngineConfig, ModelConfig
+from butterfly_amd.engine.engine import LLMEngine
+from butterfly_amd.engine.sampler import SamplingParams
+from butterfly_amd.parallel.fake import FakeWorld
+from butterfly_amd.partition import partition
+from butterfly_amd.partition.schedule import Instr, check_programs, link_bytes, programs
+from butterfly_amd.partition.search import factorizations
+
+
+@pytest.mark.parametrize("preset", ["llama3-70b", "llama3-8b", "mixtral-8x7b"])
+def test_programs_consistent_for_every_factorisation(preset):
+    cfg = ModelConfig.from_preset(preset)
+    for n in (2, 4, 8):
+        for dp, tp, pp in factorizations(n):
+            strat = {"dp": dp, "tp": tp, "pp": pp}
+            if cfg.is_moe and dp > 1 and tp == 1 and pp == 1:
+                strat["ep"] = dp
+            try:
+                plan = partition(cfg, n, strat)
+            except ValueError:
+                continue   # infeasible (heads / memory)
+            progs = programs(plan, 64)
+            check_programs(progs)
+            lb = link_bytes(plan, progs)
+            if plan.tp > 1 or plan.pp > 1 or plan.ep > 1:
+                assert lb and all(v > 0 for v in lb.values())
+            # every rank's program covers exactly its stage's layers
+            for r, p in progs.items():
+                a, b = plan.stages[plan.mesh.coord(r).pp]
+                layers = {i.note.split(":")[0] for i in p.instrs if i.op == "compute" and i.note.startswith("layer")}
+                assert layers == {f"layer {k}" for k in range(a, b)}
+
+
+def test_check_programs_catches_mismatch():
+    plan = partition(ModelConfig.from_preset("llama3-70b"), 8, {"tp": 2, "pp": 4})
+    progs = programs(plan, 16)
+    check_programs(progs)
+    # rank 3 drops one TP all-reduce: its partner would wait forever
+    p3 = progs[3]
+    k = next(i for i, ins in enumerate(p3.instrs) if ins.op == "all_reduce")
+    del p3.instrs[k]
+    with pytest.raises(ValueError, match="group"):
+        check_programs(progs)
+    # a send without the matching recv size
+    progs = programs(plan, 16)
+    p0 = progs[0]
+    k = next(i for i, ins in enumerate(p0.instrs) if ins.op == "send")
+    p0.instrs[k] = Instr("send", p0.instrs[k].group, 1, "comm")
+    with pytest.raises(ValueError, match="p2p"):
+        check_programs(progs)
+
+
+PROMPTS = [[3, 14, 15, 92, 65], [35, 89, 79, 32, 38, 46, 26], [43, 7], [38, 32, 79, 50, 28, 84]]
+
+
+def _decode_window(rank, comm, preset, mesh, stages):
+    """Prefill everything, then bracket exactly one decode step by two barriers."""
+    cfg = ModelConfig.from_preset(preset)
+    ecfg = EngineConfig(max_batch=8, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu", stage_layers=stages)
+    for p in PROMPTS:
+        eng.add_request(p, SamplingParams(max_tokens=40, ignore_eos=True))
+    groups = mesh.pp if eng.async_pp else 1
+    streak = 0
+    while eng.scheduler.num_waiting > 0 or streak < groups + 1:
+        out = eng.step()
+        streak = streak + 1 if out.kind == "decode" else 0
+    comm.barrier()
+    out = eng.step()
+    comm.barrier()
+    return out.kind, eng.async_pp
+
+
+@pytest.mark.parametrize("pp_async", ["1", "0"])
+@pytest.mark.parametrize("preset,kw", [("llama-tiny", dict(tp=2)), ("llama-tiny", dict(pp=2)),
+                                       ("llama-tiny", dict(tp=2, pp=2)), ("mixtral-tiny", dict(dp=2, ep=2)),
+                                       ("mixtral-tiny", dict(tp=2))])
+def test_program_matches_engine(preset, kw, pp_async, monkeypatch):
+    monkeypatch.setenv("BFLY_PP_ASYNC", pp_async)
+    torch.set_num_threads(1)
+    cfg = ModelConfig.from_preset(preset)
+    n = kw.get("dp", 1) * kw.get("tp", 1) * kw.get("pp", 1)
+    plan = partition(cfg, n, kw, batch_per_gpu=4 * n // kw.get("dp", 1))
+    mesh = plan.mesh
+    world = FakeWorld(mesh, timeout_s=60)
+    outs = world.run(lambda r, c: _decode_window(r, c, preset, mesh, plan.stages))
+    assert all(k == "decode" for k, _ in outs)
+    if outs[0][1]:   # asynchronous pipeline: a step is one tick carrying one request group
+        tokens, mb = len(PROMPTS) // mesh.pp, 1
+    else:            # synchronous: the whole batch in pp microbatches
+        tokens, mb = len(PROMPTS), mesh.pp
+    for r in range(mesh.world_size):
+        mine = [(op, grp, shape) for rk, op, grp, shape in world.log if rk == r]
+        bars = [i for i, e in enumerate(mine) if e[0] == "barrier"]
+        got = [e for e in mine[bars[-2] + 1: bars[-1]]]
+        want = [i for i in programs(plan, tokens, mb)[r].comm() if i.op != "recv"]
+        # the loopback log names broadcasts by source ("broadcast<src>") and records sends
+        assert [("broadcast" if op.startswith("broadcast") else op, grp) for op, grp, _ in got] == \
+            [(i.op, i.group) for i in want], (r, got, [(i.op, i.group) for i in want])
+        for (op, _, shape), i in zip(got, want):
+            n = 1
+            for s in shape:
+                n *= s
+            if op in ("all_reduce", "send"):
+                assert n * 2 == i.nbytes, (r, op, shape, i)
