@@ -84,6 +84,9 @@ class LLMEngine:
         self.device = torch.device(device)
         if stage_layers is None:
             stage_layers = balanced_stages(cfg.num_layers, mesh.pp)
+        if mesh.ep > 1 and mesh.pp > 1:
+            raise ValueError("expert parallelism with pipeline stages is not a supported layout "
+                             "(EP collectives span DP replicas of one stage)")
         a, b = stage_layers[coord.pp]
         shard = Shard(tp_rank=coord.tp, tp_size=mesh.tp, layer_start=a, layer_end=b,
                       ep_rank=coord.dp if mesh.ep > 1 else 0, ep_size=mesh.ep)
@@ -144,6 +147,8 @@ class LLMEngine:
         self.pp_first = coord.pp == 0
         self.pp_last = coord.pp == mesh.pp - 1
         self.faults = FaultInjector()
+        self._poison = False
+        self.nan_check = flags.get("BFLY_NAN_CHECK")
         # a step that outlives BFLY_STEP_TIMEOUT_S (hung collective, wedged GPU) dumps every
         # thread's stack and terminates the rank (0 = off; first steps include graph capture)
         st = flags.get("BFLY_STEP_TIMEOUT_S")
@@ -204,9 +209,30 @@ class LLMEngine:
             self.comm.check_health()
         return out
 
+    def _maybe_poison(self, t: torch.Tensor) -> torch.Tensor:
+        """Fault injection (BFLY_FAULT=rank:step:nan): this step's output becomes NaN."""
+        if self._poison:
+            self._poison = False
+            t = t.clone()
+            t.fill_(float("nan"))
+        return t
+
+    def _sample(self, logits: torch.Tensor, rids: list) -> torch.Tensor:
+        """Sample one token per row. With BFLY_NAN_CHECK the logits are also checked for
+        non-finite values (one reduction over the local vocab shard, no host sync); a poisoned
+        or corrupted step then raises in _apply_tokens instead of emitting garbage tokens."""
+        logits = self._maybe_poison(logits)
+        temps, seeds, params = self._sample_params(rids)
+        ids = self.sampler.sample(logits, temps, seeds, params)
+        if self.nan_check and logits.numel():
+            # no host sync here: a bad step marks its ids -1, _apply_tokens raises on them
+            ids = ids.masked_fill(~torch.isfinite(logits).all(), -1)
+        return ids
+
     def _step(self) -> StepOutput:
         t0 = time.perf_counter()
-        self.faults.maybe_inject(self.rank, self.steps_done)
+        if self.faults.maybe_inject(self.rank, self.steps_done) == "nan":
+            self._poison = True
         if self.async_pp:
             return self._pp_tick(t0)
         plan = self.scheduler.schedule()
@@ -243,8 +269,7 @@ class LLMEngine:
             logits = self.runner.run(fb)
             new = []
             if sample:
-                temps, seeds, params = self._sample_params(sample)
-                new = self.sampler.sample(logits, temps, seeds, params).tolist()
+                new = self._sample(logits, sample).tolist()
             out = self._apply_tokens("prefill" if plan.kind == 1 else "mixed", sample, new, t0)
             out.prefill_tokens = int(sum(plan.prefill_lens))
             return out
@@ -273,6 +298,8 @@ class LLMEngine:
         """Append one sampled token per sequence, retire finished ones, record metrics."""
         finished = []
         now = time.perf_counter()
+        if any(int(t) < 0 for t in new):
+            raise RuntimeError(f"rank {self.rank}: non-finite logits at engine step {self.steps_done}")
         for r, t in zip(rids, new):
             req = self.requests[r]
             req.output.append(int(t))
@@ -298,9 +325,7 @@ class LLMEngine:
         every rank of the replica)."""
         m = self.model
         if self.mesh.pp == 1:
-            logits = fn(None)
-            temps, seeds, params = self._sample_params(rids)
-            return self.sampler.sample(logits, temps, seeds, params)
+            return self._sample(fn(None), rids)
         # pipeline: recv residual stream -> compute -> send; last stage samples + broadcasts
         h = None
         if not self.pp_first:
@@ -309,10 +334,9 @@ class LLMEngine:
         out = fn(h)
         ids = torch.empty(R, dtype=torch.int32, device=self.device)
         if not self.pp_last:
-            self.comm.send(out, self.mesh.next_stage(self.rank))
+            self.comm.send(self._maybe_poison(out), self.mesh.next_stage(self.rank))
         else:
-            temps, seeds, params = self._sample_params(rids)
-            ids = self.sampler.sample(out, temps, seeds, params)
+            ids = self._sample(out, rids)
         self.comm.broadcast_(ids, src_in_group=self.mesh.pp - 1, group="pp")
         return ids
 
@@ -337,12 +361,11 @@ class LLMEngine:
             out = self.runner.run_decode(sub, h)
             if not self.pp_last:
                 # copy out of the graph's static output before the next replay can reuse it
-                snd = out.clone()
+                snd = self._maybe_poison(out.clone())
                 reqs.append(self.comm.isend(snd, self.mesh.next_stage(self.rank)))
                 outs.append(snd)
             else:
-                temps, seeds, params = self._sample_params(rids[a:b])
-                outs.append(self.sampler.sample(out, temps, seeds, params))
+                outs.append(self._sample(out, rids[a:b]))
         for r in reqs:
             r.wait()
         ids = torch.cat(outs) if self.pp_last else torch.empty(B, dtype=torch.int32, device=self.device)
@@ -409,10 +432,9 @@ class LLMEngine:
             out = self.runner.run_decode(inp, h)
         if not self.pp_last:
             snd = out.clone() if p.plan.kind == 2 else out   # graph outputs are reused by the next replay
-            self._sends.append(self.comm.isend(snd, self.mesh.next_stage(self.rank)))
+            self._sends.append(self.comm.isend(self._maybe_poison(snd), self.mesh.next_stage(self.rank)))
         else:
-            temps, seeds, params = self._sample_params(p.rids)
-            p.ids = self.sampler.sample(out, temps, seeds, params)
+            p.ids = self._sample(out, p.rids)
 
     # ------------------------------------------------------------------------------------
     def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list:

@@ -76,6 +76,8 @@ def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int 
     (default) a step is one tick carrying one request group (`tokens` = the group's size, one
     microbatch); the synchronous pipeline (engine._pipeline_decode) cuts the step's batch into
     `microbatches` parts that flow through the stages back to back, then broadcasts all ids."""
+    if plan.mesh.ep > 1 and plan.mesh.pp > 1:
+        raise ValueError("expert parallelism with pipeline stages is not a supported layout")
     prog = RankProgram(rank, tokens)
     M = max(1, min(microbatches, tokens))
     bounds = [tokens * i // M for i in range(M + 1)]

@@ -47,10 +47,14 @@ define("BFLY_PP_ASYNC", True, _bool, "pipeline parallelism: keep pp decode group
        "(one group per stage per tick, no fill/drain bubble) instead of per-step microbatching")
 define("BFLY_DIST_BACKEND", "", str, "torch.distributed backend override for init_distributed (default: nccl "
        "= RCCL with a GPU, gloo without; gloo lets several ranks share one GPU in tests)")
+define("BFLY_FORCE_CPU", False, _bool, "bench.py: run on the CPU reference path even when a GPU is visible "
+       "(BASELINE config 1, the gloo plumbing configuration)")
 define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
 define("BFLY_STEP_TIMEOUT_S", 0.0, float, "engine step watchdog: terminate a rank whose step exceeds this (0 = off)")
 define("BFLY_FAULT", "", str, "fault injection 'rank:step:kind' (kind: hang|exit|nan) for tests")
+define("BFLY_NAN_CHECK", True, _bool, "check the logits of every sampled step for NaN/Inf and fail the step "
+       "(one reduction over the local vocab shard per step)")
 define("BFLY_TRACE", "", str, "write a chrome-trace JSON of engine steps to this path")
 define("BFLY_ROCTX", False, _bool, "emit roctx ranges (visible in rocprofv3 --marker-trace)")
 define("BFLY_LOG_LEVEL", "INFO", str, "log level of the rank-tagged logger")

@@ -28,3 +28,72 @@ def test_bench_two_ranks(plan):
     assert res["config"]["global_batch"] == 8
     if plan == "pp2":
         assert res["config"]["pp_async_groups"] == 2
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` from a bare shell (no WORLD_SIZE): bench.py launches its own
+    ranks, relays exactly one JSON line and reports the world the collectives saw."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="2", BFLY_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "llama-tiny",
+                        "--plan", "tp2", "--steps", "4", "--warmup", "1", "--batch-per-gpu", "4",
+                        "--prompt-len", "16"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["world_size"] == 2 and res["rccl_ranks_seen"] == 2
+    assert res["backend"] == "gloo" and res["plan"]["tp"] == 2
+
+
+def test_bench_self_launch_failure_propagates():
+    """A failing rank makes the self-launched job exit non-zero (no JSON line)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="2", BFLY_DIST_BACKEND="gloo", BFLY_FAULT="1:0:exit", BFLY_COMM_TIMEOUT_S="60")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "llama-tiny",
+                        "--plan", "tp2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2",
+                        "--prompt-len", "8"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_baseline_config_1():
+    """BASELINE config 1 (GPT-2 small, 2-stage layer split on CPU/gloo) is one flag."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--baseline-config", "1", "--steps", "2",
+                        "--warmup", "1", "--batch-per-gpu", "2", "--prompt-len", "8"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert res["config"]["model"] == "GPT-2-small" and res["plan"]["pp"] == 2 and res["dtype"] == "fp32"
+
+
+def test_peer_exit_fails_survivor_within_timeout():
+    """Ranks started without our launcher (as torchrun would): rank 1 exits at step 1; rank 0
+    must terminate non-zero by itself (collective error or BFLY_COMM_TIMEOUT_S), not hang."""
+    import socket
+    import time
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(os.environ, OMP_NUM_THREADS="2", BFLY_DIST_BACKEND="gloo", BFLY_FAULT="1:3:exit",
+                   BFLY_COMM_TIMEOUT_S="30", RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model",
+                                       "llama-tiny", "--plan", "tp2", "--steps", "4", "--warmup", "1",
+                                       "--batch-per-gpu", "2", "--prompt-len", "8"], cwd=ROOT, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    try:
+        rc0 = procs[0].wait(timeout=120)
+        rc1 = procs[1].wait(timeout=30)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rc1 == 13 and rc0 != 0
+    assert time.time() - t0 < 120

@@ -108,3 +108,17 @@ def test_fp8_kv_cache_engine_cpu():
     assert [len(o) for o in out] == [6, 6]
     with pytest.raises(ValueError):
         LLMEngine(cfg, engine_cfg=EngineConfig(kv_cache_dtype="int4", **base), device="cpu")
+
+
+def test_nan_fault_fails_the_step(monkeypatch):
+    """BFLY_FAULT=rank:step:nan poisons that step's logits; the engine's non-finite check
+    turns it into an error instead of emitting tokens (SURVEY.md §5.3 fault injection)."""
+    monkeypatch.setenv("BFLY_FAULT", "0:2:nan")
+    cfg = ModelConfig.from_preset("llama-tiny")
+    ecfg = EngineConfig(max_batch=2, max_seq_len=64, kv_cache_tokens=256, use_graphs=False)
+    eng = LLMEngine(cfg, engine_cfg=ecfg, device="cpu")
+    eng.add_request([1, 2, 3], SamplingParams(max_tokens=8))
+    eng.step()
+    eng.step()
+    with pytest.raises(RuntimeError, match="non-finite"):
+        eng.step()

@@ -51,3 +51,15 @@ def test_invalid_plan_rejected():
 def test_mixtral_expert_parallel_candidate():
     p = partition("mixtral-8x7b", 8, {"dp": 8, "ep": 8})
     assert p.ep == 8 and p.shard(3).ep_rank == 3
+
+
+def test_no_expert_parallel_with_pipeline_stages():
+    """EP layouts are single-stage: the search never proposes ep > 1 with pp > 1, an explicit
+    request is infeasible, and the schedule refuses such a plan."""
+    import pytest as _pt
+
+    for n in (2, 4, 8):
+        p = partition("mixtral-8x7b", n)
+        assert not (p.ep > 1 and p.pp > 1)
+    with _pt.raises(ValueError):
+        partition("mixtral-8x7b", 4, {"dp": 2, "ep": 2, "pp": 2})

@@ -2,7 +2,7 @@
 """Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals for the decode phase (every
 dispatch after the last prefill-attention dispatch) and per decode step.
 
-usage: python tools/prof_summary.py gpurun_out/prof_x/run_kernel_trace.csv [--steps K] [--md out.md]
+usage: python tools/prof_summary.py gpurun_out/prof_x/run_kernel_trace.csv|run_results.db [--steps K] [--md out.md]
 """
 import argparse
 import csv
@@ -19,13 +19,25 @@ def short(name: str) -> str:
     return n[:70]
 
 
+def load_rows(path: str) -> list:
+    """Kernel dispatches from a rocprofv3 kernel-trace CSV or a rocpd SQLite database
+    (rocprofv3's default output format on ROCm 7: `<name>_results.db`)."""
+    if path.endswith(".db"):
+        import sqlite3
+
+        con = sqlite3.connect(path)
+        return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in con.execute("select name, start, end from kernels")]
+    return list(csv.DictReader(open(path)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=0, help="decode steps in the window (for per-step numbers)")
     ap.add_argument("--md", default=None)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
+    rows = load_rows(a.trace)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # the decode window starts after the prefill's last attention AND its trailing big-tile GEMMs
     last_prefill = max((i for i, r in enumerate(rows) if "attn_prefill" in r["Kernel_Name"]
