@@ -81,6 +81,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--baseline-config", type=int, default=None, choices=sorted(BASELINE_CONFIGS),
                     help="run BASELINE.json config N (sets model, plan and default GPU count)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the start-up collective probe (N > 1)")
     ap.add_argument("--kv-dtype", default="auto", help="KV-cache elements: auto (= bf16) | fp8")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap
@@ -133,7 +134,9 @@ def run(a) -> int:
     from butterfly_amd.engine.engine import LLMEngine
     from butterfly_amd.engine.sampler import SamplingParams
     from butterfly_amd.parallel.comm import Communicator, init_distributed
+    from butterfly_amd.parallel.probe import apply_policy, ar_policy, probe_comm, summarize
     from butterfly_amd.partition import partition
+    from butterfly_amd.partition.hw import MI355X
 
     use_gpu = torch.cuda.is_available() and os.environ.get("BFLY_FORCE_CPU", "0") != "1"
 
@@ -156,9 +159,23 @@ def run(a) -> int:
         dist.all_reduce(one)
         ranks_seen = int(one.item())
     cfg = ModelConfig.from_preset(a.model)
+    # measure this node's collectives before choosing the layout (parallel/probe.py): the
+    # partitioner prices all-reduces / hops from the table, and the runtime's all-reduce
+    # routing (IPC one-shot / two-shot / RCCL) follows the measured crossovers
+    hw = MI355X
+    probe = {}
+    if world > 1 and backend == "nccl" and not a.no_probe:
+        t_probe = time.perf_counter()
+        table = probe_comm(world)
+        pol = ar_policy(table)
+        hw = MI355X.with_comm_table(dict(table, policy=pol))
+        probe = summarize(table)
+        log(f"comm probe: {time.perf_counter() - t_probe:.1f}s, all-reduce policy {probe.get('ar_policy')}", rank)
     plan = partition(cfg, a.gpus, parse_plan(a.plan), batch_per_gpu=a.batch_per_gpu,
-                     ctx=a.prompt_len + a.warmup + a.steps)
+                     ctx=a.prompt_len + a.warmup + a.steps, hw=hw)
     mesh = plan.mesh
+    if hw.comm:
+        probe["applied"] = apply_policy(hw.comm["policy"], mesh.tp)
     comm = Communicator.from_mesh(mesh)
     log(f"model={cfg.name} gpus={a.gpus} backend={backend} ranks_seen={ranks_seen} plan={plan.name} "
         f"stages={plan.stages} est={plan.estimate['tokens_per_second']:.0f} tok/s", rank)
@@ -263,6 +280,7 @@ def run(a) -> int:
         "graphs_captured": sorted(runner.graphs),
         "graphs_failed": sorted(runner.eager_buckets),
         "custom_ar_active": comm.custom_ar is not None,
+        "comm_probe": probe or None,
         "config": {"model": MODEL_NAMES.get(a.model, a.model),
                    "global_batch": a.batch_per_gpu * a.gpus, "seq_len": a.prompt_len,
                    "parallelism": plan.name, "stages": [list(s) for s in plan.stages],

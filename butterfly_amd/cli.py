@@ -41,10 +41,19 @@ def cmd_partition(a) -> int:
         # the communication program of one decode step on the given rank (partition/schedule.py)
         from .partition.schedule import check_programs, programs
 
+        from .utils import flags
+
         B = a.batch_per_gpu * a.gpus // plan.mesh.dp
         m = plan.mesh
-        # default asynchronous pipeline: one step (tick) carries one of pp request groups
-        progs = programs(plan, B // m.pp if m.pp > 1 and m.ep == 1 else B)
+        if not 0 <= a.schedule < a.gpus:
+            print(f"--schedule: rank {a.schedule} is not in [0, {a.gpus})", file=sys.stderr)
+            return 2
+        # the engine's choice: asynchronous pipeline -> one step (tick) carries one of pp request
+        # groups; synchronous pipeline -> the step's batch is cut into pp microbatches
+        if m.pp > 1 and m.ep == 1 and flags.get("BFLY_PP_ASYNC"):
+            progs = programs(plan, B // m.pp)
+        else:
+            progs = programs(plan, B, microbatches=m.pp)
         check_programs(progs)
         print(progs[a.schedule].describe(), file=sys.stderr)
         return 0

@@ -9,7 +9,9 @@ that follow every TP all-reduce in the transformer block, removing one kernel an
 over the activations per all-reduce.
 
 Only messages up to `max_bytes` (default BFLY_CUSTOM_AR_MAX_BYTES) go here — the decode
-all-reduces; larger ones (prefill) stay on RCCL. Construction runs a self-test; if the IPC
+all-reduces; larger ones (prefill) stay on RCCL. From `two_shot_bytes` on (groups of 4 or 8)
+the kernel runs as reduce-scatter + all-gather over the same buffers: every link then carries
+2S/W instead of S bytes, at the price of a second rendezvous. Construction runs a self-test; if the IPC
 mapping, the kernel or the flag protocol misbehave on this machine, the instance reports
 `ok = False` and the communicator keeps using RCCL.
 """
@@ -27,11 +29,16 @@ log = logging.getLogger("butterfly_amd.comm")
 
 class CustomAllReduce:
     def __init__(self, ranks: list, rank_in_group: int, pg, max_bytes: int = 8 << 20,
-                 device: torch.device | None = None):
+                 device: torch.device | None = None, two_shot_bytes: int | None = None):
         ops.require_library()
         self.world = len(ranks)
         self.rank = rank_in_group
         self.cap = int(max_bytes)
+        if two_shot_bytes is None:
+            from ..utils import flags
+
+            two_shot_bytes = flags.get("BFLY_CUSTOM_AR_2SHOT_BYTES")
+        self.two_shot_bytes = int(two_shot_bytes)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         if self.world not in (2, 4, 8):
             raise ValueError("custom all-reduce supports groups of 2, 4 or 8 ranks")
@@ -86,13 +93,20 @@ class CustomAllReduce:
                 and t.is_contiguous() and t.shape[1] % 8 == 0 and t.shape[1] <= 16384
                 and t.numel() * 2 <= self.cap and t.data_ptr() % 16 == 0)
 
-    def all_reduce_(self, t) -> torch.Tensor:
+    def use_two_shot(self, t: torch.Tensor) -> bool:
+        return (self.world >= 4 and 0 < self.two_shot_bytes <= t.numel() * 2
+                and (t.shape[1] // 8) % self.world == 0)
+
+    def all_reduce_(self, t, two_shot: bool | None = None) -> torch.Tensor:
         """In place; `t` may be a deferred split-K GEMM output (ops.Partial), whose reduce the
         kernel fuses into its publish step (the result lands in t.out)."""
         if isinstance(t, ops.Partial):
-            torch.ops.bfly.custom_all_reduce(t.out, t.out, None, None, 0.0, self.bases, self.rank, self.cap, t.slabs)
+            two = self.use_two_shot(t.out) if two_shot is None else two_shot
+            torch.ops.bfly.custom_all_reduce(t.out, t.out, None, None, 0.0, self.bases, self.rank, self.cap,
+                                             t.slabs, two)
             return t.out
-        torch.ops.bfly.custom_all_reduce(t, t, None, None, 0.0, self.bases, self.rank, self.cap)
+        two = self.use_two_shot(t) if two_shot is None else two_shot
+        torch.ops.bfly.custom_all_reduce(t, t, None, None, 0.0, self.bases, self.rank, self.cap, None, two)
         return t
 
     def all_reduce_rms_norm_(self, t, w: torch.Tensor, eps: float,
@@ -104,12 +118,16 @@ class CustomAllReduce:
             t, slabs = t.out, t.slabs
         if out is None:
             out = torch.empty_like(t)
-        torch.ops.bfly.custom_all_reduce(t, out, residual, w, float(eps), self.bases, self.rank, self.cap, slabs)
+        torch.ops.bfly.custom_all_reduce(t, out, residual, w, float(eps), self.bases, self.rank, self.cap, slabs,
+                                         self.use_two_shot(t))
         return out
 
     def error(self) -> int:
         """Sticky device error word (non-zero after a flag-wait timeout)."""
         return int(torch.ops.bfly.car_error(self._ptr))
+
+    def clear_error(self) -> None:
+        torch.ops.bfly.car_clear_error(self._ptr)
 
     def _vote(self, good: bool, pg) -> bool:
         """True iff `good` on every rank of the group."""
@@ -121,15 +139,17 @@ class CustomAllReduce:
     def _self_test(self, pg) -> bool:
         good = True
         try:
+            modes = [False, True] if self.world >= 4 else [False]
             for rows, dim in ((3, 64), (130, 4096)):
                 x = torch.arange(rows * dim, device=self.device, dtype=torch.float32).view(rows, dim)
                 x = ((x % 17) + self.rank).to(torch.bfloat16)
                 want = sum(((x.float() - self.rank) + r) for r in range(self.world)).to(torch.bfloat16)
-                for _ in range(3):      # exercise both buffer parities
-                    y = x.clone()
-                    self.all_reduce_(y)
-                torch.cuda.synchronize(self.device)
-                good &= bool(torch.equal(y, want)) and self.error() == 0
+                for two in modes:
+                    for _ in range(3):      # exercise both buffer parities
+                        y = x.clone()
+                        self.all_reduce_(y, two_shot=two)
+                    torch.cuda.synchronize(self.device)
+                    good &= bool(torch.equal(y, want)) and self.error() == 0
         except Exception as e:  # noqa: BLE001 — any failure means: keep RCCL
             log.warning("custom all-reduce self-test raised %r", e)
             good = False

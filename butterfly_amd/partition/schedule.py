@@ -11,10 +11,15 @@ sampling all-gather) — written down ahead of time so that it can be
 
   * checked for cross-rank consistency without running anything (`check_programs`: every
     group collective is issued by all members in the same order with the same payload, every
-    send has its recv at the same position of the pair's stream: no deadlock, no mismatch);
+    send has its recv at the same position of the pair's stream). This catches mismatched
+    collectives and send/recv pairs; it does not simulate blocking semantics, so a wait cycle
+    ACROSS groups (e.g. a blocking send interleaved with another group's collective) is not
+    detected;
   * priced per xGMI link (`link_bytes`: bytes each directed GPU pair carries per step, ring
-    all-reduce/all-gather/reduce-scatter and point-to-point hops), which is what the
-    partitioner's cut-point objective minimises (`search.link_traffic`);
+    all-reduce/all-gather/reduce-scatter, chain broadcast and point-to-point hops). The
+    partitioner reports it per plan (`search.link_traffic`) and uses the busiest link's bytes
+    to choose among layouts whose estimated throughput is within 2 % (`search.select`); the
+    cut points themselves come from the time/memory DP;
   * compared with what the engine actually issued (tests/test_schedule.py replays a decode
     step through the loopback backend, parallel/fake.py, and diffs its log against this).
 
@@ -187,8 +192,14 @@ def link_bytes(plan: PartitionPlan, progs: dict) -> dict:
                     put(r, nxt, (n - 1) * i.nbytes)
                 elif i.op == "reduce_scatter":
                     put(r, nxt, (n - 1) / n * i.nbytes)
-                elif i.group.index(r) == n - 1:   # broadcast from the last member: a chain
-                    put(r, nxt, i.nbytes)
+                elif i.group.index(r) == n - 1:
+                    # broadcast from the last member as a chain: root -> successor -> ... ,
+                    # n-1 hops of the full payload
+                    hop = i.group.index(r)
+                    for _ in range(n - 1):
+                        a_, b_ = i.group[hop], i.group[(hop + 1) % n]
+                        put(a_, b_, i.nbytes)
+                        hop = (hop + 1) % n
     return out
 
 

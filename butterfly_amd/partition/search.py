@@ -12,13 +12,16 @@ compatible with the kv heads, pp <= layers, ep in {1, dp} for MoE):
      pipeline's ticks (slowest stage x groups; engine/pipeline.py), or with BFLY_PP_ASYNC=0
      the per-step microbatched pipeline, slowest stage plus the fill/drain share;
   4. score: throughput = generated tokens / s for the node, latency = step time.
+  5. link-aware selection (`select`): among plans within 2 % of the best objective, the
+     fewest bytes on the busiest xGMI link per generated token (from the rank programs of
+     schedule.py).
 xGMI placement: a full mesh gives every GPU pair its own link, so no two logical edges
-(ring all-reduce neighbours, pipeline neighbours) ever share a link; the plan records the
-per-link bytes per token so the traffic is visible, and placement is the identity.
+(ring all-reduce neighbours, pipeline neighbours) of different groups ever share a link and
+every bijective placement has the same per-link loads; placement is therefore the identity,
+and link traffic is minimised through the choice of layout (step 5) instead.
 """
 from __future__ import annotations
 
-import math
 from typing import Optional, Union
 
 from .._native_loader import native
@@ -60,21 +63,22 @@ def evaluate(cfg: ModelConfig, dp: int, tp: int, pp: int, ep: int, *, batch_per_
     mb = microbatches or (pp if pp > 1 else 1)
     mb = max(1, min(mb, B))
     tokens = B // mb if decode else B * ctx // mb
-    lc = cm.layer_time(tokens, tp, ctx, decode, seqs=max(1, B // mb), ep=ep)
+    lcs = cm.layer_costs(tokens, tp, ctx, decode, seqs=max(1, B // mb), ep=ep)
     first_t, last_t = cm.embed_head_time(tokens, tokens if decode else max(1, B // mb), tp)
     emb_b, head_b = cm.embed_head_bytes(tp)
     kv_per_layer = 2.0 * max(1, cfg.num_kv_heads // tp) * cfg.head_dim * 2 * B * (ctx + 64)
     cap = hw.hbm_bytes * hw.usable_hbm_fraction - 4e9
-    L = cfg.num_layers
     boundary = cm.p2p(2.0 * tokens * cfg.hidden_size) if pp > 1 else 0.0
-    cuts = native().pipeline_cuts([lc.seconds] * L, [lc.weight_bytes + kv_per_layer] * L, pp,
+    # min-max cut DP over the per-layer costs; the embedding is charged to stage 0 and the
+    # final norm + LM head + sampling to the last stage, so the cuts shift layers off them
+    cuts = native().pipeline_cuts([c.seconds for c in lcs], [c.weight_bytes + kv_per_layer for c in lcs], pp,
                                   first_t, emb_b, last_t, head_b, boundary, cap)
     if not cuts:
         return None
     stages = [(cuts[i], cuts[i + 1]) for i in range(pp)]
     stage_t = []
     for s, (a, b) in enumerate(stages):
-        t = (b - a) * lc.seconds + (first_t if s == 0 else 0) + (last_t if s == pp - 1 else 0)
+        t = sum(c.seconds for c in lcs[a:b]) + (first_t if s == 0 else 0) + (last_t if s == pp - 1 else 0)
         if s != pp - 1:
             t += boundary
         stage_t.append(t)
@@ -93,7 +97,7 @@ def evaluate(cfg: ModelConfig, dp: int, tp: int, pp: int, ep: int, *, batch_per_
     tps = tokens_per_step / step
     weight_bytes, kv_budget = [], []
     for s, (a, b) in enumerate(stages):
-        w = (b - a) * lc.weight_bytes + (emb_b if s == 0 else 0) + (head_b if s == pp - 1 else 0)
+        w = sum(c.weight_bytes for c in lcs[a:b]) + (emb_b if s == 0 else 0) + (head_b if s == pp - 1 else 0)
         weight_bytes.append(w)
         kv_budget.append(max(0.0, cap - w))
     plan = PartitionPlan(model=cfg, n_gpus=n, dp=dp, tp=tp, pp=pp, ep=ep, stages=stages,
@@ -105,6 +109,7 @@ def evaluate(cfg: ModelConfig, dp: int, tp: int, pp: int, ep: int, *, batch_per_
                                    "batch_per_replica": B, "microbatches": mb,
                                    "stage_seconds": stage_t, "decode": decode, "ctx": ctx})
     plan.link_bytes_per_token = link_traffic(plan)
+    plan.estimate["max_link_bytes_per_token"] = max(plan.link_bytes_per_token.values(), default=0.0)
     return plan
 
 
@@ -119,17 +124,20 @@ def link_traffic(plan: PartitionPlan) -> dict:
 
 def partition(cfg: Union[ModelConfig, str], n_gpus: int, strategy: Union[str, dict] = "auto",
               objective: str = "throughput", batch_per_gpu: int = 64, ctx: int = 1024,
-              hw: Hardware = MI355X, decode: bool = True) -> PartitionPlan:
+              hw: Hardware = MI355X, decode: bool = True, link_tolerance: float = 0.02) -> PartitionPlan:
     """The partitioning API: returns the best PartitionPlan for `n_gpus` GPUs.
 
     strategy: "auto" (search every factorisation), or a dict fixing some of
     {"dp", "tp", "pp", "ep"} (the rest are searched), e.g. {"tp": 2, "pp": 4}.
     objective: "throughput" (max node tokens/s) or "latency" (min per-token step time).
+    Among plans within `link_tolerance` of the best objective, the one with the least traffic
+    on its busiest xGMI link wins (`select`). `hw` may carry a measured communication table
+    (parallel/probe.py; bench.py probes the node before partitioning).
     """
     if isinstance(cfg, str):
         cfg = ModelConfig.from_preset(cfg)
     fixed = {} if strategy == "auto" else dict(strategy)
-    best, best_score = None, -math.inf
+    feasible = []
     for dp, tp, pp in factorizations(n_gpus):
         if any(fixed.get(k, v) != v for k, v in (("dp", dp), ("tp", tp), ("pp", pp))):
             continue
@@ -149,12 +157,26 @@ def partition(cfg: Union[ModelConfig, str], n_gpus: int, strategy: Union[str, di
                 continue
             p = evaluate(cfg, dp, tp, pp, ep, batch_per_gpu=batch_per_gpu, ctx=ctx,
                          objective=objective, hw=hw, decode=decode)
-            if p is None:
-                continue
-            score = p.estimate["tokens_per_second"] if objective == "throughput" else -p.estimate["token_latency_seconds"]
-            if score > best_score:
-                best, best_score = p, score
-    if best is None:
+            if p is not None:
+                feasible.append(p)
+    if not feasible:
         raise ValueError(f"no feasible partition of {cfg.name} on {n_gpus} GPUs with strategy {strategy}")
+    best = select(feasible, objective, link_tolerance)
     best.validate()
     return best
+
+
+def _score(p: PartitionPlan, objective: str) -> float:
+    return p.estimate["tokens_per_second"] if objective == "throughput" else -p.estimate["token_latency_seconds"]
+
+
+def select(plans: list, objective: str = "throughput", link_tolerance: float = 0.02) -> PartitionPlan:
+    """Link-aware choice: among the plans whose objective is within `link_tolerance` of the
+    best one, take the one that puts the fewest bytes on its busiest xGMI link per generated
+    token (ties: the better objective). The cost model already charges collective and hop time
+    to each step; this second criterion prefers the layout that leaves the links idle when the
+    estimates are too close to call."""
+    best = max(_score(p, objective) for p in plans)
+    margin = abs(best) * link_tolerance
+    close = [p for p in plans if _score(p, objective) >= best - margin]
+    return min(close, key=lambda p: (p.estimate["max_link_bytes_per_token"], -_score(p, objective)))

@@ -561,10 +561,14 @@ int64_t car_ipc_open(const Tensor& h) {
 }
 void car_ipc_close(int64_t p) { bfly::car_ipc_close(reinterpret_cast<void*>(p)); }
 int64_t car_error(int64_t p) { return bfly::car_error(reinterpret_cast<const void*>(p)); }
+void car_clear_error(int64_t p) {
+  TORCH_CHECK(bfly::car_clear_error(reinterpret_cast<void*>(p)) == 0, "car_clear_error: hipMemset failed");
+}
 
 void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tensor>& residual,
                        const c10::optional<Tensor>& w, double eps, at::IntArrayRef bases,
-                       int64_t rank, int64_t cap, const c10::optional<Tensor>& slabs) {
+                       int64_t rank, int64_t cap, const c10::optional<Tensor>& slabs,
+                       bool two_shot) {
   CHECK_GPU(inp); CHECK_BF16(inp); CHECK_BF16(out);
   TORCH_CHECK(inp.dim() == 2 && inp.is_contiguous() && out.is_contiguous() &&
                   out.sizes() == inp.sizes(), "custom_all_reduce: 2-D contiguous, same shape");
@@ -605,7 +609,8 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tenso
   }
   c10::DeviceGuard g(inp.device());
   const int rc = bfly::launch_custom_allreduce(bf(inp), bf(out), res, wp, (float)eps, rows, dim,
-                                               peers, world, (int)rank, cap, cur_stream(), sp, sk);
+                                               peers, world, (int)rank, cap, cur_stream(), sp, sk,
+                                               two_shot);
   TORCH_CHECK(rc == 0, "custom_all_reduce: launch rejected (", rc, ")");
 }
 
@@ -656,9 +661,10 @@ TORCH_LIBRARY(bfly, m) {
   m.def("car_ipc_open(Tensor handle) -> int", &car_ipc_open);
   m.def("car_ipc_close(int ptr) -> ()", &car_ipc_close);
   m.def("car_error(int ptr) -> int", &car_error);
+  m.def("car_clear_error(int ptr) -> ()", &car_clear_error);
   m.def("car_buffer_bytes(int cap) -> int", [](int64_t cap) -> int64_t { return bfly::car_buffer_bytes(cap); });
   m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, Tensor(b!)? residual, Tensor? w, float eps, "
-        "int[] bases, int rank, int cap, Tensor? slabs=None) -> ()");
+        "int[] bases, int rank, int cap, Tensor? slabs=None, bool two_shot=False) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
         "bool causal, Tensor(a!) out, Tensor? cu_seqlens_k=None, Tensor(b!)? lse=None) -> ()");
   m.def("attn_lse_merge(Tensor(a!) acc_o, Tensor(b!) acc_lse, Tensor o, Tensor lse) -> ()");

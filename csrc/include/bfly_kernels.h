@@ -99,16 +99,19 @@ constexpr int kArBlocks = 128;
 constexpr int kArMaxWorld = 8;
 constexpr long kArDataOff = 65536;
 struct ArPeers { char* base[kArMaxWorld]; };
-inline long car_buffer_bytes(long cap) { return kArDataOff + 2 * cap; }
+// flags/counters, two input buffers and two reduced-chunk buffers (two-shot), all double-buffered
+inline long car_buffer_bytes(long cap) { return kArDataOff + 4 * cap; }
 // `slabs` (optional): the input is split-K partials [sk][rows][dim] f32, reduced in the publish.
 int launch_custom_allreduce(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
                             int rows, int dim, const ArPeers& peers, int world, int rank,
-                            long cap, hipStream_t stream, const float* slabs = nullptr, int sk = 0);
+                            long cap, hipStream_t stream, const float* slabs = nullptr, int sk = 0,
+                            bool two_shot = false);
 void* car_alloc(size_t bytes);
 void car_free(void* p);
 int car_ipc_handle(void* p, unsigned char* out64);
 void* car_ipc_open(const unsigned char* h64);
 void car_ipc_close(void* p);
+int car_clear_error(void* base);
 int car_error(const void* base);
 
 // moe.hip

@@ -13,7 +13,9 @@
 //   [0, 4 KiB)        flags[kArBlocks][8]   peer r stores its epoch into slot [b][r]
 //   [4 KiB, 8 KiB)    cnt[kArBlocks]        this rank's per-block epoch counter
 //   [8 KiB]           err                   sticky error word (spin timeout)
+//   [12 KiB, 16 KiB)  flags2[kArBlocks][8]  second-rendezvous flags (two-shot)
 //   [64 KiB, +2*cap)  two data buffers; epoch parity selects one (double buffering)
+//   [+2*cap, +4*cap)  two reduced-chunk buffers (two-shot)
 //
 // Protocol for workgroup b (grid is ALWAYS kArBlocks, so row r is always owned by block
 // r % kArBlocks and its epoch advances by one per call on every rank):
@@ -25,6 +27,18 @@
 //   on every rank); cnt[b] = e.
 // Double buffering is enough: a rank can only stage call k+1 after every peer arrived at call
 // k's barrier, i.e. after every peer finished reading call k-1 (same parity).
+//
+// TWO-SHOT (reduce-scatter + all-gather, for larger messages at W = 4 / 8): the one-shot read
+// pulls the WHOLE message from every peer, S bytes per link. Two-shot splits every row into W
+// column chunks; rank p
+//   RS: sums chunk p of its block's rows over all ranks (fixed order 0..W-1, f32) and stores
+//       the bf16 result in its `red[e & 1]` buffer; fence; flags2[b][p] = e at every peer;
+//   AG: waits for flags2[b][*] >= e, then reads chunk q of every row from rank q's `red`
+//       (and fuses residual add + RMSNorm exactly as one-shot does).
+// Per-link traffic drops to 2S/W (S/4 at W = 8); the price is a second rendezvous. Results are
+// bitwise identical to one-shot (same f32 order, same bf16 rounding points). `red` double
+// buffering: a rank writes red[(e+2) & 1] only after passing call e+2's first rendezvous, i.e.
+// after every peer started call e+2, so every peer finished call e's gather.
 #include <string.h>
 
 #include "bfly_common.h"
@@ -37,13 +51,20 @@ namespace {
 constexpr long kArFlagsOff = 0;
 constexpr long kArCntOff = 4096;
 constexpr long kArErrOff = 8192;
+constexpr long kArFlags2Off = 12288;
 constexpr int kArThreads = 256;
 
+// Give-up time of a flag wait, in ticks of the 100 MHz constant clock (wall_clock64): a peer
+// that is this late is not coming (crashed or hung rank). Wall time, not an iteration count, so
+// a rank delayed by host work or by time-slicing (several ranks sharing one GPU) is waited for.
+constexpr long long kArSpinTimeoutTicks = 20LL * 100000000LL;   // 20 s
+
 __device__ __forceinline__ void spin_wait(const uint32_t* f, uint32_t e, uint32_t* err) {
-  long it = 0;
+  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e) return;
+  const long long t0 = wall_clock64();
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
     __builtin_amdgcn_s_sleep(2);
-    if (++it > (1L << 26)) {   // ~seconds: a peer never arrived. Record and give up.
+    if (wall_clock64() - t0 > kArSpinTimeoutTicks) {   // record and give up
       __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
@@ -51,7 +72,21 @@ __device__ __forceinline__ void spin_wait(const uint32_t* f, uint32_t e, uint32_
 }
 
 // MODE 0: out = sum.  MODE 1: residual = bf16(bf16(sum) + residual); out = rmsnorm(residual) * w
-template <int W, int MODE, int NV>
+// store epoch e at every peer's flag slot [b][rank] and wait until every peer stored e in ours
+template <int W>
+__device__ __forceinline__ void rendezvous(const ArPeers& peers, char* my, long off, int b, int rank,
+                                           uint32_t e) {
+  if (threadIdx.x < W) {
+    uint32_t* pf = reinterpret_cast<uint32_t*>(peers.base[threadIdx.x] + off) + b * 8 + rank;
+    __hip_atomic_store(pf, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t* f = reinterpret_cast<const uint32_t*>(my + off) + b * 8 + threadIdx.x;
+    spin_wait(f, e, reinterpret_cast<uint32_t*>(my + kArErrOff));
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+template <int W, int MODE, int NV, bool TWO>
 __global__ void __launch_bounds__(kArThreads)
 allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __restrict__ residual,
                  const bf16* __restrict__ w, float eps, int rows, int dim, ArPeers peers,
@@ -100,19 +135,86 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
   __syncthreads();
 
   // 2. rendezvous with the peers for this block
-  if (threadIdx.x < W) {
-    uint32_t* pf = reinterpret_cast<uint32_t*>(peers.base[threadIdx.x] + kArFlagsOff) + b * 8 + rank;
-    __hip_atomic_store(pf, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t* f = reinterpret_cast<const uint32_t*>(my + kArFlagsOff) + b * 8 + threadIdx.x;
-    spin_wait(f, e, reinterpret_cast<uint32_t*>(my + kArErrOff));
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  rendezvous<W>(peers, my, kArFlagsOff, b, rank, e);
 
   // 3. reduce
   const bf16* src[W];
 #pragma unroll
   for (int p = 0; p < W; ++p) src[p] = reinterpret_cast<const bf16*>(peers.base[p] + data_off);
+  if constexpr (TWO) {
+    // 3a. reduce-scatter: this rank's column chunk of the block's rows
+    const long red_off = kArDataOff + 2 * cap + (long)(e & 1) * cap;
+    const int per = nvec / W, c0 = rank * per;
+    bf16* red_mine = reinterpret_cast<bf16*>(my + red_off);
+    for (int r = b; r < rows; r += kArBlocks) {
+      const long ro = (long)r * dim;
+      for (int c = c0 + threadIdx.x; c < c0 + per; c += kArThreads) {
+        bf16x8 v[W];
+#pragma unroll
+        for (int p = 0; p < W; ++p)
+          v[p] = p == rank ? reinterpret_cast<const bf16x8*>(own + ro)[c]
+                           : reinterpret_cast<const bf16x8*>(src[p] + ro)[c];
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = bf2f(v[0][j]);
+#pragma unroll
+        for (int p = 1; p < W; ++p)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[p][j]);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+        reinterpret_cast<bf16x8*>(red_mine + ro)[c] = o;
+      }
+    }
+    __threadfence_system();
+    __syncthreads();
+    rendezvous<W>(peers, my, kArFlags2Off, b, rank, e);
+    // 3b. all-gather: chunk q of every row comes from rank q's reduced buffer
+#pragma unroll
+    for (int p = 0; p < W; ++p) src[p] = reinterpret_cast<const bf16*>(peers.base[p] + red_off);
+    for (int r = b; r < rows; r += kArBlocks) {
+      const long ro = (long)r * dim;
+      if constexpr (MODE == 0) {
+        for (int c = threadIdx.x; c < nvec; c += kArThreads)
+          reinterpret_cast<bf16x8*>(out + ro)[c] = reinterpret_cast<const bf16x8*>(src[c / per] + ro)[c];
+      } else {
+        float v[NV][8];
+        float ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int c = threadIdx.x + i * kArThreads;
+          if (c < nvec) {
+            const bf16x8 x = reinterpret_cast<const bf16x8*>(src[c / per] + ro)[c];
+            const bf16x8 rr = reinterpret_cast<const bf16x8*>(residual + ro)[c];
+            bf16x8 sres;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              sres[j] = f2bf(bf2f(x[j]) + bf2f(rr[j]));
+              v[i][j] = bf2f(sres[j]);
+              ss += v[i][j] * v[i][j];
+            }
+            reinterpret_cast<bf16x8*>(residual + ro)[c] = sres;
+          }
+        }
+        ss = block_sum(ss, red);
+        const float inv = rsqrtf(ss / (float)dim + eps);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int c = threadIdx.x + i * kArThreads;
+          if (c < nvec) {
+            const bf16x8 g = reinterpret_cast<const bf16x8*>(w)[c];
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
+            reinterpret_cast<bf16x8*>(out + ro)[c] = o;
+          }
+        }
+      }
+    }
+    if (threadIdx.x == 0) cnt[b] = e;
+    return;
+  }
   for (int r = b; r < rows; r += kArBlocks) {
     const long ro = (long)r * dim;
     if constexpr (MODE == 0) {
@@ -179,46 +281,53 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
   if (threadIdx.x == 0) cnt[b] = e;
 }
 
-template <int W>
+template <int W, bool TWO>
 int launch_w(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps, int rows,
              int dim, const ArPeers& peers, int rank, long cap, const float* slabs, int sk,
              hipStream_t stream) {
   const dim3 grid(kArBlocks), block(kArThreads);
   if (residual == nullptr) {
-    allreduce_kernel<W, 0, 1><<<grid, block, 0, stream>>>(in, out, nullptr, nullptr, 0.f, rows,
-                                                          dim, peers, rank, cap, slabs, sk);
+    allreduce_kernel<W, 0, 1, TWO><<<grid, block, 0, stream>>>(in, out, nullptr, nullptr, 0.f, rows,
+                                                               dim, peers, rank, cap, slabs, sk);
     return 0;
   }
   const int nv = (dim / 8 + kArThreads - 1) / kArThreads;
-#define AR_NV(N)                                                                          \
-  case N:                                                                                 \
-    allreduce_kernel<W, 1, N><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, \
-                                                          dim, peers, rank, cap, slabs, sk); \
+  // register rows per thread: 1, 2, 4 or 8 vectors of 8 (dim up to 16384)
+  const int nvp = nv <= 1 ? 1 : nv <= 2 ? 2 : nv <= 4 ? 4 : nv <= 8 ? 8 : 0;
+#define AR_NV(N)                                                                               \
+  case N:                                                                                      \
+    allreduce_kernel<W, 1, N, TWO><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, \
+                                                               dim, peers, rank, cap, slabs, sk); \
     return 0;
-  switch (nv) {
+  switch (nvp) {
     AR_NV(1) AR_NV(2) AR_NV(4) AR_NV(8)
-    case 3: allreduce_kernel<W, 1, 4><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk); return 0;
-    case 5: case 6: case 7:
-      allreduce_kernel<W, 1, 8><<<grid, block, 0, stream>>>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk);
-      return 0;
     default: return -1;
   }
 #undef AR_NV
+}
+
+template <int W>
+int launch_mode(bool two, const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
+                int rows, int dim, const ArPeers& peers, int rank, long cap, const float* slabs,
+                int sk, hipStream_t stream) {
+  if (two) return launch_w<W, true>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+  return launch_w<W, false>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
 }
 
 }  // namespace
 
 int launch_custom_allreduce(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
                             int rows, int dim, const ArPeers& peers, int world, int rank,
-                            long cap, hipStream_t stream, const float* slabs, int sk) {
+                            long cap, hipStream_t stream, const float* slabs, int sk, bool two_shot) {
   if (dim % 8 != 0 || dim > 16384 || rows < 0) return -2;
   if (slabs != nullptr && sk < 1) return -6;
   if ((long)rows * dim * 2 > cap) return -3;
   if (rank < 0 || rank >= world) return -4;
+  if (two_shot && (dim / 8) % world != 0) return -7;   // column chunks of whole 16-B vectors
   switch (world) {
-    case 2: return launch_w<2>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
-    case 4: return launch_w<4>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
-    case 8: return launch_w<8>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+    case 2: return launch_mode<2>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+    case 4: return launch_mode<4>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+    case 8: return launch_mode<8>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
     default: return -5;
   }
 }
@@ -254,6 +363,10 @@ void* car_ipc_open(const unsigned char* h64) {
 }
 
 void car_ipc_close(void* p) { (void)hipIpcCloseMemHandle(p); }
+
+int car_clear_error(void* base) {
+  return hipMemset(static_cast<char*>(base) + kArErrOff, 0, 4) == hipSuccess ? 0 : -1;
+}
 
 int car_error(const void* base) {
   uint32_t e = 0;

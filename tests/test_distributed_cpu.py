@@ -105,3 +105,31 @@ def test_expert_parallel_mixtral():
     outs = run_world(_dist_generate, 2, "mixtral-tiny", dict(dp=2, ep=2), halves, 6)
     assert outs[0] == _single("mixtral-tiny", halves[0])
     assert outs[1] == _single("mixtral-tiny", halves[1])
+
+
+def _probe_worker(rank, world):
+    import torch
+
+    from butterfly_amd.parallel.probe import ar_policy, probe_comm, summarize
+
+    tab = probe_comm(world, device=torch.device("cpu"), iters=2)
+    return tab, ar_policy(tab), summarize(tab)
+
+
+def test_comm_probe_plumbing_gloo():
+    """The start-up probe (parallel/probe.py) on 4 gloo ranks: groups of 2 and 4 timed at once,
+    send/recv pairs and all-to-all; every rank ends with the identical (max-reduced) table,
+    which the cost model can consume."""
+    from butterfly_amd.config import ModelConfig
+    from butterfly_amd.partition.costmodel import CostModel
+    from butterfly_amd.partition.hw import MI355X
+
+    res = run_world(_probe_worker, 4)
+    tabs = [r[0] for r in res]
+    assert all(t["all_reduce"] == tabs[0]["all_reduce"] and t["p2p"] == tabs[0]["p2p"] for t in tabs)
+    ar = tabs[0]["all_reduce"]["rccl"]
+    assert sorted(ar) == [2, 4] and all(len(v) == 6 for v in ar.values())
+    assert len(tabs[0]["p2p"]) == 3 and 4 in tabs[0]["all_to_all"]
+    assert res[0][1][4]["ipc_max"] == 0            # no IPC kernel on CPU: RCCL-only policy
+    cm = CostModel(ModelConfig.from_preset("llama3-8b"), MI355X.with_comm_table(dict(tabs[0], policy=res[0][1])))
+    assert cm.allreduce(1 << 20, 4) > 0 and cm.p2p(1 << 20) > 0

@@ -63,3 +63,53 @@ def test_no_expert_parallel_with_pipeline_stages():
         assert not (p.ep > 1 and p.pp > 1)
     with _pt.raises(ValueError):
         partition("mixtral-8x7b", 4, {"dp": 2, "ep": 2, "pp": 2})
+
+
+@settings(max_examples=25, deadline=None)
+@given(st.sampled_from(["llama3-70b", "llama3-8b", "mixtral-8x7b"]), st.sampled_from([2, 4, 8]),
+       st.sampled_from([8, 32, 64]), st.sampled_from(["throughput", "latency"]))
+def test_choice_minimises_busiest_link_among_near_best(preset, n, bpg, objective):
+    """Link-aware selection: of every feasible layout whose objective is within 2 % of the best,
+    the chosen plan has the fewest bytes per token on its busiest xGMI link."""
+    from butterfly_amd.partition.search import _tp_ok, evaluate
+
+    cfg = ModelConfig.from_preset(preset)
+    try:
+        chosen = partition(cfg, n, objective=objective, batch_per_gpu=bpg, ctx=1024)
+    except ValueError:
+        return
+    plans = []
+    for dp, tp, pp in factorizations(n):
+        if not _tp_ok(cfg, tp) or pp > cfg.num_layers:
+            continue
+        for ep in ([1, dp] if cfg.is_moe and dp > 1 and tp == 1 and pp == 1 and cfg.num_experts % dp == 0 else [1]):
+            try:
+                p = evaluate(cfg, dp, tp, pp, ep, batch_per_gpu=bpg, ctx=1024, objective=objective)
+            except ValueError:
+                p = None
+            if p is not None:
+                plans.append(p)
+    score = (lambda p: p.estimate["tokens_per_second"]) if objective == "throughput" else \
+        (lambda p: -p.estimate["token_latency_seconds"])
+    best = max(score(p) for p in plans)
+    near = [p for p in plans if score(p) >= best - abs(best) * 0.02]
+    assert chosen.estimate["max_link_bytes_per_token"] == min(p.estimate["max_link_bytes_per_token"] for p in near)
+    assert score(chosen) >= best - abs(best) * 0.02
+
+
+def test_measured_comm_table_drives_allreduce_cost():
+    """With a probe table attached, all-reduce prices come from it (log-log interpolation of the
+    implementation the runtime would pick), not from the default constants."""
+    from butterfly_amd.partition.costmodel import CostModel, interp_loglog
+    from butterfly_amd.partition.hw import MI355X
+
+    tab = {"all_reduce": {"rccl": {8: [[1 << 20, 100e-6], [8 << 20, 400e-6]]},
+                          "oneshot": {8: [[16 << 10, 10e-6], [1 << 20, 30e-6]]},
+                          "twoshot": {"8": [[1 << 20, 20e-6], [8 << 20, 50e-6]]}},
+           "p2p": [[1 << 20, 15e-6]]}
+    cm = CostModel(ModelConfig.from_preset("llama3-70b"), MI355X.with_comm_table(tab))
+    assert cm.allreduce(16 << 10, 8) == pytest.approx(10e-6)            # one-shot below 512 KiB
+    assert cm.allreduce(8 << 20, 8) == pytest.approx(50e-6)             # two-shot from 512 KiB
+    assert cm.allreduce(32 << 20, 8) > 400e-6                           # RCCL beyond the IPC buffer
+    assert cm.p2p(1 << 20) == pytest.approx(15e-6)
+    assert interp_loglog([[1, 1.0], [100, 100.0]], 10) == pytest.approx(10.0)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""GPU check + microbenchmark of the one-shot IPC all-reduce (csrc/kernels/allreduce.hip).
+"""GPU check + microbenchmark of the IPC all-reduce (csrc/kernels/allreduce.hip), one-shot and
+two-shot (reduce-scatter + all-gather, groups of 4 / 8).
 
 N ranks share cuda:0 (gloo carries only the handle exchange): exercises the IPC mapping,
 the flag protocol, both buffer parities, the fused add+RMSNorm epilogue, hipGraph capture
@@ -34,120 +35,136 @@ def data(rows, dim, r, salt):
     return (torch.randn(rows, dim, generator=g) * (r + 1)).to(torch.bfloat16).to(dev)
 
 
-# 1. plain sums, many shapes (every rank computes the same expected value)
-for salt, (rows, dim) in enumerate([(1, 8192), (7, 8192), (64, 8192), (128, 8192), (129, 1024),
-                                    (256, 8192), (512, 4096), (1, 16384)]):
-    xs = [data(rows, dim, r, salt) for r in range(world)]
-    want = torch.zeros(rows, dim, device=dev)
-    for x in xs:
-        want += x.float()
-    want = want.to(torch.bfloat16)
-    y = xs[rank].clone()
-    car.all_reduce_(y)
-    torch.cuda.synchronize()
-    if not torch.equal(y, want):
-        fails.append(f"sum {rows}x{dim}: max err {(y.float() - want.float()).abs().max().item():.3e}")
+def checks(tag, fused=True):
+    """Every correctness check in the current kernel mode (one-shot / two-shot)."""
+    # 1. plain sums, many shapes (every rank computes the same expected value)
+    for salt, (rows, dim) in enumerate([(1, 8192), (7, 8192), (64, 8192), (128, 8192), (129, 1024),
+                                        (256, 8192), (512, 4096), (1, 16384)]):
+        xs = [data(rows, dim, r, salt) for r in range(world)]
+        want = torch.zeros(rows, dim, device=dev)
+        for x in xs:
+            want += x.float()
+        want = want.to(torch.bfloat16)
+        y = xs[rank].clone()
+        car.all_reduce_(y)
+        torch.cuda.synchronize()
+        if not torch.equal(y, want):
+            fails.append(f"{tag} sum {rows}x{dim}: max err {(y.float() - want.float()).abs().max().item():.3e}")
 
-# 2. fused residual add + RMSNorm == all-reduce then rms_norm(residual=...)
-for salt, (rows, dim) in enumerate([(64, 8192), (3, 4096), (200, 8192)]):
-    xs = [data(rows, dim, r, 50 + salt) for r in range(world)]
-    res0 = data(rows, dim, 99, 50 + salt)
-    w = data(1, dim, 77, 50 + salt).view(dim)
-    s = torch.zeros(rows, dim, device=dev)
-    for x in xs:
-        s += x.float()
-    s = s.to(torch.bfloat16)
-    res_ref = res0.clone()
-    y_ref = ops.rms_norm(s, w, 1e-5, residual=res_ref)
-    res = res0.clone()
-    y = car.all_reduce_rms_norm_(xs[rank].clone(), w, 1e-5, res)
-    torch.cuda.synchronize()
-    if not torch.equal(res, res_ref):
-        fails.append(f"fused residual {rows}x{dim}")
-    err = (y.float() - y_ref.float()).abs().max().item()
-    if err > 1e-2 * max(1.0, y_ref.float().abs().max().item()):
-        fails.append(f"fused norm {rows}x{dim}: {err:.3e}")
+    # 2. fused residual add + RMSNorm == all-reduce then rms_norm(residual=...)
+    for salt, (rows, dim) in enumerate([(64, 8192), (3, 4096), (200, 8192)] if fused else []):
+        xs = [data(rows, dim, r, 50 + salt) for r in range(world)]
+        res0 = data(rows, dim, 99, 50 + salt)
+        w = data(1, dim, 77, 50 + salt).view(dim)
+        s = torch.zeros(rows, dim, device=dev)
+        for x in xs:
+            s += x.float()
+        s = s.to(torch.bfloat16)
+        res_ref = res0.clone()
+        y_ref = ops.rms_norm(s, w, 1e-5, residual=res_ref)
+        res = res0.clone()
+        y = car.all_reduce_rms_norm_(xs[rank].clone(), w, 1e-5, res)
+        torch.cuda.synchronize()
+        if not torch.equal(res, res_ref):
+            fails.append(f"{tag} fused residual {rows}x{dim}")
+        err = (y.float() - y_ref.float()).abs().max().item()
+        if err > 1e-2 * max(1.0, y_ref.float().abs().max().item()):
+            fails.append(f"{tag} fused norm {rows}x{dim}: {err:.3e}")
 
-# 2b. split-K slab input (ops.Partial): the kernel reduces the f32 slabs while publishing;
-#     equal to splitk_reduce -> all-reduce (-> add + RMSNorm)
-for salt, (sk, rows, dim) in enumerate([(4, 64, 8192), (3, 5, 4096), (8, 128, 8192)]):
-    slabs = [(torch.randn(sk, rows, dim, generator=torch.Generator().manual_seed(300 + 10 * salt + r)) * 0.3)
-             .to(dev) for r in range(world)]
-    parts = []
+    # 2b. split-K slab input (ops.Partial): the kernel reduces the f32 slabs while publishing;
+    #     equal to splitk_reduce -> all-reduce (-> add + RMSNorm)
+    for salt, (sk, rows, dim) in enumerate([(4, 64, 8192), (3, 5, 4096), (8, 128, 8192)]):
+        slabs = [(torch.randn(sk, rows, dim, generator=torch.Generator().manual_seed(300 + 10 * salt + r)) * 0.3)
+                 .to(dev) for r in range(world)]
+        parts = []
+        for r in range(world):
+            o = torch.empty(rows, dim, dtype=torch.bfloat16, device=dev)
+            torch.ops.bfly.splitk_reduce(slabs[r].contiguous(), o)
+            parts.append(o)
+        s = torch.zeros(rows, dim, device=dev)
+        for o in parts:
+            s += o.float()
+        s = s.to(torch.bfloat16)
+        y = car.all_reduce_(ops.Partial(slabs[rank].contiguous(), torch.empty(rows, dim, dtype=torch.bfloat16, device=dev)))
+        torch.cuda.synchronize()
+        # the slab sum may round differently from splitk_reduce's (fast-math reassociation): within
+        # one bf16 ulp of it, and bitwise identical on every rank
+        err = (y.float() - s.float()).abs().max().item()
+        if err > 8e-3 * max(1.0, s.float().abs().max().item()):
+            fails.append(f"{tag} slab sum sk={sk} {rows}x{dim}: max err {err:.3e}")
+        ys = [torch.empty_like(y).cpu() for _ in range(world)]
+        dist.all_gather(ys, y.cpu())
+        if not all(torch.equal(ys[0], t) for t in ys):
+            fails.append(f"{tag} slab sum sk={sk} {rows}x{dim}: ranks disagree")
+        if not fused:
+            continue
+        w = data(1, dim, 78, 60 + salt).view(dim)
+        res0 = data(rows, dim, 98, 60 + salt)
+        res_ref = res0.clone()
+        y_ref = ops.rms_norm(s, w, 1e-5, residual=res_ref)
+        res = res0.clone()
+        y = car.all_reduce_rms_norm_(ops.Partial(slabs[rank].contiguous(), torch.empty(rows, dim, dtype=torch.bfloat16,
+                                                                                        device=dev)), w, 1e-5, res)
+        torch.cuda.synchronize()
+        if (res.float() - res_ref.float()).abs().max().item() > 1.6e-2 * max(1.0, res_ref.float().abs().max().item()):
+            fails.append(f"{tag} slab fused residual sk={sk} {rows}x{dim}")
+        err = (y.float() - y_ref.float()).abs().max().item()
+        if err > 1e-2 * max(1.0, y_ref.float().abs().max().item()):
+            fails.append(f"{tag} slab fused norm sk={sk} {rows}x{dim}: {err:.3e}")
+
+    # 3. graph capture / replay
+    x = data(64, 8192, rank, 7)
+    buf = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        car.all_reduce_(buf)         # warm-up on the capture stream
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        car.all_reduce_(buf)
+    want = torch.zeros(64, 8192, device=dev)
     for r in range(world):
-        o = torch.empty(rows, dim, dtype=torch.bfloat16, device=dev)
-        torch.ops.bfly.splitk_reduce(slabs[r].contiguous(), o)
-        parts.append(o)
-    s = torch.zeros(rows, dim, device=dev)
-    for o in parts:
-        s += o.float()
-    s = s.to(torch.bfloat16)
-    y = car.all_reduce_(ops.Partial(slabs[rank].contiguous(), torch.empty(rows, dim, dtype=torch.bfloat16, device=dev)))
-    torch.cuda.synchronize()
-    # the slab sum may round differently from splitk_reduce's (fast-math reassociation): within
-    # one bf16 ulp of it, and bitwise identical on every rank
-    err = (y.float() - s.float()).abs().max().item()
-    if err > 8e-3 * max(1.0, s.float().abs().max().item()):
-        fails.append(f"slab sum sk={sk} {rows}x{dim}: max err {err:.3e}")
-    ys = [torch.empty_like(y).cpu() for _ in range(world)]
-    dist.all_gather(ys, y.cpu())
-    if not all(torch.equal(ys[0], t) for t in ys):
-        fails.append(f"slab sum sk={sk} {rows}x{dim}: ranks disagree")
-    w = data(1, dim, 78, 60 + salt).view(dim)
-    res0 = data(rows, dim, 98, 60 + salt)
-    res_ref = res0.clone()
-    y_ref = ops.rms_norm(s, w, 1e-5, residual=res_ref)
-    res = res0.clone()
-    y = car.all_reduce_rms_norm_(ops.Partial(slabs[rank].contiguous(), torch.empty(rows, dim, dtype=torch.bfloat16,
-                                                                                    device=dev)), w, 1e-5, res)
-    torch.cuda.synchronize()
-    if (res.float() - res_ref.float()).abs().max().item() > 1.6e-2 * max(1.0, res_ref.float().abs().max().item()):
-        fails.append(f"slab fused residual sk={sk} {rows}x{dim}")
-    err = (y.float() - y_ref.float()).abs().max().item()
-    if err > 1e-2 * max(1.0, y_ref.float().abs().max().item()):
-        fails.append(f"slab fused norm sk={sk} {rows}x{dim}: {err:.3e}")
+        want += data(64, 8192, r, 7).float()
+    want = want.to(torch.bfloat16)
+    for it in range(5):
+        buf.copy_(x)
+        g.replay()
+        torch.cuda.synchronize()
+        if not torch.equal(buf, want):
+            fails.append(f"{tag} graph replay {it}")
+            break
+    if car.error():
+        fails.append(f"{tag} device error word {car.error()}")
 
-# 3. graph capture / replay
-x = data(64, 8192, rank, 7)
-buf = x.clone()
-s = torch.cuda.Stream()
-s.wait_stream(torch.cuda.current_stream())
-with torch.cuda.stream(s):
-    car.all_reduce_(buf)         # warm-up on the capture stream
-torch.cuda.current_stream().wait_stream(s)
-g = torch.cuda.CUDAGraph()
-with torch.cuda.graph(g):
-    car.all_reduce_(buf)
-want = torch.zeros(64, 8192, device=dev)
-for r in range(world):
-    want += data(64, 8192, r, 7).float()
-want = want.to(torch.bfloat16)
-for it in range(5):
-    buf.copy_(x)
-    g.replay()
-    torch.cuda.synchronize()
-    if not torch.equal(buf, want):
-        fails.append(f"graph replay {it}")
-        break
-if car.error():
-    fails.append(f"device error word {car.error()}")
+# BFLY_CAR_PLAIN_ONE_SHOT=1: skip the fused one-shot checks. With 8 ranks sharing ONE GPU the
+# register-heavy fused one-shot kernel (8 peer vectors in flight per thread) does not fit
+# 8 x 128 co-resident workgroups, so the spinning ranks starve the unscheduled ones; one rank
+# per GPU (the real layout) runs 128 workgroups on 256 CUs.
+plain_one = os.environ.get("BFLY_CAR_PLAIN_ONE_SHOT") == "1"
+for tag, two_bytes in [("one-shot", 0)] + ([("two-shot", 1)] if world >= 4 else []):
+    car.two_shot_bytes = two_bytes   # 1: every message that splits into whole 16-B column chunks
+    car.clear_error()
+    checks(tag, fused=not (plain_one and two_bytes == 0))
 
 # 4. timing (kernel alone, back-to-back)
 if "--bench" in sys.argv:
-    for rows in (1, 16, 64, 128, 256):
-        t = data(rows, 8192, rank, 3)
-        for _ in range(10):
-            car.all_reduce_(t)
-        torch.cuda.synchronize()
-        dist.barrier()
-        n = 200
-        t0 = time.perf_counter()
-        for _ in range(n):
-            car.all_reduce_(t)
-        torch.cuda.synchronize()
-        us = (time.perf_counter() - t0) / n * 1e6
-        if rank == 0:
-            print(f"custom all-reduce world={world} rows={rows} dim=8192 ({rows * 16} KiB): {us:.1f} us/call", flush=True)
+    for two in ([False, True] if world >= 4 else [False]):
+        for rows in (1, 16, 64, 128, 256, 512):
+            t = data(rows, 8192, rank, 3)
+            for _ in range(10):
+                car.all_reduce_(t, two_shot=two)
+            torch.cuda.synchronize()
+            dist.barrier()
+            n = 200
+            t0 = time.perf_counter()
+            for _ in range(n):
+                car.all_reduce_(t, two_shot=two)
+            torch.cuda.synchronize()
+            us = (time.perf_counter() - t0) / n * 1e6
+            if rank == 0:
+                print(f"custom all-reduce {'two' if two else 'one'}-shot world={world} rows={rows} dim=8192 "
+                      f"({rows * 16} KiB): {us:.1f} us/call", flush=True)
 
 car.close()
 print(f"rank {rank}: custom all-reduce world={world} -> {'PASS' if not fails else 'FAIL ' + '; '.join(fails)}", flush=True)
