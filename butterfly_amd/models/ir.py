@@ -25,7 +25,8 @@ class OpSpec:
     kind: str                      # gemm | attn | norm | rope | act | route | collective | embed
     n: int = 0                     # gemm: output columns (local)
     k: int = 0                     # gemm: reduction dim (local)
-    m_scale: int = 1               # gemm rows = tokens * m_scale (EP gathers ep x tokens)
+    m_scale: int = 1               # gemm rows = tokens * m_scale (routed MoE: top-k slots per token)
+    groups: int = 1                # grouped gemm: the rows split over `groups` weight matrices
     params: tuple = ()             # (logical name, local shape) read by this op
     collective: Optional[str] = None   # all_reduce | all_gather | reduce_scatter
     group: Optional[str] = None        # tp | ep
@@ -43,7 +44,7 @@ class OpSpec:
 
     def flops(self, tokens: int) -> float:
         if self.kind == "gemm":
-            return 2.0 * tokens * self.m_scale * self.n * self.k
+            return 2.0 * tokens * self.m_scale * self.n * self.k     # groups share the rows
         return 0.0
 
     def act_bytes(self, tokens: int, dtype_bytes: int = 2) -> float:
@@ -129,13 +130,23 @@ def build_ir(cfg: ModelConfig, tp: int = 1, ep: int = 1) -> ModelIR:
             f = cfg.intermediate_size // (tp if ep == 1 else 1)
             ops.append(OpSpec("router", "route", params=((L + "moe.router.weight", (cfg.num_experts, h)),), width=h))
             if ep > 1:
-                ops.append(OpSpec("ep_dispatch", "collective", collective="all_gather", group="ep", width=h))
-            ops.append(OpSpec("experts_gate_up", "gemm", n=2 * f * e_l, k=h, m_scale=ep,
-                              params=((L + "moe.experts.gate_up", (e_l, 2 * f, h)),)))
-            ops.append(OpSpec("experts_down", "gemm", n=h, k=f * e_l, m_scale=ep,
-                              params=((L + "moe.experts.down", (e_l, h, f)),)))
+                # fixed-capacity all-to-all dispatch; each rank then runs its experts on the
+                # rows routed to them only (on average tokens x top_k rows over e_l experts)
+                kt = cfg.experts_per_token
+                ops.append(OpSpec("ep_dispatch", "collective", collective="all_to_all", group="ep", width=h))
+                ops.append(OpSpec("experts_gate_up", "gemm", n=2 * f, k=h, m_scale=kt, groups=e_l,
+                                  params=((L + "moe.experts.gate_up", (e_l, 2 * f, h)),)))
+                ops.append(OpSpec("experts_down", "gemm", n=h, k=f, m_scale=kt, groups=e_l,
+                                  params=((L + "moe.experts.down", (e_l, h, f)),)))
+                ops.append(OpSpec("ep_combine", "collective", collective="all_to_all", group="ep", width=h))
+            else:
+                # decode without EP: every local expert on every row (dense, fixed shape)
+                ops.append(OpSpec("experts_gate_up", "gemm", n=2 * f * e_l, k=h,
+                                  params=((L + "moe.experts.gate_up", (e_l, 2 * f, h)),)))
+                ops.append(OpSpec("experts_down", "gemm", n=h, k=f * e_l,
+                                  params=((L + "moe.experts.down", (e_l, h, f)),)))
             if ep > 1:
-                ops.append(OpSpec("ep_combine", "collective", collective="reduce_scatter", group="ep", width=h))
+                pass
             elif tp > 1:
                 ops.append(OpSpec("mlp_allreduce", "collective", collective="all_reduce", group="tp", width=h))
         else:

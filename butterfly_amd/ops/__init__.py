@@ -11,6 +11,7 @@ captured steps never allocate.
 from __future__ import annotations
 
 import os
+import threading
 from pathlib import Path
 
 import torch
@@ -75,12 +76,19 @@ def _gpu(t: torch.Tensor) -> bool:
 # Workspace arena
 # ---------------------------------------------------------------------------------------
 class _Arena:
+    """Named scratch buffers reused by every kernel call (split-K slabs, decode-attention
+    partials, MoE slot maps and tile lists, sampling pairs). Buffers are shared by the threads
+    of a process (an engine built on one thread and stepped on another reuses them) unless a
+    thread sets its own scope (`arena_scope`): several ranks driven from threads of ONE process
+    (the loopback backend, parallel/fake.py) must never share e.g. a MoE tile list, or one
+    rank's moe_align would steer the other's grouped GEMM outside its own activations."""
+
     def __init__(self):
         self.bufs: dict[tuple, torch.Tensor] = {}
         self.frozen = False
 
     def get(self, device, name: str, numel: int, dtype, zero: bool = False) -> torch.Tensor:
-        key = (str(device), name, dtype)
+        key = (str(device), name, dtype, getattr(_scope, "name", None))
         buf = self.bufs.get(key)
         if buf is None or buf.numel() < numel:
             if self.frozen or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
@@ -92,7 +100,13 @@ class _Arena:
         return buf
 
 
+_scope = threading.local()
 _arena = _Arena()
+
+
+def arena_scope(name) -> None:
+    """Give this host thread its own workspace buffers (None: the process-wide set)."""
+    _scope.name = name
 
 
 def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch: int = 0,

@@ -7,8 +7,9 @@ ROCm (xGMI on MI355X), "gloo" for the CPU plumbing configuration and the control
 exposes the handful of collectives the rank programs need:
 
   all_reduce_   TP sum after row-parallel O / down projections (and vocab-parallel embed)
-  all_gather    TP sampling (score, id) pairs; EP token gather
-  reduce_scatter EP combine
+  all_gather    TP sampling (score, id) pairs
+  all_to_all    EP token dispatch / return (fixed capacity on decode, graph-capturable)
+  all_to_all_v  EP dispatch on prefill steps (variable sizes, host-exchanged splits)
   send / recv   PP stage boundary activations and token feedback
   broadcast_    control-plane metadata
 
@@ -198,6 +199,29 @@ class Communicator:
                                group=g.pg)
         self.stats["calls"] += 1
         return out.to(t.device), recv_splits
+
+    def all_to_all(self, t: torch.Tensor, group: str = "ep", out: torch.Tensor | None = None) -> torch.Tensor:
+        """Equal-split all-to-all along dim 0: block r of `t` (t.shape[0] / n rows) goes to group
+        rank r; block r of the result came from group rank r. Fixed shapes and no host sync,
+        so it is stream-ordered and hipGraph-capturable on RCCL (the EP decode dispatch)."""
+        g = self.groups[group]
+        if g.size == 1:
+            if out is not None:
+                out.copy_(t)
+                return out
+            return t
+        if out is None:
+            out = torch.empty_like(t)
+        self.stats["calls"] += 1
+        if self._nccl(g):
+            dist.all_to_all_single(out, t.contiguous(), group=g.pg)
+            return out
+        # gloo: host staging (CPU tensors pass straight through)
+        src = t.detach().cpu().contiguous()
+        dst = torch.empty_like(src)
+        dist.all_to_all_single(dst, src, group=g.pg)
+        out.copy_(dst)
+        return out
 
     def all_reduce_max_int(self, values: list, group: str = "world") -> list:
         """Host-side max of a few integers over a group (control plane, e.g. EP padding)."""

@@ -45,7 +45,7 @@ class FakeWorld:
         self.slots: dict = {}
         self.seq = defaultdict(int)                 # (group ranks, rank) -> next sequence no.
         self.queues = defaultdict(deque)            # (src, dst) -> deque of tensors
-        self.log: list = []                         # (rank, op, group, shape) in issue order
+        self.log: list = []                         # (rank, op, group, shape, bytes) in issue order
         self.comms = [FakeComm(self, r) for r in range(self.n)]
 
     # -- rendezvous ---------------------------------------------------------------------------
@@ -64,7 +64,7 @@ class FakeWorld:
                     raise CommOrderError(f"collective #{seq} of group {ranks}: rank {rank} issued {sig}, "
                                          f"rank {other} issued {osig}")
             slot.contrib[rank] = (sig, t.detach().clone())
-            self.log.append((rank, op, ranks, tuple(t.shape)))
+            self.log.append((rank, op, ranks, tuple(t.shape), t.numel() * t.element_size()))
             if len(slot.contrib) == slot.n:
                 slot.result = reduce([slot.contrib[r][1] for r in ranks])
                 self.cv.notify_all()
@@ -80,7 +80,7 @@ class FakeWorld:
     def send(self, src: int, dst: int, t: torch.Tensor) -> None:
         with self.cv:
             self.queues[(src, dst)].append(t.detach().clone())
-            self.log.append((src, "send", (src, dst), tuple(t.shape)))
+            self.log.append((src, "send", (src, dst), tuple(t.shape), t.numel() * t.element_size()))
             self.cv.notify_all()
 
     def recv(self, src: int, dst: int, like: torch.Tensor) -> torch.Tensor:
@@ -99,6 +99,9 @@ class FakeWorld:
         errors: list = []
 
         def body(r):
+            from .. import ops
+
+            ops.arena_scope(("fake-rank", r))    # per-rank kernel workspaces (ops._Arena)
             try:
                 results[r] = fn(r, self.comms[r], *args)
             except BaseException as e:  # noqa: BLE001 — surfaced below
@@ -201,6 +204,22 @@ class FakeComm(Communicator):
             like = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype)
             parts.append(self.world.recv(g.ranks[r], self.rank, like))
         return torch.cat(parts, 0).to(t.device), recv_splits
+
+    def all_to_all(self, t, group="ep", out=None):
+        g = self.groups[group]
+        if g.size == 1:
+            if out is not None:
+                out.copy_(t)
+                return out
+            return t
+        me, n = g.rank_in_group, g.size
+        self.stats["calls"] += 1
+        allx = self._coll(group, "all_to_all", t.contiguous(), lambda xs: torch.stack(xs))
+        res = torch.cat([allx[r].chunk(n, 0)[me] for r in range(n)], 0)
+        if out is None:
+            return res.clone()
+        out.copy_(res)
+        return out
 
     def all_reduce_max_int(self, values, group="world"):
         g = self.groups[group]

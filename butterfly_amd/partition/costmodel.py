@@ -124,6 +124,17 @@ class CostModel:
         bus = min(hw.rccl_bus_bw, (n - 1) * link)
         return hw.collective_latency_s + 2.0 * (n - 1) / n * nbytes / bus
 
+    def all_to_all(self, nbytes: float, n: int) -> float:
+        """Equal-split all-to-all of `nbytes` per rank over `n` ranks: every peer block on its
+        own xGMI link (measured table from the probe when available)."""
+        if n <= 1:
+            return 0.0
+        tab = (self.hw.comm or {}).get("all_to_all") or {}
+        pts = tab.get(n) or tab.get(str(n))
+        if pts:
+            return interp_loglog(pts, nbytes)
+        return self.hw.collective_latency_s + nbytes / n / self.hw.xgmi_link_eff_bw
+
     def p2p(self, nbytes: float) -> float:
         pts = (self.hw.comm or {}).get("p2p")
         if pts:
@@ -144,6 +155,9 @@ class CostModel:
         """Seconds for one IR op on one rank (collectives priced against xGMI)."""
         hw, c = self.hw, self.cfg
         if op.kind == "gemm":
+            if op.groups > 1:     # one grouped launch: each group streams its own weights
+                per = self.gemm(max(1, tokens * op.m_scale // op.groups), op.n, op.k) - hw.kernel_overhead_s
+                return op.groups * per + hw.kernel_overhead_s
             return self.gemm(tokens * op.m_scale, op.n, op.k)
         if op.kind == "attn":
             D = c.head_dim
@@ -161,6 +175,8 @@ class CostModel:
             if op.collective == "all_reduce":
                 return self.allreduce(nbytes, tp)
             g = tp if op.group == "tp" else max(2, self._cur_ep)
+            if op.collective == "all_to_all":
+                return self.all_to_all(nbytes * g, g)     # `tokens` rows reserved per destination
             return hw.collective_latency_s + (g - 1) * nbytes / hw.xgmi_link_eff_bw
         # memory-bound elementwise / norm / rope / routing ops
         byts = op.act_bytes(tokens) + 2.0 * op.param_elems

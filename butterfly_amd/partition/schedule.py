@@ -6,8 +6,8 @@ step (one request group of `tokens` sequences): compute blocks (stage layer rang
 communication instructions between them, with group, peer and payload. It is the program the
 engine runs — `engine/engine.py:_run_stages` / `_pipe_stage` (recv residual stream -> stage
 -> isend, or sample + broadcast ids) and `models/transformer.py` (vocab-parallel embedding
-all-reduce, two TP all-reduces per layer, EP all-gather / reduce-scatter, vocab-parallel
-sampling all-gather) — written down ahead of time so that it can be
+all-reduce, two TP all-reduces per layer, EP fixed-capacity all-to-all dispatch and return,
+vocab-parallel sampling all-gather) — written down ahead of time so that it can be
 
   * checked for cross-rank consistency without running anything (`check_programs`: every
     group collective is issued by all members in the same order with the same payload, every
@@ -40,7 +40,7 @@ BF16 = 2
 
 @dataclass(frozen=True)
 class Instr:
-    op: str                      # compute | all_reduce | all_gather | reduce_scatter | send | recv | broadcast
+    op: str                      # compute | all_reduce | all_gather | reduce_scatter | all_to_all | send | recv | broadcast
     group: tuple = ()            # global ranks taking part (send/recv: (src, dst))
     nbytes: int = 0              # payload this rank contributes (all_gather: its own slice)
     stream: str = "compute"      # compute | comm
@@ -76,7 +76,8 @@ class RankProgram:
         return "\n".join(lines)
 
 
-def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int = 1) -> RankProgram:
+def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int = 1,
+                 dtype_bytes: int = BF16) -> RankProgram:
     """The decode-step program of `rank` for `tokens` sequences. With the asynchronous pipeline
     (default) a step is one tick carrying one request group (`tokens` = the group's size, one
     microbatch); the synchronous pipeline (engine._pipeline_decode) cuts the step's batch into
@@ -87,14 +88,15 @@ def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int 
     M = max(1, min(microbatches, tokens))
     bounds = [tokens * i // M for i in range(M + 1)]
     for m in range(M):
-        _microbatch(plan, rank, bounds[m + 1] - bounds[m], prog.instrs.append, ep_sync=(m == 0))
+        _microbatch(plan, rank, bounds[m + 1] - bounds[m], prog.instrs.append, ep_sync=(m == 0),
+                    dtype_bytes=dtype_bytes)
     if plan.mesh.pp > 1:
         prog.instrs.append(Instr("broadcast", tuple(plan.mesh.pp_group(rank)), tokens * 4, "comm",
                                  "sampled ids from the last stage"))
     return prog
 
 
-def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool) -> None:
+def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool, dtype_bytes: int = BF16) -> None:
     cfg: ModelConfig = plan.model
     mesh = plan.mesh
     c = mesh.coord(rank)
@@ -103,7 +105,7 @@ def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool)
     a, b = plan.stages[c.pp]
     first, last = c.pp == 0, c.pp == pp - 1
     h = cfg.hidden_size
-    act = tokens * h * BF16
+    act = tokens * h * dtype_bytes
     R = tokens
     moe = cfg.is_moe
     ep_g = tuple(next(g for g in mesh.all_groups("ep") if rank in g)) if ep > 1 else ()
@@ -121,18 +123,21 @@ def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool)
         if tp > 1:
             add(Instr("all_reduce", tp_g, act, "compute", f"layer {layer} attention output (+ add, RMSNorm)"))
         if moe and ep > 1:
-            add(Instr("compute", note=f"layer {layer}: router"))
-            add(Instr("all_gather", ep_g, act, "compute", f"layer {layer} EP: token rows"))
-            add(Instr("all_gather", ep_g, tokens * cfg.num_experts * 4, "compute",
-                      f"layer {layer} EP: router gates (f32)"))
-            add(Instr("compute", note=f"layer {layer}: local experts on all EP ranks' rows"))
-            add(Instr("reduce_scatter", ep_g, act * ep, "compute", f"layer {layer} EP: expert outputs"))
+            # fixed-capacity dispatch (models/transformer.py _moe_alltoall_fixed): `tokens`
+            # rows reserved per destination, expert ids + gate weights (f32) alongside
+            k = cfg.experts_per_token
+            add(Instr("compute", note=f"layer {layer}: router, pack rows per destination rank"))
+            add(Instr("all_to_all", ep_g, ep * act, "compute", f"layer {layer} EP: token rows to expert owners"))
+            add(Instr("all_to_all", ep_g, ep * tokens * 2 * k * 4, "compute",
+                      f"layer {layer} EP: expert ids + gate weights"))
+            add(Instr("compute", note=f"layer {layer}: local experts on routed rows only"))
+            add(Instr("all_to_all", ep_g, ep * act, "compute", f"layer {layer} EP: weighted expert outputs back"))
         else:
             add(Instr("compute", note=f"layer {layer}: " + ("router + experts" if moe else "gate/up, SiLU, down")))
             if tp > 1:
                 # fused with the next layer's add+RMSNorm; after a stage's last layer it is a
                 # plain all-reduce (last stage: only the sampled rows are reduced)
-                nb = R * h * BF16 if (last and layer == b - 1) else act
+                nb = R * h * dtype_bytes if (last and layer == b - 1) else act
                 add(Instr("all_reduce", tp_g, nb, "compute", f"layer {layer} FFN output"))
     if last:
         add(Instr("compute", note="final norm, LM head (vocab shard), sampling"))
@@ -184,6 +189,11 @@ def link_bytes(plan: PartitionPlan, progs: dict) -> dict:
             n = len(i.group)
             if i.op == "send":
                 put(i.group[0], i.group[1], i.nbytes)
+            elif i.op == "all_to_all" and n > 1:
+                me = i.group.index(r)
+                for j, peer in enumerate(i.group):      # direct: block j to member j
+                    if j != me:
+                        put(r, peer, i.nbytes / n)
             elif i.op in ("all_reduce", "all_gather", "reduce_scatter", "broadcast") and n > 1:
                 nxt = i.group[(i.group.index(r) + 1) % n]
                 if i.op == "all_reduce":
@@ -203,6 +213,7 @@ def link_bytes(plan: PartitionPlan, progs: dict) -> dict:
     return out
 
 
-def programs(plan: PartitionPlan, tokens: int, microbatches: int = 1) -> dict:
-    """rank_program for every rank (each DP replica decodes `tokens` sequences)."""
-    return {r: rank_program(plan, r, tokens, microbatches) for r in range(plan.n_gpus)}
+def programs(plan: PartitionPlan, tokens: int, microbatches: int = 1, dtype_bytes: int = BF16) -> dict:
+    """rank_program for every rank (each DP replica decodes `tokens` sequences); activations
+    are `dtype_bytes` wide (bf16 on the GPU, fp32 on the CPU reference path)."""
+    return {r: rank_program(plan, r, tokens, microbatches, dtype_bytes) for r in range(plan.n_gpus)}

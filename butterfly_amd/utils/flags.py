@@ -44,6 +44,8 @@ define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside t
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
 define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped expert GEMMs instead of the dense path")
+define("BFLY_EP_DECODE_A2A", True, _bool, "EP MoE on decode (and idle) steps: fixed-capacity all-to-all dispatch with "
+       "routed-rows-only expert GEMMs, graph-capturable (0: all-gather + dense local experts + reduce-scatter)")
 define("BFLY_EP_ALLTOALL", True, _bool, "EP MoE on prefill steps: dispatch tokens by all-to-all (else all-gather / reduce-scatter)")
 define("BFLY_PP_ASYNC", True, _bool, "pipeline parallelism: keep pp decode groups in flight across steps "
        "(one group per stage per tick, no fill/drain bubble) instead of per-step microbatching")

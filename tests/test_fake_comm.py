@@ -30,7 +30,7 @@ def test_fake_world_matches_single(preset, kw):
     ref = _gen(preset, Mesh(), None, PROMPTS)
     outs = world.run(lambda r, c: _gen(preset, mesh, c, PROMPTS))
     assert all(o == ref for o in outs)
-    ops = {op for _, op, _, _ in world.log}
+    ops = {op for _, op, _, _, _ in world.log}
     assert ("all_reduce" in ops) == (mesh.tp > 1) and ("send" in ops) == (mesh.pp > 1)
 
 

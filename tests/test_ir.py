@@ -32,7 +32,13 @@ def test_ir_moe_ep_ops():
     layer = build_ir(c, 1, ep=8).layers[0]
     names = [o.name for o in layer.ops]
     assert names.index("ep_dispatch") < names.index("experts_gate_up") < names.index("ep_combine")
-    assert layer.op("experts_gate_up").m_scale == 8
+    # routed decode: top-k slot rows per token, split over the local experts (grouped GEMM),
+    # dispatched and returned by all-to-all
+    g = layer.op("experts_gate_up")
+    assert g.m_scale == c.experts_per_token and g.groups == 1 and g.n == 2 * c.intermediate_size
+    assert [o.collective for o in layer.ops if o.kind == "collective"] == ["all_to_all", "all_to_all"]
+    l2 = build_ir(c, 1, ep=2).layers[0]
+    assert l2.op("experts_down").groups == 4
 
 
 def test_costmodel_decode_is_weight_bound_at_small_batch():
