@@ -424,10 +424,9 @@ class TransformerLM:
             if self.ep > 1 and fb.ep_alltoall and flags.get("BFLY_EP_ALLTOALL"):
                 return self._moe_alltoall(pre, x, topk_ids, topk_w), False
             if self.ep > 1 and flags.get("BFLY_EP_DECODE_A2A"):
-                if not fb.is_prefill:
-                    # graph-bucket padding rows (no cache slot) route nowhere
-                    topk_ids = topk_ids.masked_fill((fb.slots < 0).unsqueeze(1), -1)
-                return self._moe_alltoall_fixed(pre, x, topk_ids, topk_w, max(fb.ep_tokens, T)), False
+                # decode: graph-bucket padding rows (no cache slot) route nowhere
+                return self._moe_alltoall_fixed(pre, x, topk_ids, topk_w, max(fb.ep_tokens, T),
+                                                None if fb.is_prefill else fb.slots), False
             if self.ep > 1:
                 # DP-attention + expert-parallel FFN: every EP rank contributes Tp rows (zero
                 # padded), each computes its local experts on all ranks' tokens, and the
@@ -494,46 +493,30 @@ class TransformerLM:
         return out.to(x.dtype)
 
     def _moe_alltoall_fixed(self, pre: str, x: torch.Tensor, topk_ids: torch.Tensor,
-                            topk_w: torch.Tensor, cap: int) -> torch.Tensor:
+                            topk_w: torch.Tensor, cap: int, slots: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Expert-parallel MoE over a FIXED-capacity all-to-all (decode; SURVEY.md §2.7-B B2,
         §3.2 (5)). Every EP rank reserves `cap` rows (the EP-agreed padded token count) per
         destination: a token goes once to each rank owning one of its top-k experts, at the
         position given by a running count over the tokens bound there, so no capacity can
         overflow and no token is dropped. Shapes are static and nothing waits on the host,
-        so the layer replays inside the decode hipGraph. The receiver computes ONLY routed
-        rows (moe_align + grouped GEMMs skip padding, whose expert ids are -1); a second
-        all-to-all brings each rank's weighted partial sums back, summed in f32 at the source.
+        so the layer replays inside the decode hipGraph. Packing (ep_pack_kernel: positions,
+        row copies, metadata) and the return combine (ep_combine_kernel) are one kernel each.
+        The receiver computes ONLY routed rows (moe_align + grouped GEMMs skip padding, whose
+        expert ids are -1); a second all-to-all brings each rank's weighted partial sums
+        back, summed in f32 at the source.
         Link bytes equal the all-gather they replace; the MFMA work drops from ep x T rows
         of every local expert to the rows actually routed to it."""
         d = self.dims
-        T, H = x.shape
         k = topk_ids.shape[1]
         El, ep = d.experts, self.ep
-        dev = x.device
-        ids = topk_ids.long()
-        dest = torch.where(ids >= 0, torch.div(ids.clamp(min=0), El, rounding_mode="floor"), ep)   # [T, k]
-        hit = torch.zeros(T, ep + 1, dtype=torch.int32, device=dev)
-        hit.scatter_(1, dest, 1)
-        hit = hit[:, :ep]                                                   # [T, ep] 0/1
-        pos = torch.cumsum(hit, 0) - 1
-        base = torch.arange(ep, device=dev) * cap
-        trash = ep * cap
-        slot = torch.where(hit > 0, base + pos, trash).view(-1)            # [T * ep]
-        send = x.new_zeros(trash + 1, H)
-        send.index_copy_(0, slot, x.unsqueeze(1).expand(T, ep, H).reshape(T * ep, H))
-        # per destination: the expert ids that live there (others -1) and their gate weights
-        owner = dest.unsqueeze(1) == torch.arange(ep, device=dev).view(1, ep, 1)     # [T, ep, k]
-        mids = torch.where(owner, ids.unsqueeze(1).float(), -1.0)
-        mw = torch.where(owner, topk_w.float().unsqueeze(1), 0.0)
-        meta = torch.full((trash + 1, 2 * k), -1.0, dtype=torch.float32, device=dev)
-        meta.index_copy_(0, slot, torch.cat([mids, mw], 2).view(T * ep, 2 * k))
-        xr = self.comm.all_to_all(send[:trash], "ep")
-        mr = self.comm.all_to_all(meta[:trash], "ep")
-        yr = ops.moe_sparse_ffn(xr, mr[:, :k].round().to(torch.int32).contiguous(), mr[:, k:].contiguous(),
-                                self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"], d.expert0, El, d.ffn)
-        back = torch.cat([self.comm.all_to_all(yr, "ep"), yr.new_zeros(1, H)])
-        out = back.index_select(0, slot).view(T, ep, H).float().sum(1)
-        return out.to(x.dtype)
+        send, meta, slot = ops.ep_pack(x, topk_ids, topk_w, slots, El, ep, cap)
+        xr = self.comm.all_to_all(send, "ep")
+        mr = self.comm.all_to_all(meta, "ep")
+        ids_r = mr[:, :k].contiguous().view(torch.int32)     # int32 bits travel in the f32 block
+        yr = ops.moe_sparse_ffn(xr, ids_r, mr[:, k:].contiguous(),
+                                self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"], d.expert0, El, d.ffn,
+                                expected_slots=cap * k)     # on average T x k routed slots per rank
+        return ops.ep_combine(self.comm.all_to_all(yr, "ep"), slot)
 
     # ------------------------------------------------------------------------------------
     # KV cache layout helpers

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import os
 import threading
+from typing import Optional
 from pathlib import Path
 
 import torch
@@ -363,7 +364,8 @@ def moe_route(x, wr, top_k: int, gates=None, topk_ids=None, topk_w=None):
     return gates, topk_ids, topk_w
 
 
-def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, ffn: int):
+def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, ffn: int,
+                   expected_slots: Optional[int] = None):
     """Routed expert FFN: permute the (token, k) pairs of the local experts into per-expert
     row slots (moe_align), grouped gate/up GEMM with fused SiLU over gathered token rows,
     grouped down GEMM, weighted combine back to token order. Only routed rows are computed
@@ -377,19 +379,68 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
         return torch.zeros(T, H, dtype=x.dtype, device=x.device)
     L = torch.ops.bfly
     dev = x.device
+    # tile rows from the expected rows per expert (all slots are local in the EP dispatch):
+    # one 128-row tile reads each expert's weights once where two 64-row tiles would twice
+    # `expected_slots`: (token, k) pairs expected to be local (the EP dispatch pads with
+    # non-local / empty slots; they cost nothing but must not size the launch)
+    exp = TK if expected_slots is None else max(1, min(TK, expected_slots))
+    bm = 128 if exp >= 96 * num_local else 64
     rows = _arena.get(dev, "moe_rows", TK, torch.int32)[:TK]
     slot_of = _arena.get(dev, "moe_slot", TK, torch.int32)[:TK]
-    nt = L.moe_max_tiles(TK, num_local)
+    nt = L.moe_max_tiles(TK, num_local, bm)
     tiles = _arena.get(dev, "moe_tiles", nt * 4, torch.int32)[:nt * 4].view(nt, 4)
     count = _arena.get(dev, "moe_count", 1, torch.int32)[:1]
-    L.moe_align(topk_ids, e0, num_local, rows, slot_of, tiles, count)
+    L.moe_align(topk_ids, e0, num_local, rows, slot_of, tiles, count, bm)
     hmid = torch.empty(TK, ffn, dtype=x.dtype, device=dev)
-    L.moe_grouped_gemm(x, gu_w, hmid, rows, tiles, count, 2 * ffn * H, 2 * ffn, H, num_local, EPILOGUES["silu"])
-    y = torch.empty(TK, H, dtype=x.dtype, device=dev)
-    L.moe_grouped_gemm(hmid, down_w, y, None, tiles, count, ffn, H, ffn, num_local, EPILOGUES["none"])
+    L.moe_grouped_gemm(x, gu_w, hmid, rows, tiles, count, 2 * ffn * H, 2 * ffn, H, num_local, EPILOGUES["silu"], bm)
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    sk = moe_down_splits(exp, num_local, H, ffn, bm)
+    if sk > 1:
+        # decode-sized expert batches: split K of the down projection over sk workgroups so the
+        # chip fills; the slab reduce is folded into the weighted combine
+        part = _arena.get(dev, "moe_part", sk * TK * H, torch.float32)[: sk * TK * H].view(sk, TK, H)
+        L.moe_grouped_gemm(hmid, down_w, hmid.new_empty(TK, H), None, tiles, count, ffn, H, ffn, num_local,
+                           EPILOGUES["none"], bm, part)
+        L.moe_combine_slabs(part, slot_of, topk_w, out)
+        return out
+    y = torch.empty(TK, H, dtype=x.dtype, device=dev)
+    L.moe_grouped_gemm(hmid, down_w, y, None, tiles, count, ffn, H, ffn, num_local, EPILOGUES["none"], bm)
     L.moe_combine(y, slot_of, topk_w, out)
     return out
+
+
+def ep_pack(x, ids, w, slots, experts_per_rank: int, ep: int, cap: int):
+    """Pack a fixed-capacity EP dispatch (see ops.reference.ep_pack for the layout)."""
+    if not _gpu(x):
+        return ref.ep_pack(x, ids, w, slots, experts_per_rank, ep, cap)
+    T, H = x.shape
+    k = ids.shape[1]
+    send = torch.empty(ep * cap, H, dtype=x.dtype, device=x.device)
+    meta = torch.empty(ep * cap, 2 * k, dtype=torch.float32, device=x.device)
+    slot = torch.empty(T, ep, dtype=torch.int32, device=x.device)
+    torch.ops.bfly.ep_pack(x.contiguous(), ids.contiguous(), w.contiguous(), slots, experts_per_rank, ep, cap,
+                           send, meta, slot)
+    return send, meta, slot
+
+
+def ep_combine(back, slot):
+    """Sum each token's returned partial outputs (one per rank it was sent to)."""
+    if not _gpu(back):
+        return ref.ep_combine(back, slot)
+    out = torch.empty(slot.shape[0], back.shape[1], dtype=back.dtype, device=back.device)
+    torch.ops.bfly.ep_combine(back, slot, out)
+    return out
+
+
+def moe_down_splits(TK: int, num_local: int, H: int, ffn: int, bm: int, cus: int = 256) -> int:
+    """Split-K factor of the grouped down projection: enough workgroups for ~2 per CU, with
+    at least 16 K-tiles (1024 columns) per split."""
+    tiles = -(-TK // bm) + (num_local if TK >= num_local else 0)
+    wgs = max(1, tiles) * (H // 128)
+    sk = 1
+    while wgs * sk * 2 <= 2 * cus and (ffn // 64) // (sk * 2) >= 16 and sk < 8:
+        sk *= 2
+    return sk
 
 
 def moe_gate_scale_(h, gates, e0: int, num_local: int):

@@ -341,3 +341,44 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
         y = linear(h, down_w[:, el * ffn:(el + 1) * ffn].contiguous())
         out[tok] += w_e.unsqueeze(-1).float() * y.float()
     return out.to(x.dtype)
+
+
+def ep_pack(x, ids, w, slots, experts_per_rank: int, ep: int, cap: int):
+    """Fixed-capacity EP dispatch (reference of ep_pack_kernel): token t goes once to every
+    rank d owning one of its experts, at row d * cap + (number of earlier tokens bound for d).
+    Returns send [ep*cap, H], meta [ep*cap, 2k] f32 (expert ids local to the row's rank as
+    int32 bits, -1 otherwise; gate weights), slot [T, ep] int32 (-1: not sent)."""
+    T, H = x.shape
+    k = ids.shape[1]
+    idl = ids.long()
+    if slots is not None:
+        idl = idl.masked_fill((slots < 0).unsqueeze(1), -1)
+    dest = torch.where(idl >= 0, torch.div(idl.clamp(min=0), experts_per_rank, rounding_mode="floor"), ep)
+    hit = torch.zeros(T, ep + 1, dtype=torch.int64)
+    if T:
+        hit.scatter_(1, dest, 1)
+    hit = hit[:, :ep]
+    pos = torch.cumsum(hit, 0) - hit
+    slot = torch.where(hit > 0, torch.arange(ep) * cap + pos, -1)
+    send = torch.zeros(ep * cap, H, dtype=x.dtype)
+    mid = torch.full((ep * cap, k), -1, dtype=torch.int32)
+    mw = torch.zeros(ep * cap, k, dtype=torch.float32)
+    for t in range(T):
+        for d in range(ep):
+            r = int(slot[t, d])
+            if r < 0:
+                continue
+            send[r] = x[t]
+            mine = dest[t] == d
+            mid[r] = torch.where(mine, idl[t], -1).to(torch.int32)
+            mw[r] = torch.where(mine, w[t].float(), 0.0)
+    meta = torch.cat([mid.view(torch.float32), mw], 1)
+    return send, meta, slot.to(torch.int32)
+
+
+def ep_combine(back, slot):
+    """out[t] = sum of back[slot[t, d]] over the ranks d token t was sent to (f32 sum)."""
+    T, ep = slot.shape
+    ext = torch.cat([back.float(), back.new_zeros(1, back.shape[1]).float()])
+    idx = torch.where(slot >= 0, slot.long(), back.shape[0])
+    return ext.index_select(0, idx.view(-1)).view(T, ep, -1).sum(1).to(back.dtype)

@@ -457,20 +457,21 @@ void moe_route(const Tensor& x, const Tensor& wr, int64_t top_k, Tensor& gates, 
   TORCH_CHECK(rc == 0, "moe_route: unsupported (E <= 64, k <= 8, H % 8 == 0)");
 }
 
-int64_t moe_max_tiles(int64_t TK, int64_t El) { return bfly::moe_max_tiles(TK, El, bfly::kMoeGroupBM); }
+int64_t moe_max_tiles(int64_t TK, int64_t El, int64_t bm) { return bfly::moe_max_tiles(TK, El, (int)bm); }
 
 void moe_align(const Tensor& topk_ids, int64_t e0, int64_t num_local, Tensor& rows, Tensor& slot_of,
-               Tensor& tiles, Tensor& count) {
+               Tensor& tiles, Tensor& count, int64_t bm) {
+  TORCH_CHECK(bm == 64 || bm == 128, "moe_align: tile rows 64 or 128");
   CHECK_GPU(topk_ids); CHECK_I32(topk_ids); CHECK_I32(rows); CHECK_I32(slot_of); CHECK_I32(tiles); CHECK_I32(count);
   TORCH_CHECK(topk_ids.dim() == 2 && topk_ids.is_contiguous(), "moe_align: topk_ids [T, k]");
   const int T = topk_ids.size(0), K = topk_ids.size(1);
   TORCH_CHECK(num_local > 0 && num_local <= 64, "moe_align: 1..64 local experts");
   TORCH_CHECK(rows.numel() >= (long)T * K && slot_of.numel() == (long)T * K, "moe_align: rows / slot_of size");
   TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 4 && tiles.is_contiguous() &&
-                  tiles.size(0) >= bfly::moe_max_tiles(T * K, num_local, bfly::kMoeGroupBM), "moe_align: tiles [max_tiles, 4]");
+                  tiles.size(0) >= bfly::moe_max_tiles(T * K, num_local, (int)bm), "moe_align: tiles [max_tiles, 4]");
   TORCH_CHECK(count.numel() == 1, "moe_align: count");
   c10::DeviceGuard g(topk_ids.device());
-  const int rc = bfly::launch_moe_align(topk_ids.data_ptr<int>(), T, K, e0, num_local, bfly::kMoeGroupBM,
+  const int rc = bfly::launch_moe_align(topk_ids.data_ptr<int>(), T, K, e0, num_local, (int)bm,
                                         rows.data_ptr<int>(), slot_of.data_ptr<int>(),
                                         reinterpret_cast<int4*>(tiles.data_ptr<int>()), count.data_ptr<int>(), cur_stream());
   TORCH_CHECK(rc == 0, "moe_align: rejected (", rc, ")");
@@ -478,7 +479,7 @@ void moe_align(const Tensor& topk_ids, int64_t e0, int64_t num_local, Tensor& ro
 
 void moe_grouped_gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& rows,
                       const Tensor& tiles, const Tensor& count, int64_t w_estride, int64_t n, int64_t k,
-                      int64_t num_experts, int64_t epilogue) {
+                      int64_t num_experts, int64_t epilogue, int64_t bm, const c10::optional<Tensor>& part) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_I32(tiles); CHECK_I32(count);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) >= k, "moe_grouped_gemm: x");
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0, "moe_grouped_gemm: w");
@@ -497,10 +498,21 @@ void moe_grouped_gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::
     TORCH_CHECK(x.size(0) >= out.size(0), "moe_grouped_gemm: slot rows");
   }
   TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 4, "moe_grouped_gemm: tiles");
+  int sk = 1;
+  float* pp = nullptr;
+  if (part.has_value()) {   // split-K: f32 slabs [sk][slots][n], reduced by moe_combine_slabs
+    const Tensor& pt = *part;
+    CHECK_GPU(pt);
+    TORCH_CHECK(pt.scalar_type() == at::kFloat && pt.dim() == 3 && pt.is_contiguous() && pt.size(1) == out.size(0) &&
+                    pt.size(2) == n && epilogue == bfly::EPI_NONE, "moe_grouped_gemm: part [sk, slots, n] f32");
+    sk = (int)pt.size(0);
+    pp = pt.data_ptr<float>();
+  }
   c10::DeviceGuard g(x.device());
   const int rc = bfly::launch_gemm_grouped(bf(x), x.stride(0), bf(w), ldw, w_estride, n, k, epilogue, rp,
                                            reinterpret_cast<const int4*>(tiles.data_ptr<int>()), count.data_ptr<int>(),
-                                           tiles.size(0), bf(out), out.stride(0), cur_stream());
+                                           tiles.size(0), bf(out), out.stride(0), cur_stream(), (int)bm,
+                                           (int)out.size(0), sk, pp);
   TORCH_CHECK(rc == 0, "moe_grouped_gemm: rejected (", rc, ")");
 }
 
@@ -514,6 +526,57 @@ void moe_combine(const Tensor& y, const Tensor& slot_of, const Tensor& topk_w, T
   const int rc = bfly::launch_moe_combine(bf(y), slot_of.data_ptr<int>(), topk_w.data_ptr<float>(), T, K, H, bf(out),
                                           cur_stream());
   TORCH_CHECK(rc == 0, "moe_combine: H % 8");
+}
+
+void moe_combine_slabs(const Tensor& part, const Tensor& slot_of, const Tensor& topk_w, Tensor& out) {
+  CHECK_GPU(part); CHECK_I32(slot_of); CHECK_BF16(out);
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.dim() == 3 && part.is_contiguous(), "moe_combine_slabs: part");
+  TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.dim() == 2 && topk_w.is_contiguous(), "moe_combine_slabs: topk_w");
+  const int T = topk_w.size(0), K = topk_w.size(1), H = out.size(1);
+  TORCH_CHECK(slot_of.numel() == (long)T * K && out.size(0) == T && out.is_contiguous() && part.size(2) == H &&
+                  part.size(1) >= (long)T * K, "moe_combine_slabs: shapes");
+  c10::DeviceGuard g(part.device());
+  const int rc = bfly::launch_moe_combine_slabs(part.data_ptr<float>(), (int)part.size(0), part.size(1) * (long)H,
+                                                slot_of.data_ptr<int>(), topk_w.data_ptr<float>(), T, K, H, bf(out),
+                                                cur_stream());
+  TORCH_CHECK(rc == 0, "moe_combine_slabs: H % 4");
+}
+
+void ep_pack(const Tensor& x, const Tensor& ids, const Tensor& w, const c10::optional<Tensor>& slots,
+             int64_t experts_per_rank, int64_t ep, int64_t cap, Tensor& send, Tensor& meta, Tensor& slot) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_I32(ids); CHECK_BF16(send); CHECK_I32(slot);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "ep_pack: x [T, H] contiguous");
+  const int T = x.size(0), H = x.size(1);
+  TORCH_CHECK(ids.dim() == 2 && ids.size(0) == T && ids.is_contiguous(), "ep_pack: ids [T, k]");
+  const int K = ids.size(1);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == (long)T * K, "ep_pack: w [T, k] f32");
+  TORCH_CHECK(cap >= T && send.is_contiguous() && send.size(0) == ep * cap && send.size(1) == H, "ep_pack: send [ep*cap, H]");
+  TORCH_CHECK(meta.scalar_type() == at::kFloat && meta.is_contiguous() && meta.size(0) == ep * cap &&
+                  meta.size(1) == 2 * K, "ep_pack: meta [ep*cap, 2k] f32");
+  TORCH_CHECK(slot.is_contiguous() && slot.numel() == (long)T * ep, "ep_pack: slot [T, ep]");
+  const int* sp = nullptr;
+  if (slots.has_value()) {
+    CHECK_I32(*slots);
+    TORCH_CHECK(slots->numel() == T, "ep_pack: slots [T]");
+    sp = slots->data_ptr<int>();
+  }
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_ep_pack(bf(x), ids.data_ptr<int>(), w.data_ptr<float>(), sp, T, K, H,
+                                      (int)experts_per_rank, (int)ep, (int)cap, bf(send), meta.data_ptr<float>(),
+                                      slot.data_ptr<int>(), cur_stream());
+  TORCH_CHECK(rc == 0, "ep_pack: rejected (", rc, ")");
+}
+
+void ep_combine(const Tensor& back, const Tensor& slot, Tensor& out) {
+  CHECK_GPU(back); CHECK_BF16(back); CHECK_I32(slot); CHECK_BF16(out);
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && back.is_contiguous() && back.size(1) == out.size(1),
+              "ep_combine: shapes");
+  const int T = out.size(0);
+  TORCH_CHECK(T == 0 || slot.numel() % T == 0, "ep_combine: slot [T, ep]");
+  const int ep = T ? (int)(slot.numel() / T) : 2;
+  c10::DeviceGuard g(back.device());
+  const int rc = bfly::launch_ep_combine(bf(back), slot.data_ptr<int>(), T, out.size(1), ep, bf(out), cur_stream());
+  TORCH_CHECK(rc == 0, "ep_combine: rejected (", rc, ")");
 }
 
 void moe_gate_scale(Tensor& h, const Tensor& gates, int64_t e0, int64_t num_local) {
@@ -648,12 +711,16 @@ TORCH_LIBRARY(bfly, m) {
         "Tensor(c!)? part_ml, Tensor(d!)? counters=None) -> ()");
   m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
-  m.def("moe_max_tiles(int tk, int num_local) -> int", &moe_max_tiles);
+  m.def("moe_max_tiles(int tk, int num_local, int bm=64) -> int", &moe_max_tiles);
   m.def("moe_align(Tensor topk_ids, int e0, int num_local, Tensor(a!) rows, Tensor(b!) slot_of, Tensor(c!) tiles, "
-        "Tensor(d!) count) -> ()");
+        "Tensor(d!) count, int bm=64) -> ()");
   m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? rows, Tensor tiles, Tensor count, int w_estride, "
-        "int n, int k, int num_experts, int epilogue) -> ()");
+        "int n, int k, int num_experts, int epilogue, int bm=64, Tensor(b!)? part=None) -> ()");
   m.def("moe_combine(Tensor y, Tensor slot_of, Tensor topk_w, Tensor(a!) out) -> ()");
+  m.def("moe_combine_slabs(Tensor part, Tensor slot_of, Tensor topk_w, Tensor(a!) out) -> ()");
+  m.def("ep_pack(Tensor x, Tensor ids, Tensor w, Tensor? slots, int experts_per_rank, int ep, int cap, "
+        "Tensor(a!) send, Tensor(b!) meta, Tensor(c!) slot) -> ()");
+  m.def("ep_combine(Tensor back, Tensor slot, Tensor(a!) out) -> ()");
   m.def("probe(int which, Tensor(a!) out) -> ()");
   m.def("car_alloc(int bytes) -> int", &car_alloc);
   m.def("car_free(int ptr) -> ()", &car_free);
@@ -696,4 +763,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_grouped_gemm", &moe_grouped_gemm);
   m.impl("moe_combine", &moe_combine);
+  m.impl("moe_combine_slabs", &moe_combine_slabs);
+  m.impl("ep_pack", &ep_pack);
+  m.impl("ep_combine", &ep_combine);
 }

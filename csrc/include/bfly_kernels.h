@@ -129,7 +129,13 @@ int launch_moe_combine(const bf16* y, const int* slot_of, const float* w, int T,
 constexpr int kMoeGroupBM = 64;
 int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w_estride, int N,
                         int K, int epi, const int* rows, const int4* tiles, const int* count,
-                        int max_tiles, bf16* out, long ldo, hipStream_t stream);
+                        int max_tiles, bf16* out, long ldo, hipStream_t stream, int bm = 64,
+                        int slots = 0, int sk = 1, float* part = nullptr);
+int launch_ep_pack(const bf16* x, const int* ids, const float* w, const int* slots, int T, int K, int H,
+                   int El, int ep, int cap, bf16* send, float* meta, int* slot, hipStream_t stream);
+int launch_ep_combine(const bf16* back, const int* slot, int T, int H, int ep, bf16* out, hipStream_t stream);
+int launch_moe_combine_slabs(const float* part, int sk, long slab, const int* slot_of, const float* w,
+                             int T, int K, int H, bf16* out, hipStream_t stream);
 
 // probe.hip
 void launch_probe(int which, float* out, hipStream_t stream);

@@ -343,12 +343,15 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
   int tile, m0, n0;
+  const int m_slab = M;             // split-K slab row stride (grouped: all row slots)
+  bool single = false;              // grouped: this expert has one row tile (W read once)
   if constexpr (GROUPED) {
     if ((int)blockIdx.x >= *gcount) return;
     const int4 info = gtiles[blockIdx.x];
     W += (long)info.x * w_estride;
     m0 = info.y;
     M = info.z;                     // rows [m0, M) of the permuted slot space
+    single = info.w != 0;
     n0 = blockIdx.z * BN;
     tile = 0;
   } else {
@@ -362,7 +365,8 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   const int ktiles = K / kBK;
   const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
   const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
-  const bool w_nt = !GROUPED && M <= BM && g_tile_w_nt;   // each W byte read by one workgroup
+  // each W byte read by one workgroup: stream it non-temporally
+  const bool w_nt = (GROUPED ? single : M <= BM) && g_tile_w_nt;
 
   f32x4 acc[TI][TJ];
 #pragma unroll
@@ -423,7 +427,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
         const int n = n0 + wn * WN + 16 * j + (lane & 15);
         const float v = acc[i][j][r];
         if (part) {
-          part[(long)blockIdx.y * M * N + (long)m * N + n] = v;
+          part[(long)blockIdx.y * m_slab * N + (long)m * N + n] = v;
         } else if (epi == EPI_SILU) {
           if (j & 1) continue;
           const float u = acc[i][j + 1][r];
@@ -1038,15 +1042,18 @@ static GemmPlan select_plan(int M, int N, int K, int epi) {
   return p;
 }
 
-// Grouped expert GEMM (MoE): fixed 64x128 tile, 3-stage pipeline; grid = (max tiles, 1,
-// N / 128) with the device tile list deciding which workgroups run.
-constexpr int kGroupBM = 64;
-int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w_estride, int N,
-                        int K, int epi, const int* rows, const int4* tiles, const int* count,
-                        int max_tiles, bf16* out, long ldo, hipStream_t stream) {
-  if (N % 128 != 0 || K % kBK != 0 || max_tiles <= 0) return -1;
-  if (epi != EPI_NONE && epi != EPI_SILU) return -1;
-  constexpr int BM = kGroupBM, BN = 128, WMW = 2, ST = 3;
+// Grouped expert GEMM (MoE): BM x 128 tile (BM = 64 or 128 rows per expert tile, chosen by
+// the caller from the expected rows per expert), 3-stage pipeline; grid = (max tiles, sk,
+// N / 128) with the device tile list deciding which workgroups run. sk > 1 splits K and
+// writes f32 slabs part[sk][slots][N] (consumed by moe_combine_slabs: the split-K reduce is
+// fused into the weighted combine) — decode-sized expert batches otherwise leave most CUs
+// idle on the down projection (N = hidden: 32 column tiles per expert tile).
+template <int BM>
+static int launch_grouped_bm(const bf16* X, long ldx, const bf16* W, long ldw, long w_estride, int N,
+                             int K, int epi, const int* rows, const int4* tiles, const int* count,
+                             int max_tiles, int slots, int sk, float* part, bf16* out, long ldo,
+                             hipStream_t stream) {
+  constexpr int BN = 128, WMW = 2, ST = 3;
   const size_t lds = (size_t)ST * (BM + BN) * kBK * 2;
   static bool attr_set = false;
   if (!attr_set && lds > 65536) {
@@ -1054,10 +1061,27 @@ int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  dim3 grid(max_tiles, 1, N / BN);
+  dim3 grid(max_tiles, sk, N / BN);
   gemm_tile_kernel<BM, BN, WMW, ST, true><<<grid, kTileThreads, lds, stream>>>(
-      X, ldx, W, ldw, 0, N, K, epi, nullptr, out, ldo, nullptr, nullptr, rows, tiles, count, w_estride);
+      X, ldx, W, ldw, slots, N, K, epi, nullptr, out, ldo, sk > 1 ? part : nullptr, nullptr, rows,
+      tiles, count, w_estride);
   return 0;
+}
+
+int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w_estride, int N,
+                        int K, int epi, const int* rows, const int4* tiles, const int* count,
+                        int max_tiles, bf16* out, long ldo, hipStream_t stream, int bm, int slots,
+                        int sk, float* part) {
+  if (N % 128 != 0 || K % kBK != 0 || max_tiles <= 0) return -1;
+  if (epi != EPI_NONE && epi != EPI_SILU) return -1;
+  if (sk < 1 || sk > K / kBK || (sk > 1 && (part == nullptr || epi != EPI_NONE || slots <= 0))) return -2;
+  if (bm == 128)
+    return launch_grouped_bm<128>(X, ldx, W, ldw, w_estride, N, K, epi, rows, tiles, count, max_tiles,
+                                  slots, sk, part, out, ldo, stream);
+  if (bm == 64)
+    return launch_grouped_bm<64>(X, ldx, W, ldw, w_estride, N, K, epi, rows, tiles, count, max_tiles,
+                                 slots, sk, part, out, ldo, stream);
+  return -3;
 }
 
 int gemm_check(int M, int N, int K, int epi) {

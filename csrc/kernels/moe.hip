@@ -135,7 +135,9 @@ moe_align_kernel(const int* __restrict__ topk_ids, int TK, int K, int e0, int El
     int off = 0, nt = 0;
     for (int e = 0; e < El; ++e) {
       cur[e] = off;
-      for (int r = off; r < off + cnt[e]; r += BM) tiles[nt++] = int4{e, r, min(r + BM, off + cnt[e]), 0};
+      // .w = 1: the expert's rows fit one tile, so its weights are read exactly once
+      for (int r = off; r < off + cnt[e]; r += BM)
+        tiles[nt++] = int4{e, r, min(r + BM, off + cnt[e]), cnt[e] <= BM ? 1 : 0};
       off += cnt[e];
     }
     *count = nt;
@@ -171,6 +173,167 @@ moe_combine_kernel(const bf16* __restrict__ y, const int* __restrict__ slot_of,
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
     *reinterpret_cast<bf16x8*>(out + t * H + c) = o;
+  }
+}
+
+// out[t] = sum_j w[t, j] * sum_s part[s][slot_of[t, j]]: the weighted combine with the
+// grouped down GEMM's split-K reduce folded in (f32 throughout, one bf16 rounding)
+__global__ void __launch_bounds__(256)
+moe_combine_slabs_kernel(const float* __restrict__ part, int sk, long slab, const int* __restrict__ slot_of,
+                         const float* __restrict__ w, int K, int H, bf16* __restrict__ out) {
+  const long t = blockIdx.x;
+  for (int c = threadIdx.x * 4; c < H; c += 256 * 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < K; ++j) {
+      const int sl = slot_of[t * K + j];
+      if (sl < 0) continue;
+      const float g = w[t * K + j];
+      f32x4 y = *reinterpret_cast<const f32x4*>(part + (long)sl * H + c);
+      for (int s = 1; s < sk; ++s) y += *reinterpret_cast<const f32x4*>(part + s * slab + (long)sl * H + c);
+      acc += g * y;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[t * H + c + q] = f2bf(acc[q]);
+  }
+}
+
+int launch_moe_combine_slabs(const float* part, int sk, long slab, const int* slot_of, const float* w,
+                             int T, int K, int H, bf16* out, hipStream_t stream) {
+  if (H % 4 != 0 || sk < 1) return -1;
+  if (T <= 0) return 0;
+  moe_combine_slabs_kernel<<<T, 256, 0, stream>>>(part, sk, slab, slot_of, w, K, H, out);
+  return 0;
+}
+
+// ---- expert-parallel dispatch over a fixed-capacity all-to-all (decode) ----------------
+// Token t goes once to every EP rank d owning one of its top-k experts (El experts per rank),
+// into row d * cap + pos[t][d], pos = number of earlier tokens bound for d (a stable order,
+// so no capacity can overflow: cap >= T). Every workgroup recomputes the prefix counts it
+// needs from the (tiny) id array instead of a separate scan kernel.
+template <int EP>
+__device__ __forceinline__ void ep_hits(const int* ids, int t, int K, int El, const int* slots, bool (&h)[EP]) {
+#pragma unroll
+  for (int d = 0; d < EP; ++d) h[d] = false;
+  if (slots != nullptr && slots[t] < 0) return;   // graph padding row: routes nowhere
+  for (int j = 0; j < K; ++j) {
+    const int e = ids[t * K + j];
+    if (e >= 0) {
+      const int d = e / El;
+#pragma unroll
+      for (int q = 0; q < EP; ++q) h[q] |= (q == d);
+    }
+  }
+}
+
+// grid = cap workgroups (cap >= T). Block b: (1) counts, over tokens t' < b and over all
+// tokens, the hits per destination; (2) if b < T, copies row b to each destination it hits
+// and writes that row's metadata (expert ids local to d as int32 bits, gate weights; other
+// slots -1 / 0) and slot[b][d] (-1: not sent); (3) for every destination whose total count
+// is <= b, marks metadata row d * cap + b empty (all ids -1).
+template <int EP>
+__global__ void __launch_bounds__(256)
+ep_pack_kernel(const bf16* __restrict__ x, const int* __restrict__ ids, const float* __restrict__ w,
+               const int* __restrict__ slots, int T, int K, int H, int El, int cap,
+               bf16* __restrict__ send, float* __restrict__ meta, int* __restrict__ slot) {
+  __shared__ int red[2][EP][4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int before[EP], total[EP];
+#pragma unroll
+  for (int d = 0; d < EP; ++d) before[d] = total[d] = 0;
+  for (int t = tid; t < T; t += 256) {
+    bool h[EP];
+    ep_hits<EP>(ids, t, K, El, slots, h);
+#pragma unroll
+    for (int d = 0; d < EP; ++d) {
+      total[d] += h[d];
+      before[d] += (h[d] && t < b);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < EP; ++d) {
+    const float tb = wave_sum((float)before[d]), tt = wave_sum((float)total[d]);
+    if (lane == 0) { red[0][d][wv] = (int)tb; red[1][d][wv] = (int)tt; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int d = 0; d < EP; ++d) {
+    before[d] = red[0][d][0] + red[0][d][1] + red[0][d][2] + red[0][d][3];
+    total[d] = red[1][d][0] + red[1][d][1] + red[1][d][2] + red[1][d][3];
+  }
+  const int M2 = 2 * K;
+  if (b < T) {
+    bool h[EP];
+    ep_hits<EP>(ids, b, K, El, slots, h);
+#pragma unroll
+    for (int d = 0; d < EP; ++d) {
+      if (tid == 0) slot[b * EP + d] = h[d] ? d * cap + before[d] : -1;
+      if (!h[d]) continue;
+      const long row = (long)d * cap + before[d];
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(x + (long)b * H);
+      bf16x8* dst = reinterpret_cast<bf16x8*>(send + row * H);
+      for (int c = tid; c < H / 8; c += 256) dst[c] = src[c];
+      if (tid < K) {
+        const int e = ids[b * K + tid];
+        const bool mine = e >= 0 && e / El == d;
+        meta[row * M2 + tid] = __int_as_float(mine ? e : -1);
+        meta[row * M2 + K + tid] = mine ? w[b * K + tid] : 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < EP; ++d) {
+    if (b >= total[d] && tid < K) {
+      const long row = (long)d * cap + b;
+      meta[row * M2 + tid] = __int_as_float(-1);
+      meta[row * M2 + K + tid] = 0.f;
+    }
+  }
+}
+
+// out[t] = sum over destinations d that t was sent to of back[slot[t][d]] (f32, fixed d order)
+template <int EP>
+__global__ void __launch_bounds__(256)
+ep_combine_kernel(const bf16* __restrict__ back, const int* __restrict__ slot, int H, bf16* __restrict__ out) {
+  const long t = blockIdx.x;
+  int sl[EP];
+#pragma unroll
+  for (int d = 0; d < EP; ++d) sl[d] = slot[t * EP + d];
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < EP; ++d) {
+      if (sl[d] < 0) continue;
+      const bf16x8 v = reinterpret_cast<const bf16x8*>(back + (long)sl[d] * H)[c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += bf2f(v[q]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
+    reinterpret_cast<bf16x8*>(out + t * H)[c] = o;
+  }
+}
+
+int launch_ep_pack(const bf16* x, const int* ids, const float* w, const int* slots, int T, int K, int H,
+                   int El, int ep, int cap, bf16* send, float* meta, int* slot, hipStream_t stream) {
+  if (H % 8 != 0 || K > 64 || cap < T || cap <= 0 || El <= 0) return -1;
+  const dim3 grid(cap);
+  switch (ep) {
+    case 2: ep_pack_kernel<2><<<grid, 256, 0, stream>>>(x, ids, w, slots, T, K, H, El, cap, send, meta, slot); return 0;
+    case 4: ep_pack_kernel<4><<<grid, 256, 0, stream>>>(x, ids, w, slots, T, K, H, El, cap, send, meta, slot); return 0;
+    case 8: ep_pack_kernel<8><<<grid, 256, 0, stream>>>(x, ids, w, slots, T, K, H, El, cap, send, meta, slot); return 0;
+    default: return -2;
+  }
+}
+
+int launch_ep_combine(const bf16* back, const int* slot, int T, int H, int ep, bf16* out, hipStream_t stream) {
+  if (H % 8 != 0) return -1;
+  if (T <= 0) return 0;
+  switch (ep) {
+    case 2: ep_combine_kernel<2><<<T, 256, 0, stream>>>(back, slot, H, out); return 0;
+    case 4: ep_combine_kernel<4><<<T, 256, 0, stream>>>(back, slot, H, out); return 0;
+    case 8: ep_combine_kernel<8><<<T, 256, 0, stream>>>(back, slot, H, out); return 0;
+    default: return -2;
   }
 }
 

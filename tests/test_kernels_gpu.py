@@ -377,6 +377,33 @@ def test_moe_sparse_ffn(T, E, El, e0, k, H, F):
     _close(got, dense, 3e-2, 3e-2)
 
 
+@pytest.mark.parametrize("T,El,e0,H,F,pad,expect", [(64, 1, 3, 1024, 4096, 0, None),     # bm 128, split-K
+                                                    (200, 2, 2, 512, 2048, 0, None),     # bm 128, 2 experts
+                                                    (512, 1, 5, 1024, 4096, 384, 256),   # EP dispatch padding
+                                                    (96, 4, 0, 512, 4096, 0, None)])     # bm 64, split-K
+def test_moe_sparse_ffn_decode_shapes(T, El, e0, H, F, pad, expect):
+    """Decode-sized routed expert batches: 128-row expert tiles (weights read once, non-temporal),
+    the split-K grouped down projection whose f32 slabs are reduced inside the weighted combine
+    (moe_combine_slabs), and EP-dispatch padding rows (expert ids -1) that must cost and change
+    nothing — all against the fp32 reference."""
+    E, k = 8, 2
+    x = _bf(T, H, seed=90)
+    wr = _bf(E, H, seed=91)
+    _, ids, w = ops.moe_route(x, wr, k)
+    if pad:
+        ids[T - pad:] = -1            # padding slots of the fixed-capacity dispatch
+    gu = _bf(El * 2 * F, H, scale=1.0 / math.sqrt(H), seed=92)
+    dn = _bf(H, El * F, scale=1.0 / math.sqrt(F), seed=93)
+    exp = expect if expect is not None else T * k
+    bm = 128 if exp >= 96 * El else 64
+    assert ops.moe_down_splits(exp, El, H, F, bm) > 1
+    got = ops.moe_sparse_ffn(x, ids, w, gu, dn, e0, El, F, expected_slots=expect)
+    want = ref.moe_sparse_ffn(x.cpu().float(), ids.cpu(), w.cpu(), gu.cpu().float(), dn.cpu().float(), e0, El, F)
+    _close(got, want, 3e-2, 3e-2)
+    if pad:
+        assert got[T - pad:].abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_attn_prefill_lse_and_key_offsets(causal):
     """K3 with LSE output, and (non-causal) keys taken from other rows than the queries — the
@@ -467,3 +494,29 @@ def test_rope_kv_and_kv_append_fp8_cache():
     ops.kv_append(kk, vv, slots, kc2, vc2)
     assert torch.equal(kc2.view(torch.uint8), kc.view(torch.uint8))
     assert torch.equal(vc2.view(torch.uint8), vc.view(torch.uint8))
+
+
+@pytest.mark.parametrize("T,cap,ep,El,with_slots", [(64, 64, 8, 1, False), (37, 48, 4, 2, True), (5, 8, 2, 4, True)])
+def test_ep_pack_and_combine(T, cap, ep, El, with_slots):
+    """Fixed-capacity EP dispatch packing (ep_pack_kernel) equals the reference layout exactly
+    (row positions, copied rows, int32-bit expert ids, weights, empty metadata rows), and the
+    return combine sums each token's returned rows."""
+    E, k, H = ep * El, 2, 256
+    x = _bf(T, H, seed=95)
+    wr = _bf(E, H, seed=96)
+    _, ids, w = ops.moe_route(x, wr, k)
+    slots = None
+    if with_slots:
+        slots = torch.arange(T, dtype=torch.int32, device=DEV)
+        slots[::3] = -1                     # graph padding rows: route nowhere
+    send, meta, slot = ops.ep_pack(x, ids, w, slots, El, ep, cap)
+    rs, rm, rslot = ref.ep_pack(x.cpu(), ids.cpu(), w.cpu(), None if slots is None else slots.cpu(), El, ep, cap)
+    assert torch.equal(slot.cpu(), rslot)
+    sent = rslot[rslot >= 0].long()
+    assert torch.equal(send.cpu()[sent], rs[sent])
+    assert torch.equal(meta.cpu().view(torch.int32)[:, :k], rm.view(torch.int32)[:, :k])
+    assert torch.equal(meta.cpu()[:, k:], rm[:, k:])
+    back = _bf(ep * cap, H, seed=97)
+    got = ops.ep_combine(back, slot)
+    want = ref.ep_combine(back.cpu(), rslot)
+    _close(got, want, 1e-2, 1e-2)
