@@ -52,6 +52,9 @@ class Request:
     finish_time: Optional[float] = None
     finished: bool = False
     finish_reason: Optional[str] = None
+    n_gen: int = 0                # tokens generated, including ones whose value is still in flight
+    stopping: bool = False        # stop token seen while a plan holding the sequence is in flight
+    sched_done: bool = False      # released from the scheduler
 
     @property
     def tokens(self) -> list:
@@ -127,7 +130,9 @@ class LLMEngine:
                                               self.mixed, self.prefix_cache)
         self._tick = 0
         self._inflight: list = []        # PipePlans entered at ticks k-pp+1 .. k
-        self._pending: Optional[PipePlan] = None   # left the last stage; ids not yet applied
+        self._pending: Optional[PipePlan] = None   # left the last stage at the previous tick
+        self._valued: Optional[PipePlan] = None    # advanced; token values applied next tick
+        self._last_left: dict = {}                  # group -> its plan that left most recently
         self._sends: list = []
         d = self.model.dims
         self.sampler = Sampler(self.comm, cfg.vocab_size, d.vocab0, mesh.tp)
@@ -186,14 +191,15 @@ class LLMEngine:
         return rid
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.num_waiting + self.scheduler.num_running > 0
+        return (self.scheduler.num_waiting + self.scheduler.num_running > 0
+                or self._pending is not None or self._valued is not None)
 
     def _sample_params(self, rids):
         temps = [self.requests[r].params.temperature for r in rids]
         if all(t <= 0 for t in temps):
             return None, None, None
         tt = torch.tensor(temps, dtype=torch.float32, device=self.device)
-        seeds = torch.tensor([(self.requests[r].params.seed or r) * 1000003 + len(self.requests[r].output)
+        seeds = torch.tensor([(self.requests[r].params.seed or r) * 1000003 + self.requests[r].n_gen
                               for r in rids], dtype=torch.int64, device=self.device)
         return tt, seeds, [self.requests[r].params for r in rids]
 
@@ -303,6 +309,7 @@ class LLMEngine:
         for r, t in zip(rids, new):
             req = self.requests[r]
             req.output.append(int(t))
+            req.n_gen = len(req.output)
             if req.first_token_time is None:
                 req.first_token_time = now
             self.scheduler.on_token(r)
@@ -375,9 +382,13 @@ class LLMEngine:
     # ------------------------------------------------------------------------------------
     # asynchronous pipeline (engine/pipeline.py): one tick = every stage advances one group
     def _pp_tick(self, t0: float) -> StepOutput:
-        """Tick k: stage s runs the group that entered at tick k - s. Returns the tokens of the
-        group that left the last stage at tick k - 1 (applied now, right before that group is
-        scheduled again), or an empty 'pipeline' output while the pipe fills."""
+        """Tick k: stage s runs the group that entered at tick k - s. No host wait on this or
+        the previous tick's device work: the group that left the last stage at tick k - 1 is
+        ADVANCED now (value-free bookkeeping: lengths, length limits, KV slots — right before
+        that group is scheduled again) and its first-stage input ids are gathered on the
+        device from the broadcast ids; the token VALUES, copied to pinned host memory
+        asynchronously, are applied one tick later (they landed long ago). Returns the tokens
+        applied this tick, or an empty 'pipeline' output while the pipe fills."""
         pp, s = self.mesh.pp, self.coord.pp
         k = self._tick
         self._tick += 1
@@ -390,12 +401,18 @@ class LLMEngine:
         # their device work before blocking on the previous tick's ids (keeps the GPU fed)
         mine = next((p for p in self._inflight if p.tick == k - s), None)
         if s > 0 and mine is not None:
-            self._pp_stage_work(mine)
+            with trace.range("pp.stage_work", tick=k, stage=s):
+                self._pp_stage_work(mine)
         out = StepOutput("pipeline", [], [], [], 0.0)
-        if self._pending is not None:
+        if self._valued is not None:          # left at tick k - 2: values are on the host
+            v, self._valued = self._valued, None
+            out = self._apply_values(v, t0)
+            out.prefill_tokens = v.tokens if v.plan.kind == 1 else 0
+        if self._pending is not None:         # left at tick k - 1: advance, values next tick
             p, self._pending = self._pending, None
-            out = self._apply_tokens(p.kind, p.rids, p.ids.tolist(), t0)
-            out.prefill_tokens = p.tokens if p.plan.kind == 1 else 0
+            self._advance(p)
+            self._last_left[p.group] = p
+            self._valued = p
         # schedule the group entering stage 0 (every rank: replicated deterministic state)
         g = k % pp
         plan = self.scheduler.groups[g].schedule()
@@ -404,7 +421,8 @@ class LLMEngine:
             T = sum(plan.prefill_lens) if plan.kind == 1 else len(rids)
             self._inflight.append(PipePlan(k, g, plan, rids, T, list(plan.cow)))
             if s == 0:
-                self._pp_stage_work(self._inflight[-1])
+                with trace.range("pp.stage_work", tick=k, stage=0):
+                    self._pp_stage_work(self._inflight[-1])
         # the plan that entered pp-1 ticks ago leaves the last stage now: broadcast its ids
         leaving = next((p for p in self._inflight if p.tick == k - pp + 1), None)
         if leaving is not None:
@@ -412,9 +430,94 @@ class LLMEngine:
             if leaving.ids is None:
                 leaving.ids = torch.empty(len(leaving.rids), dtype=torch.int32, device=self.device)
             self.comm.broadcast_(leaving.ids, src_in_group=pp - 1, group="pp")
+            # stream-ordered copy to pinned host memory; read one tick later
+            if leaving.ids.is_cuda:
+                leaving.host = torch.empty(len(leaving.rids), dtype=torch.int32, pin_memory=True)
+                leaving.host.copy_(leaving.ids, non_blocking=True)
+                leaving.event = torch.cuda.Event()
+                leaving.event.record()
+            else:
+                leaving.host = leaving.ids
             self._pending = leaving
         out.seconds = time.perf_counter() - t0
         return out
+
+    def _advance(self, p: PipePlan) -> None:
+        """Value-free part of applying a plan that left the pipeline: one more token per
+        sequence (KV length, scheduler state), length-limit completion, and the deferred
+        release of sequences whose stop token was seen while this plan was in flight."""
+        for r in p.rids:
+            req = self.requests[r]
+            if req.sched_done:
+                continue
+            if req.stopping:                  # stopped earlier; this plan's token is discarded
+                req.stopping = False
+                req.sched_done = True
+                self.scheduler.finish(r)
+                continue
+            self.scheduler.on_token(r)
+            req.n_gen += 1
+            if req.n_gen >= req.params.max_tokens:
+                req.sched_done = True
+                self.scheduler.finish(r)
+
+    def _apply_values(self, p: PipePlan, t0: float) -> StepOutput:
+        """Token values of a plan advanced one tick ago: append them, detect stop tokens
+        (releasing the sequence now, or when the plan that still holds it leaves)."""
+        if p.event is not None:
+            with trace.range("pp.values_wait", tick=self._tick):
+                p.event.synchronize()         # recorded two ticks ago: normally long done
+        new = [int(t) for t in p.host.tolist()]
+        if any(t < 0 for t in new):
+            raise RuntimeError(f"rank {self.rank}: non-finite logits at engine step {self.steps_done}")
+        now = time.perf_counter()
+        rids, toks, finished = [], [], []
+        inflight = {r for q in self._inflight for r in q.rids}
+        if self._pending is not None:
+            inflight.update(self._pending.rids)
+        for r, t in zip(p.rids, new):
+            req = self.requests[r]
+            if req.finished:
+                continue                      # a token after the stop token: discarded
+            req.output.append(t)
+            rids.append(r)
+            toks.append(t)
+            if req.first_token_time is None:
+                req.first_token_time = now
+            stop = not req.params.ignore_eos and (t in req.params.stop_token_ids or
+                                                  (self.eos is not None and t == self.eos))
+            if stop or len(req.output) >= req.params.max_tokens:
+                req.finished, req.finish_time = True, now
+                req.finish_reason = "stop" if stop else "length"
+                finished.append(r)
+                if stop and not req.sched_done:
+                    if r in inflight:
+                        req.stopping = True   # released when that plan leaves (_advance)
+                    else:
+                        req.sched_done = True
+                        self.scheduler.finish(r)
+        dt = time.perf_counter() - t0
+        self.metrics.observe_step(p.kind, len(rids), dt)
+        return StepOutput(p.kind, rids, toks, finished, dt)
+
+    def _first_stage_ids(self, p: PipePlan):
+        """Input ids of a decode plan entering stage 0: the sequences' last tokens. Those
+        sampled by the group's previous plan (values not on the host yet) are gathered on the
+        device from its broadcast ids; older ones come from the host."""
+        src = self._last_left.get(p.group)
+        where = {r: i for i, r in enumerate(src.rids)} if src is not None and src is self._valued else {}
+        if not where or not any(r in where for r in p.rids):
+            return np.asarray([self.requests[r].tokens[-1] for r in p.rids], dtype=np.int32)
+        host = [0 if r in where else self.requests[r].tokens[-1] for r in p.rids]
+        rows = [i for i, r in enumerate(p.rids) if r in where]
+        idx = [where[p.rids[i]] for i in rows]
+        dev = src.ids.device
+        ids = torch.tensor(host, dtype=torch.int32).to(dev, non_blocking=True)
+        if len(rows) == len(p.rids):
+            return src.ids.index_select(0, torch.tensor(idx, dtype=torch.long).to(dev, non_blocking=True))
+        ids[torch.tensor(rows, dtype=torch.long).to(dev, non_blocking=True)] = \
+            src.ids.index_select(0, torch.tensor(idx, dtype=torch.long).to(dev, non_blocking=True))
+        return ids
 
     def _pp_stage_work(self, p: PipePlan) -> None:
         """recv the residual stream (stage > 0) -> run this stage -> isend (not last) or sample
@@ -428,7 +531,8 @@ class LLMEngine:
         if p.plan.kind == 1:
             out = self.runner.run(self.runner.prefill_batch(p.plan, lambda r: self.requests[r].tokens), h)
         else:
-            inp = self.runner.decode_inputs(p.plan, [self.requests[r].tokens[-1] for r in p.rids])
+            ids = self._first_stage_ids(p) if self.pp_first else np.zeros(len(p.rids), dtype=np.int32)
+            inp = self.runner.decode_inputs(p.plan, ids)
             out = self.runner.run_decode(inp, h)
         if not self.pp_last:
             snd = out.clone() if p.plan.kind == 2 else out   # graph outputs are reused by the next replay

@@ -19,6 +19,14 @@ import torch
 from .batch import ForwardBatch
 
 
+def _to_dev(a, dev) -> torch.Tensor:
+    """Host array (staged through numpy) or a tensor already on the device (e.g. input ids
+    gathered from the previous pipeline tick's broadcast) -> tensor on `dev`."""
+    if isinstance(a, torch.Tensor):
+        return a.to(dev, non_blocking=True)
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)
+
+
 class _DecodeGraph:
     def __init__(self, bucket: int, max_blocks: int, device, hidden: int, first: bool):
         i32 = dict(dtype=torch.int32, device=device)
@@ -129,14 +137,15 @@ class ModelRunner:
     def decode_inputs(self, plan, last_tokens: list) -> dict:
         B = len(plan.seq_ids)
         self.kv.manager.fill_decode_tables(list(plan.seq_ids), self._tables_host[:B], self._ctx_host[:B])
-        return dict(ids=np.asarray(last_tokens, dtype=np.int32),
+        ids = last_tokens if isinstance(last_tokens, torch.Tensor) else np.asarray(last_tokens, dtype=np.int32)
+        return dict(ids=ids,
                     pos=np.asarray(plan.decode_positions, dtype=np.int32),
                     slots=np.asarray(plan.decode_slots, dtype=np.int32),
                     tables=self._tables_host[:B], ctx=self._ctx_host[:B])
 
     def decode_batch(self, inp: dict, ep_tokens: int = 0) -> ForwardBatch:
         dev = self.device
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+        t = lambda a: _to_dev(a, dev)  # noqa: E731
         return ForwardBatch(input_ids=t(inp["ids"]), positions=t(inp["pos"]), slots=t(inp["slots"]),
                             is_prefill=False, block_tables=t(inp["tables"]), ctx_lens=t(inp["ctx"]),
                             max_ctx=self.max_seq_len, logits_idx=None, ep_tokens=ep_tokens)
@@ -178,7 +187,7 @@ class ModelRunner:
     def _stage(self, g: _DecodeGraph, inp: dict, hidden_in) -> None:
         B = len(inp["ids"])
         dev = self.device
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)  # noqa: E731
+        t = lambda a: _to_dev(a, dev)  # noqa: E731
         g.input_ids[:B].copy_(t(inp["ids"]))
         g.positions[:B].copy_(t(inp["pos"]))
         g.slots[:B].copy_(t(inp["slots"]))

@@ -13,8 +13,11 @@ its weights once per tick for one group, and one group's tokens leave the last s
 Determinism across ranks: every rank of the replica runs the same tick loop, schedules the
 entering group itself (the schedulers are replicated, as in the synchronous engine), receives
 the sampled ids of the group leaving the last stage by a broadcast over the pp group, and
-applies them to its scheduler at the start of the next tick — which is exactly when that group
-is scheduled again (it entered pp ticks earlier). A group's block tables, positions and tokens
+advances its scheduler by one token per sequence at the start of the next tick — exactly when
+that group is scheduled again (it entered pp ticks earlier). The token VALUES are not needed
+for that: stage 0 gathers the group's new input ids from the broadcast tensor on the device,
+and the host reads the values (copied asynchronously to pinned memory) one tick later, so no
+tick waits on the device (engine._pp_tick). A group's block tables, positions and tokens
 only change at its own scheduling / completion, so a plan made at tick k stays valid while
 stages 1..pp-1 process it at ticks k+1..k+pp-1.
 """
@@ -71,6 +74,8 @@ class PipePlan:
     tokens: int               # rows of the residual stream between stages
     cow: list = field(default_factory=list)
     ids: Optional[object] = None   # sampled ids tensor (last stage / after broadcast)
+    host: Optional[object] = None  # pinned host copy of `ids` (async D2H at broadcast time)
+    event: Optional[object] = None # marks that copy complete
 
     @property
     def kind(self) -> str:

@@ -66,6 +66,10 @@ class Tracer:
 
 
 TRACER = Tracer()
+if TRACER.enabled:
+    import atexit
+
+    atexit.register(TRACER.dump)     # BFLY_TRACE=path (may contain {rank}): written at exit
 
 
 @contextlib.contextmanager

@@ -60,12 +60,19 @@ def _mixed_generate(rank, world, preset, mesh_kw, max_batch, async_pp):
 
     from butterfly_amd.parallel.comm import Communicator
 
+    saved = os.environ.get("BFLY_PP_ASYNC")
     os.environ["BFLY_PP_ASYNC"] = "1" if async_pp else "0"
     mesh = Mesh(**mesh_kw)
     comm = Communicator.from_mesh(mesh) if world > 1 else None
     cfg = ModelConfig.from_preset(preset)
     ecfg = EngineConfig(max_batch=max_batch, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
-    eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")
+    try:
+        eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")   # reads the flag
+    finally:   # the single-process reference runs in the test process: do not leak the flag
+        if saved is None:
+            os.environ.pop("BFLY_PP_ASYNC", None)
+        else:
+            os.environ["BFLY_PP_ASYNC"] = saved
     rids = [eng.add_request(p, SamplingParams(max_tokens=3 + 2 * i, ignore_eos=True))
             for i, p in enumerate(PROMPTS + PROMPTS[:2])]
     for _ in range(5):
@@ -133,3 +140,35 @@ def test_comm_probe_plumbing_gloo():
     assert res[0][1][4]["ipc_max"] == 0            # no IPC kernel on CPU: RCCL-only policy
     cm = CostModel(ModelConfig.from_preset("llama3-8b"), MI355X.with_comm_table(dict(tabs[0], policy=res[0][1])))
     assert cm.allreduce(1 << 20, 4) > 0 and cm.p2p(1 << 20) > 0
+
+
+def _stop_generate(rank, world, stop_tok):
+    """Async pipeline with a stop token that fires while the stopped sequence's next plan is
+    already in flight (values are applied one tick late)."""
+    from butterfly_amd.parallel.comm import Communicator
+
+    mesh = Mesh(pp=2) if world > 1 else Mesh()
+    comm = Communicator.from_mesh(mesh) if world > 1 else None
+    cfg = ModelConfig.from_preset("llama-tiny")
+    ecfg = EngineConfig(max_batch=4, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")
+    params = [SamplingParams(max_tokens=12, stop_token_ids=[stop_tok]), SamplingParams(max_tokens=12)]
+    rids = [eng.add_request(p, params[i % 2]) for i, p in enumerate(PROMPTS)]
+    while eng.has_unfinished():
+        eng.step()
+    kv_free = eng.kv.manager.num_free
+    return [eng.requests[r].output for r in rids], [eng.requests[r].finish_reason for r in rids], kv_free
+
+
+def test_async_pipeline_stop_token_matches_single():
+    """Lagged token values (engine._pp_tick): a sequence that emits its stop token is cut at
+    exactly the same place as in a single-process run, the extra in-flight token is dropped,
+    and every KV block comes back."""
+    free_ref = _stop_generate(0, 1, 0)
+    # pick a stop token the first prompt actually produces mid-sequence
+    stop_tok = free_ref[0][0][4]
+    ref_out, ref_reason, ref_free = _stop_generate(0, 1, stop_tok)
+    outs = run_world(_stop_generate, 2, stop_tok)
+    assert ref_reason[0] == "stop"
+    for out, reason, free in outs:
+        assert out == ref_out and reason == ref_reason and free == ref_free
