@@ -176,8 +176,9 @@ def gumbel_uniform(seed: int, idx: torch.Tensor) -> torch.Tensor:
     return torch.tensor(out, dtype=torch.float32)
 
 
-def sample(logits, temps=None, seeds=None, vstart=0):
-    """Greedy (temp <= 0) or Gumbel-max temperature sampling; returns (ids int32, scores f32)."""
+def sample(logits, temps=None, seeds=None, vstart=0, thresh=None):
+    """Greedy (temp <= 0) or Gumbel-max temperature sampling; returns (ids int32, scores f32).
+    `thresh[r]`: tokens whose logit / temperature is below it are excluded (top-k / top-p)."""
     lf = logits.float()
     rows, V = lf.shape
     ids, scores = [], []
@@ -186,7 +187,9 @@ def sample(logits, temps=None, seeds=None, vstart=0):
         s = lf[r]
         if t > 0:
             u = gumbel_uniform(int(seeds[r]), torch.arange(vstart, vstart + V))
-            s = s / t - torch.log(-torch.log(u))
+            s = s * (1.0 / t)
+            keep = s >= float(thresh[r]) if thresh is not None else torch.ones_like(s, dtype=torch.bool)
+            s = torch.where(keep, s - torch.log(-torch.log(u)), torch.full_like(s, float("-inf")))
         i = int(torch.argmax(s))
         ids.append(i + vstart)
         scores.append(float(s[i]))

@@ -193,7 +193,7 @@ void embed(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) 
 
 void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
             const c10::optional<Tensor>& seeds, int64_t vstart, Tensor& out_ids,
-            Tensor& out_scores, Tensor& workspace) {
+            Tensor& out_scores, Tensor& workspace, const c10::optional<Tensor>& thresh) {
   CHECK_GPU(logits); CHECK_BF16(logits);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0, "sample: logits");
   CHECK_ALIGN16(logits);
@@ -213,10 +213,16 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
     TORCH_CHECK(seeds->scalar_type() == at::kLong && seeds->numel() == rows, "sample: seeds");
     sp = seeds->data_ptr<int64_t>();
   }
+  const float* thp = nullptr;
+  if (thresh.has_value()) {
+    TORCH_CHECK(thresh->scalar_type() == at::kFloat && thresh->numel() == rows && thresh->is_contiguous(),
+                "sample: thresh [rows] f32");
+    thp = thresh->data_ptr<float>();
+  }
   c10::DeviceGuard g(logits.device());
   bfly::launch_sample(bf(logits), logits.stride(0), rows, V, vstart, tp, sp,
                       reinterpret_cast<uint64_t*>(workspace.data_ptr()), out_ids.data_ptr<int>(),
-                      out_scores.data_ptr<float>(), cur_stream());
+                      out_scores.data_ptr<float>(), cur_stream(), thp);
 }
 
 int64_t gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
@@ -695,7 +701,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("init_hash(Tensor(a!) out, int grow0, int gcol0, int gcols, int seed, float amp) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vstart) -> ()");
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
-        "Tensor(b!) out_scores, Tensor(c!) workspace) -> ()");
+        "Tensor(b!) out_scores, Tensor(c!) workspace, Tensor? thresh=None) -> ()");
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace, "
         "Tensor? bias=None) -> ()");

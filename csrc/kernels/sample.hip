@@ -7,6 +7,11 @@
 // its score. With tensor parallelism the caller all-gathers (score, id) pairs and takes the
 // max: scores are comparable across ranks because the Gumbel noise is keyed on the GLOBAL
 // vocab index and the per-row seed, not on the rank.
+//
+// Top-k / top-p: `thresh[row]` (optional) is a lower bound on the temperature-scaled logit;
+// tokens below it are excluded before the Gumbel-max. Gumbel-max over the kept set samples
+// exactly the renormalised truncated distribution, so filtering reduces to one threshold per
+// row (computed from the global top candidates by the sampler, engine/sampler.py).
 #include "bfly_common.h"
 #include "bfly_kernels.h"
 
@@ -48,13 +53,15 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 __global__ void __launch_bounds__(kSampleThreads)
 sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, int chunk,
                       int vstart, const float* __restrict__ temps,
-                      const long* __restrict__ seeds, uint64_t* __restrict__ partial) {
+                      const long* __restrict__ seeds, const float* __restrict__ thresh,
+                      uint64_t* __restrict__ partial) {
   __shared__ uint64_t red[kSampleThreads / 64];
   const int row = blockIdx.x, c = blockIdx.y;
   const float temp = temps ? temps[row] : 0.f;
   const bool greedy = temp <= 0.f;
   const float inv_t = greedy ? 1.f : 1.f / temp;
   const uint64_t seed = seeds ? (uint64_t)seeds[row] : 0;
+  const float thr = (thresh != nullptr && !greedy) ? thresh[row] : -INFINITY;
   const int begin = c * chunk, end = min(V, begin + chunk);
   const bf16* lr = logits + (long)row * row_stride;
   uint64_t best = 0;
@@ -64,14 +71,22 @@ sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, i
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float s = bf2f(v[j]);
-        if (!greedy) s = s * inv_t - __logf(-__logf(uniform01(seed, (uint32_t)(vstart + i + j))));
+        if (!greedy) {
+          s = s * inv_t;
+          if (s < thr) continue;            // outside the top-k / top-p set
+          s -= __logf(-__logf(uniform01(seed, (uint32_t)(vstart + i + j))));
+        }
         const uint64_t key = ((uint64_t)ordered_f32(s) << 32) | (uint32_t)(~(uint32_t)(vstart + i + j));
         best = umax64(best, key);
       }
     } else {
       for (int j = 0; i + j < end; ++j) {
         float s = bf2f(lr[i + j]);
-        if (!greedy) s = s * inv_t - __logf(-__logf(uniform01(seed, (uint32_t)(vstart + i + j))));
+        if (!greedy) {
+          s = s * inv_t;
+          if (s < thr) continue;
+          s -= __logf(-__logf(uniform01(seed, (uint32_t)(vstart + i + j))));
+        }
         const uint64_t key = ((uint64_t)ordered_f32(s) << 32) | (uint32_t)(~(uint32_t)(vstart + i + j));
         best = umax64(best, key);
       }
@@ -101,7 +116,7 @@ __global__ void sample_final_kernel(const uint64_t* __restrict__ partial, int ch
 
 void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vstart,
                    const float* temps, const long* seeds, uint64_t* workspace, int* out_ids,
-                   float* out_scores, hipStream_t stream) {
+                   float* out_scores, hipStream_t stream, const float* thresh) {
   if (rows <= 0) return;
   int chunks = (V + 4095) / 4096;
   if (chunks > kSampleMaxChunks) chunks = kSampleMaxChunks;
@@ -110,7 +125,7 @@ void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vst
   chunks = (V + chunk - 1) / chunk;
   dim3 g1(rows, chunks);
   sample_partial_kernel<<<g1, kSampleThreads, 0, stream>>>(logits, row_stride, V, chunk, vstart,
-                                                           temps, seeds, workspace);
+                                                           temps, seeds, thresh, workspace);
   sample_final_kernel<<<rows, 64, 0, stream>>>(workspace, chunks, out_ids, out_scores);
 }
 

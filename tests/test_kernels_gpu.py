@@ -116,6 +116,31 @@ def test_sample_gumbel_matches_reference():
     assert ids.cpu().tolist() == ids_ref.tolist()
 
 
+def test_sample_topk_topp_on_device():
+    """Filtered sampling (top-k / top-p thresholds + the thresholded Gumbel kernel) on the GPU
+    picks exactly what the fp32 reference picks with the same thresholds, and every pick lies
+    in the exact truncated set."""
+    from butterfly_amd.engine.sampler import Sampler, SamplingParams
+
+    V = 4096
+    logits = _bf(4, V, scale=3.0, seed=17)
+    params = [SamplingParams(temperature=0.8, top_k=20), SamplingParams(temperature=1.0, top_p=0.4),
+              SamplingParams(temperature=0.6, top_k=50, top_p=0.7), SamplingParams(temperature=0.0)]
+    temps = torch.tensor([p.temperature for p in params], device=DEV)
+    seeds = torch.tensor([3, 5, 7, 9], dtype=torch.int64, device=DEV)
+    smp = Sampler(None, V, 0, 1)
+    thr = smp.thresholds(logits, temps, params)
+    ids, _ = ops.sample(logits, temps, seeds, vstart=0, thresh=thr)
+    ids_ref, _ = ref.sample(logits.cpu(), temps.cpu(), seeds.cpu(), vstart=0, thresh=thr.cpu())
+    assert ids.cpu().tolist() == ids_ref.tolist()
+    got = smp.sample(logits, temps, seeds, params)
+    assert torch.equal(got.cpu(), ids.cpu())
+    for r, p in enumerate(params[:3]):
+        s = logits[r].float() / p.temperature
+        assert s[int(ids[r])] >= thr[r]
+    assert int(ids[3]) == int(logits[3].float().argmax())
+
+
 GEMM_SHAPES = [
     (1, 256, 1024), (5, 1280, 8192), (16, 4096, 4096), (33, 512, 768), (64, 2048, 1024),
     (65, 256, 512), (128, 1024, 2048), (300, 384, 640), (1024, 1024, 1024), (7, 16128, 8192),

@@ -52,10 +52,12 @@ def record(engine, store, forced=None):
             full = engine.comm.all_gather(logits.t().contiguous(), "tp").t()
         full = full[:, : cfg.vocab_size].float().cpu()
         ids = orig(logits, rids)
+        # n_gen: tokens generated so far (the asynchronous pipeline applies VALUES a tick late,
+        # so len(output) lags; n_gen is the position being sampled)
         for i, r in enumerate(rids):
-            store[(r, len(engine.requests[r].output))] = full[i]
+            store[(r, engine.requests[r].n_gen)] = full[i]
         if forced is not None:
-            ids = torch.tensor([forced[r][len(engine.requests[r].output)] for r in rids], dtype=torch.int32,
+            ids = torch.tensor([forced[r][engine.requests[r].n_gen] for r in rids], dtype=torch.int32,
                                device=logits.device)
         return ids
     engine._sample = _sample
