@@ -96,25 +96,45 @@ def iter_hf_tensors(src: Path) -> Iterator[tuple[str, torch.Tensor]]:
 
 def convert_hf(src: str | Path, dst: str | Path, dtype: torch.dtype = torch.bfloat16,
                name: str = "hf") -> ModelConfig:
-    """Convert a HuggingFace model directory (config.json + *.safetensors) to butterfly-ckpt."""
+    """Convert a HuggingFace model directory (config.json + *.safetensors) to butterfly-ckpt.
+
+    Streams one HF shard at a time: each input file becomes one output file
+    (`hf-NNNNN.safetensors`), so peak host memory is one shard (~5 GB for the 70B release),
+    not the whole model (~141 GB). The manifest points every logical tensor at its file.
+    """
     src, dst = Path(src), Path(dst)
     hf_cfg = json.loads((src / "config.json").read_text())
     cfg = ModelConfig.from_hf(hf_cfg, name=name)
-    out: dict[str, torch.Tensor] = {}
-    for k, t in iter_hf_tensors(src):
-        it = _gpt2_map(k, t, cfg.hidden_size) if cfg.arch == "gpt2" else _llama_map(k, t)
-        for ln, tt in it:
-            out[ln] = tt.to(dtype).contiguous()
-    if cfg.tie_embeddings:
-        out.pop("lm_head.weight", None)
-    elif "lm_head.weight" not in out and "embed_tokens.weight" in out:
-        out["lm_head.weight"] = out["embed_tokens.weight"].clone()
+    files = sorted(src.glob("*.safetensors"))
+    if not files:
+        raise FileNotFoundError(f"no *.safetensors in {src}")
     dst.mkdir(parents=True, exist_ok=True)
-    fname = "rank-00000.safetensors"
-    save_file(out, str(dst / fname), metadata={"format": FORMAT, "source": "huggingface"})
-    tensors = {n: {"shape": list(t.shape), "dtype": _DT[t.dtype],
-                   "shards": [{"file": fname, "split_dim": None, "offset": 0, "length": t.shape[0]}]}
-               for n, t in out.items()}
+    tensors: dict[str, dict] = {}
+
+    def _write(fname: str, out: dict[str, torch.Tensor]) -> None:
+        save_file(out, str(dst / fname), metadata={"format": FORMAT, "source": "huggingface"})
+        for n, t in out.items():
+            tensors[n] = {"shape": list(t.shape), "dtype": _DT[t.dtype],
+                          "shards": [{"file": fname, "split_dim": None, "offset": 0,
+                                      "length": t.shape[0]}]}
+
+    for i, f in enumerate(files):
+        out: dict[str, torch.Tensor] = {}
+        with safe_open(str(f), framework="pt", device="cpu") as fh:
+            for k in fh.keys():
+                t = fh.get_tensor(k)
+                it = _gpt2_map(k, t, cfg.hidden_size) if cfg.arch == "gpt2" else _llama_map(k, t)
+                for ln, tt in it:
+                    if ln == "lm_head.weight" and cfg.tie_embeddings:
+                        continue
+                    out[ln] = tt.to(dtype).contiguous()
+        if out:
+            _write(f"hf-{i:05d}.safetensors", out)
+        del out
+    if not cfg.tie_embeddings and "lm_head.weight" not in tensors and "embed_tokens.weight" in tensors:
+        ef = tensors["embed_tokens.weight"]["shards"][0]["file"]
+        with safe_open(str(dst / ef), framework="pt", device="cpu") as fh:
+            _write("hf-lm_head.safetensors", {"lm_head.weight": fh.get_tensor("embed_tokens.weight")})
     manifest = {"format": FORMAT, "version": VERSION, "model": cfg.to_dict(), "plan": {},
                 "dtype": _DT[dtype], "tensors": tensors}
     (dst / "manifest.json").write_text(json.dumps(manifest, indent=1))
