@@ -106,7 +106,7 @@ class LLM:
         eng = self.engine
         t0 = time.perf_counter()
         rids = [eng.add_request(x, params) for x in ids]
-        while eng.has_unfinished():
+        while eng.has_unfinished_global():
             eng.step()
         outs = []
         for p, r in zip(mine, rids):

@@ -217,6 +217,12 @@ class EngineConfig:
     # |x| <= 448): half the KV bytes per token, so twice the cached tokens and half the KV
     # traffic of a decode step; attention math stays bf16 (csrc/include/bfly_kv.h)
     kv_cache_dtype: str = "auto"
+    # context-parallel prefill across data-parallel replicas (pp == 1, no EP): a prompt of at
+    # least this many tokens is prefilled by ALL dp replicas together (ring or Ulysses
+    # attention, parallel/context_parallel.py), its K/V collected in the cache of the replica
+    # that then decodes it. 0 = off. Replicas step in lockstep while it is on.
+    cp_prefill_min_tokens: int = 0
+    cp_attention: str = "ring"        # "ring" | "ulysses"
 
 
 def load_config_file(path: str | Path) -> dict:

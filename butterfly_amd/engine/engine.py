@@ -15,11 +15,17 @@ Per step:
              one step = one tick in which every stage advances one group (engine/pipeline.py);
              otherwise each step splits the batch into microbatches (fill/drain per step).
   TP       : handled inside the model (all-reduces) and the sampler (score/id all-gather).
+  CP       : (EngineConfig.cp_prefill_min_tokens, pp == 1, no EP) a long prompt is prefilled
+             by every data-parallel replica together, context-parallel (ring / Ulysses), and
+             its K/V lands in the cache of the replica that decodes it (`_cp_step`). The
+             replicas then agree once per step on whether such a prefill is due, so they
+             step in lockstep (`lockstep_dp`, `has_unfinished_global`).
 """
 from __future__ import annotations
 
 import itertools
 import time
+from collections import deque
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -159,6 +165,23 @@ class LLMEngine:
         st = flags.get("BFLY_STEP_TIMEOUT_S")
         self.watchdog = StepWatchdog(st) if st > 0 else None
         self.steps_done = 0
+        # context-parallel prefill of long prompts over the DP replicas (parallel/context_parallel.py)
+        self.cp_min = engine_cfg.cp_prefill_min_tokens if (
+            mesh.dp > 1 and mesh.pp == 1 and mesh.ep == 1) else 0
+        self._cp_queue: deque = deque()
+
+    @property
+    def lockstep_dp(self) -> bool:
+        """Every step is collective over the data-parallel group (EP MoE layers, CP prefill
+        agreement): the replicas must keep stepping until ALL of them are done."""
+        return self.mesh.ep > 1 or bool(self.cp_min)
+
+    def has_unfinished_global(self) -> bool:
+        """has_unfinished() of this replica, or of any replica when steps are collective."""
+        mine = int(self.has_unfinished())
+        if not self.lockstep_dp:
+            return bool(mine)
+        return bool(self.comm.all_reduce_max_int([mine], "dp")[0])
 
     # ------------------------------------------------------------------------------------
     def _activation_reserve(self) -> int:
@@ -184,14 +207,16 @@ class LLMEngine:
         if len(prompt) + params.max_tokens > self.ecfg.max_seq_len:
             raise ValueError(f"prompt ({len(prompt)}) + max_tokens ({params.max_tokens}) exceeds max_seq_len")
         self.requests[rid] = Request(rid, list(prompt), params, arrival=time.perf_counter())
-        if self.prefix_cache:
+        if self.cp_min and len(prompt) >= self.cp_min:
+            self._cp_queue.append(rid)        # prefilled by the DP group together (_cp_step)
+        elif self.prefix_cache:
             self.scheduler.add(rid, len(prompt), params.max_tokens, list(prompt))
         else:
             self.scheduler.add(rid, len(prompt), params.max_tokens)
         return rid
 
     def has_unfinished(self) -> bool:
-        return (self.scheduler.num_waiting + self.scheduler.num_running > 0
+        return (self.scheduler.num_waiting + self.scheduler.num_running > 0 or bool(self._cp_queue)
                 or self._pending is not None or self._valued is not None)
 
     def _sample_params(self, rids):
@@ -241,6 +266,10 @@ class LLMEngine:
             self._poison = True
         if self.async_pp:
             return self._pp_tick(t0)
+        if self.cp_min:
+            out = self._cp_step(t0)
+            if out is not None:
+                return out
         plan = self.scheduler.schedule()
         ep_pad, any_prefill = 0, plan.kind == 1
         if self.mesh.ep > 1:
@@ -299,6 +328,50 @@ class LLMEngine:
                     len(rids), len(rids), rids)
             kind = "decode"
         return self._apply_tokens(kind, rids, tokens.tolist(), t0)
+
+    def _cp_step(self, t0: float) -> Optional[StepOutput]:
+        """Context-parallel prefill across the DP replicas. Every replica offers the head of its
+        long-prompt queue (if its scheduler could admit it now); the lowest offering replica
+        owns this step: its prompt is broadcast, every replica prefills one chunk of it (the
+        owner last in chunk order, so it holds the final token and its logits), and the owner's
+        cache collects the whole prompt's K/V in passing (context_parallel KV sink). The owner
+        samples the first token; the sequence then decodes there like any other. Returns None
+        when no replica has a long prompt due (the caller runs a normal step)."""
+        from ..parallel.context_parallel import cp_prefill, split_lengths
+
+        dp, me = self.mesh.dp, self.coord.dp
+        want = [0] * dp
+        if self._cp_queue:
+            L = len(self.requests[self._cp_queue[0]].prompt)
+            if self.scheduler.can_admit_prefilled(L):
+                want[me] = L
+        want = self.comm.all_reduce_max_int(want, "dp")
+        owner = next((i for i, n in enumerate(want) if n > 0), None)
+        if owner is None:
+            return None
+        L = want[owner]
+        g = self.comm.groups["dp"]
+        rid = self._cp_queue[0] if me == owner else None
+        prompt = self.comm.broadcast_ints(self.requests[rid].prompt if rid is not None else None, L, owner, "dp")
+        order = [r for i, r in enumerate(g.ranks) if i != owner] + [g.ranks[owner]]
+        sink = None
+        if rid is not None:
+            self._cp_queue.popleft()
+            req = self.requests[rid]
+            slots = self.scheduler.admit_prefilled(rid, L, req.params.max_tokens)
+            if not slots:
+                raise RuntimeError("context-parallel prefill: admission check and allocation disagree")
+            sink = [list(slots)]
+        with trace.range("engine.cp_prefill", tokens=L, owner=owner):
+            logits = cp_prefill(self.model, [prompt], order, order.index(self.rank), g.pg, self.kv.layers,
+                                attn=self.ecfg.cp_attention, sink_slots=sink, has_sink=True, broadcast=False)
+        mine = split_lengths(L, dp)[order.index(self.rank)]
+        self.metrics.inc("cp_prefill_tokens", mine)
+        if rid is None:
+            return StepOutput("cp-prefill", [], [], [], time.perf_counter() - t0, prefill_tokens=mine)
+        out = self._apply_tokens("prefill", [rid], self._sample(logits, [rid]).tolist(), t0)
+        out.prefill_tokens = mine
+        return out
 
     def _apply_tokens(self, kind: str, rids: list, new: list, t0: float) -> StepOutput:
         """Append one sampled token per sequence, retire finished ones, record metrics."""
@@ -543,7 +616,7 @@ class LLMEngine:
     # ------------------------------------------------------------------------------------
     def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list:
         rids = [self.add_request(p, params) for p in prompts]
-        while self.has_unfinished():
+        while self.has_unfinished_global():
             self.step()
         return [self.requests[r].output for r in rids]
 

@@ -10,6 +10,12 @@ biases, MoE). The model holds only its shard (models/shard.py) and runs one pipe
                 gate/up GEMM epilogue | GELU MLP | dense-dispatch MoE) -> TP all-reduce
   last stage  : final norm on the rows that need logits -> vocab-parallel LM head
 
+Sequence parallelism (BFLY_SEQ_PARALLEL, TP prefill steps, `_forward_sp`): the residual
+stream lives split by tokens over the TP group; each all-reduce becomes a reduce-scatter
+(into the rank's token shard, where the residual add + norm run on 1/tp of the rows) and an
+all-gather of the normed activations feeding the next column-parallel GEMM. Same link bytes
+as the all-reduce; norm work and residual memory drop by tp (SURVEY.md §2.6 SP).
+
 The residual stream is carried as (residual, pending delta): each block's "add + norm" is
 ONE kernel (rms_norm with residual=...), so the residual add never costs its own pass.
 
@@ -90,6 +96,8 @@ class TransformerLM:
             self.cos, self.sin = ops.rope_tables(cfg.head_dim, cfg.max_position, cfg.rope_theta,
                                                  cfg.rope_scaling, device=self.device)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.seq_parallel = self.tp > 1 and self.ep == 1 and flags.get("BFLY_SEQ_PARALLEL")
+        self.sp_min_tokens = flags.get("BFLY_SEQ_PARALLEL_MIN_TOKENS")
 
     # ------------------------------------------------------------------------------------
     # parameters
@@ -299,49 +307,22 @@ class TransformerLM:
                 hidden_in: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Run this stage. Returns logits [R, vocab_local] on the last stage, else the
         residual stream [T, hidden] to send to the next stage."""
-        c, d = self.cfg, self.dims
+        if (self.seq_parallel and fb.is_prefill and fb.cp is None
+                and fb.num_tokens >= max(self.sp_min_tokens, self.tp)):
+            return self._forward_sp(fb, kv_caches, hidden_in)
         residual = self.embed(fb) if self.first else hidden_in
         if residual is None:
             raise ValueError("non-first pipeline stage needs hidden_in")
         if not self.first:
             residual = residual.clone()   # updated in place by the fused add+norm
         delta, partial = None, False      # FFN output of the previous layer (un-reduced if partial)
-        T = fb.num_tokens
-        D = c.head_dim
         for li, i in enumerate(self.layer_ids):
             pre = f"l{i}."
             if delta is None:
                 x = self._norm(residual, self.p[pre + "in_w"], self.p.get(pre + "in_b"))
             else:
                 x = self._add_norm(delta, pre + "in", residual, partial)
-            # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
-            # when no all-reduce sits in between (tp == 1)
-            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
-            kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
-            slots = fb.slots if kc is not None else None
-            if c.pos_emb == "rope":
-                qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
-            elif kc is not None:
-                k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
-                v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
-                ops.kv_append(k3, v3, fb.slots, kc, vc)
-            q = qkv[:, : d.hq * D].view(T, d.hq, D)
-            if fb.is_prefill:
-                k = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
-                v = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
-                if fb.cp is not None:   # context parallel: ring (K/V circulate) or Ulysses
-                    from ..parallel import context_parallel as cpx
-
-                    fn = cpx.ulysses_attention if fb.cp.attn == "ulysses" else cpx.ring_attention
-                    attn = fn(q, k, v, fb.cp, self.scale)
-                elif fb.num_decode or fb.prefix_lens is not None:
-                    attn = self._mixed_attention(q, k, v, fb, kc, vc)
-                else:
-                    attn = ops.attn_prefill(q, k, v, fb.cu_seqlens, fb.max_seqlen, self.scale, True)
-            else:
-                attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
-            o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
-            o = ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce)
+            o = self._attention_block(li, pre, x, fb, kv_caches)
             x = self._add_norm(o, pre + "post", residual, self.tp > 1)
             delta, partial = self._ffn(pre, x, fb)
         if not self.last:
@@ -361,6 +342,98 @@ class TransformerLM:
         else:
             x = self._norm(r, self.p["final_w"], self.p.get("final_b"))
         return ops.linear(x, self.head_weight)
+
+    def _attention_block(self, li: int, pre: str, x: torch.Tensor, fb: ForwardBatch,
+                         kv_caches: Optional[list]):
+        """normed x [T, h] -> QKV GEMM -> RoPE + KV append -> attention -> O GEMM (TP-partial)."""
+        c, d = self.cfg, self.dims
+        T, D = fb.num_tokens, c.head_dim
+        # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
+        # when no all-reduce sits in between (tp == 1)
+        qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
+        kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
+        slots = fb.slots if kc is not None else None
+        if c.pos_emb == "rope":
+            qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
+        elif kc is not None:
+            k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
+            v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
+            ops.kv_append(k3, v3, fb.slots, kc, vc)
+        q = qkv[:, : d.hq * D].view(T, d.hq, D)
+        if fb.is_prefill:
+            k = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
+            v = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
+            if fb.cp is not None:   # context parallel: ring (K/V circulate) or Ulysses
+                from ..parallel import context_parallel as cpx
+
+                fn = cpx.ulysses_attention if fb.cp.attn == "ulysses" else cpx.ring_attention
+                sink = None
+                if fb.cp.sink and kc is not None:   # this rank collects the prompt's K/V
+                    sink = (lambda r, kk, vv, kc=kc, vc=vc:
+                            ops.kv_append(kk.contiguous(), vv.contiguous(), fb.cp.sink[r], kc, vc))
+                attn = fn(q, k, v, fb.cp, self.scale, sink)
+            elif fb.num_decode or fb.prefix_lens is not None:
+                attn = self._mixed_attention(q, k, v, fb, kc, vc)
+            else:
+                attn = ops.attn_prefill(q, k, v, fb.cu_seqlens, fb.max_seqlen, self.scale, True)
+        else:
+            attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
+        o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
+        return ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce)
+
+    # ------------------------------------------------------------------------------------
+    # sequence parallelism (TP prefill)
+    # ------------------------------------------------------------------------------------
+    def _sp_pad(self, t: torch.Tensor, Tp: int) -> torch.Tensor:
+        t = ops.materialize(t)
+        if t.shape[0] == Tp:
+            return t
+        return torch.cat([t, t.new_zeros(Tp - t.shape[0], *t.shape[1:])])
+
+    def _sp_scatter(self, t, Tp: int) -> torch.Tensor:
+        """TP-partial [T, h] -> this rank's token shard [Tp / tp, h] of the sum (reduce-scatter)."""
+        return self.comm.reduce_scatter(self._sp_pad(t, Tp), "tp")
+
+    def _sp_gather(self, xs: torch.Tensor, T: int) -> torch.Tensor:
+        """Token shards -> the full [T, h] activation on every TP rank (all-gather)."""
+        return self.comm.all_gather(xs.contiguous(), "tp")[:T]
+
+    def _forward_sp(self, fb: ForwardBatch, kv_caches: Optional[list],
+                    hidden_in: Optional[torch.Tensor]) -> torch.Tensor:
+        """forward() with the residual stream split by tokens over the TP group: rank r keeps
+        rows [r * Ts, (r + 1) * Ts) (T padded to tp * Ts with zero rows, which stay zero
+        through the norms). Every block: reduce-scatter the partial output into the shard,
+        residual add + norm there, all-gather the normed rows for the next GEMM."""
+        c = self.cfg
+        T, tp = fb.num_tokens, self.tp
+        Ts = (T + tp - 1) // tp
+        Tp, r0 = Ts * tp, self.shard.tp_rank * Ts
+        if self.first:
+            # vocab-parallel embedding: each rank holds a partial sum of every row
+            res = self._sp_scatter(ops.embed(fb.input_ids, self.p["embed"], vstart=self.dims.vocab0), Tp)
+            if c.pos_emb == "learned":
+                pos = self._sp_pad(fb.positions.view(-1, 1), Tp)[r0:r0 + Ts].view(-1)
+                res = ops.add(res, ops.embed(pos, self.p["pos_embed"], vstart=0))
+        else:
+            if hidden_in is None:
+                raise ValueError("non-first pipeline stage needs hidden_in")
+            res = self._sp_pad(hidden_in, Tp)[r0:r0 + Ts].clone()
+        delta = None
+        for li, i in enumerate(self.layer_ids):
+            pre = f"l{i}."
+            w, b = self.p[pre + "in_w"], self.p.get(pre + "in_b")
+            xs = self._norm(res, w, b) if delta is None else self._norm(self._sp_scatter(delta, Tp), w, b, residual=res)
+            o = self._attention_block(li, pre, self._sp_gather(xs, T), fb, kv_caches)
+            xs = self._norm(self._sp_scatter(o, Tp), self.p[pre + "post_w"], self.p.get(pre + "post_b"), residual=res)
+            delta, _ = self._ffn(pre, self._sp_gather(xs, T), fb)
+        if delta is not None:
+            res = ops.add(res, self._sp_scatter(delta, Tp))
+        full = self._sp_gather(res, T)
+        if not self.last:
+            return full
+        if fb.logits_idx is not None:
+            full = full.index_select(0, fb.logits_idx)
+        return ops.linear(self._norm(full, self.p["final_w"], self.p.get("final_b")), self.head_weight)
 
     def _mixed_attention(self, q, k, v, fb: ForwardBatch, kc, vc) -> torch.Tensor:
         """Attention of a mixed step: paged decode for the first num_decode rows; for the

@@ -233,6 +233,18 @@ class Communicator:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.pg)
         return [int(v) for v in t.tolist()]
 
+    def broadcast_ints(self, values: Optional[list], n: int, src_in_group: int, group: str = "dp") -> list:
+        """Host list of n integers from one group rank to all (control plane: e.g. the prompt
+        of an engine context-parallel step). Device-staged on RCCL, host tensors on gloo."""
+        g = self.groups[group]
+        if g.size == 1:
+            return list(values)
+        dev = "cuda" if self._nccl(g) else "cpu"
+        t = torch.tensor(values, dtype=torch.int64, device=dev) if g.rank_in_group == src_in_group \
+            else torch.empty(n, dtype=torch.int64, device=dev)
+        dist.broadcast(t, g.ranks[src_in_group], group=g.pg)
+        return [int(v) for v in t.tolist()]
+
     def _world_nccl(self) -> bool:
         return dist.is_initialized() and dist.get_backend() == "nccl"
 

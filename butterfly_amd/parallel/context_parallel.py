@@ -21,6 +21,13 @@ ring, two all-to-alls re-shard the attention from "all heads of 1/cp of the toke
 of the heads of all tokens" and back; attention then runs as ordinary causal flash attention
 over whole sequences. It needs Hkv % cp == 0 (GQA: at most 8-way for Llama-3) and moves
 q/k/v/o once each, where the ring moves K/V cp-1 times; the ring has no head constraint.
+
+KV sink (the serving engine's use, engine/engine.py `_cp_step`): one rank of the group — the
+one that will DECODE the sequence, placed last in chunk order so it also holds the final
+token's logits — collects the whole prompt's K/V into its own paged cache. With the ring this
+costs no extra traffic: every other rank's chunk passes through every rank during the cp-1
+hops, and the sink appends each one (kv_append at its slots) as it arrives. With Ulysses the
+chunks are all-gathered once more after the attention.
 """
 from __future__ import annotations
 
@@ -47,6 +54,7 @@ class CPContext:
     pg: Optional[object]         # torch process group of `ranks` (None when cp == 1)
     lens: list                   # lens[r][i] = tokens of sequence i held by cp rank r
     attn: str = "ring"           # "ring" | "ulysses"
+    sink: Optional[list] = None  # on the KV sink rank: sink[r] = its cache slots of chunk r (int32)
 
     @property
     def size(self) -> int:
@@ -101,16 +109,18 @@ class _RingHop:
 
 
 def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CPContext,
-                   scale: float) -> torch.Tensor:
+                   scale: float, kv_sink=None) -> torch.Tensor:
     """Causal attention of this rank's query chunk against the whole sequence, whose K/V chunks
     live on the other CP ranks. q [T, Hq, D], k/v [T, Hkv, D] (this rank's tokens, packed per
-    sequence as ctx.lens[rank]); returns [T, Hq, D] in q's dtype."""
+    sequence as ctx.lens[rank]); returns [T, Hq, D] in q's dtype. `kv_sink(r, k, v)` (sink
+    rank only) receives every other rank's chunk as it passes."""
     r, n = ctx.rank, ctx.size
     dev = q.device
     cu_r = ctx.cu(r, dev)
     out, lse = ops.attn_prefill(q, k, v, cu_r, ctx.max_len(r), scale, True, return_lse=True)
     if n == 1:
         return out
+    sink = kv_sink
     acc_o, acc_lse = out.float(), lse
     Hkv, D = k.shape[1], k.shape[2]
     cur = torch.stack([k, v], 1).contiguous()         # [T, 2, Hkv, D]: one message per hop
@@ -119,6 +129,8 @@ def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CPCon
         nxt = torch.empty(ctx.tokens(src), 2, Hkv, D, dtype=k.dtype, device=dev)
         hop = _RingHop(ctx, cur, nxt)
         cur = hop.wait()
+        if sink is not None and ctx.tokens(src) > 0:
+            sink(src, cur[:, 0], cur[:, 1])
         if src < r and ctx.tokens(src) > 0:            # earlier positions: fully visible
             o_j, lse_j = ops.attn_prefill(q, cur[:, 0], cur[:, 1], cu_r, ctx.max_len(r), scale, False,
                                           cu_seqlens_k=ctx.cu(src, dev), return_lse=True)
@@ -126,9 +138,32 @@ def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CPCon
     return acc_o.to(q.dtype)
 
 
+def _pg_order(ctx: CPContext) -> list:
+    """Chunk indices sorted by their rank's position in the process group (collectives that
+    index by group rank, e.g. all_to_all_single, see the group's own order; the chunk order
+    of an engine CP step puts the sink rank last whatever its group rank)."""
+    if ctx.pg is None:
+        return list(range(ctx.size))
+    return sorted(range(ctx.size), key=lambda j: dist.get_group_rank(ctx.pg, ctx.ranks[j]))
+
+
 def _a2a(send: torch.Tensor, send_rows: list, recv_rows: list, ctx: CPContext) -> torch.Tensor:
-    """all-to-all along dim 0: rows [sum(send_rows[:j]), +send_rows[j]) go to rank j; the
-    blocks received from every rank (recv_rows[j] from rank j) come back concatenated."""
+    """all-to-all along dim 0: rows [sum(send_rows[:j]), +send_rows[j]) go to chunk rank j;
+    the blocks received from every chunk rank (recv_rows[j] from j) come back concatenated."""
+    order = _pg_order(ctx)
+    if order != list(range(ctx.size)):
+        offs = [sum(send_rows[:j]) for j in range(ctx.size)]
+        send = torch.cat([send[offs[j]:offs[j] + send_rows[j]] for j in order])
+        got = _a2a_pg(send, [send_rows[j] for j in order], [recv_rows[j] for j in order], ctx)
+        blocks, a = {}, 0
+        for j in order:
+            blocks[j] = got[a:a + recv_rows[j]]
+            a += recv_rows[j]
+        return torch.cat([blocks[j] for j in range(ctx.size)])
+    return _a2a_pg(send, send_rows, recv_rows, ctx)
+
+
+def _a2a_pg(send: torch.Tensor, send_rows: list, recv_rows: list, ctx: CPContext) -> torch.Tensor:
     out = torch.empty((sum(recv_rows),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
     if _nccl(ctx.pg):
         dist.all_to_all_single(out, send.contiguous(), output_split_sizes=list(recv_rows),
@@ -140,9 +175,36 @@ def _a2a(send: torch.Tensor, send_rows: list, recv_rows: list, ctx: CPContext) -
     return out.copy_(host)
 
 
+def _gather_chunks(k: torch.Tensor, v: torch.Tensor, ctx: CPContext, kv_sink) -> None:
+    """Every rank's K/V chunk to the sink rank (Ulysses keeps no whole-head K/V anywhere):
+    one all-gather of the chunks padded to the longest; only the sink keeps the result."""
+    n, r = ctx.size, ctx.rank
+    Tm = max(ctx.tokens(j) for j in range(n))
+    Hkv, D = k.shape[1], k.shape[2]
+    mine = torch.zeros(Tm, 2, Hkv, D, dtype=k.dtype, device=k.device)
+    mine[: k.shape[0], 0], mine[: k.shape[0], 1] = k, v
+    order = _pg_order(ctx)
+    if _nccl(ctx.pg):
+        got = torch.empty(n * Tm, 2, Hkv, D, dtype=k.dtype, device=k.device)
+        dist.all_gather_into_tensor(got, mine, group=ctx.pg)
+    else:
+        host = [torch.empty(Tm, 2, Hkv, D, dtype=k.dtype) for _ in range(n)]
+        dist.all_gather(host, mine.detach().cpu(), group=ctx.pg)
+        got = torch.cat(host).to(k.device)
+    if kv_sink is None:
+        return
+    for gi, j in enumerate(order):           # gathered blocks come in group-rank order
+        if j != r and ctx.tokens(j) > 0:
+            blk = got[gi * Tm: gi * Tm + ctx.tokens(j)]
+            kv_sink(j, blk[:, 0], blk[:, 1])
+
+
 def ulysses_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CPContext,
-                      scale: float) -> torch.Tensor:
+                      scale: float, kv_sink=None) -> torch.Tensor:
     """Same contract as ring_attention, by sequence<->head all-to-alls (Hkv % cp == 0)."""
+    if ctx.sink is not None:
+        # collective: every rank takes part when the step has a sink rank
+        _gather_chunks(k, v, ctx, kv_sink)
     n, r = ctx.size, ctx.rank
     T, Hq, D = q.shape
     Hkv = k.shape[1]
@@ -175,26 +237,46 @@ def ulysses_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, ctx: CP
 
 def cp_prefill(model, prompts: list, ctx_ranks: list, rank_in_group: int, pg=None,
                kv_caches: Optional[list] = None, slots: Optional[list] = None,
-               attn: str = "ring") -> torch.Tensor:
-    """Context-parallel prefill of `prompts` (token lists) by the CP group `ctx_ranks`; this
-    rank processes its chunk of every prompt. `slots[i]` (optional) are the paged-cache slots of
-    THIS rank's chunk of prompt i in `kv_caches` (its local KV shard). `attn`: "ring" or
-    "ulysses" (all-to-all; head counts divisible by cp). Returns the last-token
-    logits [nseq, vocab_local] on every rank of the group (broadcast from the last rank)."""
+               attn: str = "ring", sink_slots: Optional[list] = None, has_sink: bool = False,
+               broadcast: bool = True) -> torch.Tensor:
+    """Context-parallel prefill of `prompts` (token lists) by the CP group `ctx_ranks` (chunk
+    order; group ranks of `pg`); this rank processes its chunk of every prompt. `slots[i]`
+    (optional) are the paged-cache slots of THIS rank's chunk of prompt i in `kv_caches` (its
+    local KV shard). `sink_slots[i]` (optional, the sink rank only; `has_sink` on every rank
+    of such a step) are this rank's cache slots of EVERY token of prompt i: the whole prompt's
+    K/V lands in its cache. `attn`: "ring" or "ulysses" (all-to-all; head counts divisible by
+    cp). Returns the last-token logits [nseq, vocab_local] on every rank of the group
+    (broadcast from the last rank), or, with broadcast=False, on the last rank only (others
+    get an empty tensor)."""
     from ..engine.batch import ForwardBatch
 
     cp = len(ctx_ranks)
     per_seq = [split_lengths(len(p), cp) for p in prompts]
     lens = [[per_seq[i][r] for i in range(len(prompts))] for r in range(cp)]
-    ctx = CPContext(list(ctx_ranks), rank_in_group, pg, lens, attn)
+    dev = model.device
+    sink = None
+    if sink_slots is not None:
+        sink = []
+        for r in range(cp):
+            sl_r = []
+            for i in range(len(prompts)):
+                a = sum(per_seq[i][:r])
+                sl_r.extend(sink_slots[i][a:a + per_seq[i][r]])
+            sink.append(torch.tensor(sl_r, dtype=torch.int32, device=dev))
+        slots = None
+    elif has_sink:
+        sink = []                 # marks a sink step on the other ranks (Ulysses gathers)
+    ctx = CPContext(list(ctx_ranks), rank_in_group, pg, lens, attn, sink)
     ids, pos, sl = [], [], []
     for i, p in enumerate(prompts):
         a = sum(per_seq[i][:rank_in_group])
         n = per_seq[i][rank_in_group]
         ids.extend(p[a:a + n])
         pos.extend(range(a, a + n))
-        sl.extend(slots[i] if slots is not None else [-1] * n)
-    dev = model.device
+        if sink_slots is not None:
+            sl.extend(sink_slots[i][a:a + n])
+        else:
+            sl.extend(slots[i] if slots is not None else [-1] * n)
     i32 = dict(dtype=torch.int32, device=dev)
     cu = ctx.cu(rank_in_group, dev)
     last = rank_in_group == cp - 1
@@ -203,7 +285,7 @@ def cp_prefill(model, prompts: list, ctx_ranks: list, rank_in_group: int, pg=Non
                       slots=torch.tensor(sl, **i32), is_prefill=True, cu_seqlens=cu,
                       max_seqlen=ctx.max_len(rank_in_group), logits_idx=logits_idx, cp=ctx)
     logits = model.forward(fb, kv_caches)
-    if cp == 1:
+    if cp == 1 or not broadcast:
         return logits
     V = model.dims.vocab
     buf = logits.contiguous() if last else torch.empty(len(prompts), V, dtype=model.dtype, device=dev)

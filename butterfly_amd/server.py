@@ -107,7 +107,7 @@ class ServingLoop:
             if stop and self._all_idle():      # collective: every rank evaluates it
                 return
             finished, tokens = [], []
-            if eng.has_unfinished() or self.llm.plan.ep > 1:
+            if eng.has_unfinished() or eng.lockstep_dp:
                 out = eng.step()
                 if self.streaming:
                     tokens = [(r, t) for r, t in zip(out.rids, out.new_tokens) if r in self.streaming]

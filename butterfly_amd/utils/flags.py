@@ -43,6 +43,9 @@ define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0:
 define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
+define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism: the residual stream and the norms are "
+       "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
+define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")
 define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped expert GEMMs instead of the dense path")
 define("BFLY_EP_DECODE_A2A", True, _bool, "EP MoE on decode (and idle) steps: fixed-capacity all-to-all dispatch with "
        "routed-rows-only expert GEMMs, graph-capturable (0: all-gather + dense local experts + reduce-scatter)")

@@ -27,6 +27,9 @@ void register_scheduler(py::module_& m) {
            py::keep_alive<1, 2>())
       .def("add", &Scheduler::add, py::arg("sid"), py::arg("prompt_len"), py::arg("max_new_tokens"),
            py::arg("tokens") = std::vector<int32_t>{})
+      .def("admit_prefilled", &Scheduler::admit_prefilled, py::arg("sid"), py::arg("prompt_len"),
+           py::arg("max_new_tokens"))
+      .def("can_admit_prefilled", &Scheduler::can_admit_prefilled)
       .def_property_readonly("prefix_hit_tokens", &Scheduler::prefix_hit_tokens)
       .def("on_token", &Scheduler::on_token)
       .def("finish", &Scheduler::finish)

@@ -64,6 +64,22 @@ class Scheduler {
 
   int64_t prefix_hit_tokens() const { return prefix_hit_tokens_; }
 
+  // Context-parallel prefill (engine CP across data-parallel replicas): the prompt was run by
+  // the replica's CP group outside this scheduler and its K/V arrives in this rank's pages.
+  // Allocate them and enter the sequence as running with its prompt fully cached. Returns the
+  // slots of the prompt's tokens; empty when it does not fit now (batch or KV pages).
+  std::vector<int32_t> admit_prefilled(int64_t sid, int64_t prompt_len, int64_t max_new_tokens) {
+    if (info_.count(sid)) throw std::invalid_argument("duplicate sequence id");
+    if ((int)running_.size() >= max_batch_ || !can_admit_prefilled(prompt_len)) return {};
+    info_[sid] = Info{prompt_len, 0, max_new_tokens, false, {}};
+    running_.push_back(sid);
+    return kv_.allocate(sid, prompt_len);
+  }
+  bool can_admit_prefilled(int64_t prompt_len) const {
+    return (int)running_.size() < max_batch_ && kv_.blocks_needed(prompt_len + 1) <= kv_.num_free();
+  }
+
+
   // Record one generated token (after a prefill or decode step produced it).
   void on_token(int64_t sid) { info_.at(sid).generated++; }
 

@@ -12,12 +12,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout,extra", [("tp2", []), ("pp2", []), ("dp2xep2", []),
-                                          ("pp2", ["-", "graphs"])])
-def test_sharded_layout_on_one_gpu(layout, extra):
+@pytest.mark.parametrize("layout,extra,env", [("tp2", [], {}), ("pp2", [], {}), ("dp2xep2", [], {}),
+                                              ("pp2", ["-", "graphs"], {}),
+                                              ("tp2", [], {"BFLY_SEQ_PARALLEL": "1",
+                                                           "BFLY_SEQ_PARALLEL_MIN_TOKENS": "1"})])
+def test_sharded_layout_on_one_gpu(layout, extra, env):
     r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", "2", "--",
                         sys.executable, os.path.join(ROOT, "tools", "gpu_dist_check.py"), layout] + extra,
-                       cwd=ROOT, capture_output=True, text=True, timeout=600)
+                       cwd=ROOT, env=dict(os.environ, **env), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert r.stdout.count("PASS") == 2, r.stdout[-4000:]
 
@@ -42,10 +44,11 @@ def test_bench_two_ranks_on_one_gpu(plan):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,attn", [(2, "ring"), (3, "ring"), (2, "ulysses")])
-def test_context_parallel_prefill_on_one_gpu(n, attn):
+@pytest.mark.parametrize("n,attn,mode", [(2, "ring", "-"), (3, "ring", "-"), (2, "ulysses", "-"),
+                                         (2, "ring", "engine"), (2, "ulysses", "engine")])
+def test_context_parallel_prefill_on_one_gpu(n, attn, mode):
     r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", str(n), "--",
-                        sys.executable, os.path.join(ROOT, "tools", "gpu_cp_check.py"), "-", attn],
+                        sys.executable, os.path.join(ROOT, "tools", "gpu_cp_check.py"), "-", attn, mode],
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert r.stdout.count("PASS") == n, r.stdout[-4000:]
