@@ -83,6 +83,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the start-up collective probe (N > 1)")
     ap.add_argument("--kv-dtype", default="auto", help="KV-cache elements: auto (= bf16) | fp8")
+    ap.add_argument("--sync-decode", action="store_true",
+                    help="single-stage layouts: host waits for each step's tokens before scheduling the "
+                         "next (default: EngineConfig.async_decode, the next step overlaps the host work)")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap
 
@@ -192,7 +195,7 @@ def run(a) -> int:
                         kv_cache_tokens=replica_batch * (max_seq + 32),
                         use_graphs=not a.no_graphs,
                         graph_batch_sizes=[replica_batch],
-                        kv_cache_dtype=a.kv_dtype)
+                        kv_cache_dtype=a.kv_dtype, async_decode=not a.sync_decode)
     t0 = time.perf_counter()
     device = None if use_gpu else torch.device("cpu")
     eng = LLMEngine(cfg, mesh, ecfg, comm=comm, stage_layers=plan.stages, device=device)
@@ -286,7 +289,8 @@ def run(a) -> int:
                    "parallelism": plan.name, "stages": [list(s) for s in plan.stages],
                    "hipgraph": bool(runner.graphs) and not runner.eager_buckets,
                    "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""),
-                   "pp_async_groups": groups if groups > 1 else None},
+                   "pp_async_groups": groups if groups > 1 else None,
+                   "async_decode": bool(eng.async_pp and mesh.pp == 1)},
     }
     if rank == 0:
         line = json.dumps(res)

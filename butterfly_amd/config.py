@@ -222,6 +222,11 @@ class EngineConfig:
     # attention, parallel/context_parallel.py), its K/V collected in the cache of the replica
     # that then decodes it. 0 = off. Replicas step in lockstep while it is on.
     cp_prefill_min_tokens: int = 0
+    # overlapped decode for single-stage layouts (pp == 1, no EP): the asynchronous pipeline of
+    # engine/pipeline.py with one group, so the host schedules step k+1 (inputs gathered on the
+    # device from step k's sampled ids) while step k still runs, and token values reach the
+    # host one step late. Replaces mixed chunked prefill (prefill steps run on their own).
+    async_decode: bool = False
     cp_attention: str = "ring"        # "ring" | "ulysses"
 
 

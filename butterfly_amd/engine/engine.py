@@ -122,7 +122,10 @@ class LLMEngine:
         native = __import__("butterfly_amd._native_loader", fromlist=["native"]).native()
         # pipeline parallelism without per-step fill/drain: pp request groups in flight
         # (engine/pipeline.py); EP layouts keep the synchronous path (EP collectives span DP ranks)
-        self.async_pp = mesh.pp > 1 and mesh.ep == 1 and flags.get("BFLY_PP_ASYNC")
+        # (pp == 1 with EngineConfig.async_decode: the same machinery with one group overlaps
+        # the host's scheduling of step k+1 with the device's step k)
+        self.async_pp = mesh.ep == 1 and flags.get("BFLY_PP_ASYNC") and (
+            mesh.pp > 1 or bool(engine_cfg.async_decode))
         self.mixed = self.prefix_cache = False
         if self.async_pp:
             self.scheduler = GroupedScheduler(native, self.kv.manager, mesh.pp, engine_cfg.max_batch,
@@ -167,7 +170,7 @@ class LLMEngine:
         self.steps_done = 0
         # context-parallel prefill of long prompts over the DP replicas (parallel/context_parallel.py)
         self.cp_min = engine_cfg.cp_prefill_min_tokens if (
-            mesh.dp > 1 and mesh.pp == 1 and mesh.ep == 1) else 0
+            mesh.dp > 1 and mesh.pp == 1 and mesh.ep == 1 and not self.async_pp) else 0
         self._cp_queue: deque = deque()
 
     @property

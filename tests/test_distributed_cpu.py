@@ -53,7 +53,7 @@ def test_model_parallel_matches_single(preset, mesh_kw, world):
         assert o == ref
 
 
-def _mixed_generate(rank, world, preset, mesh_kw, max_batch, async_pp):
+def _mixed_generate(rank, world, preset, mesh_kw, max_batch, async_pp, async_decode=False):
     """Requests of different lengths, more than the batch holds (admission while the pipeline
     runs), one request added mid-run; per-request outputs."""
     import os
@@ -65,9 +65,11 @@ def _mixed_generate(rank, world, preset, mesh_kw, max_batch, async_pp):
     mesh = Mesh(**mesh_kw)
     comm = Communicator.from_mesh(mesh) if world > 1 else None
     cfg = ModelConfig.from_preset(preset)
-    ecfg = EngineConfig(max_batch=max_batch, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    ecfg = EngineConfig(max_batch=max_batch, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5,
+                        async_decode=async_decode)
     try:
         eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")   # reads the flag
+        assert eng.async_pp == (async_pp and (mesh.pp > 1 or async_decode))
     finally:   # the single-process reference runs in the test process: do not leak the flag
         if saved is None:
             os.environ.pop("BFLY_PP_ASYNC", None)
@@ -81,6 +83,23 @@ def _mixed_generate(rank, world, preset, mesh_kw, max_batch, async_pp):
     while eng.has_unfinished():
         eng.step()
     return [eng.requests[r].output for r in rids]
+
+
+def test_async_decode_single_stage_matches_single():
+    """EngineConfig.async_decode (pp == 1): step k+1 is scheduled and its input ids gathered on
+    the device before step k's token values reach the host; same tokens, stop handling and
+    admission as the synchronous engine."""
+    assert _mixed_generate(0, 1, "llama-tiny", {}, 4, True, async_decode=True) == \
+        _mixed_generate(0, 1, "llama-tiny", {}, 4, False)
+
+
+@pytest.mark.parametrize("preset,mesh_kw,world", [
+    ("llama-tiny", dict(tp=2), 2),
+])
+def test_async_decode_tp_matches_single(preset, mesh_kw, world):
+    ref = _mixed_generate(0, 1, preset, {}, 4, False)
+    for o in run_world(_mixed_generate, world, preset, mesh_kw, 4, True, True):
+        assert o == ref
 
 
 @pytest.mark.parametrize("preset,mesh_kw,world", [
