@@ -326,13 +326,14 @@ attn_decode_combine_kernel(const float* __restrict__ part_o, const float* __rest
 // ---------------------------------------------------------------------------------------
 // Prefill
 // ---------------------------------------------------------------------------------------
-// 256 query rows (8 waves x 32) and a 4-deep 128 KiB K/V ring (3 deep: 0-2 % slower). Measured
-// alternative: 128 rows /
-// 2 stages (two workgroups per CU, uncoupled barriers) is 6-15 % slower: one tile of compute
-// does not hide the K/V fetch (profiles/r1_attn_prefill_valu_trim.log).
-constexpr int kPfBQ = 256, kPfBKV = 64, kPfWaves = kPfBQ / 32, kPfStages = 4;
+// 256 query rows (8 waves x 32) and an S-deep 32 KiB-per-tile K/V ring (S = 3 by default: with
+// the VALU trimmed, 3 deep is 1-2 % faster than 4). Measured alternative: 128 rows / 2 stages
+// (two workgroups per CU, uncoupled barriers) is 6-15 % slower: one tile of compute does not
+// hide the K/V fetch (profiles/r1_attn_prefill_valu_trim.log).
+constexpr int kPfBQ = 256, kPfBKV = 64, kPfWaves = kPfBQ / 32;
 constexpr int kPfIters = 16 / kPfWaves;   // 16 pieces of 4 key rows per K (and V) tile
 constexpr int kPfThreads = kPfWaves * 64;
+constexpr int kPfLPW = 2 * kPfIters;      // LDS-DMA instructions per wave per staged tile
 
 // Byte offset of 16-B chunk `ch` (0..15) of row `row` in a [rows][128 x bf16] LDS image
 // (T10 image (b): conflict-free for 32x32x16 row reads and for the transposed reads).
@@ -351,6 +352,14 @@ typedef __attribute__((address_space(1))) void* pf_gbl_t;
 template <int N>
 __device__ __forceinline__ void pf_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until this wave's DMA pieces of a tile landed, leaving `after` later tiles in flight
+__device__ __forceinline__ void pf_wait_tiles(int after) {
+  if (after >= 3) pf_vm_wait<3 * kPfLPW>();
+  else if (after == 2) pf_vm_wait<2 * kPfLPW>();
+  else if (after == 1) pf_vm_wait<kPfLPW>();
+  else pf_vm_wait<0>();
 }
 
 // Stage one 64-key K/V tile (2 x 16 KiB) by LDS-DMA: each wave-instruction writes 4 rows
@@ -373,13 +382,155 @@ __device__ __forceinline__ void pf_stage(const bf16* __restrict__ k, long k_stri
   }
 }
 
-// Causal varlen flash attention. Workgroup = kPfBQ query rows of one head (32 rows per wave;
-// two waves per SIMD so one wave's softmax overlaps the other's MFMAs); 64-key K/V tiles in a
-// kPfStages-deep LDS-DMA ring (counted vmcnt, one raw barrier per tile). Per wave: S^T = K Q^T on
-// 32x32x16 MFMAs (the lane owns one query column: row max/sum are lane-local plus one swap),
-// P^T built in registers from the accumulator, O^T += V^T P^T with V fed by transposed LDS
-// reads (ds_read_b64_tr_b16).
-template <int D>
+// S^T tiles of one 64-key tile: s[kt][r] = S[key = kv0 + 32kt + (r&3) + 8(r>>2) + 4hi][query c]
+__device__ __forceinline__ void pf_qk(const char* kb, const bf16x8 (&qf)[8], int lane,
+                                      f32x16 (&s)[2]) {
+  const int hi = lane >> 5, c = lane & 31;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    s[kt] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + pf_off(c, 2 * ks + hi) + kt * 32 * 256);
+      s[kt] = mfma32(kf, qf[ks], s[kt]);
+    }
+  }
+}
+
+// Row max of a tile's raw scores (masked first on diagonal / ragged tiles): 4 independent
+// v_max3 chains (fmaxf on MFMA results would add canonicalising v_max_f32 per element under
+// this build's float flags), then the other half-wave's keys by v_permlane32_swap instead of an
+// LDS bpermute round trip. Returns the max in the scaled log2 domain. The mask compares each
+// element's compile-time key offset with ONE per-lane limit (the last visible key relative
+// to the tile and the lane's half): a compare and a select per element, no per-element
+// index math or scalar mask merging.
+template <bool MASK>
+__device__ __forceinline__ float pf_tile_max(f32x16 (&s)[2], int lim, float scale_log2) {
+  if (MASK) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        s[kt][r] = (32 * kt + (r & 3) + 8 * (r >> 2)) <= lim ? s[kt][r] : kNegInf;
+  }
+  float tc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int kt = c >> 1, r0 = 8 * (c & 1);
+    tc[c] = pf_max3(s[kt][r0], s[kt][r0 + 1], s[kt][r0 + 2]);
+    tc[c] = pf_max3(tc[c], s[kt][r0 + 3], s[kt][r0 + 4]);
+    tc[c] = pf_max3(tc[c], s[kt][r0 + 5], s[kt][r0 + 6]);
+    tc[c] = pf_max3(tc[c], s[kt][r0 + 7], tc[c]);
+  }
+  float tmax = pf_max3(pf_max3(tc[0], tc[1], tc[2]), tc[3], tc[3]);
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+  return pf_max3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), __uint_as_float(sw[1])) * scale_log2;  // scale > 0
+}
+
+// P^T = exp2(S * scale - m) as bf16 MFMA B fragments (one FMA and a bare v_exp_f32 per element:
+// no denormal range fix-up, p underflowing to 0 is what softmax wants); returns the row sum.
+__device__ __forceinline__ float pf_exp(const f32x16 (&s)[2], float scale_log2, float mb,
+                                        bf16x8 (&pb)[2][2]) {
+  float ps = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][8 * h + j], scale_log2, -mb));
+        ps += pv;
+        pb[kt][h][j] = f2bf(pv);
+      }
+  return ps;
+}
+
+// O^T[d][q] += V^T[d][key] P^T[key][q]; the A operand comes from transposed LDS reads.
+__device__ __forceinline__ void pf_pv(const char* vb, const bf16x8 (&pb)[2][2], int lane,
+                                      f32x16 (&o)[4]) {
+  const int hi = lane >> 5, tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int ch = 4 * dt + 2 * tg + (tp >> 1);
+    const int vlo = pf_off(4 * hi + tq, ch) + 8 * (tp & 1), vhi = pf_off(4 * hi + tq + 8, ch) + 8 * (tp & 1);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rows = (32 * kt + 16 * h) * 256;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(vb + vlo + rows));
+        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(vb + vhi + rows));
+        // Assemble the fragment as whole dwords (element-wise bf16 inserts from the
+        // v4i16 result were miscompiled: hipcc kept only the low dword and duplicated it).
+        const u32x2 a2 = __builtin_bit_cast(u32x2, lo);
+        const u32x2 b2 = __builtin_bit_cast(u32x2, hi4);
+        const u32x4 w4 = {a2.x, a2.y, b2.x, b2.y};
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, w4);
+        o[dt] = mfma32(vf, pb[kt][h], o[dt]);
+      }
+  }
+}
+
+// K/V tile staging by buffer_load ... lds: the buffer descriptor (SGPRs) starts at the tile's
+// first key row and ends at the chunk's last one, so per tile only scalar work moves the
+// window, the per-lane byte offsets stay constant (computed once), and rows past the end read
+// as zeros (masked anyway) instead of needing a per-lane clamp. (The 64-bit per-lane address
+// math of global_load_lds cost ~45 VALU per tile, next to ~200 of softmax.)
+struct PfDma {
+  int k[kPfIters], v[kPfIters];   // per-lane byte offsets of the lane's 16 B in each piece
+};
+
+__device__ __forceinline__ PfDma pf_dma_offsets(long k_stride, long v_stride, int wid, int lane) {
+  PfDma d;
+#pragma unroll
+  for (int i = 0; i < kPfIters; ++i) {
+    const int row = (i * kPfWaves + wid) * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ pf_swz(row);
+    d.k[i] = (int)((row * k_stride + ch * 8) * 2);
+    d.v[i] = (int)((row * v_stride + ch * 8) * 2);
+  }
+  return d;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pf_rsrc(const bf16* base, long rows, long stride) {
+  const long bytes = rows * stride * 2;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                           0x00020000);
+}
+
+__device__ __forceinline__ void pf_stage_buf(const bf16* __restrict__ k, long k_stride,
+                                             const bf16* __restrict__ v, long v_stride, int s0, int L,
+                                             int kh, int t, char* kb, int wid, const PfDma& d) {
+  const long r0 = (long)s0 + (long)t * kPfBKV;
+  const long rows = L - t * kPfBKV;
+  const auto rk = pf_rsrc(k + r0 * k_stride + (long)kh * 128, rows, k_stride);
+  const auto rv = pf_rsrc(v + r0 * v_stride + (long)kh * 128, rows, v_stride);
+#pragma unroll
+  for (int i = 0; i < kPfIters; ++i) {
+    const int piece = i * kPfWaves + wid;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (pf_lds_t)(kb + piece * 1024), 16, d.k[i], 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (pf_lds_t)(kb + kPfBKV * 256 + piece * 1024), 16, d.v[i], 0, 0, 0);
+  }
+}
+
+// Deferred rescale threshold (log2 units): a tile whose row max exceeds the running max by at
+// most this much keeps the old max, so P stays <= 2^8 and the O rescale (64 multiplies per
+// lane) is skipped; the decision is wave-uniform and taken before the tile is exponentiated
+// (cdna_hip_programming.md T13).
+constexpr float kPfRescaleThr = 8.f;
+
+// Causal varlen flash attention. Workgroup = kPfBQ query rows of one head (32 rows per wave,
+// two waves per SIMD); 64-key K/V tiles in an S-deep LDS-DMA ring (counted vmcnt, one raw
+// barrier per tile). Per wave: S^T = K Q^T on 32x32x16 MFMAs (the lane owns one query column:
+// row max/sum are lane-local plus one swap), P^T built in registers from the accumulator,
+// O^T += V^T P^T with V fed by transposed LDS reads (ds_read_b64_tr_b16).
+// The loop is VALU-bound next to its MFMAs (rocprofv3: ~10 VALU per MFMA), so the template
+// flags trim VALU: BUFDMA (scalar tile windows, above), DEFER (skip the O rescale), and PRIO
+// (waves 4-7, which lose VALU arbitration to their older SIMD partners, at s_setprio 1).
+// Measured and dropped (profiles/r2_attn_prefill_variants.log): a 5-stage ring (-7 % on
+// 16k tokens), waves 4-7 running PV one tile late (-15..-25 %), a one-tile software pipeline
+// of QK(t+1) beside softmax(t) (spills at 256 VGPRs, -35 %).
+template <int D, int S, bool PRIO, bool DEFER, bool BUFDMA>
 __global__ void __launch_bounds__(kPfThreads)
 attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
                     long k_stride, const bf16* __restrict__ v, long v_stride,
@@ -389,7 +540,8 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   static_assert(D == 128, "prefill kernel is specialised for D=128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = 2 * kPfBKV * D * 2;  // K | V, 32 KiB
-  constexpr int LPW = 2 * kPfIters;                 // glds per wave per stage
+  constexpr int V_OFF = kPfBKV * 256;
+  constexpr int AHEAD = S - 1;                      // tiles staged ahead of the one consumed
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int seq = blockIdx.y, h = blockIdx.z;
   const int s0 = cu_seqlens[seq];
@@ -403,6 +555,8 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   if (q0 >= L) return;
   const int kh = h / (Hq / Hkv);
   const int hi = lane >> 5, c = lane & 31;
+  const bool cz = causal != 0;
+  if (PRIO && __builtin_amdgcn_readfirstlane(wid) >= kPfWaves / 2) __builtin_amdgcn_s_setprio(1);
 
   // Q^T fragments (B operand of 32x32x16): lane holds Q[row c][d = 16ks + 8hi + j].
   const int qrow = q0 + 32 * wid + c;
@@ -413,6 +567,8 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) qf[ks] = qp[2 * ks];
   }
+  PfDma dma{};
+  if (BUFDMA) dma = pf_dma_offsets(k_stride, v_stride, wid, lane);
 
   f32x16 o[4];
 #pragma unroll
@@ -422,113 +578,52 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
   const int kv_end = causal ? min(Lk, q0 + kPfBQ) : Lk;
   const int ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
   const int wave_qmax = q0 + 32 * wid + 31;
+  // last visible key of this lane's query (causal) or of the chunk, for the masked tiles
+  const int last_key = cz ? min(qrow, Lk - 1) : Lk - 1;
 
+  auto stage = [&](int t, char* dst) {
+    if (BUFDMA) pf_stage_buf(k, k_stride, v, v_stride, sk0, Lk, kh, t, dst, wid, dma);
+    else pf_stage(k, k_stride, v, v_stride, sk0, Lk, kh, t, dst, wid, lane);
+  };
 #pragma unroll
-  for (int st = 0; st < kPfStages - 1; ++st)
-    if (st < ntiles) pf_stage(k, k_stride, v, v_stride, sk0, Lk, kh, st, smem + st * STAGE_BYTES, wid, lane);
+  for (int st = 0; st < AHEAD; ++st)
+    if (st < ntiles) stage(st, smem + st * STAGE_BYTES);
   int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
-    // tile t landed; the (up to kPfStages - 2) tiles issued after it may still fly
-    if (kPfStages > 3 && t + 2 < ntiles) pf_vm_wait<LPW * (kPfStages > 3 ? 2 : 0)>();
-    else if (kPfStages > 2 && t + 1 < ntiles) pf_vm_wait<LPW * (kPfStages > 2 ? 1 : 0)>();
-    else pf_vm_wait<0>();
+    // tile t landed; the (up to AHEAD - 1) tiles issued after it may still fly
+    pf_wait_tiles(min(ntiles - 1, t + AHEAD - 1) - t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (t + kPfStages - 1 < ntiles) {
-      int nb = buf + kPfStages - 1;
-      if (nb >= kPfStages) nb -= kPfStages;
-      pf_stage(k, k_stride, v, v_stride, sk0, Lk, kh, t + kPfStages - 1, smem + nb * STAGE_BYTES, wid, lane);
+    if (t + AHEAD < ntiles) {
+      int nb = buf + AHEAD;
+      if (nb >= S) nb -= S;
+      stage(t + AHEAD, smem + nb * STAGE_BYTES);
     }
     const int kv0 = t * kPfBKV;
     const char* kb = smem + buf * STAGE_BYTES;
-    const char* vb = kb + kPfBKV * 256;
-    if (!(causal && kv0 > wave_qmax)) {
-      // S^T tiles: st[kt][r] = S[key = kv0 + 32kt + (r&3) + 8(r>>2) + 4hi][query c]
+    if (!(cz && kv0 > wave_qmax)) {
       f32x16 sc[2];
+      pf_qk(kb, qf, lane, sc);
+      // masking only on the diagonal / ragged-end tiles (wave-uniform branch)
+      const bool need_mask = (cz && kv0 + kPfBKV - 1 > q0 + 32 * wid) || kv0 + kPfBKV > Lk;
+      const int lim = last_key - kv0 - 4 * hi;
+      const float tmax = need_mask ? pf_tile_max<true>(sc, lim, scale_log2) : pf_tile_max<false>(sc, lim, scale_log2);
+      float alpha = 1.f;
+      // (first tile: tmax - (-inf) = inf, or NaN on an all-masked row: both take the rescale)
+      if (!DEFER || !__all(tmax - m <= kPfRescaleThr)) {
+        const float mn = fmaxf(m, tmax);
+        const float mb = mn == kNegInf ? 0.f : mn;
+        alpha = __builtin_amdgcn_exp2f(m - mb);
+        m = mn;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        sc[kt] = f32x16{};
-        const int row = 32 * kt + c;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + pf_off(row, 2 * ks + hi));
-          sc[kt] = mfma32(kf, qf[ks], sc[kt]);
-        }
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
       }
-      // Masking only on the diagonal / ragged-end tiles (wave-uniform branch); the softmax
-      // works on raw scores: max first, then one FMA (score * scale - max) per element and a
-      // bare v_exp_f32 (no denormal range fix-up: p underflowing to 0 is what softmax wants).
-      // This trims the VALU work per tile, which bounds this kernel next to the MFMAs.
-      const bool need_mask = (causal && kv0 + kPfBKV - 1 > q0 + 32 * wid) || kv0 + kPfBKV > Lk;
-      if (need_mask) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kv0 + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            const bool ok = key < Lk && (!causal || key <= qrow);
-            sc[kt][r] = ok ? sc[kt][r] : kNegInf;
-          }
-      }
-      // row max: 4 independent v_max3 chains (fmaxf on MFMA results would add canonicalising
-      // v_max_f32 per element under this build's float flags)
-      float tc[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int kt = c >> 1, r0 = 8 * (c & 1);
-        tc[c] = pf_max3(sc[kt][r0], sc[kt][r0 + 1], sc[kt][r0 + 2]);
-        tc[c] = pf_max3(tc[c], sc[kt][r0 + 3], sc[kt][r0 + 4]);
-        tc[c] = pf_max3(tc[c], sc[kt][r0 + 5], sc[kt][r0 + 6]);
-        tc[c] = pf_max3(tc[c], sc[kt][r0 + 7], tc[c]);
-      }
-      float tmax = pf_max3(pf_max3(tc[0], tc[1], tc[2]), tc[3], tc[3]);
-      {  // the other half-wave's keys: v_permlane32_swap instead of an LDS bpermute round trip
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-        tmax = pf_max3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), __uint_as_float(sw[1])) * scale_log2;  // scale > 0
-      }
-      const float mn = fmaxf(m, tmax);
-      const float mb = mn == kNegInf ? 0.f : mn;
-      const float alpha = __builtin_amdgcn_exp2f(m - mb);
-      m = mn;
+      const float mb = m == kNegInf ? 0.f : m;
       bf16x8 pb[2][2];
-      float ps = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kt][8 * s + j], scale_log2, -mb));
-            ps += pv;
-            pb[kt][s][j] = f2bf(pv);
-          }
-      lsum = lsum * alpha + ps;
-      // O^T[d][q] += V^T[d][key] P^T[key][q]; A operand via transposed LDS reads.
-      const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        o[dt] *= alpha;
-        const int ch = 4 * dt + 2 * tg + (tp >> 1);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const int krow = 32 * kt + 16 * s + 4 * hi + tq;
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s4_ptr)(vb + pf_off(krow, ch) + 8 * (tp & 1)));
-            const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s4_ptr)(vb + pf_off(krow + 8, ch) + 8 * (tp & 1)));
-            // Assemble the fragment as whole dwords (element-wise bf16 inserts from the
-            // v4i16 result were miscompiled: hipcc kept only the low dword and duplicated it).
-            const u32x2 a2 = __builtin_bit_cast(u32x2, lo);
-            const u32x2 b2 = __builtin_bit_cast(u32x2, hi4);
-            const u32x4 w4 = {a2.x, a2.y, b2.x, b2.y};
-            const bf16x8 vf = __builtin_bit_cast(bf16x8, w4);
-            o[dt] = mfma32(vf, pb[kt][s], o[dt]);
-          }
-      }
+      lsum = lsum * alpha + pf_exp(sc, scale_log2, mb, pb);
+      pf_pv(kb + V_OFF, pb, lane, o);
     }
-    if (++buf == kPfStages) buf = 0;
+    if (++buf == S) buf = 0;
   }
   lsum += __shfl_xor(lsum, 32, 64);
   if (qrow >= L) return;
@@ -611,17 +706,30 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid((max_seqlen + kPfBQ - 1) / kPfBQ, nseq, Hq);
-  const size_t lds = (size_t)kPfStages * 2 * kPfBKV * D * 2;  // stages x (K | V) 32 KiB
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_kernel<128>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
+  // variant (BFLY_ATTN_PF_VARIANT, A/B timing): ring depth, priority, deferred rescale, buffer DMA.
+  // 16x1024 / 4x4096 / 1x16384 tokens (64 q / 8 kv heads): 390 / 537 / 740 TF/s (variant 1) ->
+  // 471 / 610 / 800 (variant 0); profiles/r2_attn_prefill_variants.log
+  const char* ev = getenv("BFLY_ATTN_PF_VARIANT");
+  const int var = ev ? atoi(ev) : 0;
+  const int* cuk = cu_k != nullptr ? cu_k : cu_seqlens;
+#define PF_VARIANT(ID, S_, PR_, DF_, BD_)                                                         \
+  if (var == ID) {                                                                                \
+    const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;                                           \
+    static bool attr = false;                                                                     \
+    if (!attr) {                                                                                  \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_kernel<128, S_, PR_, DF_, BD_>), \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
+      attr = true;                                                                                \
+    }                                                                                             \
+    attn_prefill_kernel<128, S_, PR_, DF_, BD_><<<grid, kPfThreads, lds, stream>>>(               \
+        q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cuk, Hq, Hkv, scale_log2, causal ? 1 : 0, \
+        out, o_stride, lse);                                                                      \
+    return 0;                                                                                     \
   }
-  attn_prefill_kernel<128><<<grid, kPfThreads, lds, stream>>>(
-      q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cu_k != nullptr ? cu_k : cu_seqlens, Hq, Hkv,
-      scale_log2, causal ? 1 : 0, out, o_stride, lse);
-  return 0;
+  PF_VARIANT(0, 3, true, true, true)      // default
+  PF_VARIANT(1, 4, false, false, false)   // round-1 kernel, for A/B
+#undef PF_VARIANT
+  return -5;
 }
 
 // K16: merge a partial attention result over another key chunk into running accumulators
