@@ -445,6 +445,18 @@ __device__ __forceinline__ float pf_exp(const f32x16 (&s)[2], float scale_log2, 
   return ps;
 }
 
+// pf_exp without the row sum (MFSUM: the sum comes from the matrix core, below).
+__device__ __forceinline__ void pf_exp_nosum(const f32x16 (&s)[2], float scale_log2, float mb,
+                                             bf16x8 (&pb)[2][2]) {
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        pb[kt][h][j] = f2bf(__builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][8 * h + j], scale_log2, -mb)));
+}
+
 // O^T[d][q] += V^T[d][key] P^T[key][q]; the A operand comes from transposed LDS reads.
 __device__ __forceinline__ void pf_pv(const char* vb, const bf16x8 (&pb)[2][2], int lane,
                                       f32x16 (&o)[4]) {
@@ -530,7 +542,7 @@ constexpr float kPfRescaleThr = 8.f;
 // Measured and dropped (profiles/r2_attn_prefill_variants.log): a 5-stage ring (-7 % on
 // 16k tokens), waves 4-7 running PV one tile late (-15..-25 %), a one-tile software pipeline
 // of QK(t+1) beside softmax(t) (spills at 256 VGPRs, -35 %).
-template <int D, int S, bool PRIO, bool DEFER, bool BUFDMA>
+template <int D, int S, bool PRIO, bool DEFER, bool BUFDMA, bool MFSUM>
 __global__ void __launch_bounds__(kPfThreads)
 attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
                     long k_stride, const bf16* __restrict__ v, long v_stride,
@@ -574,6 +586,11 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
   float m = kNegInf, lsum = 0.f;
+  // MFSUM: the softmax row sums as a fifth 32-row block of O^T whose A operand is all ones:
+  // 4 extra MFMAs per tile (the matrix pipe has slack) replace 32 f32 adds per lane (the VALU
+  // does not), and the sum is of the same bf16 P that multiplies V.
+  f32x16 osum = f32x16{};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
 
   const int kv_end = causal ? min(Lk, q0 + kPfBQ) : Lk;
   const int ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
@@ -617,15 +634,25 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
         m = mn;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        if (MFSUM) osum *= alpha;
       }
       const float mb = m == kNegInf ? 0.f : m;
       bf16x8 pb[2][2];
-      lsum = lsum * alpha + pf_exp(sc, scale_log2, mb, pb);
+      if (MFSUM) {
+        pf_exp_nosum(sc, scale_log2, mb, pb);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) osum = mfma32(ones, pb[kt][hh], osum);
+      } else {
+        lsum = lsum * alpha + pf_exp(sc, scale_log2, mb, pb);
+      }
       pf_pv(kb + V_OFF, pb, lane, o);
     }
     if (++buf == S) buf = 0;
   }
-  lsum += __shfl_xor(lsum, 32, 64);
+  if (MFSUM) lsum = osum[0];   // every row of the ones block holds the full key sum
+  else lsum += __shfl_xor(lsum, 32, 64);
   if (qrow >= L) return;
   // natural-log sum of exp(score * scale) over the visible keys (-inf: none), for merging
   // partial attention over key chunks (attn_lse_merge_kernel)
@@ -712,22 +739,23 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   const char* ev = getenv("BFLY_ATTN_PF_VARIANT");
   const int var = ev ? atoi(ev) : 0;
   const int* cuk = cu_k != nullptr ? cu_k : cu_seqlens;
-#define PF_VARIANT(ID, S_, PR_, DF_, BD_)                                                         \
+#define PF_VARIANT(ID, S_, PR_, DF_, BD_, MS_)                                                         \
   if (var == ID) {                                                                                \
     const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;                                           \
     static bool attr = false;                                                                     \
     if (!attr) {                                                                                  \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_kernel<128, S_, PR_, DF_, BD_>), \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_kernel<128, S_, PR_, DF_, BD_, MS_>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
       attr = true;                                                                                \
     }                                                                                             \
-    attn_prefill_kernel<128, S_, PR_, DF_, BD_><<<grid, kPfThreads, lds, stream>>>(               \
+    attn_prefill_kernel<128, S_, PR_, DF_, BD_, MS_><<<grid, kPfThreads, lds, stream>>>(               \
         q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cuk, Hq, Hkv, scale_log2, causal ? 1 : 0, \
         out, o_stride, lse);                                                                      \
     return 0;                                                                                     \
   }
-  PF_VARIANT(0, 3, true, true, true)      // default
-  PF_VARIANT(1, 4, false, false, false)   // round-1 kernel, for A/B
+  PF_VARIANT(0, 3, true, true, true, false)     // default
+  PF_VARIANT(1, 4, false, false, false, false)  // round-1 kernel, for A/B
+  PF_VARIANT(2, 3, true, true, true, true)      // row sums on the matrix core: neutral (+-1 %)
 #undef PF_VARIANT
   return -5;
 }
