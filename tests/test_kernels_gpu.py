@@ -592,3 +592,17 @@ def test_attn_prefill_long_vs_fp32(lens, Hq, Hkv, heads):
         err = (got - want[h]).abs().max().item()
         rel = ((got - want[h]).norm() / want[h].norm()).item()
         assert err < 3e-2 and rel < 1e-2, (h, err, rel)
+
+
+@pytest.mark.parametrize("epi", ["none", "silu"])
+def test_linear_large_m_library_path(epi, monkeypatch):
+    """Plain prefill GEMMs at M >= BFLY_GEMM_LIBRARY_MIN_M go to hipBLASLt (SwiGLU through our
+    interleaved silu_mul); same result as the fp32 reference and as our own big-tile kernel."""
+    monkeypatch.setattr(ops, "_LIB_MIN_M", 4096)
+    x, w = _bf(4096, 512, seed=90), _bf(1024, 512, seed=91, scale=0.05)
+    lib = ops.linear(x, w, epilogue=epi)
+    monkeypatch.setattr(ops, "_LIB_MIN_M", 1 << 62)
+    own = ops.linear(x, w, epilogue=epi)
+    want = ref.linear(x.float(), w.float(), epilogue=epi)
+    _close(lib, want, 3e-2, 3e-2)
+    _close(lib, own, 3e-2, 3e-2)
