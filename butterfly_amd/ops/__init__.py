@@ -260,7 +260,8 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     epilogue): when the plan splits K, return a `Partial` whose reduce the consumer fuses."""
     if not _gpu(x):
         return ref.linear(x, w, bias, epilogue, out)
-    if bias is None and x.shape[0] >= _library_min_m() and not torch.cuda.is_current_stream_capturing():
+    if (bias is None and epilogue == "none" and x.shape[0] >= _library_min_m()
+            and not torch.cuda.is_current_stream_capturing()):
         return _linear_library(x, w, epilogue, out)
     if defer and bias is None and epilogue == "none":
         M, N = x.shape[0], w.shape[0]
@@ -301,10 +302,12 @@ def _library_min_m() -> int:
 
 
 def _linear_library(x, w, epilogue: str, out):
-    """Plain prefill GEMM on hipBLASLt (torch.matmul): at M >= BFLY_GEMM_LIBRARY_MIN_M it runs
-    1.50-1.59 PF/s against 1.20-1.30 for gemm_big_kernel on the Llama-3-70B projections
-    (profiles/r2_gemm_prefill_vs_hipblaslt.log). The SwiGLU epilogue then runs as our
-    interleaved silu_mul kernel (one extra pass over the gate/up output, ~4 % of the GEMM)."""
+    """Plain (epilogue-free) prefill GEMM on hipBLASLt (torch.matmul): at M >= 6144 it runs
+    1.50-1.59 PF/s against 1.20-1.30 for gemm_big_kernel on the Llama-3-70B QKV / O / down
+    projections (profiles/r2_gemm_prefill_vs_hipblaslt.log). Fused ops stay on our kernels:
+    the SwiGLU gate/up GEMM (linear(..., epilogue="silu")) always runs gemm_big_kernel with the
+    activation in its epilogue, as do bias epilogues, split-K-deferred decode GEMMs and the MoE
+    grouped GEMMs. (`epilogue="silu"` here = hipBLASLt + our interleaved silu_mul, for A/B.)"""
     M, N = x.shape[0], w.shape[0]
     if epilogue == "none":
         if out is None:

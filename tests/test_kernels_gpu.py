@@ -596,11 +596,12 @@ def test_attn_prefill_long_vs_fp32(lens, Hq, Hkv, heads):
 
 @pytest.mark.parametrize("epi", ["none", "silu"])
 def test_linear_large_m_library_path(epi, monkeypatch):
-    """Plain prefill GEMMs at M >= BFLY_GEMM_LIBRARY_MIN_M go to hipBLASLt (SwiGLU through our
-    interleaved silu_mul); same result as the fp32 reference and as our own big-tile kernel."""
+    """Plain prefill GEMMs at M >= BFLY_GEMM_LIBRARY_MIN_M go to hipBLASLt (the A/B form of the
+    SwiGLU one: hipBLASLt + our interleaved silu_mul); same result as the fp32 reference and as
+    our own big-tile kernel, which linear() keeps for the fused SwiGLU GEMM."""
     monkeypatch.setattr(ops, "_LIB_MIN_M", 4096)
     x, w = _bf(4096, 512, seed=90), _bf(1024, 512, seed=91, scale=0.05)
-    lib = ops.linear(x, w, epilogue=epi)
+    lib = ops._linear_library(x, w, epi, None)
     monkeypatch.setattr(ops, "_LIB_MIN_M", 1 << 62)
     own = ops.linear(x, w, epilogue=epi)
     want = ref.linear(x.float(), w.float(), epilogue=epi)
