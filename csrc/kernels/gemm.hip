@@ -596,6 +596,9 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
 // distinct 16-B slots of the bank line (the DMA writes lane-linearly, so the swizzle is
 // applied on the per-lane SOURCE address). Tiles are walked in GROUP_M super-rows inside each
 // XCD's contiguous range, so the 32 CUs of an XCD share X and W panels in their L2.
+// Measured and dropped (profiles/r2_gemm_big_variants.log, M = 8192): splitting each K-step
+// into two 16-MFMA phases (finer ping-pong, each with half the fragment reads and DMA) -12..-16 %;
+// one static s_setprio 1 for the second wave group instead of the per-cluster flips -12..-17 %.
 // ---------------------------------------------------------------------------------------
 constexpr int kBigThreads = 512;
 constexpr int kBigBK = 32;
