@@ -26,6 +26,10 @@
 //    DMA writes lane-linearly; rule 21) which makes every ds_read_b128 lane group hit 16
 //    distinct bank slots; bijective XCD-aware tile remap (T1).
 #include "bfly_common.h"
+
+#include <cstdio>
+#include <string>
+#include <vector>
 #include "bfly_kernels.h"
 
 namespace bfly {
@@ -881,7 +885,40 @@ static bool tuned_enabled() {   // BFLY_GEMM_TUNED=0: heuristic plans only (A/B 
   return on;
 }
 
+// BFLY_GEMM_PLAN="N,K,Mbucket:kind,mt,nt,wk,bm,bn,sk;..." forces plans for whole-model A/B runs
+// (a shape's plan measured inside the decode step, where the neighbouring kernels and the
+// cache state differ from an isolated sweep). Parsed once.
+struct PlanOverride { int N, K, M; GemmPlan p; };
+static const std::vector<PlanOverride>& plan_overrides() {
+  static const std::vector<PlanOverride> v = [] {
+    std::vector<PlanOverride> out;
+    const char* e = getenv("BFLY_GEMM_PLAN");
+    if (!e) return out;
+    std::string s(e);
+    size_t pos = 0;
+    while (pos < s.size()) {
+      size_t end = s.find(';', pos);
+      if (end == std::string::npos) end = s.size();
+      PlanOverride o{};
+      if (sscanf(s.substr(pos, end - pos).c_str(), "%d,%d,%d:%d,%d,%d,%d,%d,%d,%d", &o.N, &o.K, &o.M, &o.p.kind,
+                 &o.p.mt, &o.p.nt, &o.p.wk, &o.p.bm, &o.p.bn, &o.p.sk) == 10)
+        out.push_back(o);
+      pos = end + 1;
+    }
+    return out;
+  }();
+  return v;
+}
+
 GemmPlan plan_gemm(int M, int N, int K) {
+  if (!plan_overrides().empty()) {
+    static const int kB[] = {1, 16, 32, 64, 128, 256, 512};
+    int bucket = 0;
+    for (int b : kB)
+      if (b >= M) { bucket = b; break; }
+    for (const PlanOverride& o : plan_overrides())
+      if (o.N == N && o.K == K && o.M == bucket) return o.p;
+  }
   if (!tuned_enabled()) return plan_gemm_heuristic(M, N, K);
   // token-count buckets of the sweep: M uses the entry of its bucket, or the heuristic plan
   // when the sweep found nothing better there
