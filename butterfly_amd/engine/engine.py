@@ -143,6 +143,19 @@ class LLMEngine:
         self._valued: Optional[PipePlan] = None    # advanced; token values applied next tick
         self._last_left: dict = {}                  # group -> its plan that left most recently
         self._sends: list = []
+        # boundary activations of the async pipeline (overlap executor): the
+        # receive of the group arriving next tick is posted at the end of this tick on a
+        # dedicated comm stream, into one of two persistent buffers; the compute stream waits
+        # on it only when that group's stage work starts, and a buffer is re-posted only after
+        # an event marks the compute that read it
+        self._prepost = bool(self.async_pp and coord.pp > 0 and flags.get("BFLY_PP_PREPOST")
+                             and self.comm.prepost_ok())
+        self._posted: dict = {}           # plan tick -> (buffer view, work, slot)
+        self._bbufs: list = []
+        self._bslot = 0
+        self._bevents: list = [None, None]
+        self._comm_stream = (torch.cuda.Stream(self.device)
+                             if self._prepost and self.device.type == "cuda" else None)
         d = self.model.dims
         self.sampler = Sampler(self.comm, cfg.vocab_size, d.vocab0, mesh.tp)
         if self.device.type == "cuda":
@@ -515,8 +528,33 @@ class LLMEngine:
             else:
                 leaving.host = leaving.ids
             self._pending = leaving
+        if self._prepost:
+            self._prepost_recv(k + 1 - s)
         out.seconds = time.perf_counter() - t0
         return out
+
+    def _prepost_recv(self, tick: int) -> None:
+        """Post the receive of the plan that enters this stage next tick (it entered stage 0 at
+        `tick` and is already in flight; its previous stage sent it this tick)."""
+        p = next((q for q in self._inflight if q.tick == tick), None)
+        if p is None or tick in self._posted:
+            return
+        H = self.cfg.hidden_size
+        if not self._bbufs:
+            rows = max(self.ecfg.max_prefill_tokens, self.ecfg.max_batch)
+            self._bbufs = [torch.empty(rows, H, dtype=self.model.dtype, device=self.device) for _ in range(2)]
+        slot = self._bslot
+        self._bslot ^= 1
+        buf = self._bbufs[slot][: p.tokens]
+        src = self.mesh.prev_stage(self.rank)
+        if self._comm_stream is not None:
+            if self._bevents[slot] is not None:      # the compute that read this buffer is done
+                self._comm_stream.wait_event(self._bevents[slot])
+            with torch.cuda.stream(self._comm_stream):
+                work = self.comm.irecv(buf, src)
+        else:
+            work = self.comm.irecv(buf, src)
+        self._posted[tick] = (buf, work, slot)
 
     def _advance(self, p: PipePlan) -> None:
         """Value-free part of applying a plan that left the pipeline: one more token per
@@ -598,8 +636,12 @@ class LLMEngine:
     def _pp_stage_work(self, p: PipePlan) -> None:
         """recv the residual stream (stage > 0) -> run this stage -> isend (not last) or sample
         (last stage: ids kept on the plan for the broadcast)."""
-        h = None
-        if not self.pp_first:
+        h, posted = None, self._posted.pop(p.tick, None)
+        if posted is not None:
+            h, work, slot = posted
+            work.wait()          # RCCL: the compute stream waits for the transfer, the host does not
+            self.metrics.inc("pp_preposted_recvs")
+        elif not self.pp_first:
             h = torch.empty(p.tokens, self.cfg.hidden_size, dtype=self.model.dtype, device=self.device)
             self.comm.recv(h, self.mesh.prev_stage(self.rank))
         if p.cow:
@@ -610,6 +652,10 @@ class LLMEngine:
             ids = self._first_stage_ids(p) if self.pp_first else np.zeros(len(p.rids), dtype=np.int32)
             inp = self.runner.decode_inputs(p.plan, ids)
             out = self.runner.run_decode(inp, h)
+        if posted is not None and self._comm_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record()          # after every kernel that reads the boundary buffer
+            self._bevents[posted[2]] = ev
         if not self.pp_last:
             snd = out.clone() if p.plan.kind == 2 else out   # graph outputs are reused by the next replay
             self._sends.append(self.comm.isend(self._maybe_poison(snd), self.mesh.next_stage(self.rank)))

@@ -233,6 +233,10 @@ class Communicator:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.pg)
         return [int(v) for v in t.tolist()]
 
+    def prepost_ok(self) -> bool:
+        """Receives may be posted ahead of their use (non-blocking, stream-ordered): RCCL."""
+        return self._world_nccl()
+
     def broadcast_ints(self, values: Optional[list], n: int, src_in_group: int, group: str = "dp") -> list:
         """Host list of n integers from one group rank to all (control plane: e.g. the prompt
         of an engine context-parallel step). Device-staged on RCCL, host tensors on gloo."""

@@ -45,6 +45,8 @@ define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the
 define("BFLY_GEMM_LIBRARY_MIN_M", 6144, int, "plain (epilogue-free) GEMMs with at least this many rows (prefill "
        "QKV / O / down) run on hipBLASLt; fused GEMMs (SwiGLU, bias) always run the HIP kernels; 0 = never")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
+define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
+       "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
 define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism: the residual stream and the norms are "
        "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
 define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")

@@ -8,6 +8,7 @@ from butterfly_amd.config import EngineConfig, ModelConfig
 from butterfly_amd.engine.engine import LLMEngine
 from butterfly_amd.engine.sampler import SamplingParams
 from butterfly_amd.parallel.fake import FakeWorld
+from butterfly_amd.parallel.mesh import Mesh
 from butterfly_amd.partition import partition
 from butterfly_amd.partition.schedule import Instr, check_programs, link_bytes, programs
 from butterfly_amd.partition.search import factorizations
@@ -106,3 +107,44 @@ def test_program_matches_engine(preset, kw, pp_async, monkeypatch):
         for (op, _, nb), i in zip(got, want):
             # every payload, EP dispatch / sampling gather / broadcast included
             assert nb == i.nbytes, (r, op, nb, i)
+
+
+def _generate_prepost(rank, comm, preset, mesh, stages):
+    cfg = ModelConfig.from_preset(preset)
+    ecfg = EngineConfig(max_batch=8, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu", stage_layers=stages)
+    rids = [eng.add_request(p, SamplingParams(max_tokens=3 + 2 * i, ignore_eos=True)) for i, p in enumerate(PROMPTS)]
+    while eng.has_unfinished():
+        eng.step()
+    return [eng.requests[r].output for r in rids], eng.metrics.counters.get("pp_preposted_recvs", 0), eng._prepost
+
+
+@pytest.mark.parametrize("preset,kw", [("llama-tiny", dict(pp=2)), ("llama-tiny", dict(tp=2, pp=2)),
+                                       ("llama-small", dict(pp=4))])
+def test_async_pipeline_preposted_receives(preset, kw, monkeypatch):
+    """Overlap executor (engine._prepost_recv): every non-first stage posts the boundary receive
+    of the group arriving next tick at the end of the current tick, into one of two persistent
+    buffers. On the loopback backend (its irecv completes on the spot, so a receive posted
+    too early or out of order would hang or mismatch shapes) the tokens must equal the
+    single-process engine's and almost every stage tick must have used a pre-posted receive."""
+    monkeypatch.setenv("BFLY_PP_ASYNC", "1")
+    monkeypatch.setenv("BFLY_PP_PREPOST", "1")
+    torch.set_num_threads(1)
+    cfg = ModelConfig.from_preset(preset)
+    ecfg = EngineConfig(max_batch=8, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    single = LLMEngine(cfg, Mesh(), ecfg, device="cpu")
+    rids = [single.add_request(p, SamplingParams(max_tokens=3 + 2 * i, ignore_eos=True)) for i, p in enumerate(PROMPTS)]
+    while single.has_unfinished():
+        single.step()
+    want = [single.requests[r].output for r in rids]
+    n = kw.get("tp", 1) * kw["pp"]
+    plan = partition(cfg, n, kw, batch_per_gpu=8)
+    mesh = plan.mesh
+    world = FakeWorld(mesh, timeout_s=60)
+    outs = world.run(lambda r, c: _generate_prepost(r, c, preset, mesh, plan.stages))
+    for r, (toks, used, on) in enumerate(outs):
+        assert toks == want
+        first = mesh.coord(r).pp == 0
+        assert on == (not first)
+        if not first:
+            assert used > 0
