@@ -98,7 +98,16 @@ def cmd_launch(a) -> int:
     if not cmd:
         print("launch: missing program", file=sys.stderr)
         return 2
-    return launch(cmd, a.nproc, a.master_port)
+    placement = None
+    if a.plan:
+        from .partition import PartitionPlan
+
+        plan = PartitionPlan.from_json(open(a.plan).read())
+        if plan.n_gpus != a.nproc:
+            print(f"launch: plan is for {plan.n_gpus} GPUs, -n {a.nproc}", file=sys.stderr)
+            return 2
+        placement = plan.placement or None
+    return launch(cmd, a.nproc, a.master_port, placement=placement)
 
 
 def cmd_ckpt(a) -> int:
@@ -182,6 +191,7 @@ def main(argv=None) -> int:
     la = sub.add_parser("launch")
     la.add_argument("-n", "--nproc", type=int, default=1)
     la.add_argument("--master-port", type=int, default=None)
+    la.add_argument("--plan", default=None, help="PartitionPlan JSON: its placement maps ranks to GPUs")
     la.add_argument("cmd", nargs=argparse.REMAINDER)
     la.set_defaults(fn=cmd_launch)
     c = sub.add_parser("ckpt")

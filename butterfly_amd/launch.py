@@ -5,6 +5,11 @@ LOCAL_RANK, MASTER_ADDR=127.0.0.1, MASTER_PORT, HSA_ENABLE_IPC_MODE_LEGACY=0 for
 prefixes each child's output with its rank, and fails fast: when any rank exits non-zero the
 others are terminated and the launcher returns that code. The launcher itself never touches
 the GPU, so it can start GPU programs safely.
+
+`placement` (a PartitionPlan's mesh rank -> GPU index map, `launch --plan plan.json`) sets each
+rank's LOCAL_RANK, the device index every entry point binds (init_distributed -> set_device and
+the RCCL communicator's device). The partitioner emits the identity on the fully connected
+xGMI mesh (partition/search.py), but a hand-edited plan is honoured.
 """
 from __future__ import annotations
 
@@ -30,12 +35,15 @@ def _pump(stream, prefix: str, out) -> None:
 
 
 def launch(cmd: list, nproc: int, master_port: int | None = None, env_extra: dict | None = None,
-           prefix_output: bool = True) -> int:
+           prefix_output: bool = True, placement: list | None = None) -> int:
+    if placement is not None and sorted(placement) != list(range(nproc)):
+        raise ValueError(f"placement {placement} is not a permutation of 0..{nproc - 1}")
     port = master_port or _free_port()
     procs = []
     for r in range(nproc):
         env = dict(os.environ)
-        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+        dev = placement[r] if placement is not None else r
+        env.update(RANK=str(r), LOCAL_RANK=str(dev), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         env.update(env_extra or {})
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if prefix_output else None,

@@ -97,3 +97,24 @@ def test_peer_exit_fails_survivor_within_timeout():
                 p.kill()
     assert rc1 == 13 and rc0 != 0
     assert time.time() - t0 < 120
+
+
+def test_launch_honours_plan_placement(tmp_path):
+    """`launch --plan` binds rank r to GPU placement[r] through LOCAL_RANK (the device index
+    init_distributed and the RCCL communicator use); the launcher never touches the GPU."""
+    import subprocess
+    import sys
+
+    from butterfly_amd.config import ModelConfig
+    from butterfly_amd.partition import partition
+
+    plan = partition(ModelConfig.from_preset("llama-tiny"), 2, {"tp": 2})
+    plan.placement = [1, 0]
+    pf = tmp_path / "plan.json"
+    pf.write_text(plan.to_json())
+    prog = "import os; print('R', os.environ['RANK'], 'L', os.environ['LOCAL_RANK'])"
+    r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", "2", "--plan", str(pf), "--",
+                        sys.executable, "-c", prog], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = sorted(l.split("] ", 1)[1] for l in r.stdout.splitlines() if "] R " in l)
+    assert got == ["R 0 L 1", "R 1 L 0"], r.stdout
