@@ -265,16 +265,12 @@ class LLMEngine:
         return t
 
     def _sample(self, logits: torch.Tensor, rids: list) -> torch.Tensor:
-        """Sample one token per row. With BFLY_NAN_CHECK the logits are also checked for
-        non-finite values (one reduction over the local vocab shard, no host sync); a poisoned
-        or corrupted step then raises in _apply_tokens instead of emitting garbage tokens."""
+        """Sample one token per row. With BFLY_NAN_CHECK the sampling kernel also flags rows
+        with non-finite logits (id -1, no extra kernel, no host sync); a poisoned or corrupted
+        step then raises in _apply_tokens instead of emitting garbage tokens."""
         logits = self._maybe_poison(logits)
         temps, seeds, params = self._sample_params(rids)
-        ids = self.sampler.sample(logits, temps, seeds, params)
-        if self.nan_check and logits.numel():
-            # no host sync here: a bad step marks its ids -1, _apply_tokens raises on them
-            ids = ids.masked_fill(~torch.isfinite(logits).all(), -1)
-        return ids
+        return self.sampler.sample(logits, temps, seeds, params, check_finite=bool(self.nan_check))
 
     def _step(self) -> StepOutput:
         t0 = time.perf_counter()

@@ -54,12 +54,15 @@ class Sampler:
         return logits[:, :n]
 
     def sample(self, logits: torch.Tensor, temps: Optional[torch.Tensor] = None,
-               seeds: Optional[torch.Tensor] = None, params: Optional[list] = None) -> torch.Tensor:
-        """logits: [R, vocab_local]. Returns int32 token ids [R] (identical on every TP rank)."""
+               seeds: Optional[torch.Tensor] = None, params: Optional[list] = None,
+               check_finite: bool = False) -> torch.Tensor:
+        """logits: [R, vocab_local]. Returns int32 token ids [R] (identical on every TP rank).
+        `check_finite`: a row with an Inf / NaN logit on any TP rank samples -1 on every rank
+        (the kernel scores it +inf, so it wins the TP merge)."""
         if params and any(p.needs_filter for p in params):
-            return self._sample_filtered(logits, params, seeds)
+            return self._sample_filtered(logits, params, seeds, check_finite)
         lv = self._local_valid(logits)
-        ids, scores = ops.sample(lv, temps, seeds, vstart=self.vocab_start)
+        ids, scores = ops.sample(lv, temps, seeds, vstart=self.vocab_start, check_finite=check_finite)
         if self.tp == 1:
             return ids
         pair = torch.stack([scores, ids.to(torch.float32)], 1)        # ids < 2^24: exact in f32
@@ -103,14 +106,15 @@ class Sampler:
         # tolerance: the kernel scales by a reciprocal multiply, torch above by a division
         return thr - 1e-5 * thr.abs() - 1e-6
 
-    def _sample_filtered(self, logits, params, seeds):
+    def _sample_filtered(self, logits, params, seeds, check_finite: bool = False):
         lv = self._local_valid(logits)
         R = lv.shape[0]
         temps = torch.tensor([p.temperature for p in params], dtype=torch.float32).to(lv.device)
         if seeds is None:
             seeds = torch.zeros(R, dtype=torch.int64, device=lv.device)
         thr = self.thresholds(lv, temps, params)
-        ids, scores = ops.sample(lv, temps, seeds, vstart=self.vocab_start, thresh=thr.contiguous())
+        ids, scores = ops.sample(lv, temps, seeds, vstart=self.vocab_start, thresh=thr.contiguous(),
+                                 check_finite=check_finite)
         if self.tp == 1:
             return ids
         pair = torch.stack([scores, ids.to(torch.float32)], 1)

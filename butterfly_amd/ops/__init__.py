@@ -239,18 +239,20 @@ def embed(ids, table, vstart: int = 0, out=None):
     return out
 
 
-def sample(logits, temps=None, seeds=None, vstart: int = 0, out_ids=None, out_scores=None, thresh=None):
+def sample(logits, temps=None, seeds=None, vstart: int = 0, out_ids=None, out_scores=None, thresh=None,
+           check_finite: bool = False):
     """Greedy / Gumbel-max sampling over a (vocab-shard of) logits -> (ids int32, scores f32).
-    `thresh` [rows] f32: per-row lower bound on logit / temperature (top-k / top-p filter)."""
+    `thresh` [rows] f32: per-row lower bound on logit / temperature (top-k / top-p filter).
+    `check_finite`: rows with an Inf / NaN logit get id -1 and score +inf (the NaN guard)."""
     if not _gpu(logits):
-        return ref.sample(logits, temps, seeds, vstart, thresh)
+        return ref.sample(logits, temps, seeds, vstart, thresh, check_finite)
     rows = logits.shape[0]
     if out_ids is None:
         out_ids = torch.empty(rows, dtype=torch.int32, device=logits.device)
     if out_scores is None:
         out_scores = torch.empty(rows, dtype=torch.float32, device=logits.device)
     ws = _arena.get(logits.device, "sample", rows * 64, torch.int64)
-    torch.ops.bfly.sample(logits, temps, seeds, vstart, out_ids, out_scores, ws, thresh)
+    torch.ops.bfly.sample(logits, temps, seeds, vstart, out_ids, out_scores, ws, thresh, check_finite)
     return out_ids, out_scores
 
 

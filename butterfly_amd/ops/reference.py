@@ -176,13 +176,18 @@ def gumbel_uniform(seed: int, idx: torch.Tensor) -> torch.Tensor:
     return torch.tensor(out, dtype=torch.float32)
 
 
-def sample(logits, temps=None, seeds=None, vstart=0, thresh=None):
+def sample(logits, temps=None, seeds=None, vstart=0, thresh=None, check_finite=False):
     """Greedy (temp <= 0) or Gumbel-max temperature sampling; returns (ids int32, scores f32).
-    `thresh[r]`: tokens whose logit / temperature is below it are excluded (top-k / top-p)."""
+    `thresh[r]`: tokens whose logit / temperature is below it are excluded (top-k / top-p).
+    `check_finite`: a row with an Inf / NaN logit gives id -1, score +inf."""
     lf = logits.float()
     rows, V = lf.shape
     ids, scores = [], []
     for r in range(rows):
+        if check_finite and not bool(torch.isfinite(lf[r]).all()):
+            ids.append(-1)
+            scores.append(float("inf"))
+            continue
         t = float(temps[r]) if temps is not None else 0.0
         s = lf[r]
         if t > 0:

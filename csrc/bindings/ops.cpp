@@ -193,7 +193,8 @@ void embed(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) 
 
 void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
             const c10::optional<Tensor>& seeds, int64_t vstart, Tensor& out_ids,
-            Tensor& out_scores, Tensor& workspace, const c10::optional<Tensor>& thresh) {
+            Tensor& out_scores, Tensor& workspace, const c10::optional<Tensor>& thresh,
+            bool check_finite) {
   CHECK_GPU(logits); CHECK_BF16(logits);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0, "sample: logits");
   CHECK_ALIGN16(logits);
@@ -222,7 +223,7 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
   c10::DeviceGuard g(logits.device());
   bfly::launch_sample(bf(logits), logits.stride(0), rows, V, vstart, tp, sp,
                       reinterpret_cast<uint64_t*>(workspace.data_ptr()), out_ids.data_ptr<int>(),
-                      out_scores.data_ptr<float>(), cur_stream(), thp);
+                      out_scores.data_ptr<float>(), cur_stream(), thp, check_finite ? 1 : 0);
 }
 
 int64_t gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
@@ -701,7 +702,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("init_hash(Tensor(a!) out, int grow0, int gcol0, int gcols, int seed, float amp) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vstart) -> ()");
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
-        "Tensor(b!) out_scores, Tensor(c!) workspace, Tensor? thresh=None) -> ()");
+        "Tensor(b!) out_scores, Tensor(c!) workspace, Tensor? thresh=None, bool check_finite=False) -> ()");
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace, "
         "Tensor? bias=None) -> ()");

@@ -54,7 +54,8 @@ void launch_embed(const int* ids, const bf16* table, bf16* out, int T, int dim, 
 constexpr int kSampleMaxChunks = 64;
 void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vstart,
                    const float* temps, const long* seeds, uint64_t* workspace, int* out_ids,
-                   float* out_scores, hipStream_t stream, const float* thresh = nullptr);
+                   float* out_scores, hipStream_t stream, const float* thresh = nullptr,
+                   int check_finite = 0);
 
 // gemm.hip
 GemmPlan plan_gemm(int M, int N, int K);

@@ -8,6 +8,9 @@
 // max: scores are comparable across ranks because the Gumbel noise is keyed on the GLOBAL
 // vocab index and the per-row seed, not on the rank.
 //
+// check_finite: a row whose logits shard holds an Inf or NaN yields id -1 and score +inf (so
+// it also wins the TP merge on every rank): the engine's NaN guard without extra kernels.
+//
 // Top-k / top-p: `thresh[row]` (optional) is a lower bound on the temperature-scaled logit;
 // tokens below it are excluded before the Gumbel-max. Gumbel-max over the kept set samples
 // exactly the renormalised truncated distribution, so filtering reduces to one threshold per
@@ -54,8 +57,10 @@ __global__ void __launch_bounds__(kSampleThreads)
 sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, int chunk,
                       int vstart, const float* __restrict__ temps,
                       const long* __restrict__ seeds, const float* __restrict__ thresh,
-                      uint64_t* __restrict__ partial) {
+                      uint64_t* __restrict__ partial, int check_finite) {
   __shared__ uint64_t red[kSampleThreads / 64];
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) s_bad = 0;
   const int row = blockIdx.x, c = blockIdx.y;
   const float temp = temps ? temps[row] : 0.f;
   const bool greedy = temp <= 0.f;
@@ -65,11 +70,13 @@ sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, i
   const int begin = c * chunk, end = min(V, begin + chunk);
   const bf16* lr = logits + (long)row * row_stride;
   uint64_t best = 0;
+  uint32_t nonfinite = 0;   // OR of exponent-all-ones tests (Inf / NaN bf16)
   for (int i = begin + threadIdx.x * 8; i < end; i += kSampleThreads * 8) {
     if (i + 8 <= end) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(lr + i);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+        nonfinite |= (uint32_t)((__builtin_bit_cast(uint16_t, v[j]) & 0x7F80u) == 0x7F80u);
         float s = bf2f(v[j]);
         if (!greedy) {
           s = s * inv_t;
@@ -81,6 +88,7 @@ sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, i
       }
     } else {
       for (int j = 0; i + j < end; ++j) {
+        nonfinite |= (uint32_t)((__builtin_bit_cast(uint16_t, lr[i + j]) & 0x7F80u) == 0x7F80u);
         float s = bf2f(lr[i + j]);
         if (!greedy) {
           s = s * inv_t;
@@ -94,11 +102,13 @@ sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, i
   }
   best = wave_max_u64(best);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();   // also orders s_bad's initialisation before the atomics below
+  if (check_finite && nonfinite) atomicOr(&s_bad, 1);
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t b = red[0];
     for (int w = 1; w < kSampleThreads / 64; ++w) b = umax64(b, red[w]);
-    partial[(long)row * gridDim.y + c] = b;
+    partial[(long)row * gridDim.y + c] = s_bad ? ~0ULL : b;   // ~0: a NaN key, never a real one
   }
 }
 
@@ -109,14 +119,15 @@ __global__ void sample_final_kernel(const uint64_t* __restrict__ partial, int ch
   for (int c = threadIdx.x; c < chunks; c += 64) b = umax64(b, partial[(long)row * chunks + c]);
   b = wave_max_u64(b);
   if (threadIdx.x == 0) {
-    out_ids[row] = (int)(~(uint32_t)b);
-    if (out_scores) out_scores[row] = unordered_f32((uint32_t)(b >> 32));
+    const bool bad = b == ~0ULL;
+    out_ids[row] = bad ? -1 : (int)(~(uint32_t)b);
+    if (out_scores) out_scores[row] = bad ? INFINITY : unordered_f32((uint32_t)(b >> 32));
   }
 }
 
 void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vstart,
                    const float* temps, const long* seeds, uint64_t* workspace, int* out_ids,
-                   float* out_scores, hipStream_t stream, const float* thresh) {
+                   float* out_scores, hipStream_t stream, const float* thresh, int check_finite) {
   if (rows <= 0) return;
   int chunks = (V + 4095) / 4096;
   if (chunks > kSampleMaxChunks) chunks = kSampleMaxChunks;
@@ -125,7 +136,7 @@ void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vst
   chunks = (V + chunk - 1) / chunk;
   dim3 g1(rows, chunks);
   sample_partial_kernel<<<g1, kSampleThreads, 0, stream>>>(logits, row_stride, V, chunk, vstart,
-                                                           temps, seeds, thresh, workspace);
+                                                           temps, seeds, thresh, workspace, check_finite);
   sample_final_kernel<<<rows, 64, 0, stream>>>(workspace, chunks, out_ids, out_scores);
 }
 

@@ -607,3 +607,21 @@ def test_linear_large_m_library_path(epi, monkeypatch):
     want = ref.linear(x.float(), w.float(), epilogue=epi)
     _close(lib, want, 3e-2, 3e-2)
     _close(lib, own, 3e-2, 3e-2)
+
+
+def test_sample_check_finite():
+    """The NaN guard inside the sampling kernels: rows with an Inf / NaN logit give id -1 and
+    score +inf, every other row samples exactly as without the check."""
+    lg = _bf(6, 50000, seed=95)
+    lg[1, 777] = float("nan")
+    lg[4, 49999] = float("inf")
+    temps = torch.tensor([0.0, 0.0, 0.7, 0.0, 1.0, 0.9], device=DEV)
+    seeds = torch.arange(6, dtype=torch.int64, device=DEV) * 7 + 1
+    ids, sc = ops.sample(lg, temps, seeds, check_finite=True)
+    ids0, sc0 = ops.sample(lg, temps, seeds)
+    ids, sc, ids0 = ids.cpu(), sc.cpu(), ids0.cpu()
+    assert ids[1] == -1 and ids[4] == -1 and torch.isinf(sc[1]) and torch.isinf(sc[4])
+    keep = [0, 2, 3, 5]
+    assert torch.equal(ids[keep], ids0[keep])
+    rid, _ = ref.sample(lg.cpu(), temps.cpu(), seeds.cpu(), 0, None, True)
+    assert torch.equal(rid.cpu(), ids)
