@@ -73,10 +73,13 @@ sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, i
   uint32_t nonfinite = 0;   // OR of exponent-all-ones tests (Inf / NaN bf16)
   for (int i = begin + threadIdx.x * 8; i < end; i += kSampleThreads * 8) {
     if (i + 8 <= end) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lr + i);
+      const u32x4 raw = *reinterpret_cast<const u32x4*>(lr + i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)   // bf16 exponent all ones: Inf or NaN
+        nonfinite |= (uint32_t)((raw[k] & 0x7F80u) == 0x7F80u) | (uint32_t)((raw[k] & 0x7F800000u) == 0x7F800000u);
+      const bf16x8 v = __builtin_bit_cast(bf16x8, raw);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        nonfinite |= (uint32_t)((__builtin_bit_cast(uint16_t, v[j]) & 0x7F80u) == 0x7F80u);
         float s = bf2f(v[j]);
         if (!greedy) {
           s = s * inv_t;
@@ -88,7 +91,8 @@ sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, i
       }
     } else {
       for (int j = 0; i + j < end; ++j) {
-        nonfinite |= (uint32_t)((__builtin_bit_cast(uint16_t, lr[i + j]) & 0x7F80u) == 0x7F80u);
+        const uint32_t bits = reinterpret_cast<const uint16_t*>(lr)[i + j];
+        nonfinite |= (uint32_t)((bits & 0x7F80u) == 0x7F80u);
         float s = bf2f(lr[i + j]);
         if (!greedy) {
           s = s * inv_t;
