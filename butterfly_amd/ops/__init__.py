@@ -377,6 +377,38 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_c
     return out
 
 
+def attn_decode_rope(qkv, positions, cos, sin, slots, k_cache, v_cache, block_tables, ctx_lens,
+                     n_q: int, scale: float, max_ctx: int, part_tokens: int = DECODE_PART_TOKENS, out=None):
+    """rope_kv + attn_decode in one kernel for a decode step: `qkv` [B, (Hq + 2 Hkv) D] is the
+    QKV projection output (or a deferred split-K `Partial` of it, reduced in the kernel); the
+    new token's K/V are written at `slots` and attention runs over the cached positions plus
+    the new token. Returns attention out [B, Hq, D]. bf16 caches only."""
+    if isinstance(qkv, Partial):
+        rows, slabs = qkv.out, qkv.slabs
+    else:
+        rows, slabs = qkv, None
+    if not _gpu(rows):
+        rows = ref.rope_kv(rows, positions, cos, sin, n_q, k_cache.shape[1], slots, k_cache, v_cache)
+        B, D = rows.shape[0], k_cache.shape[3]
+        q = rows[:, : n_q * D].view(B, n_q, D)
+        return ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx, part_tokens, out)
+    B, Hkv, D = rows.shape[0], k_cache.shape[1], k_cache.shape[3]
+    if out is None:
+        out = torch.empty(B, n_q, D, dtype=rows.dtype, device=rows.device)
+    if part_tokens <= 0:
+        part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
+    ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
+    po = pml = cnt = None
+    if ns > 1:
+        po = _arena.get(rows.device, "attn_o", B * Hkv * ns * 16 * D, torch.float32)
+        pml = _arena.get(rows.device, "attn_ml", B * Hkv * ns * 16 * 2, torch.float32)
+        if FUSED_DECODE_COMBINE:
+            cnt = _arena.get(rows.device, "attn_cnt", B * Hkv, torch.int32, zero=True)
+    torch.ops.bfly.attn_decode_rope(rows, slabs, positions, cos, sin, slots, k_cache, v_cache, block_tables,
+                                    ctx_lens, n_q, scale, max_ctx, part_tokens, out, po, pml, cnt)
+    return out
+
+
 def init_hash_(out, grow0: int, gcol0: int, gcols: int, seed: int, amp: float):
     """Fill a 2-D (view of a) weight shard with partition-independent hashed uniform values."""
     if not _gpu(out):

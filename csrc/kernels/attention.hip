@@ -85,14 +85,53 @@ __device__ __forceinline__ void decode_split_done(const float* __restrict__ part
   }
 }
 
-template <int D, int BS, typename CT>
+// Fused decode prologue (FUSED): the kernel takes the QKV projection's row (bf16, or the f32
+// split-K slabs of the QKV GEMM, reduced here), applies RoPE to its query fragments in
+// registers (the rotate-half partner of every d the lane holds is in the lane's own fragments),
+// attends over the CACHED keys only (positions < ctx - 1), and the workgroup whose split holds
+// position ctx - 1 adds the new token's key/value analytically and writes them into their cache
+// page. That replaces the rope_kv launch before every decode attention (its kernel, its
+// boundary, and the round trip of q through memory). Numerics follow rope_kv exactly: the
+// row is rounded to bf16 before the rotation, the rotated values to bf16 after it.
+struct DecRope {
+  const bf16* qkv;          // [B, (Hq + 2 Hkv) D] bf16 (when part == nullptr)
+  const float* part;        // or the QKV GEMM's split-K slabs [sk][B][(Hq + 2 Hkv) D]
+  int sk;
+  long slab;
+  const int* positions;     // [B]
+  const float* cos_t;       // [max_pos, D/2]
+  const float* sin_t;
+  const int* slots;         // [B] cache slot of the new token (< 0: do not cache)
+  void* k_w;                // the caches (written at the new token's slot)
+  void* v_w;
+};
+
+// 8 consecutive values of one QKV row as floats, rounded to bf16 (the value rope_kv would see)
+__device__ __forceinline__ void dec_row8(const DecRope& rp, long row_off, int col, float (&x)[8]) {
+  if (rp.part) {
+    const float* pr = rp.part + row_off + col;
+    f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+    for (int k = 1; k < rp.sk; ++k) {
+      lo += *reinterpret_cast<const f32x4*>(pr + k * rp.slab);
+      hi += *reinterpret_cast<const f32x4*>(pr + k * rp.slab + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { x[j] = bf2f(f2bf(lo[j])); x[j + 4] = bf2f(f2bf(hi[j])); }
+  } else {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(rp.qkv + row_off + col);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = bf2f(v[j]);
+  }
+}
+
+template <int D, int BS, typename CT, bool FUSED = false>
 __global__ void __launch_bounds__(kAttnThreads)
 attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restrict__ k_cache,
                    const CT* __restrict__ v_cache, const int* __restrict__ block_tables,
                    int bt_stride, const int* __restrict__ ctx_lens, int Hq, int Hkv,
                    float scale_log2, int part_tokens, bf16* __restrict__ out,
                    float* __restrict__ part_o, float* __restrict__ part_ml,
-                   int* __restrict__ counters) {
+                   int* __restrict__ counters, DecRope rp = DecRope{}) {
   static_assert(D == 128 && BS == 32, "decode kernel is specialised for D=128, BS=32");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -100,14 +139,17 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   const int G = Hq / Hkv;
   const int ctx = ctx_lens[b];
   const int tok0 = s * part_tokens;
-  const int tok1 = min(ctx, tok0 + part_tokens);
+  // FUSED: the cache holds positions < ctx - 1; the new token (ctx - 1) is added separately
+  const int tok1 = min(FUSED ? ctx - 1 : ctx, tok0 + part_tokens);
+  const bool has_new = FUSED && ctx > 0 && ctx - 1 >= tok0 && ctx - 1 < tok0 + part_tokens;
   const long part_base = ((long)(b * Hkv + h) * nsplit + s);
 
   __shared__ float s_o[4][8][4][64];
   __shared__ float s_m[4][16], s_l[4][16];
+  __shared__ float s_snew[16], s_vnew[D];
   __shared__ int s_last;
 
-  if (tok0 >= tok1) {  // empty split: mark it so the combine skips it
+  if (tok0 >= tok1 && !has_new) {  // empty split: mark it so the combine skips it
     if (nsplit > 1 && threadIdx.x < 16) {
       part_ml[(part_base * 16 + threadIdx.x) * 2 + 0] = kNegInf;
       part_ml[(part_base * 16 + threadIdx.x) * 2 + 1] = 0.f;
@@ -126,7 +168,62 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   auto d_off = [&](int ds) { return kF8 ? 64 * (ds >> 1) + 16 * g + 8 * (ds & 1) : 32 * ds + 8 * g; };
   // Q^T fragment (B operand): lane holds Q[row r][d]; rows >= G are zero.
   bf16x8 qf[4];
-  {
+  if constexpr (FUSED) {
+    // RoPE in registers: d_off(ds) and d_off(ds + 2) = d_off(ds) + 64 are rotation partners
+    const int qr = r < G ? r : 0;
+    const long row_off = (long)b * (Hq + 2 * Hkv) * D;
+    const int pos = rp.positions[b];
+    const float* cr = rp.cos_t + (long)pos * (D / 2);
+    const float* sr = rp.sin_t + (long)pos * (D / 2);
+    auto rot = [&](int col0, bf16x8 (&f)[4]) {
+      float x[4][8];
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) dec_row8(rp, row_off, col0 + d_off(ds), x[ds]);
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float c = cr[d_off(ds) + j], sn = sr[d_off(ds) + j];
+          f[ds][j] = f2bf(x[ds][j] * c - x[ds + 2][j] * sn);
+          f[ds + 2][j] = f2bf(x[ds + 2][j] * c + x[ds][j] * sn);
+        }
+    };
+    rot((h * G + qr) * D, qf);
+    if (r >= G)
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) qf[ds] = bf16x8{};
+    if (has_new && wid == 0) {
+      // the new token's key: rotated like the queries, dotted with every query row here
+      bf16x8 kn[4];
+      rot((Hq + h) * D, kn);
+      float dot = 0.f;
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += bf2f(qf[ds][j]) * bf2f(kn[ds][j]);
+      dot += __shfl_xor(dot, 16, 64);
+      dot += __shfl_xor(dot, 32, 64);
+      if (g == 0) s_snew[r] = r < G ? dot * scale_log2 : kNegInf;
+      const int slot = rp.slots ? rp.slots[b] : -1;
+      if (slot >= 0 && r == 0) {   // lanes g = 0..3 hold all 128 d of the key
+        CT* kp = static_cast<CT*>(rp.k_w) + (((long)(slot / BS) * Hkv + h) * BS + slot % BS) * D;
+#pragma unroll
+        for (int ds = 0; ds < 4; ++ds) KV<CT>::store8(kp + d_off(ds), kn[ds]);
+      }
+    }
+    if (has_new && threadIdx.x < D / 8) {   // the new token's value (transposed V page)
+      float x[8];
+      const int d0 = threadIdx.x * 8;
+      dec_row8(rp, row_off, (Hq + Hkv + h) * D + d0, x);
+      const int slot = rp.slots ? rp.slots[b] : -1;
+      CT* vp = slot >= 0 ? static_cast<CT*>(rp.v_w) + ((long)(slot / BS) * Hkv + h) * D * BS + slot % BS : nullptr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s_vnew[d0 + j] = x[j];
+        if (vp) KV<CT>::store1(vp + (long)(d0 + j) * BS, f2bf(x[j]));
+      }
+    }
+  } else {
     const int qr = r < G ? r : 0;
     const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D;
 #pragma unroll
@@ -267,6 +364,7 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
     float M = kNegInf;
 #pragma unroll
     for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][qr]);
+    if (has_new) M = fmaxf(M, s_snew[qr]);
     const float Mb = M == kNegInf ? 0.f : M;
     float L = 0.f, O = 0.f;
     const int dt = d >> 4, i = d & 3, ln = qr + 16 * ((d & 15) >> 2);
@@ -275,6 +373,11 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
       const float f = exp2f(s_m[w][qr] - Mb);
       L += f * s_l[w][qr];
       O += f * s_o[w][dt][i][ln];
+    }
+    if (has_new) {   // p of the new key, rounded to bf16 like every P that meets V
+      const float pn = bf2f(f2bf(exp2f(s_snew[qr] - Mb)));
+      L += pn;
+      O += pn * bf2f(f2bf(s_vnew[d]));
     }
     if (nsplit == 1) {
       out[((long)b * Hq + h * G + qr) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
@@ -699,9 +802,10 @@ int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const 
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
                        bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                       int* counters, int kv_fp8) {
+                       int* counters, int kv_fp8, const DecRope* rope) {
   if (B <= 0) return 0;
   if (D != 128 || block_size != 32 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
+  if (rope != nullptr && kv_fp8) return -6;   // fused RoPE: bf16 caches only
   if (part_tokens <= 0) part_tokens = attn_decode_part_tokens(B, Hkv, max_ctx);
   if (part_tokens % block_size != 0) return -2;
   if (attn_decode_splits(max_ctx, part_tokens) > 256) return -4;
@@ -710,7 +814,11 @@ int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const 
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(nsplit, Hkv, B);
   int* cnt = nsplit > 1 ? counters : nullptr;
-  if (kv_fp8)
+  if (rope != nullptr)
+    attn_decode_kernel<128, 32, bf16, true><<<grid, kAttnThreads, 0, stream>>>(
+        q, q_stride, static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), block_tables,
+        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, cnt, *rope);
+  else if (kv_fp8)
     attn_decode_kernel<128, 32, fp8_t><<<grid, kAttnThreads, 0, stream>>>(
         q, q_stride, static_cast<const fp8_t*>(k_cache), static_cast<const fp8_t*>(v_cache), block_tables,
         bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, cnt);
@@ -723,6 +831,28 @@ int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const 
     attn_decode_combine_kernel<128><<<g2, 128, 0, stream>>>(part_o, part_ml, nsplit, Hq, Hkv, out);
   }
   return 0;
+}
+
+int launch_attn_decode_rope(const bf16* qkv, const float* part, int sk, const int* positions,
+                            const float* cos_t, const float* sin_t, const int* slots, void* k_cache,
+                            void* v_cache, const int* block_tables, int bt_stride, const int* ctx_lens,
+                            int B, int Hq, int Hkv, int D, int block_size, float scale, int max_ctx,
+                            int part_tokens, bf16* out, float* part_o, float* part_ml, hipStream_t stream,
+                            int* counters, int kv_fp8) {
+  DecRope rp;
+  rp.qkv = qkv;
+  rp.part = part;
+  rp.sk = sk;
+  rp.slab = (long)B * (Hq + 2 * Hkv) * D;
+  rp.positions = positions;
+  rp.cos_t = cos_t;
+  rp.sin_t = sin_t;
+  rp.slots = slots;
+  rp.k_w = k_cache;
+  rp.v_w = v_cache;
+  return launch_attn_decode(qkv, 0, k_cache, v_cache, block_tables, bt_stride, ctx_lens, B, Hq, Hkv, D,
+                            block_size, scale, max_ctx, part_tokens, out, part_o, part_ml, stream, counters,
+                            kv_fp8, &rp);
 }
 
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
