@@ -47,8 +47,9 @@ define("BFLY_GEMM_LIBRARY_MIN_M", 6144, int, "plain (epilogue-free) GEMMs with a
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
-define("BFLY_FUSED_DECODE_ROPE", True, _bool, "decode steps: RoPE and the new token's KV-cache append run inside the "
-       "decode attention kernel (one launch instead of rope_kv + attn_decode; bf16 caches)")
+define("BFLY_FUSED_DECODE_ROPE", False, _bool, "decode steps: RoPE and the new token's KV-cache append inside the "
+       "decode attention kernel (one launch instead of rope_kv + attn_decode; bf16 caches). Off: measured 1 % "
+       "slower on the 70B B=64 step (every workgroup's serial prologue costs more than the launch it saves)")
 define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism: the residual stream and the norms are "
        "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
 define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")

@@ -93,6 +93,10 @@ __device__ __forceinline__ void decode_split_done(const float* __restrict__ part
 // page. That replaces the rope_kv launch before every decode attention (its kernel, its
 // boundary, and the round trip of q through memory). Numerics follow rope_kv exactly: the
 // row is rounded to bf16 before the rotation, the rotated values to bf16 after it.
+// Measured (profiles/r2_fused_decode_rope_ab.log, 70B B=64): 30.58 vs 30.26 ms per step
+// unfused, so it is off by default (BFLY_FUSED_DECODE_ROPE): each of the ~512 workgroups pays
+// the prologue's dependent loads (positions -> tables, slabs) and a barrier before its first
+// MFMA, more in sum than the rope_kv launch and boundary it removes.
 struct DecRope {
   const bf16* qkv;          // [B, (Hq + 2 Hkv) D] bf16 (when part == nullptr)
   const float* part;        // or the QKV GEMM's split-K slabs [sk][B][(Hq + 2 Hkv) D]
@@ -147,6 +151,7 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   __shared__ float s_o[4][8][4][64];
   __shared__ float s_m[4][16], s_l[4][16];
   __shared__ float s_snew[16], s_vnew[D];
+  __shared__ __attribute__((aligned(16))) bf16 s_rows[FUSED ? 17 : 1][D];   // rotated q rows (+ new key)
   __shared__ int s_last;
 
   if (tok0 >= tok1 && !has_new) {  // empty split: mark it so the combine skips it
@@ -168,62 +173,7 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   auto d_off = [&](int ds) { return kF8 ? 64 * (ds >> 1) + 16 * g + 8 * (ds & 1) : 32 * ds + 8 * g; };
   // Q^T fragment (B operand): lane holds Q[row r][d]; rows >= G are zero.
   bf16x8 qf[4];
-  if constexpr (FUSED) {
-    // RoPE in registers: d_off(ds) and d_off(ds + 2) = d_off(ds) + 64 are rotation partners
-    const int qr = r < G ? r : 0;
-    const long row_off = (long)b * (Hq + 2 * Hkv) * D;
-    const int pos = rp.positions[b];
-    const float* cr = rp.cos_t + (long)pos * (D / 2);
-    const float* sr = rp.sin_t + (long)pos * (D / 2);
-    auto rot = [&](int col0, bf16x8 (&f)[4]) {
-      float x[4][8];
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) dec_row8(rp, row_off, col0 + d_off(ds), x[ds]);
-#pragma unroll
-      for (int ds = 0; ds < 2; ++ds)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float c = cr[d_off(ds) + j], sn = sr[d_off(ds) + j];
-          f[ds][j] = f2bf(x[ds][j] * c - x[ds + 2][j] * sn);
-          f[ds + 2][j] = f2bf(x[ds + 2][j] * c + x[ds][j] * sn);
-        }
-    };
-    rot((h * G + qr) * D, qf);
-    if (r >= G)
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) qf[ds] = bf16x8{};
-    if (has_new && wid == 0) {
-      // the new token's key: rotated like the queries, dotted with every query row here
-      bf16x8 kn[4];
-      rot((Hq + h) * D, kn);
-      float dot = 0.f;
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dot += bf2f(qf[ds][j]) * bf2f(kn[ds][j]);
-      dot += __shfl_xor(dot, 16, 64);
-      dot += __shfl_xor(dot, 32, 64);
-      if (g == 0) s_snew[r] = r < G ? dot * scale_log2 : kNegInf;
-      const int slot = rp.slots ? rp.slots[b] : -1;
-      if (slot >= 0 && r == 0) {   // lanes g = 0..3 hold all 128 d of the key
-        CT* kp = static_cast<CT*>(rp.k_w) + (((long)(slot / BS) * Hkv + h) * BS + slot % BS) * D;
-#pragma unroll
-        for (int ds = 0; ds < 4; ++ds) KV<CT>::store8(kp + d_off(ds), kn[ds]);
-      }
-    }
-    if (has_new && threadIdx.x < D / 8) {   // the new token's value (transposed V page)
-      float x[8];
-      const int d0 = threadIdx.x * 8;
-      dec_row8(rp, row_off, (Hq + Hkv + h) * D + d0, x);
-      const int slot = rp.slots ? rp.slots[b] : -1;
-      CT* vp = slot >= 0 ? static_cast<CT*>(rp.v_w) + ((long)(slot / BS) * Hkv + h) * D * BS + slot % BS : nullptr;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s_vnew[d0 + j] = x[j];
-        if (vp) KV<CT>::store1(vp + (long)(d0 + j) * BS, f2bf(x[j]));
-      }
-    }
-  } else {
+  if constexpr (!FUSED) {
     const int qr = r < G ? r : 0;
     const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D;
 #pragma unroll
@@ -315,6 +265,69 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   raw_t kA[2][4], vA[8], kB[2][4], vB[8];
   int p = p0 + wid;
   if (p < p1) load_page(p, kA, vA);
+  if constexpr (FUSED) {
+    // (the first KV page is already in flight) The workgroup's G query rows -- and, in the
+    // split that holds the new token, its key -- are rotated ONCE, spread over all threads
+    // (thread = one rotation pair of one row), staged in LDS as bf16, then read back as MFMA
+    // fragments; the value row goes to LDS and its cache page by 16 threads.
+    const long row_off = (long)b * (Hq + 2 * Hkv) * D;
+    const int pos = rp.positions[b];
+    const float* cr = rp.cos_t + (long)pos * (D / 2);
+    const float* sr = rp.sin_t + (long)pos * (D / 2);
+    const int nrows = G + (has_new ? 1 : 0);
+    for (int e = threadIdx.x; e < nrows * (D / 16); e += kAttnThreads) {
+      const int row = e / (D / 16), p0r = (e % (D / 16)) * 8;     // 8 pairs (d, d + 64)
+      const int head = row < G ? h * G + row : Hq + h;
+      float x[8], y[8];
+      dec_row8(rp, row_off, head * D + p0r, x);
+      dec_row8(rp, row_off, head * D + p0r + D / 2, y);
+      bf16x8 a, c2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float cs = cr[p0r + j], sn = sr[p0r + j];
+        a[j] = f2bf(x[j] * cs - y[j] * sn);
+        c2[j] = f2bf(y[j] * cs + x[j] * sn);
+      }
+      *reinterpret_cast<bf16x8*>(&s_rows[row][p0r]) = a;
+      *reinterpret_cast<bf16x8*>(&s_rows[row][p0r + D / 2]) = c2;
+    }
+    const int slot = rp.slots ? rp.slots[b] : -1;
+    if (has_new && threadIdx.x < D / 8) {   // the new token's value (transposed V page)
+      float x[8];
+      const int d0 = threadIdx.x * 8;
+      dec_row8(rp, row_off, (Hq + Hkv + h) * D + d0, x);
+      CT* vp = slot >= 0 ? static_cast<CT*>(rp.v_w) + ((long)(slot / BS) * Hkv + h) * D * BS + slot % BS : nullptr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s_vnew[d0 + j] = x[j];
+        if (vp) KV<CT>::store1(vp + (long)(d0 + j) * BS, f2bf(x[j]));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+      const int qr = r < G ? r : 0;
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        qf[ds] = *reinterpret_cast<const bf16x8*>(&s_rows[qr][d_off(ds)]);
+        if (r >= G) qf[ds] = bf16x8{};
+      }
+    }
+    if (has_new && wid == 0) {
+      float dot = 0.f;
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        const bf16x8 kn = *reinterpret_cast<const bf16x8*>(&s_rows[G][d_off(ds)]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += bf2f(qf[ds][j]) * bf2f(kn[j]);
+        if (slot >= 0 && r == 0)   // lanes g = 0..3 hold all 128 d of the key
+          KV<CT>::store8(static_cast<CT*>(rp.k_w) + (((long)(slot / BS) * Hkv + h) * BS + slot % BS) * D + d_off(ds), kn);
+      }
+      dot += __shfl_xor(dot, 16, 64);
+      dot += __shfl_xor(dot, 32, 64);
+      if (g == 0) s_snew[r] = r < G ? dot * scale_log2 : kNegInf;
+    }
+  }
   if constexpr (sizeof(CT) == 2) {
     while (p < p1) {
       if (p + 4 < p1) load_page(p + 4, kB, vB);
