@@ -657,7 +657,9 @@ constexpr float kPfRescaleThr = 8.f;
 // (waves 4-7, which lose VALU arbitration to their older SIMD partners, at s_setprio 1).
 // Measured and dropped (profiles/r2_attn_prefill_variants.log): a 5-stage ring (-7 % on
 // 16k tokens), waves 4-7 running PV one tile late (-15..-25 %), a one-tile software pipeline
-// of QK(t+1) beside softmax(t) (spills at 256 VGPRs, -35 %).
+// of QK(t+1) beside softmax(t) (spills at 256 VGPRs, -35 %), and a 4-wave x 64-row layout
+// with K/V fragments shared by two subtiles, one wave per SIMD (-25..-35 %: nothing left to
+// hide the softmax -> PV chain; profiles/r2_attn_prefill_wide_variant.log).
 template <int D, int S, bool PRIO, bool DEFER, bool BUFDMA, bool MFSUM>
 __global__ void __launch_bounds__(kPfThreads)
 attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
