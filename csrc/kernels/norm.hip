@@ -68,6 +68,9 @@ rmsnorm_kernel(const bf16* __restrict__ x, long x_stride, bf16* __restrict__ res
 // (its deferred reduce fused here). 1024 threads per row and every slab load of a thread
 // issued before the adds: at decode the rows are few (the batch), so each workgroup must keep
 // many loads in flight to stream its sk x dim x 4 bytes.
+// Measured and dropped (profiles/r2_norm_split_ab.log): cutting each row over 2048-column
+// workgroups with a last-arriver rescale is 0.6-0.9 ms per 70B step SLOWER, since each
+// workgroup's agent-scope release writes back its XCD's L2 and the hand-off crosses XCDs.
 constexpr int kNormPartThreads = 1024;
 
 template <int NV>
