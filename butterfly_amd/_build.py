@@ -2,7 +2,8 @@
 
 Products (in-tree, so they travel to the GPU box with the repo snapshot):
   butterfly_amd/_C.so       HIP/CDNA4 kernels (csrc/kernels/*.hip, --offload-arch=gfx950) +
-                            torch.ops.bfly registrations (csrc/bindings/*.cpp).
+                            torch.ops.bfly registrations (csrc/bindings/*.cpp), including the
+                            native RCCL communicator (rccl_comm.cpp, linked to torch's RCCL).
   butterfly_amd/_native.so  Host C++ runtime (csrc/runtime/*.cpp): paged-KV block allocator,
                             partition cut-point search, request scheduler core. pybind11,
                             no torch / HIP dependency, so it loads and is tested on CPU.
@@ -102,6 +103,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = True) -> P
     if rebuilt or force or not out.exists():
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs),
                 f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+                "-lrccl",   # torch's own librccl.so (csrc/bindings/rccl_comm.cpp)
                 f"-Wl,-rpath,{tlib}"]
         _link(link, out)
         if verbose:

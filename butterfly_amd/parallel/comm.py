@@ -14,7 +14,10 @@ exposes the handful of collectives the rank programs need:
   broadcast_    control-plane metadata
 
 Small TP all-reduces (decode) can be routed to a one-shot peer-to-peer kernel
-(parallel/custom_allreduce.py) instead of RCCL; everything else stays on RCCL.
+(parallel/custom_allreduce.py) instead of RCCL; everything else stays on RCCL. With
+BFLY_NATIVE_RCCL=1 the data-path collectives of every multi-rank group go to the rank's own
+RCCL communicators (parallel/rccl.py: world init + one ncclCommSplit per mesh axis) instead of
+torch's ProcessGroups; control-plane ops (host integers, barriers) stay on torch.
 Every op is stream-ordered and allocation-free when given outputs, so it can be captured
 in a hipGraph together with the compute kernels.
 """
@@ -36,6 +39,7 @@ class GroupHandle:
     ranks: list
     pg: Optional[object]          # torch ProcessGroup, None when size == 1
     rank_in_group: int
+    native: Optional[object] = None   # parallel/rccl.RcclComm (BFLY_NATIVE_RCCL) for the data path
 
     @property
     def size(self) -> int:
@@ -78,6 +82,8 @@ class Communicator:
         comm = cls(mesh, rank, groups)
         from ..utils import flags
 
+        if flags.get("BFLY_NATIVE_RCCL") and dist.get_backend() == "nccl" and torch.cuda.is_available():
+            comm.enable_native_rccl()
         if flags.get("BFLY_CUSTOM_AR") and mesh.tp > 1 and torch.cuda.is_available():
             comm.enable_custom_all_reduce(flags.get("BFLY_CUSTOM_AR_MAX_BYTES"))
         return comm
@@ -111,6 +117,8 @@ class Communicator:
         if group == "tp" and self.custom_ar is not None and self.custom_ar.should_use(t):
             return self.custom_ar.all_reduce_(t)
         t = ops.materialize(t)
+        if g.native is not None:
+            return g.native.all_reduce_(t)
         dist.all_reduce(t, group=g.pg)
         return t
 
@@ -144,11 +152,30 @@ class Communicator:
             car.close()
         return self.custom_ar is not None
 
+    def enable_native_rccl(self) -> dict:
+        """Create the rank's native RCCL communicators (collective over the world): the world
+        one from a broadcast unique id, then one ncclCommSplit per mesh axis. Returns
+        {axis: RcclComm} for the groups that now use them."""
+        from .rccl import RcclComm, split_mesh
+
+        world = RcclComm.world()
+        natives = split_mesh(world, self.mesh, self.rank)
+        for axis, nc in natives.items():
+            self.groups[axis].native = nc
+        self.groups["world"].native = world
+        return natives
+
     def check_health(self) -> None:
         """Raise if the IPC all-reduce recorded a peer-wait timeout (a rank stopped arriving:
-        its results since then are not trustworthy). Cheap: one 4-byte device read."""
+        its results since then are not trustworthy) or a native RCCL communicator reports an
+        asynchronous error. Cheap: one 4-byte device read plus host queries."""
         if self.custom_ar is not None and self.custom_ar.error():
             raise RuntimeError(f"rank {self.rank}: custom all-reduce peer wait timed out")
+        for name, g in self.groups.items():
+            if g is not None and g.native is not None:
+                err = g.native.async_error()
+                if err:
+                    raise RuntimeError(f"rank {self.rank}: RCCL communicator '{name}' async error {err}")
 
     def all_gather(self, t: torch.Tensor, group: str = "tp", out: torch.Tensor | None = None) -> torch.Tensor:
         g = self.groups[group]
@@ -159,6 +186,8 @@ class Communicator:
             return t
         if out is None:
             out = torch.empty((g.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if g.native is not None:
+            return g.native.all_gather(t, out)
         if self._nccl(g):
             dist.all_gather_into_tensor(out, t.contiguous(), group=g.pg)
         else:  # gloo: list form
@@ -172,6 +201,8 @@ class Communicator:
         n = t.shape[0] // g.size
         if out is None:
             out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if g.native is not None:
+            return g.native.reduce_scatter(t, out)
         if self._nccl(g):
             dist.reduce_scatter_tensor(out, t.contiguous(), group=g.pg)
         else:  # gloo has no reduce_scatter: all-reduce then slice
@@ -213,6 +244,8 @@ class Communicator:
         if out is None:
             out = torch.empty_like(t)
         self.stats["calls"] += 1
+        if g.native is not None:
+            return g.native.all_to_all(t, out)
         if self._nccl(g):
             dist.all_to_all_single(out, t.contiguous(), group=g.pg)
             return out

@@ -1,0 +1,140 @@
+"""Native RCCL communicators over csrc/bindings/rccl_comm.cpp.
+
+The world communicator is created from a 128-byte unique id that rank 0 draws and ships over
+the control plane (one torch.distributed broadcast); every mesh axis then gets its own
+communicator by `ncclCommSplit` of the world one (color = which group of the axis the rank is
+in, key = its position), so a rank holds one RCCL communicator per axis without a second
+bootstrap. The data-path collectives are single stream-ordered RCCL calls on torch's current
+stream: no work objects, watchdog events or allocator stream records, so they capture into
+the decode hipGraph like the kernels around them.
+
+Enabled by BFLY_NATIVE_RCCL=1 (parallel/comm.py routes all-reduce / all-gather /
+reduce-scatter / all-to-all of groups larger than one rank here). RCCL refuses two ranks on
+one device, so on a one-GPU box only nranks = 1 communicators can be exercised; the multi-rank
+path needs a multi-GPU node.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+_OPS = {"sum": 0, "max": 1, "min": 2, "prod": 3}
+
+
+def _lib():
+    from .. import ops
+
+    if not ops.load_library():
+        raise RuntimeError(f"native RCCL needs butterfly_amd/_C.so: {ops._load_error}")
+    return torch.ops.bfly
+
+
+def version() -> int:
+    """RCCL version code of the library torch loaded (e.g. 22606 = 2.26.6)."""
+    return int(_lib().rccl_version())
+
+
+class RcclComm:
+    """One RCCL communicator (a handle into the native table) and the global ranks it spans."""
+
+    def __init__(self, handle: int, ranks: list):
+        self.handle = int(handle)
+        self.ranks = list(ranks)
+        self._closed = False
+
+    # -- construction ---------------------------------------------------------------------
+    @classmethod
+    def create(cls, uid: torch.Tensor, nranks: int, rank: int, ranks: Optional[list] = None) -> "RcclComm":
+        """ncclCommInitRank on the current device with an id every member already holds."""
+        h = _lib().rccl_init(uid.cpu().contiguous(), nranks, rank)
+        return cls(h, ranks if ranks is not None else list(range(nranks)))
+
+    @classmethod
+    def world(cls, pg=None) -> "RcclComm":
+        """Collective over the torch.distributed world (or `pg`): rank 0's id is broadcast on
+        the existing process group, then every rank joins."""
+        lib = _lib()
+        n, r = dist.get_world_size(pg), dist.get_rank(pg)
+        uid = lib.rccl_unique_id() if r == 0 else torch.zeros(128, dtype=torch.uint8)
+        dev = "cuda" if dist.get_backend(pg) == "nccl" else "cpu"
+        t = uid.to(dev)
+        dist.broadcast(t, dist.get_global_rank(pg, 0) if pg is not None else 0, group=pg)
+        return cls.create(t.cpu(), n, r)
+
+    def split(self, color: int, key: int, ranks: Optional[list] = None) -> Optional["RcclComm"]:
+        """ncclCommSplit (collective over this communicator): ranks passing the same color form
+        one communicator ordered by key; color < 0 leaves the rank out (returns None)."""
+        h = _lib().rccl_split(self.handle, int(color), int(key))
+        return None if h < 0 else RcclComm(h, ranks if ranks is not None else [])
+
+    # -- queries ----------------------------------------------------------------------------
+    def info(self) -> tuple:
+        """(rank in communicator, size, device ordinal)."""
+        r, n, d = _lib().rccl_info(self.handle)
+        return int(r), int(n), int(d)
+
+    @property
+    def size(self) -> int:
+        return self.info()[1]
+
+    def async_error(self) -> int:
+        """0 when healthy, else the ncclResult_t of an asynchronous failure."""
+        return int(_lib().rccl_async_error(self.handle))
+
+    # -- collectives (stream-ordered on torch's current stream) -----------------------------
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        _lib().rccl_all_reduce(self.handle, t, _OPS[op])
+        return t
+
+    def all_gather(self, t: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        _lib().rccl_all_gather(self.handle, t.contiguous(), out)
+        return out
+
+    def reduce_scatter(self, t: torch.Tensor, out: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        _lib().rccl_reduce_scatter(self.handle, t.contiguous(), out, _OPS[op])
+        return out
+
+    def all_to_all(self, t: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        _lib().rccl_all_to_all(self.handle, t.contiguous(), out)
+        return out
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        _lib().rccl_broadcast(self.handle, t, int(root))
+        return t
+
+    def send(self, t: torch.Tensor, peer: int) -> None:
+        _lib().rccl_send(self.handle, t.contiguous(), int(peer))
+
+    def recv(self, t: torch.Tensor, peer: int) -> torch.Tensor:
+        _lib().rccl_recv(self.handle, t, int(peer))
+        return t
+
+    @staticmethod
+    def group_start() -> None:
+        _lib().rccl_group_start()
+
+    @staticmethod
+    def group_end() -> None:
+        _lib().rccl_group_end()
+
+    def close(self, abort: bool = False) -> None:
+        if not self._closed:
+            self._closed = True
+            _lib().rccl_release(self.handle, abort)
+
+
+def split_mesh(world: RcclComm, mesh, rank: int) -> dict:
+    """One communicator per mesh axis with more than one rank, split from `world` (collective:
+    every rank calls this with the same mesh). Returns {axis: RcclComm}."""
+    out = {}
+    for axis in ("tp", "pp", "dp"):
+        groups = mesh.all_groups(axis)
+        if len(groups[0]) <= 1:
+            continue
+        color = next(i for i, g in enumerate(groups) if rank in g)
+        comm = world.split(color, groups[color].index(rank), groups[color])
+        if comm is not None:
+            out[axis] = comm
+    return out

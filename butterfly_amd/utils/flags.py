@@ -50,6 +50,9 @@ define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each
 define("BFLY_FUSED_DECODE_ROPE", False, _bool, "decode steps: RoPE and the new token's KV-cache append inside the "
        "decode attention kernel (one launch instead of rope_kv + attn_decode; bf16 caches). Off: measured 1 % "
        "slower on the 70B B=64 step (every workgroup's serial prologue costs more than the launch it saves)")
+define("BFLY_NATIVE_RCCL", False, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "
+       "all-to-all) on the rank's own RCCL communicators (world init + ncclCommSplit per mesh axis, "
+       "parallel/rccl.py) instead of torch ProcessGroups; multi-rank path needs a multi-GPU node")
 define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism: the residual stream and the norms are "
        "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
 define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")
