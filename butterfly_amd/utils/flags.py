@@ -42,6 +42,7 @@ define("BFLY_CUSTOM_AR_2SHOT_BYTES", 512 << 10, int, "IPC all-reduces of at leas
 define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0: heuristic plans only; read by the kernel library)")
 define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
+define("BFLY_GEMM_SLAB_WT", False, _bool, "write split-K partial slabs write-through (sc1); measured slower in the decode step, off (read by the kernel library)")
 define("BFLY_GEMM_LIBRARY_MIN_M", 6144, int, "plain (epilogue-free) GEMMs with at least this many rows (prefill "
        "QKV / O / down) run on hipBLASLt; fused GEMMs (SwiGLU, bias) always run the HIP kernels; 0 = never")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")

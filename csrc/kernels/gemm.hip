@@ -47,6 +47,41 @@ __device__ __forceinline__ void store_out(bf16* out, long ldo, int m, int n, flo
   out[(long)m * ldo + n] = f2bf(v);
 }
 
+// Four consecutive output columns of one row (the tile / decode-ring accumulators hold 4
+// consecutive n per lane: W is their MFMA A operand). 8-B store when the row start allows it.
+__device__ __forceinline__ void store_out4(bf16* out, long ldo, int m, int n, f32x4 v, bool vec) {
+  bf16* p = out + (long)m * ldo + n;
+  if (vec) {
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
+    *reinterpret_cast<bf16x4*>(p) = o;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = f2bf(v[r]);
+  }
+}
+
+// Split-K partial slabs: 16 B per lane through a buffer descriptor, plain (write-back) stores.
+// BFLY_GEMM_SLAB_WT=1 makes them write-through (`sc1`, aux 16), so a launch would not end with
+// MBs of dirty f32 lines to write back before its consumer starts (MI355X_MICROARCH.md
+// 'boundary': + B / 6 TB/s for B dirty bytes). Measured in the whole decode step it is SLOWER:
+// Llama-3-70B 30.28-30.32 vs 29.99-30.02 ms, Llama-3-8B 5.58 vs 5.49 ms
+// (profiles/r2_slab_writethrough_ab.log), so it stays off.
+__constant__ int g_slab_wt = 0;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(float* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                           (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
+}
+
+__device__ __forceinline__ void store_slab4(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
+  if (g_slab_wt)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
 // Reduce split-K partial slabs [SK][M][N] (f32) and apply the epilogue.
 __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int SK, int M, int N,
                                           int epi, const bf16* __restrict__ bias,
@@ -318,6 +353,47 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int chunk) 
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + slot * 16);
 }
 
+// Epilogue of the tile and decode-ring GEMMs. W is their MFMA A operand, so the accumulators
+// hold C^T: acc[i][j][r] = C[m = mw + 16i + (lane&15)][n = nw + 16j + 4(lane>>4) + r] — four
+// consecutive columns per lane, stored as one 16-B slab write or one 8-B bf16 write.
+// `pslab`: this workgroup's split-K slab from row m0 on (nullptr: apply the epilogue).
+template <int TI, int TJ>
+__device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw, int nw, int lane,
+                                              int M, int N, int epi, const bf16* __restrict__ bias,
+                                              bf16* __restrict__ out, long ldo, float* __restrict__ pslab,
+                                              int m0) {
+  const int lr = lane & 15, lc = 4 * (lane >> 4);
+  const auto rs = slab_rsrc(pslab, pslab ? (long)(M - m0) * N * 4 : 0);
+  const bool vec = (ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int m = mw + 16 * i + lr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int n = nw + 16 * j + lc;
+      if (pslab) {
+        store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j]);
+      } else if (epi == EPI_SILU) {
+        if constexpr (TJ % 2 == 0) {   // gate/up 16-row groups pair up inside the wave
+          if (j & 1) continue;
+          f32x4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = silu(acc[i][j][r]) * acc[i][j + 1][r];
+          store_out4(out, ldo, m, nw / 2 + 16 * (j / 2) + lc, h, vec);
+        }
+      } else {
+        f32x4 v = acc[i][j];
+        if (epi == EPI_BIAS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += bf2f(bias[n + r]);
+        }
+        store_out4(out, ldo, m, n, v, vec);
+      }
+    }
+  }
+}
+
 // STAGES-deep glds pipeline: K-tiles kt+1 .. kt+STAGES-1 stay in flight (LDS-DMA) while the
 // MFMAs consume tile kt. Each iteration waits with a COUNTED vmcnt (only tile kt must have
 // landed) and a raw s_barrier (a __syncthreads() would drain every in-flight DMA:
@@ -414,35 +490,12 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);   // C^T tile
     }
     if (++buf == STAGES) buf = 0;
   }
-
-  // Epilogue: acc[i][j][r] = C[m = m0 + wm*WM + 16i + (lane>>4)*4 + r][n = n0 + wn*WN + 16j + (lane&15)]
-#pragma unroll
-  for (int i = 0; i < TI; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * WM + 16 * i + (lane >> 4) * 4 + r;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int n = n0 + wn * WN + 16 * j + (lane & 15);
-        const float v = acc[i][j][r];
-        if (part) {
-          part[(long)blockIdx.y * m_slab * N + (long)m * N + n] = v;
-        } else if (epi == EPI_SILU) {
-          if (j & 1) continue;
-          const float u = acc[i][j + 1][r];
-          const int f = (n0 + wn * WN) / 2 + 16 * (j / 2) + (lane & 15);
-          store_out(out, ldo, m, f, silu(v) * u);
-        } else {
-          store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
-        }
-      }
-    }
-  }
+  tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
+                        part ? part + (long)blockIdx.y * m_slab * N + (long)m0 * N : nullptr, m0);
   if (part && counters && splitk_arrive(counters + tile, gridDim.y, reinterpret_cast<int*>(smem)))
     splitk_fixup(part, gridDim.y, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
 }
@@ -555,38 +608,14 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
       for (int j = 0; j < TJ; ++j) {
         const bf16x8 b = lds_frag(Bs, wn * WN + 16 * j + (lane & 15), ks * 4 + (lane >> 4));
 #pragma unroll
-        for (int i = 0; i < TI; ++i) acc[i][j] = mfma16(af[i], b, acc[i][j]);
+        for (int i = 0; i < TI; ++i) acc[i][j] = mfma16(b, af[i], acc[i][j]);   // C^T tile
       }
     }
     if (++xslot == SX) xslot = 0;
     if (++wslot == SW) wslot = 0;
   }
-
-  // Epilogue: acc[i][j][r] = C[m0 + wm*WM + 16i + (lane>>4)*4 + r][n0 + wn*WN + 16j + (lane&15)]
-#pragma unroll
-  for (int i = 0; i < TI; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * WM + 16 * i + (lane >> 4) * 4 + r;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int n = n0 + wn * WN + 16 * j + (lane & 15);
-        const float v = acc[i][j][r];
-        if (part) {
-          part[(long)blockIdx.y * M * N + (long)m * N + n] = v;
-        } else if (epi == EPI_SILU) {
-          if constexpr (TJ % 2 == 0) {   // gate/up 16-row groups pair up inside the wave
-            if (j & 1) continue;
-            const float u = acc[i][j + 1][r];
-            store_out(out, ldo, m, (n0 + wn * WN) / 2 + 16 * (j / 2) + (lane & 15), silu(v) * u);
-          }
-        } else {
-          store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
-        }
-      }
-    }
-  }
+  tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
+                        part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -793,11 +822,12 @@ static void init_nt_policy() {
   static bool done = false;
   if (done) return;
   done = true;
+  const int zero = 0;
   const char* e = getenv("BFLY_GEMM_NT_WEIGHTS");
-  if (e && e[0] == '0') {
-    const int zero = 0;
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile_w_nt), &zero, sizeof(int));
-  }
+  if (e && e[0] == '0') (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile_w_nt), &zero, sizeof(int));
+  const int one = 1;
+  e = getenv("BFLY_GEMM_SLAB_WT");
+  if (e && e[0] == '1') (void)hipMemcpyToSymbol(HIP_SYMBOL(g_slab_wt), &one, sizeof(int));
 }
 
 template <int BM, int BN, int WMW, int STAGES>
