@@ -181,12 +181,22 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
       } else {
         float v[NV][8];
         float ss = 0.f;
+        // every remote and local load of the row first: the residual stores below may alias
+        // them for the compiler, which would otherwise serialise one xGMI round trip per vector
+        bf16x8 xs[NV], rs[NV];
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
           const int c = threadIdx.x + i * kArThreads;
           if (c < nvec) {
-            const bf16x8 x = reinterpret_cast<const bf16x8*>(src[c / per] + ro)[c];
-            const bf16x8 rr = reinterpret_cast<const bf16x8*>(residual + ro)[c];
+            xs[i] = reinterpret_cast<const bf16x8*>(src[c / per] + ro)[c];
+            rs[i] = reinterpret_cast<const bf16x8*>(residual + ro)[c];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int c = threadIdx.x + i * kArThreads;
+          if (c < nvec) {
+            const bf16x8 x = xs[i], rr = rs[i];
             bf16x8 sres;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -218,37 +228,69 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
   for (int r = b; r < rows; r += kArBlocks) {
     const long ro = (long)r * dim;
     if constexpr (MODE == 0) {
-      for (int c = threadIdx.x; c < nvec; c += kArThreads) {
-        bf16x8 v[W];
+      // U vectors per thread per round, all peers' loads issued before the first store (the
+      // stores may alias them for the compiler: one xGMI round trip per round, not per vector).
+      // 8 loads per thread in flight at most: the VGPR budget keeps 8 ranks' grids co-resident
+      // when ranks share a GPU (the flag rendezvous needs every peer's workgroup running).
+      constexpr int U = W >= 8 ? 1 : 8 / W;
+      for (int c0 = threadIdx.x; c0 < nvec; c0 += U * kArThreads) {
+        bf16x8 v[U][W];
 #pragma unroll
-        for (int p = 0; p < W; ++p)
-          v[p] = p == rank ? reinterpret_cast<const bf16x8*>(own + ro)[c]
-                           : reinterpret_cast<const bf16x8*>(src[p] + ro)[c];
-        float acc[8];
+        for (int u = 0; u < U; ++u) {
+          const int c = c0 + u * kArThreads;
+          if (c < nvec) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = bf2f(v[0][j]);
+            for (int p = 0; p < W; ++p)
+              v[u][p] = p == rank ? reinterpret_cast<const bf16x8*>(own + ro)[c]
+                                  : reinterpret_cast<const bf16x8*>(src[p] + ro)[c];
+          }
+        }
 #pragma unroll
-        for (int p = 1; p < W; ++p)
+        for (int u = 0; u < U; ++u) {
+          const int c = c0 + u * kArThreads;
+          if (c < nvec) {
+            float acc[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[p][j]);
-        bf16x8 o;
+            for (int j = 0; j < 8; ++j) acc[j] = bf2f(v[u][0][j]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
-        reinterpret_cast<bf16x8*>(out + ro)[c] = o;
+            for (int p = 1; p < W; ++p)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[u][p][j]);
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+            reinterpret_cast<bf16x8*>(out + ro)[c] = o;
+          }
+        }
       }
     } else {
       float v[NV][8];
       float ss = 0.f;
+      // the peers' vectors (and the residual) of CH register rows are loaded before the first
+      // residual store, which may alias them for the compiler: one xGMI round trip per chunk
+      // instead of per vector (at most 16 loads per thread in flight: see MODE 0)
+      constexpr int CH = (16 / W) < NV ? (16 / W) : NV;
 #pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int c = threadIdx.x + i * kArThreads;
+      for (int i0 = 0; i0 < NV; i0 += CH) {
+      bf16x8 xs[CH][W], rs[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int c = threadIdx.x + (i0 + u) * kArThreads;
         if (c < nvec) {
-          bf16x8 x[W];
 #pragma unroll
           for (int p = 0; p < W; ++p)
-            x[p] = p == rank ? reinterpret_cast<const bf16x8*>(own + ro)[c]
-                             : reinterpret_cast<const bf16x8*>(src[p] + ro)[c];
-          const bf16x8 rr = reinterpret_cast<const bf16x8*>(residual + ro)[c];
+            xs[u][p] = p == rank ? reinterpret_cast<const bf16x8*>(own + ro)[c]
+                                 : reinterpret_cast<const bf16x8*>(src[p] + ro)[c];
+          rs[u] = reinterpret_cast<const bf16x8*>(residual + ro)[c];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int i = i0 + u;
+        const int c = threadIdx.x + i * kArThreads;
+        if (c < nvec) {
+          const bf16x8* x = xs[u];
+          const bf16x8 rr = rs[u];
           bf16x8 s;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -262,6 +304,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
           }
           reinterpret_cast<bf16x8*>(residual + ro)[c] = s;
         }
+      }
       }
       ss = block_sum(ss, red);
       const float inv = rsqrtf(ss / (float)dim + eps);
