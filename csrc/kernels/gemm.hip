@@ -754,37 +754,14 @@ gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);   // C^T tile
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
     if (++buf == S) buf = 0;
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
-
-  // Epilogue: acc[i][j][r] = C[m0 + wm*128 + 16i + (lane>>4)*4 + r][n0 + wn*64 + 16j + (lane&15)]
-#pragma unroll
-  for (int i = 0; i < TI; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * 128 + 16 * i + (lane >> 4) * 4 + r;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int n = n0 + wn * 64 + 16 * j + (lane & 15);
-        const float v = acc[i][j][r];
-        if (part) {
-          part[(long)blockIdx.y * M * N + (long)m * N + n] = v;
-        } else if (epi == EPI_SILU) {
-          if (j & 1) continue;
-          const float u = acc[i][j + 1][r];
-          const int f = (n0 + wn * 64) / 2 + 16 * (j / 2) + (lane & 15);
-          store_out(out, ldo, m, f, silu(v) * u);
-        } else {
-          store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
-        }
-      }
-    }
-  }
+  tile_epilogue<TI, TJ>(acc, m0 + wm * 128, n0 + wn * 64, lane, M, N, epi, bias, out, ldo,
+                        part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
 }
 
 // ---------------------------------------------------------------------------------------
