@@ -137,26 +137,39 @@ class CustomAllReduce:
         return bool(flag.item())
 
     def _self_test(self, pg) -> bool:
+        """Every call is followed by a group vote on its error word, so a flag wait that timed
+        out (peer stores never seen, e.g. no cross-device visibility) costs the spin limit once:
+        the group stops together (a rank that went on alone would wait out every later call).
+        Every rank runs the same sequence of votes whatever fails locally."""
         good = True
-        try:
-            modes = [False, True] if self.world >= 4 else [False]
-            for rows, dim in ((3, 64), (130, 4096)):
-                x = torch.arange(rows * dim, device=self.device, dtype=torch.float32).view(rows, dim)
-                x = ((x % 17) + self.rank).to(torch.bfloat16)
-                want = sum(((x.float() - self.rank) + r) for r in range(self.world)).to(torch.bfloat16)
-                for two in modes:
-                    for _ in range(3):      # exercise both buffer parities
-                        y = x.clone()
-                        self.all_reduce_(y, two_shot=two)
+        modes = [False, True] if self.world >= 4 else [False]
+        cases = [(rows, dim, two) for rows, dim in ((3, 64), (130, 4096)) for two in modes]
+        for rows, dim, two in cases:
+            x = torch.arange(rows * dim, device=self.device, dtype=torch.float32).view(rows, dim)
+            x = ((x % 17) + self.rank).to(torch.bfloat16)
+            want = sum(((x.float() - self.rank) + r) for r in range(self.world)).to(torch.bfloat16)
+            y = None
+            for _ in range(3):      # exercise both buffer parities
+                try:
+                    y = x.clone()
+                    self.all_reduce_(y, two_shot=two)
                     torch.cuda.synchronize(self.device)
-                    good &= bool(torch.equal(y, want)) and self.error() == 0
-        except Exception as e:  # noqa: BLE001 — any failure means: keep RCCL
-            log.warning("custom all-reduce self-test raised %r", e)
-            good = False
-        ok = self._vote(good, pg)
-        if not ok:
+                    call_ok = self.error() == 0
+                except Exception as e:  # noqa: BLE001 — any failure means: keep RCCL
+                    log.warning("custom all-reduce self-test raised %r", e)
+                    call_ok = False
+                if not self._vote(call_ok, pg):
+                    good = False
+                    break
+            if not good:
+                break
+            good = bool(torch.equal(y, want))
+            if not self._vote(good, pg):
+                good = False
+                break
+        if not good:
             log.warning("custom all-reduce self-test failed on some rank; using RCCL")
-        return ok
+        return good
 
     def close(self) -> None:
         L = torch.ops.bfly
