@@ -121,3 +121,34 @@ class LLM:
 
     def metrics(self) -> dict:
         return self.engine.metrics.summary()
+
+    # ---- request-state snapshots (engine/state.py) -------------------------
+    def save_state(self, directory) -> Optional[Path]:
+        """Write this replica's request state to <directory>/replica-<dp>.json (one rank per
+        replica writes; the others return None)."""
+        from .engine import state
+
+        c = self.plan.mesh.coord(self.rank)
+        if c.tp != 0 or c.pp != 0:
+            return None
+        return state.save(self.engine, state.replica_path(directory, c.dp))
+
+    def resume(self, directory) -> list:
+        """Replay a snapshot written by save_state() or by EngineConfig.snapshot_every into this
+        (fresh) LLM: re-admit the replica's unfinished requests (prompt + tokens generated so far
+        are prefilled again), run them to completion, and return every request of the snapshot,
+        finished ones included, in request-id order."""
+        from .engine import state
+
+        eng = self.engine
+        rids = eng.restore(state.load(state.replica_path(directory, self.dp_rank)))
+        t0 = time.perf_counter()
+        while eng.has_unfinished_global():
+            eng.step()
+        self.last_generate_s = time.perf_counter() - t0
+        outs = []
+        for r in rids:
+            req = eng.requests[r]
+            outs.append(RequestOutput(prompt=req.prompt, token_ids=list(req.output), text=None,
+                                      finish_reason=req.finish_reason))
+        return outs

@@ -228,6 +228,10 @@ class EngineConfig:
     # host one step late. Replaces mixed chunked prefill (prefill steps run on their own).
     async_decode: bool = False
     cp_attention: str = "ring"        # "ring" | "ulysses"
+    # request-state snapshots (engine/state.py): every `snapshot_every` steps one rank per DP
+    # replica writes <snapshot_dir>/replica-<dp>.json; LLM(..., resume=dir) replays it
+    snapshot_dir: Optional[str] = None
+    snapshot_every: int = 0
 
 
 def load_config_file(path: str | Path) -> dict:

@@ -44,6 +44,7 @@ from .batch import empty_batch
 from .kv_cache import KVCache, device_kv_budget, kv_blocks_for_budget
 from .model_runner import ModelRunner
 from .pipeline import GroupedScheduler, PipePlan
+from . import state
 from .sampler import Sampler, SamplingParams
 
 
@@ -231,6 +232,31 @@ class LLMEngine:
             self.scheduler.add(rid, len(prompt), params.max_tokens)
         return rid
 
+    def _admit_resumed(self, req: Request) -> None:
+        """Scheduler admission of a restored request (engine/state.py): its prompt plus the
+        tokens it already generated are prefilled as one sequence, the rest is generated."""
+        toks = req.tokens
+        remaining = req.params.max_tokens - len(req.output)
+        if len(toks) + remaining > self.ecfg.max_seq_len:
+            raise ValueError(f"restored request {req.rid} exceeds max_seq_len")
+        if self.prefix_cache:
+            self.scheduler.add(req.rid, len(toks), remaining, list(toks))
+        else:
+            self.scheduler.add(req.rid, len(toks), remaining)
+
+    def reset_ids(self, next_id: int) -> None:
+        self._ids = itertools.count(next_id)
+
+    # request-state snapshots (engine/state.py)
+    def snapshot(self) -> dict:
+        return state.snapshot(self)
+
+    def restore(self, snap: dict) -> list:
+        return state.restore(self, snap)
+
+    def save_state(self, path) -> None:
+        state.save(self, path)
+
     def has_unfinished(self) -> bool:
         return (self.scheduler.num_waiting + self.scheduler.num_running > 0 or bool(self._cp_queue)
                 or self._pending is not None or self._valued is not None)
@@ -254,6 +280,7 @@ class LLMEngine:
         self.steps_done += 1
         if self.steps_done % 256 == 0:
             self.comm.check_health()
+        state.maybe_periodic(self)
         return out
 
     def _maybe_poison(self, t: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,93 @@
+"""Request-state snapshots (engine/state.py, SURVEY.md §5.4 "resume = reload weights + replay
+request state"): an engine interrupted mid-generation and restored into a fresh engine must
+produce the same tokens as an uninterrupted run — greedy and seeded temperature sampling, with
+the synchronous (mixed chunked prefill) and the overlapped (async decode) step loops."""
+import json
+
+import pytest
+import torch
+
+from butterfly_amd.config import EngineConfig, ModelConfig
+from butterfly_amd.engine import state
+from butterfly_amd.engine.engine import LLMEngine
+from butterfly_amd.engine.sampler import SamplingParams
+
+PROMPTS = [[(7 * i + 3 * j) % 900 + 1 for j in range(n)] for i, n in enumerate((12, 3, 40, 7, 25))]
+
+
+def _params(i):
+    if i % 2:
+        return SamplingParams(max_tokens=5 + 2 * i, temperature=0.8, seed=100 + i, ignore_eos=True)
+    return SamplingParams(max_tokens=5 + 2 * i, ignore_eos=True)
+
+
+def _engine(async_decode, **kw):
+    torch.set_num_threads(1)
+    cfg = ModelConfig.from_preset("llama-tiny")
+    ecfg = EngineConfig(max_batch=4, max_seq_len=128, max_prefill_tokens=32, kv_cache_tokens=2048,
+                        use_graphs=False, seed=3, async_decode=async_decode, **kw)
+    return LLMEngine(cfg, engine_cfg=ecfg, device="cpu")
+
+
+def _run_all(eng):
+    while eng.has_unfinished():
+        eng.step()
+    return {r: list(q.output) for r, q in eng.requests.items()}
+
+
+@pytest.mark.parametrize("async_decode", [False, True])
+@pytest.mark.parametrize("stop_after", [3, 9])
+def test_resume_matches_uninterrupted(async_decode, stop_after, tmp_path):
+    ref = _engine(async_decode)
+    for i, p in enumerate(PROMPTS):
+        ref.add_request(p, _params(i))
+    want = _run_all(ref)
+
+    a = _engine(async_decode)
+    for i, p in enumerate(PROMPTS):
+        a.add_request(p, _params(i))
+    for _ in range(stop_after):
+        a.step()
+    path = tmp_path / "replica-000.json"
+    a.save_state(path)
+    snap = json.loads(path.read_text())
+    assert snap["format"] == state.FORMAT and len(snap["requests"]) == len(PROMPTS)
+    assert any(r["output"] for r in snap["requests"])            # interrupted mid-generation
+    assert not all(r["finished"] for r in snap["requests"])
+
+    b = _engine(async_decode)                                     # fresh engine, same weights
+    rids = b.restore(state.load(path))
+    assert sorted(rids) == sorted(want)
+    got = _run_all(b)
+    assert got == want
+    # ids handed out after a restore do not collide with restored ones
+    assert b.add_request([1, 2, 3], SamplingParams(max_tokens=2)) == max(want) + 1
+
+
+def test_periodic_snapshots_and_api_resume(tmp_path):
+    from butterfly_amd.api import LLM
+
+    eng = _engine(False, snapshot_dir=str(tmp_path), snapshot_every=2)
+    for i, p in enumerate(PROMPTS):
+        eng.add_request(p, _params(i))
+    for _ in range(4):
+        eng.step()
+    snap = state.load(state.replica_path(tmp_path, 0))
+    assert snap["steps_done"] == 4 and not list(tmp_path.glob("*.tmp*"))
+    ref = _run_all(eng)
+
+    llm = LLM("llama-tiny", plan=None, engine_config=EngineConfig(max_batch=4, max_seq_len=128,
+                                                                 max_prefill_tokens=32, kv_cache_tokens=2048,
+                                                                 use_graphs=False, seed=3))
+    outs = llm.resume(tmp_path)
+    assert [o.token_ids for o in outs] == [ref[r] for r in sorted(ref)]
+    assert all(o.finish_reason == "length" for o in outs)
+
+
+def test_restore_rejects_other_model(tmp_path):
+    eng = _engine(False)
+    eng.add_request([1, 2], SamplingParams(max_tokens=2))
+    snap = eng.snapshot()
+    snap["model"] = "llama3-70b"
+    with pytest.raises(ValueError):
+        _engine(False).restore(snap)
