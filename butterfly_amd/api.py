@@ -149,6 +149,6 @@ class LLM:
         outs = []
         for r in rids:
             req = eng.requests[r]
-            outs.append(RequestOutput(prompt=req.prompt, token_ids=list(req.output), text=None,
-                                      finish_reason=req.finish_reason))
+            outs.append(RequestOutput(prompt=req.prompt, token_ids=list(req.output),
+                                      text=self.tokenizer.decode(req.output), finish_reason=req.finish_reason))
         return outs

@@ -67,12 +67,22 @@ def cmd_generate(a) -> int:
     from .config import EngineConfig
     from .engine.sampler import SamplingParams
 
+    from .engine import state
+
+    snap_every = a.snapshot_every if a.snapshot_dir else 0
     llm = LLM(a.model, plan=_strategy(a.plan),
-              engine_config=EngineConfig(max_batch=8, max_seq_len=a.max_seq_len, use_graphs=not a.no_graphs),
+              engine_config=EngineConfig(max_batch=8, max_seq_len=a.max_seq_len, use_graphs=not a.no_graphs,
+                                         snapshot_dir=a.snapshot_dir, snapshot_every=snap_every),
               tokenizer=a.tokenizer)
     prompts = a.prompt or ["Hello"]
-    outs = llm.generate(prompts, SamplingParams(max_tokens=a.max_tokens, temperature=a.temperature,
-                                                seed=a.seed, ignore_eos=True))
+    restart = int(os.environ.get("BFLY_RESTART", "0") or 0)
+    if a.snapshot_dir and restart > 0 and state.replica_path(a.snapshot_dir, llm.dp_rank).exists():
+        # restarted job: replay the request state of the failed attempt (engine/state.py)
+        outs = llm.resume(a.snapshot_dir)
+        print(f"resumed {len(outs)} requests from {a.snapshot_dir} (restart {restart})", file=sys.stderr)
+    else:
+        outs = llm.generate(prompts, SamplingParams(max_tokens=a.max_tokens, temperature=a.temperature,
+                                                    seed=a.seed, ignore_eos=True))
     if llm.rank == 0:
         for o in outs:
             print(json.dumps({"prompt": o.prompt, "text": o.text, "token_ids": o.token_ids,
@@ -107,7 +117,7 @@ def cmd_launch(a) -> int:
             print(f"launch: plan is for {plan.n_gpus} GPUs, -n {a.nproc}", file=sys.stderr)
             return 2
         placement = plan.placement or None
-    return launch(cmd, a.nproc, a.master_port, placement=placement)
+    return launch(cmd, a.nproc, a.master_port, placement=placement, max_restarts=a.max_restarts)
 
 
 def cmd_ckpt(a) -> int:
@@ -174,6 +184,9 @@ def main(argv=None) -> int:
     g.add_argument("--plan", default="auto")
     g.add_argument("--tokenizer", default=None)
     g.add_argument("--no-graphs", action="store_true")
+    g.add_argument("--snapshot-dir", default=None,
+                   help="write request-state snapshots here; a restarted job (launch --max-restarts) resumes from them")
+    g.add_argument("--snapshot-every", type=int, default=4, help="engine steps between snapshots")
     g.set_defaults(fn=cmd_generate)
     s = sub.add_parser("serve")
     s.add_argument("--model", default="llama-tiny")
@@ -192,6 +205,8 @@ def main(argv=None) -> int:
     la.add_argument("-n", "--nproc", type=int, default=1)
     la.add_argument("--master-port", type=int, default=None)
     la.add_argument("--plan", default=None, help="PartitionPlan JSON: its placement maps ranks to GPUs")
+    la.add_argument("--max-restarts", type=int, default=0,
+                    help="start a failed job again up to N times (BFLY_RESTART=<attempt> in its environment)")
     la.add_argument("cmd", nargs=argparse.REMAINDER)
     la.set_defaults(fn=cmd_launch)
     c = sub.add_parser("ckpt")

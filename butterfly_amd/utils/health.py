@@ -118,6 +118,10 @@ class FaultInjector:
         spec = spec if spec is not None else flags.get("BFLY_FAULT")
         self.rank = self.step = None
         self.kind = None
+        # a restarted job (launch --max-restarts, BFLY_RESTART > 0) is the recovery path: the
+        # fault is injected into the first attempt only
+        if spec and os.environ.get("BFLY_RESTART", "0") not in ("", "0"):
+            spec = None
         if spec:
             r, s, k = spec.split(":")
             self.rank, self.step, self.kind = int(r), int(s), k
