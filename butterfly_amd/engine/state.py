@@ -31,8 +31,6 @@ VERSION = 1
 
 
 def snapshot(engine) -> dict:
-    from .engine import Request  # noqa: F401  (type of engine.requests values)
-
     reqs = []
     for rid in sorted(engine.requests):
         r = engine.requests[rid]

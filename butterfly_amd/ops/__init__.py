@@ -38,7 +38,8 @@ def load_library(path: str | os.PathLike | None = None) -> bool:
     global _loaded, _load_error
     if _loaded:
         return True
-    p = Path(path) if path else _LIB_PATH
+    # BFLY_KERNEL_LIB: another build of the kernel library (same-box A/B runs of kernel changes)
+    p = Path(path) if path else Path(os.environ.get("BFLY_KERNEL_LIB") or _LIB_PATH)
     if not p.exists():
         _load_error = f"{p} not built (run `python -m butterfly_amd._build`)"
         return False
