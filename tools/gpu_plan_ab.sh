@@ -1,11 +1,11 @@
 # In-situ decode GEMM plan A/B: the whole 70B decode step with one projection's plan forced
-# (BFLY_GEMM_PLAN), 1 GPU. Each line of gpurun_out/plan_ab.log: variant, ms/step, tok/s.
+# (BFLY_GEMM_PLAN), 1 GPU (BENCH_ARGS: extra bench.py arguments, e.g. another --model). Each line of gpurun_out/plan_ab.log: variant, ms/step, tok/s.
 # Variants: lines "name N,K,Mbucket:kind,mt,nt,wk,bm,bn,sk" of the file given as $1
 # ("name -" = the tuned table), default the round-2 first list below.
 cd $GRAFT_REPO_ROOT
 run() {
   name=$1; shift
-  timeout -k 10 300 env "$@" python bench.py --steps 24 --warmup 3 < /dev/null > gpurun_out/plan_ab_$name.log 2>&1
+  timeout -k 10 300 env "$@" python bench.py --steps 24 --warmup 3 $BENCH_ARGS < /dev/null > gpurun_out/plan_ab_$name.log 2>&1
   rc=$?
   echo "$name rc=$rc $(tail -1 gpurun_out/plan_ab_$name.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])' 2>/dev/null)" >> gpurun_out/plan_ab.log
   if [ $rc -ne 0 ]; then exit $rc; fi
