@@ -791,6 +791,159 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
 }
 
 // ---------------------------------------------------------------------------------------
+// Persistent prefill: one workgroup per CU walks the (query block, sequence, head) items in
+// heaviest-first order (item i: query block index descending, then sequence, then head, so the
+// 8 query heads of a kv head run side by side and share K/V in L2), i = blockIdx.x + j * grid.
+// The K/V ring runs ACROSS items: the tiles of the next item are staged while the current
+// item's last tiles are computed, and no workgroup launch, Q/ring prologue or grid tail sits
+// between items. Short prompts gain most (a 1024-token causal block is 4-16 tiles of work next
+// to a fixed per-workgroup start). Per tile the math is attn_prefill_kernel's (BUFDMA staging,
+// deferred rescale, wave priority); the wave-local vmcnt wait counts the tiles issued after the
+// consumed one (later stores and Q loads only make the wait conservative).
+// ---------------------------------------------------------------------------------------
+struct PfItem {
+  int valid, ntiles;        // valid = item index in range; ntiles = 0: nothing to do
+  int s0, L, sk0, Lk, q0, h, kh;
+};
+
+__device__ __forceinline__ PfItem pf_item(int i, int nqb, int nseq, int Hq, int Hkv,
+                                          const int* __restrict__ cu_seqlens, const int* __restrict__ cu_k,
+                                          bool causal) {
+  PfItem it{};
+  const int per = nseq * Hq;
+  if (i >= nqb * per) return it;
+  it.valid = 1;
+  const int qr = i / per, rem = i - qr * per;
+  const int seq = rem / Hq;
+  it.h = rem - seq * Hq;
+  it.kh = it.h / (Hq / Hkv);
+  it.s0 = cu_seqlens[seq];
+  it.L = cu_seqlens[seq + 1] - it.s0;
+  it.sk0 = cu_k[seq];
+  it.Lk = cu_k[seq + 1] - it.sk0;
+  it.q0 = (causal ? nqb - 1 - qr : qr) * kPfBQ;
+  if (it.q0 >= it.L || it.Lk <= 0) return it;   // ntiles = 0
+  const int kv_end = causal ? min(it.Lk, it.q0 + kPfBQ) : it.Lk;
+  it.ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
+  return it;
+}
+
+template <int D, int S>
+__global__ void __launch_bounds__(kPfThreads)
+attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
+                            long k_stride, const bf16* __restrict__ v, long v_stride,
+                            const int* __restrict__ cu_seqlens, const int* __restrict__ cu_k, int nseq,
+                            int nqb, int Hq, int Hkv, float scale_log2, int causal,
+                            bf16* __restrict__ out, long o_stride, float* __restrict__ lse) {
+  static_assert(D == 128 && S >= 2, "persistent prefill kernel is specialised for D=128");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int STAGE_BYTES = 2 * kPfBKV * D * 2;
+  constexpr int AHEAD = S - 1;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int hi = lane >> 5, c = lane & 31;
+  const bool cz = causal != 0;
+  const int G = gridDim.x;
+  if (__builtin_amdgcn_readfirstlane(wid) >= kPfWaves / 2) __builtin_amdgcn_s_setprio(1);
+  const PfDma dma = pf_dma_offsets(k_stride, v_stride, wid, lane);
+
+  auto next_item = [&](int& idx, PfItem& it) {
+    do {
+      idx += G;
+      it = pf_item(idx, nqb, nseq, Hq, Hkv, cu_seqlens, cu_k, cz);
+    } while (it.valid && it.ntiles == 0);
+  };
+  // consume cursor (C: the item being computed) and issue cursor (I: the next tile to stage)
+  int ci = (int)blockIdx.x - G;
+  PfItem C{};
+  next_item(ci, C);
+  if (!C.valid) return;
+  int ii = ci, it_t = 0;
+  PfItem I = C;
+  int issued = 0, consumed = 0, islot = 0, cslot = 0;
+  auto issue_one = [&]() {
+    if (!I.valid) return;
+    pf_stage_buf(k, k_stride, v, v_stride, I.sk0, I.Lk, I.kh, it_t, smem + islot * STAGE_BYTES, wid, dma);
+    if (++islot == S) islot = 0;
+    ++issued;
+    if (++it_t == I.ntiles) {
+      it_t = 0;
+      next_item(ii, I);
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < AHEAD; ++st) issue_one();
+
+  while (true) {
+    // ---- item start: Q fragments and softmax state of this lane's query row
+    const int qrow = C.q0 + 32 * wid + c;
+    bf16x8 qf[8];
+    {
+      const int qr = qrow < C.L ? qrow : C.L - 1;
+      const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (long)(C.s0 + qr) * q_stride + (long)C.h * D + 8 * hi);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) qf[ks] = qp[2 * ks];
+    }
+    f32x16 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+    float m = kNegInf, lsum = 0.f;
+    const int wave_qmax = C.q0 + 32 * wid + 31;
+    const int last_key = cz ? min(qrow, C.Lk - 1) : C.Lk - 1;
+    for (int t = 0; t < C.ntiles; ++t) {
+      // this tile landed; the tiles issued after it may still fly
+      pf_wait_tiles(min(issued - consumed - 1, AHEAD - 1));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue_one();                      // into the slot every wave finished reading last tile
+      const char* kb = smem + cslot * STAGE_BYTES;
+      const int kv0 = t * kPfBKV;
+      if (!(cz && kv0 > wave_qmax)) {
+        f32x16 sc[2];
+        pf_qk(kb, qf, lane, sc);
+        const bool need_mask = (cz && kv0 + kPfBKV - 1 > C.q0 + 32 * wid) || kv0 + kPfBKV > C.Lk;
+        const int lim = last_key - kv0 - 4 * hi;
+        const float tmax = need_mask ? pf_tile_max<true>(sc, lim, scale_log2) : pf_tile_max<false>(sc, lim, scale_log2);
+        float alpha = 1.f;
+        if (!__all(tmax - m <= kPfRescaleThr)) {
+          const float mn = fmaxf(m, tmax);
+          const float mb = mn == kNegInf ? 0.f : mn;
+          alpha = __builtin_amdgcn_exp2f(m - mb);
+          m = mn;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        }
+        const float mb = m == kNegInf ? 0.f : m;
+        bf16x8 pb[2][2];
+        lsum = lsum * alpha + pf_exp(sc, scale_log2, mb, pb);
+        pf_pv(kb + kPfBKV * 256, pb, lane, o);
+      }
+      if (++cslot == S) cslot = 0;
+      ++consumed;
+    }
+    // ---- item end: normalise and store this lane's query row (no barrier: the next item's
+    // first wait + barrier orders the ring; these stores only make that wait conservative)
+    lsum += __shfl_xor(lsum, 32, 64);
+    if (qrow < C.L) {
+      if (lse != nullptr && hi == 0)
+        lse[(long)(C.s0 + qrow) * Hq + C.h] = lsum > 0.f ? (m + __log2f(lsum)) * 0.69314718055994531f : kNegInf;
+      const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+      bf16* op = out + (long)(C.s0 + qrow) * o_stride + (long)C.h * D;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          bf16x4 w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = f2bf(o[dt][4 * a + j] * inv);
+          *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * a + 4 * hi) = w;
+        }
+    }
+    next_item(ci, C);
+    if (!C.valid) break;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------------------
 int attn_decode_splits(int max_ctx, int part_tokens) {
@@ -881,9 +1034,31 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   // variant (BFLY_ATTN_PF_VARIANT, A/B timing): ring depth, priority, deferred rescale, buffer DMA.
   // 16x1024 / 4x4096 / 1x16384 tokens (64 q / 8 kv heads): 390 / 537 / 740 TF/s (variant 1) ->
   // 471 / 610 / 800 (variant 0); profiles/r2_attn_prefill_variants.log
+  // variant 3 (default): the persistent item walk, 423 / 583 / 804 -> 663 / 862 / 925 TF/s at
+  // 16x1024 / 4x4096 / 1x16384 (profiles/r2_attn_prefill_persistent.log)
   const char* ev = getenv("BFLY_ATTN_PF_VARIANT");
-  const int var = ev ? atoi(ev) : 0;
+  int var = ev ? atoi(ev) : 3;
   const int* cuk = cu_k != nullptr ? cu_k : cu_seqlens;
+  if (var == 3 && cu_k != nullptr) var = 0;   // persistent walk: self-attention only (Lk = L > 0)
+  if (var == 3) {
+    constexpr int S_ = 3;
+    const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;
+    static int ncu = 0;
+    if (ncu == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_persist_kernel<128, S_>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    const int nqb = (max_seqlen + kPfBQ - 1) / kPfBQ;
+    const long items = (long)nqb * nseq * Hq;
+    const int g = (int)(items < ncu ? items : ncu);
+    attn_prefill_persist_kernel<128, S_><<<g, kPfThreads, lds, stream>>>(
+        q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cuk, nseq, nqb, Hq, Hkv, scale_log2,
+        causal ? 1 : 0, out, o_stride, lse);
+    return 0;
+  }
 #define PF_VARIANT(ID, S_, PR_, DF_, BD_, MS_)                                                         \
   if (var == ID) {                                                                                \
     const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;                                           \
@@ -898,7 +1073,7 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
         out, o_stride, lse);                                                                      \
     return 0;                                                                                     \
   }
-  PF_VARIANT(0, 3, true, true, true, false)     // default
+  PF_VARIANT(0, 3, true, true, true, false)     // one workgroup per item (context-parallel ring steps)
   PF_VARIANT(1, 4, false, false, false, false)  // round-1 kernel, for A/B
   PF_VARIANT(2, 3, true, true, true, true)      // row sums on the matrix core: neutral (+-1 %)
 #undef PF_VARIANT
