@@ -764,6 +764,104 @@ gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
                         part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
 }
 
+// Persistent variant of gemm_big_kernel (no split-K): one workgroup per CU walks its output
+// tiles (round j = the one-tile-per-workgroup grid's j-th wave of G workgroups, same XCD remap
+// and GROUP_M order), and the glds ring runs ACROSS tiles: the next tile's first
+// K-steps are staged while this tile's last ones are computed, and the epilogue (register ->
+// global stores, no barrier) sits between two K-steps of one flattened loop. The wave groups'
+// ping-pong stagger is set up once per launch instead of once per tile. (The same structure
+// took the prefill attention kernel from 423 to 663 TF/s at 16 x 1024 tokens.) Measured here it
+// is 13-19 % slower than one workgroup per tile (gate_up M = 8192: 6553 vs 5707 us; the tile
+// order matching the one-tile grid's and per-tile accumulator scopes did not change that), so
+// it is opt-in (BFLY_GEMM_BIG_PERSIST=1) and kept for A/B.
+template <int S>
+__global__ void __launch_bounds__(kBigThreads)
+gemm_big_persist_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
+                        int M, int N, int K, int epi, const bf16* __restrict__ bias,
+                        bf16* __restrict__ out, long ldo) {
+  constexpr int BM = 256, BN = 256, TI = 8, TJ = 4;
+  constexpr int A_BYTES = BM * kBigBK * 2, STAGE_BYTES = 2 * A_BYTES;
+  constexpr int LPW = 4;   // glds per wave per stage (2 for X, 2 for W)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int ntile_all = mtiles * ntiles;
+  const int G = gridDim.x;
+  const int my_tiles = (int)blockIdx.x < ntile_all ? (ntile_all - (int)blockIdx.x + G - 1) / G : 0;
+  const int ktiles = K / kBigBK;
+  const int total = my_tiles * ktiles;   // flattened (tile, K-step) count of this workgroup
+  if (total == 0) return;
+  auto tile_mn = [&](int j, int& m0, int& n0) {
+    // round j does what the one-tile-per-workgroup grid dispatches j-th: workgroups
+    // j*G .. j*G+G-1 of it, through the same XCD remap and GROUP_M order
+    const int t = xcd_remap(j * G + (int)blockIdx.x, ntile_all);
+    const int per_group = kBigGroupM * ntiles;
+    const int g = t / per_group, first_m = g * kBigGroupM;
+    const int gsize = min(mtiles - first_m, kBigGroupM);
+    m0 = (first_m + (t % per_group) % gsize) * BM;
+    n0 = ((t % per_group) / gsize) * BN;
+  };
+  // stage cursor: the flattened step it stages next, as (tile, K-step) and that tile's origin
+  int sj = 0, skt = 0, sm0, sn0;
+  tile_mn(0, sm0, sn0);
+  auto stage_next = [&](char* b) {
+    big_stage(X, ldx, sm0, M, skt * kBigBK, b, wid, lane);
+    big_stage(W, ldw, sn0, N, skt * kBigBK, b + A_BYTES, wid, lane);
+    if (++skt == ktiles) {
+      skt = 0;
+      if (++sj < my_tiles) tile_mn(sj, sm0, sn0);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < total) stage_next(smem + s * STAGE_BYTES);
+  big_wait<S, LPW>(min(S - 1, total) - 1);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+  int buf = 0;
+  for (int j = 0; j < my_tiles; ++j) {   // tiles; the K-step loop below is gemm_big_kernel's
+    int m0, n0;
+    tile_mn(j, m0, n0);
+    f32x4 acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int q = 0; q < TJ; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int g0 = j * ktiles;
+    for (int g = g0; g < g0 + ktiles; ++g) {
+      const char* As = smem + buf * STAGE_BYTES;
+      const char* Bs = As + A_BYTES;
+      bf16x8 bfr[TJ], af[TI];
+#pragma unroll
+      for (int q = 0; q < TJ; ++q) bfr[q] = big_frag(Bs, wn * 64 + 16 * q + (lane & 15), lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = big_frag(As, wm * 128 + 16 * i + (lane & 15), lane >> 4);
+      if (g + S - 1 < total) {
+        int nbuf = buf + S - 1;
+        if (nbuf >= S) nbuf -= S;
+        stage_next(smem + nbuf * STAGE_BYTES);
+      }
+      // step g+1 must have landed; steps g+2 .. g+S-1 (issued) may still fly
+      big_wait<S, LPW>(min(total - 1, g + S - 1) - (g + 1));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int q = 0; q < TJ; ++q) acc[i][q] = mfma16(bfr[q], af[i], acc[i][q]);   // C^T tile
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+      if (++buf == S) buf = 0;
+    }
+    tile_epilogue<TI, TJ>(acc, m0 + wm * 128, n0 + wn * 64, lane, M, N, epi, bias, out, ldo, nullptr, m0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
+}
+
 // ---------------------------------------------------------------------------------------
 // Host dispatch
 // ---------------------------------------------------------------------------------------
@@ -859,6 +957,25 @@ static void run_big(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
                         hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 256 * kBigBK * 2);
   }
   const size_t lds = (size_t)stages * 2 * 256 * kBigBK * 2;
+  // BFLY_GEMM_BIG_PERSIST=1: the persistent tile walk (opt-in: measured 13-19 % SLOWER than one
+  // workgroup per tile on the 70B prefill shapes, profiles/r2_gemm_big_persistent_ab.log)
+  static int persist = -1;
+  if (persist < 0) {
+    const char* e = getenv("BFLY_GEMM_BIG_PERSIST");
+    persist = (e && e[0] == '1') ? 1 : 0;
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_persist_kernel<4>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 256 * kBigBK * 2);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_persist_kernel<5>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 256 * kBigBK * 2);
+  }
+  if (persist && sk == 1) {
+    const int g = tiles < num_cus() ? tiles : num_cus();
+    if (stages == 5)
+      gemm_big_persist_kernel<5><<<g, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo);
+    else
+      gemm_big_persist_kernel<4><<<g, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo);
+    return;
+  }
   dim3 grid(tiles, sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
   if (stages == 5)
