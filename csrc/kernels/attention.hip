@@ -802,8 +802,8 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
 // consumed one (later stores and Q loads only make the wait conservative).
 // ---------------------------------------------------------------------------------------
 struct PfItem {
-  int valid, ntiles;        // valid = item index in range; ntiles = 0: nothing to do
-  int s0, L, sk0, Lk, q0, h, kh;
+  int valid, rows, ntiles;  // valid: item index in range; rows: query rows to write (q0 < L);
+  int s0, L, sk0, Lk, q0, h, kh;   // ntiles: K/V tiles (0 with no keys: O = 0, lse = -inf)
 };
 
 __device__ __forceinline__ PfItem pf_item(int i, int nqb, int nseq, int Hq, int Hkv,
@@ -822,7 +822,9 @@ __device__ __forceinline__ PfItem pf_item(int i, int nqb, int nseq, int Hq, int 
   it.sk0 = cu_k[seq];
   it.Lk = cu_k[seq + 1] - it.sk0;
   it.q0 = (causal ? nqb - 1 - qr : qr) * kPfBQ;
-  if (it.q0 >= it.L || it.Lk <= 0) return it;   // ntiles = 0
+  if (it.q0 >= it.L) return it;   // rows = ntiles = 0
+  it.rows = 1;
+  if (it.Lk <= 0) return it;      // no keys (an empty key chunk): rows written, no tiles
   const int kv_end = causal ? min(it.Lk, it.q0 + kPfBQ) : it.Lk;
   it.ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
   return it;
@@ -846,19 +848,21 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
   if (__builtin_amdgcn_readfirstlane(wid) >= kPfWaves / 2) __builtin_amdgcn_s_setprio(1);
   const PfDma dma = pf_dma_offsets(k_stride, v_stride, wid, lane);
 
-  auto next_item = [&](int& idx, PfItem& it) {
+  // consume cursor (C: the item being computed; items with query rows) and issue cursor
+  // (I: the item whose next tile is staged; items with K/V tiles)
+  auto next_item = [&](int& idx, PfItem& it, bool need_tiles) {
     do {
       idx += G;
       it = pf_item(idx, nqb, nseq, Hq, Hkv, cu_seqlens, cu_k, cz);
-    } while (it.valid && it.ntiles == 0);
+    } while (it.valid && (need_tiles ? it.ntiles == 0 : it.rows == 0));
   };
-  // consume cursor (C: the item being computed) and issue cursor (I: the next tile to stage)
   int ci = (int)blockIdx.x - G;
   PfItem C{};
-  next_item(ci, C);
+  next_item(ci, C, false);
   if (!C.valid) return;
   int ii = ci, it_t = 0;
   PfItem I = C;
+  if (I.ntiles == 0) next_item(ii, I, true);
   int issued = 0, consumed = 0, islot = 0, cslot = 0;
   auto issue_one = [&]() {
     if (!I.valid) return;
@@ -867,7 +871,7 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
     ++issued;
     if (++it_t == I.ntiles) {
       it_t = 0;
-      next_item(ii, I);
+      next_item(ii, I, true);
     }
   };
 #pragma unroll
@@ -938,7 +942,7 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
           *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * a + 4 * hi) = w;
         }
     }
-    next_item(ci, C);
+    next_item(ci, C, false);
     if (!C.valid) break;
   }
 }
@@ -1039,7 +1043,6 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   const char* ev = getenv("BFLY_ATTN_PF_VARIANT");
   int var = ev ? atoi(ev) : 3;
   const int* cuk = cu_k != nullptr ? cu_k : cu_seqlens;
-  if (var == 3 && cu_k != nullptr) var = 0;   // persistent walk: self-attention only (Lk = L > 0)
   if (var == 3) {
     constexpr int S_ = 3;
     const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;
