@@ -140,6 +140,7 @@ def run(a) -> int:
     from butterfly_amd.parallel.probe import apply_policy, ar_policy, probe_comm, summarize
     from butterfly_amd.partition import partition
     from butterfly_amd.partition.hw import MI355X
+    from butterfly_amd.utils import flags
 
     use_gpu = torch.cuda.is_available() and os.environ.get("BFLY_FORCE_CPU", "0") != "1"
 
@@ -154,6 +155,25 @@ def run(a) -> int:
         # one GPU per rank; ranks sharing a GPU (gloo test mode) all use device 0
         torch.cuda.set_device(local % torch.cuda.device_count())
     backend = dist.get_backend() if world > 1 else ("single-gpu" if use_gpu else "single-cpu")
+    # bounded-time checks of every cross-device path before anything depends on them
+    # (parallel/preflight.py): failed features fall back on every rank, a failed mandatory
+    # check ends the job here, a hang exits 75 naming the rank and the check
+    preflight = None
+    if world > 1 and flags.get("BFLY_PREFLIGHT"):
+        from butterfly_amd.parallel.preflight import PreflightError, run_preflight
+
+        try:
+            rep = run_preflight()
+        except PreflightError as e:
+            print(f"[bench] rank {rank}: {e}", file=sys.stderr, flush=True)
+            return 3
+        preflight = rep.summary()
+        log(f"preflight {preflight['seconds']}s: checks {preflight['checks']} disabled {rep.disabled} "
+            f"enabled {rep.enabled}", rank)
+        if not rep.allow_tp and a.plan == "auto":
+            a.plan = f"dp{world}"
+        if flags.get("BFLY_DISABLE_GRAPHS"):
+            a.no_graphs = True
     ranks_seen = 1
     if world > 1:
         # proof that the collective backend spans every rank: all-reduce of ones on the world
@@ -169,7 +189,7 @@ def run(a) -> int:
     probe = {}
     if world > 1 and backend == "nccl" and not a.no_probe:
         t_probe = time.perf_counter()
-        table = probe_comm(world)
+        table = probe_comm(world, custom_ar=flags.get("BFLY_CUSTOM_AR"))
         pol = ar_policy(table)
         hw = MI355X.with_comm_table(dict(table, policy=pol))
         probe = summarize(table)
@@ -284,6 +304,8 @@ def run(a) -> int:
         "graphs_failed": sorted(runner.eager_buckets),
         "custom_ar_active": comm.custom_ar is not None,
         "comm_probe": probe or None,
+        "preflight": preflight,
+        "native_rccl": any(g is not None and g.native is not None for g in comm.groups.values()),
         "config": {"model": MODEL_NAMES.get(a.model, a.model),
                    "global_batch": a.batch_per_gpu * a.gpus, "seq_len": a.prompt_len,
                    "parallelism": plan.name, "stages": [list(s) for s in plan.stages],

@@ -133,15 +133,16 @@ class LLM:
             return None
         return state.save(self.engine, state.replica_path(directory, c.dp))
 
-    def resume(self, directory) -> list:
+    def resume(self, directory, job: Optional[str] = None) -> list:
         """Replay a snapshot written by save_state() or by EngineConfig.snapshot_every into this
         (fresh) LLM: re-admit the replica's unfinished requests (prompt + tokens generated so far
         are prefilled again), run them to completion, and return every request of the snapshot,
-        finished ones included, in request-id order."""
+        finished ones included, in request-id order. `job`: only a snapshot with this job
+        fingerprint (engine/state.py job_fingerprint) is accepted."""
         from .engine import state
 
         eng = self.engine
-        rids = eng.restore(state.load(state.replica_path(directory, self.dp_rank)))
+        rids = state.restore(eng, state.load(state.replica_path(directory, self.dp_rank)), job=job)
         t0 = time.perf_counter()
         while eng.has_unfinished_global():
             eng.step()

@@ -75,14 +75,23 @@ def cmd_generate(a) -> int:
                                          snapshot_dir=a.snapshot_dir, snapshot_every=snap_every),
               tokenizer=a.tokenizer)
     prompts = a.prompt or ["Hello"]
+    params = SamplingParams(max_tokens=a.max_tokens, temperature=a.temperature, seed=a.seed, ignore_eos=True)
     restart = int(os.environ.get("BFLY_RESTART", "0") or 0)
-    if a.snapshot_dir and restart > 0 and state.replica_path(a.snapshot_dir, llm.dp_rank).exists():
+    # the snapshot carries this job's fingerprint: a restart resumes only its own job's state,
+    # never a stale snapshot an earlier, different job left in the directory
+    job = state.job_fingerprint(a.model, prompts, params)
+    llm.engine.job_id = job
+    snap = state.replica_path(a.snapshot_dir, llm.dp_rank) if a.snapshot_dir else None
+    if snap is not None and restart == 0 and snap.exists() and llm.engine.coord.tp == 0 and llm.engine.coord.pp == 0:
+        snap.unlink()      # first attempt: whatever is there belongs to another run
+    if snap is not None and restart > 0 and snap.exists() and state.snapshot_job(snap) == job:
         # restarted job: replay the request state of the failed attempt (engine/state.py)
-        outs = llm.resume(a.snapshot_dir)
+        outs = llm.resume(a.snapshot_dir, job=job)
         print(f"resumed {len(outs)} requests from {a.snapshot_dir} (restart {restart})", file=sys.stderr)
     else:
-        outs = llm.generate(prompts, SamplingParams(max_tokens=a.max_tokens, temperature=a.temperature,
-                                                    seed=a.seed, ignore_eos=True))
+        if snap is not None and restart > 0 and snap.exists():
+            print(f"ignoring {snap}: written by another job", file=sys.stderr)
+        outs = llm.generate(prompts, params)
     if llm.rank == 0:
         for o in outs:
             print(json.dumps({"prompt": o.prompt, "text": o.text, "token_ids": o.token_ids,

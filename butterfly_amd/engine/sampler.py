@@ -8,13 +8,13 @@ keeps the max (SURVEY.md §2.7-C "TP sampling"). No full-vocab gather, graph-cap
 Filtered path (top-k / top-p): on the device, no host round trip, graph-capturable. Gumbel-max
 restricted to a token subset samples the renormalised truncated distribution exactly, so
 top-k / top-p reduce to one threshold per row on logit / temperature, passed to the same
-kernel. The threshold comes from the row's global top-C candidates (C = 1024: each TP rank
-takes its local top-C, the group all-gathers C values per row and keeps the global top-C) and
-the global softmax normaliser (log-sum-exp all-gathered over TP):
-  top-k : the k-th largest scaled logit (k > C is treated as C);
-  top-p : among the candidates (after top-k), the last token whose preceding cumulative
-          probability is <= p; if the candidates hold less than p of the mass the nucleus is
-          truncated to them (a bounded nucleus of C tokens).
+kernel. The threshold is EXACT: a radix select over the order-preserving 32-bit keys of the
+scaled logits (ops.topkp_threshold, sample.hip tkp_*), 4 histogram passes of 8 bits per
+filter, with every histogram SUM-all-reduced over the TP group so the vocab shards select
+together. No candidate cap, no sort, no full-vocab gather:
+  top-k : the k-th largest scaled logit (ties at it are kept);
+  top-p : on the top-k-renormalised distribution, the smallest token value whose strictly
+          larger tokens hold <= p of the mass (every token whose preceding mass is <= p).
 """
 from __future__ import annotations
 
@@ -70,41 +70,21 @@ class Sampler:
         best = allp[:, :, 0].argmax(0)                                 # ties -> lowest rank
         return allp.gather(0, best.view(1, -1, 1).expand(1, -1, 2))[0, :, 1].to(torch.int32)
 
-    CANDIDATES = 1024
-
     def thresholds(self, lv: torch.Tensor, temps: torch.Tensor, params: list) -> torch.Tensor:
-        """Per-row lower bound on logit / temperature implementing top-k / top-p (see module
-        doc). Torch ops on the device plus two small TP all-gathers; no host sync."""
-        R, Vl = lv.shape
+        """Per-row lower bound on logit / temperature implementing top-k / top-p (module doc).
+        Radix-select kernels plus, under TP, one MAX and 4-8 SUM all-reduces of [R, 512]
+        histograms; no host sync."""
+        R = lv.shape[0]
         dev = lv.device
-        t = temps.clamp(min=1e-6).view(R, 1)
-        scaled = lv.float() / t
-        # the same candidate count on every TP rank and for any split: min(C, whole vocab)
-        C = min(self.CANDIDATES, self.vocab_size)
-        vals = torch.topk(scaled, min(C, Vl), dim=1).values              # [R, <=C] descending
-        if vals.shape[1] < C:                                            # small shard: pad
-            vals = torch.cat([vals, vals.new_full((R, C - vals.shape[1]), float("-inf"))], 1)
-        lse = torch.logsumexp(scaled, dim=1)
+        top_k = torch.tensor([max(0, int(p.top_k)) for p in params], dtype=torch.int32).to(dev, non_blocking=True)
+        top_p = torch.tensor([float(p.top_p) for p in params], dtype=torch.float32).to(dev, non_blocking=True)
+        use_k = any(p.top_k > 0 and p.temperature > 0 for p in params)
+        use_p = any(p.top_p < 1.0 and p.temperature > 0 for p in params)
+        rsum = rmax = None
         if self.tp > 1:
-            allv = self.comm.all_gather(vals.contiguous(), "tp").view(self.tp, R, C)
-            vals = torch.topk(allv.permute(1, 0, 2).reshape(R, self.tp * C), C, dim=1).values
-            lse = torch.logsumexp(self.comm.all_gather(lse.contiguous(), "tp").view(self.tp, R), 0)
-        k = torch.tensor([min(p.top_k, C) if p.top_k > 0 else 0 for p in params], dtype=torch.long).to(dev)
-        top_p = torch.tensor([p.top_p for p in params], dtype=torch.float32).to(dev)
-        neg = torch.full((R,), float("-inf"), device=dev)
-        has_k = k > 0
-        thr_k = torch.where(has_k, vals.gather(1, (k - 1).clamp(min=0).view(R, 1)).view(R), neg)
-        in_k = (~has_k).view(R, 1) | (torch.arange(C, device=dev).view(1, C) < k.view(R, 1))
-        # top-p on the top-k-renormalised distribution (top-k applied first, as usual)
-        den = torch.where(has_k, torch.logsumexp(vals.masked_fill(~in_k, float("-inf")), 1), lse)
-        probs = torch.exp(vals - den.view(R, 1)).masked_fill(~in_k, 0.0)
-        before = probs.cumsum(1) - probs                                 # mass ahead of each token
-        drop = (before > top_p.view(R, 1)) | ~in_k
-        last = torch.where(drop.any(1), drop.int().argmax(1) - 1, torch.full_like(k, C - 1)).clamp(min=0)
-        thr_p = torch.where(top_p < 1.0, vals.gather(1, last.view(R, 1)).view(R), neg)
-        thr = torch.maximum(thr_k, thr_p)
-        # tolerance: the kernel scales by a reciprocal multiply, torch above by a division
-        return thr - 1e-5 * thr.abs() - 1e-6
+            rsum = lambda t: self.comm.all_reduce_(t, "tp")          # noqa: E731
+            rmax = lambda t: self.comm.all_reduce_max_(t, "tp")      # noqa: E731
+        return ops.topkp_threshold(lv, temps, top_k, top_p, rsum, rmax, use_k, use_p)
 
     def _sample_filtered(self, logits, params, seeds, check_finite: bool = False):
         lv = self._local_valid(logits)

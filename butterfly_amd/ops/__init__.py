@@ -129,6 +129,7 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
         _arena.get(device, "attn_ml", max_batch * num_kv_heads * ns * 16 * 2, torch.float32)
         _arena.get(device, "attn_cnt", max_batch * num_kv_heads, torch.int32, zero=True)
     _arena.get(device, "sample", max(max_batch, max_tokens, 1) * 64, torch.int64)
+    _arena.get(device, "tkp", max(max_batch, max_tokens, 1) * 521, torch.float32)
 
 
 # ---------------------------------------------------------------------------------------
@@ -255,6 +256,36 @@ def sample(logits, temps=None, seeds=None, vstart: int = 0, out_ids=None, out_sc
     ws = _arena.get(logits.device, "sample", rows * 64, torch.int64)
     torch.ops.bfly.sample(logits, temps, seeds, vstart, out_ids, out_scores, ws, thresh, check_finite)
     return out_ids, out_scores
+
+
+def topkp_threshold(logits, temps, top_k, top_p, reduce_sum=None, reduce_max=None,
+                    use_k: bool = True, use_p: bool = True):
+    """Exact per-row top-k / top-p threshold on logit / temperature by radix select (4 passes
+    of 8 bits per filter, sample.hip tkp_*). `reduce_sum(t)` / `reduce_max(t)`: in-place
+    all-reduces over the TP group applied to every histogram / the row maxima, so vocab shards
+    select together (None: unsharded). `use_k` / `use_p`: skip a filter no row uses. Returns
+    thresh [R] f32 (-inf = unfiltered row), the `thresh` argument of `sample`."""
+    if not _gpu(logits):
+        return ref.topkp_threshold(logits, temps, top_k, top_p, reduce_sum, reduce_max, use_k, use_p)
+    R = logits.shape[0]
+    L = torch.ops.bfly
+    ws = _arena.get(logits.device, "tkp", R * 521, torch.float32)[: R * 521]
+    ws.zero_()
+    L.tkp_begin(logits, temps, top_k, top_p, ws)
+    if reduce_max is not None:
+        reduce_max(ws[R * 8:R * 9].view(torch.int32))
+    hist = ws[R * 9:].view(R, 512)
+    for phase, on in ((0, use_k), (1, use_p)):
+        if not on:
+            continue
+        for p in range(4):
+            L.tkp_pass(logits, temps, ws, p, phase)
+            if reduce_sum is not None:
+                reduce_sum(hist)
+            L.tkp_select(top_p, ws, R, p, phase)
+    thr = torch.empty(R, dtype=torch.float32, device=logits.device)
+    L.tkp_final(ws, R, thr)
+    return thr
 
 
 def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = False):

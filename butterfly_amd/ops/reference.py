@@ -12,6 +12,7 @@ Semantics match the kernels exactly, including in-place side effects and cache l
 from __future__ import annotations
 
 import math
+import struct
 
 import torch
 import torch.nn.functional as F
@@ -200,6 +201,97 @@ def sample(logits, temps=None, seeds=None, vstart=0, thresh=None, check_finite=F
         scores.append(float(s[i]))
     return (torch.tensor(ids, dtype=torch.int32, device=logits.device),
             torch.tensor(scores, dtype=torch.float32, device=logits.device))
+
+
+def ordered_key(s: torch.Tensor) -> torch.Tensor:
+    """Order-preserving map of f32 values to u32 keys (held in int64), as in sample.hip."""
+    u = s.float().contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    return torch.where((u & 0x80000000) != 0, (~u) & 0xFFFFFFFF, u | 0x80000000)
+
+
+def unordered_key(k: int) -> float:
+    u = (k & 0x7FFFFFFF) if (k & 0x80000000) else (~k & 0xFFFFFFFF)
+    return struct.unpack("<f", struct.pack("<I", u))[0]
+
+
+def topkp_threshold(logits, temps, top_k, top_p, reduce_sum=None, reduce_max=None,
+                    use_k: bool = True, use_p: bool = True):
+    """Exact top-k / top-p thresholds on s = logit * (1 / temperature) by the same 4-pass,
+    8-bit radix select as the tkp_* kernels (sample.hip), pass for pass: `reduce_sum` /
+    `reduce_max` (in-place all-reduces over the TP group, or None) see the same histograms
+    and row maxima, so a vocab-parallel CPU run exercises the GPU path's collective pattern.
+    Returns thresh [R] f32 (-inf: row unfiltered)."""
+    lf = logits.float()
+    R, V = lf.shape
+    inv_t = torch.where(temps > 0, 1.0 / temps.float().clamp(min=1e-30), torch.ones_like(temps.float()))
+    s = lf * inv_t.view(R, 1)
+    key = ordered_key(s)
+    smax = (ordered_key(s.max(1).values if V else torch.full((R,), float("-inf"))) ^ 0x80000000)
+    smax = torch.where(smax >= 2 ** 31, smax - 2 ** 32, smax).to(torch.int32)
+    if reduce_max is not None:
+        reduce_max(smax)
+    mx = torch.tensor([unordered_key((int(v) & 0xFFFFFFFF) ^ 0x80000000) for v in smax.tolist()],
+                      dtype=torch.float32)
+    k_act = [bool(temps[r] > 0 and top_k[r] > 0) for r in range(R)]
+    p_act = [bool(temps[r] > 0 and top_p[r] < 1.0) for r in range(R)]
+    tk_pre, k_rem = [0] * R, [int(top_k[r]) for r in range(R)]
+    tp_pre, m_above, z = [0] * R, [0.0] * R, [0.0] * R
+    mass = torch.exp(s - mx.view(R, 1))
+    for phase, on in ((0, use_k), (1, use_p)):
+        if not on:
+            continue
+        for p in range(4):
+            shift = 24 - 8 * p
+            hist = torch.zeros(R, 512, dtype=torch.float32)
+            for r in range(R):
+                if not (k_act[r] if phase == 0 else p_act[r]):
+                    continue
+                kr = key[r]
+                sel = torch.ones(V, dtype=torch.bool)
+                if phase == 1 and k_act[r]:
+                    sel &= kr >= tk_pre[r]
+                if p > 0:
+                    sel &= (kr >> (shift + 8)) == (tk_pre[r] if phase == 0 else tp_pre[r])
+                d = (kr[sel] >> shift) & 255
+                hist[r, :256] = torch.bincount(d, minlength=256).float()
+                if phase == 1:
+                    hist[r, 256:] = torch.zeros(256).index_add_(0, d, mass[r][sel])
+            if reduce_sum is not None:
+                reduce_sum(hist)
+            for r in range(R):
+                cnt, ms = hist[r, :256].tolist(), hist[r, 256:].tolist()
+                if phase == 0:
+                    if not k_act[r]:
+                        continue
+                    if p == 0 and sum(cnt) < k_rem[r]:
+                        k_act[r] = False
+                        continue
+                    run = 0.0
+                    for d in range(255, -1, -1):
+                        if run < k_rem[r] <= run + cnt[d]:
+                            tk_pre[r] = (tk_pre[r] << 8) | d
+                            k_rem[r] -= int(run)
+                            break
+                        run += cnt[d]
+                else:
+                    if not p_act[r]:
+                        continue
+                    if p == 0:
+                        z[r], m_above[r] = float(sum(ms)), 0.0
+                    lim = float(top_p[r]) * z[r]
+                    run, best, best_above = 0.0, 255, 0.0
+                    for d in range(255, -1, -1):
+                        if cnt[d] > 0 and m_above[r] + run <= lim:
+                            best, best_above = d, run
+                        run += ms[d]
+                    tp_pre[r] = (tp_pre[r] << 8) | best
+                    m_above[r] += best_above
+    out = torch.full((R,), float("-inf"), dtype=torch.float32)
+    for r in range(R):
+        if k_act[r] or p_act[r]:
+            kk = max(tk_pre[r] if k_act[r] else 0, tp_pre[r] if p_act[r] else 0)
+            out[r] = unordered_key(kk)
+    return out
 
 
 def linear(x, w, bias=None, epilogue="none", out=None):

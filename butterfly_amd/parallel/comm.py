@@ -122,6 +122,17 @@ class Communicator:
         dist.all_reduce(t, group=g.pg)
         return t
 
+    def all_reduce_max_(self, t: torch.Tensor, group: str = "tp") -> torch.Tensor:
+        """In-place element-wise max over the group (stream-ordered, capturable on RCCL)."""
+        g = self.groups[group]
+        if g.size == 1:
+            return t
+        self.stats["calls"] += 1
+        if g.native is not None:
+            return g.native.all_reduce_(t, "max")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.pg)
+        return t
+
     def all_reduce_rms_norm_(self, t: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor,
                              group: str = "tp") -> torch.Tensor:
         """residual += all_reduce(t); return rms_norm(residual) * w — one fused kernel on the

@@ -153,6 +153,13 @@ class FakeComm(Communicator):
         t.copy_(self._coll(group, "all_reduce", t, lambda xs: torch.stack([x.float() for x in xs]).sum(0).to(xs[0].dtype)))
         return t
 
+    def all_reduce_max_(self, t, group="tp"):
+        if self.groups[group].size == 1:
+            return t
+        self.stats["calls"] += 1
+        t.copy_(self._coll(group, "all_reduce_max", t, lambda xs: torch.stack(xs).max(0).values))
+        return t
+
     def all_reduce_rms_norm_(self, t, w, eps, residual, group="tp"):
         from .. import ops
 

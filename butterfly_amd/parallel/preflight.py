@@ -1,0 +1,561 @@
+"""Multi-GPU preflight: bounded-time checks of every cross-device path before a multi-rank
+job partitions the model (VERDICT r2 "Next round" item 1; aims: "distributing inference
+across multiple nodes", /root/reference/README.md:2, and the low-overhead communication
+layer, /root/reference/CLAUDE.md:20).
+
+Every rank calls `run_preflight()` right after torch.distributed is initialised. Each check
+runs under a watchdog with its own deadline, and every outcome is voted on over a separate
+gloo (TCPStore) control group, so a broken RCCL cannot also break the vote. Three outcomes:
+
+  pass      the feature stays on (native RCCL communicators are switched ON by a pass)
+  fail      the feature is switched off on EVERY rank (environment flags read later by the
+            communicator / engine): IPC all-reduce -> RCCL, native RCCL -> torch ProcessGroups,
+            collective capture -> eager decode, comm-stream pre-post -> plain receives;
+            a failed mandatory check (world collectives, point-to-point on every rank pair)
+            ends the job with a non-zero exit naming the check
+  hang      the watchdog prints `PREFLIGHT-HANG rank=R check=NAME after=Ts` on stderr and
+            ends the process with exit code 75 (os._exit from a watchdog thread, never a
+            re-exec); the launcher then takes the other ranks down
+
+Checks, in order (G = needs a GPU and the RCCL backend; skipped on CPU / gloo):
+  world_collectives  all_reduce / all_gather / reduce_scatter / all_to_all / broadcast on the
+                     world group, results checked                            (mandatory)
+  p2p_all_pairs      batched isend / irecv with every peer (shifts 1 .. world-1): every
+                     possible pipeline edge, payload checked                 (mandatory)
+  subgroups          all_reduce inside groups of 2 and 4 consecutive ranks (TP candidates)
+  comm_stream_recv   G: irecv posted on a side stream, consumed through an event (the
+                     asynchronous pipeline's pre-posted boundary receive)
+  graph_collective   G: a torch-ProcessGroup all_reduce captured in a CUDA graph and replayed;
+                     the replay runs only if EVERY rank captured
+  native_rccl        G: own RCCL communicators (parallel/rccl.py): world init, split, all_reduce,
+                     all_gather, all_to_all, grouped send/recv, plus capture + replay
+  custom_ar          G: the IPC one-shot / two-shot all-reduce (parallel/custom_allreduce.py)
+                     for groups of 2, 4 and 8 ranks: its own self-test, then bitwise against
+                     RCCL's all-reduce, then captured in a graph and replayed
+
+Fault injection for tests: BFLY_PREFLIGHT_INJECT="check:kind[:rank],..." with kind fail
+(the check reports failure), raise (the check raises) or hang (the check never returns).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import threading
+import time
+import traceback
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+HANG_EXIT_CODE = 75
+MANDATORY = ("world_collectives", "p2p_all_pairs")
+
+
+class PreflightError(RuntimeError):
+    """A mandatory check failed on some rank: the job cannot run multi-rank."""
+
+
+@dataclass
+class PreflightReport:
+    results: dict = field(default_factory=dict)     # check -> {"ok": bool|None, "ms": float, "detail": str}
+    disabled: list = field(default_factory=list)    # features switched off
+    enabled: list = field(default_factory=list)     # features switched on
+    env: dict = field(default_factory=dict)         # environment flags set
+    allow_tp: bool = True                           # sub-groups work (TP / PP plans allowed)
+    seconds: float = 0.0
+
+    def summary(self) -> dict:
+        return {"checks": {k: v["ok"] for k, v in self.results.items()},
+                "ms": {k: round(v["ms"], 1) for k, v in self.results.items()},
+                "failed_detail": {k: v["detail"] for k, v in self.results.items() if v["ok"] is False},
+                "disabled": self.disabled, "enabled": self.enabled, "env": self.env,
+                "allow_tp": self.allow_tp, "seconds": round(self.seconds, 2)}
+
+
+# ---------------------------------------------------------------------------------------------
+# watchdog
+# ---------------------------------------------------------------------------------------------
+class _Watchdog:
+    """One thread; `arm(name, deadline)` before a check, `disarm()` after. A check still armed
+    at its deadline is reported on stderr and the process exits HANG_EXIT_CODE."""
+
+    def __init__(self, rank: int, exit_fn: Callable[[int], None] = os._exit):
+        self.rank = rank
+        self.exit_fn = exit_fn
+        self._cv = threading.Condition()
+        self._armed: Optional[tuple] = None
+        self._stop = False
+        self._t = threading.Thread(target=self._loop, name="bfly-preflight-watchdog", daemon=True)
+        self._t.start()
+
+    def arm(self, name: str, seconds: float) -> None:
+        with self._cv:
+            self._armed = (name, time.monotonic(), time.monotonic() + seconds)
+            self._cv.notify()
+
+    def disarm(self) -> None:
+        with self._cv:
+            self._armed = None
+            self._cv.notify()
+
+    def close(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+
+    def _loop(self) -> None:
+        with self._cv:
+            while not self._stop:
+                if self._armed is None:
+                    self._cv.wait()
+                    continue
+                name, t0, dl = self._armed
+                now = time.monotonic()
+                if now < dl:
+                    self._cv.wait(dl - now)
+                    continue
+                msg = f"PREFLIGHT-HANG rank={self.rank} check={name} after={now - t0:.1f}s"
+                try:
+                    sys.stderr.write(msg + "\n")
+                    sys.stderr.flush()
+                    traceback.print_stack(sys._current_frames().get(threading.main_thread().ident), file=sys.stderr)
+                    sys.stderr.flush()
+                finally:
+                    self.exit_fn(HANG_EXIT_CODE)
+                return
+
+
+# ---------------------------------------------------------------------------------------------
+# fault injection
+# ---------------------------------------------------------------------------------------------
+def _injections(rank: int) -> dict:
+    """{check: kind} for this rank from BFLY_PREFLIGHT_INJECT."""
+    out = {}
+    for item in filter(None, (os.environ.get("BFLY_PREFLIGHT_INJECT") or "").split(",")):
+        parts = item.strip().split(":")
+        if len(parts) < 2:
+            continue
+        if len(parts) >= 3 and parts[2] != "" and int(parts[2]) != rank:
+            continue
+        out[parts[0]] = parts[1]
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# checks: each returns (ok: bool | None (= not applicable), detail: str)
+# ---------------------------------------------------------------------------------------------
+def _dev() -> torch.device:
+    if dist.get_backend() == "nccl" and torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _sync(dev) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def check_world_collectives(rank: int, world: int) -> tuple:
+    dev = _dev()
+    n = 4096
+    x = torch.full((n,), float(rank + 1), device=dev)
+    dist.all_reduce(x)
+    want = world * (world + 1) / 2
+    if not bool((x == want).all()):
+        return False, f"all_reduce gave {float(x[0])}, want {want}"
+    g = torch.empty(world * 8, device=dev)
+    dist.all_gather_into_tensor(g, torch.full((8,), float(rank), device=dev)) if dev.type == "cuda" else \
+        dist.all_gather(list(g.chunk(world)), torch.full((8,), float(rank)))
+    if g.view(world, 8)[:, 0].tolist() != [float(r) for r in range(world)]:
+        return False, "all_gather order"
+    if dev.type == "cuda":
+        rs_in = torch.arange(world * 8, dtype=torch.float32, device=dev)
+        rs = torch.empty(8, device=dev)
+        dist.reduce_scatter_tensor(rs, rs_in)
+        if not bool((rs == world * torch.arange(rank * 8, rank * 8 + 8, dtype=torch.float32, device=dev)).all()):
+            return False, "reduce_scatter"
+    a_in = torch.tensor([float(rank * 100 + j) for j in range(world)], device=dev)
+    a_out = torch.empty(world, device=dev)
+    dist.all_to_all_single(a_out, a_in)
+    if a_out.tolist() != [float(j * 100 + rank) for j in range(world)]:
+        return False, f"all_to_all gave {a_out.tolist()}"
+    b = torch.full((16,), float(rank), device=dev)
+    dist.broadcast(b, 0)
+    if not bool((b == 0).all()):
+        return False, "broadcast"
+    _sync(dev)
+    return True, ""
+
+
+def check_p2p_all_pairs(rank: int, world: int) -> tuple:
+    dev = _dev()
+    bad = []
+    for shift in range(1, world):
+        dst, src = (rank + shift) % world, (rank - shift) % world
+        out = torch.full((1024,), float(rank * 1000 + dst), device=dev)
+        inp = torch.empty(1024, device=dev)
+        ops = [dist.P2POp(dist.isend, out, dst), dist.P2POp(dist.irecv, inp, src)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        _sync(dev)
+        if not bool((inp == float(src * 1000 + rank)).all()):
+            bad.append(src)
+    return (not bad), (f"wrong payload from ranks {bad}" if bad else "")
+
+
+def check_subgroups(rank: int, world: int, pgs: dict) -> tuple:
+    if not pgs:
+        return None, "no proper sub-groups at this world size"
+    dev = _dev()
+    for n, mine in pgs.items():
+        x = torch.full((256,), float(rank), device=dev)
+        dist.all_reduce(x, group=mine)
+        lo = (rank // n) * n
+        want = sum(range(lo, lo + n))
+        _sync(dev)
+        if not bool((x == want).all()):
+            return False, f"groups of {n}: got {float(x[0])}, want {want}"
+    return True, ""
+
+
+def check_comm_stream_recv(rank: int, world: int) -> tuple:
+    """A pipeline chain 0 -> 1 -> ... -> world-1 (the real stage order: a rank never sends to
+    the peer it receives from, so no send waits behind a receive on one p2p stream)."""
+    dev = _dev()
+    if dev.type != "cuda" or world < 2:
+        return None, "needs RCCL"
+    side = torch.cuda.Stream(dev)
+    ok = True
+    work = sw = None
+    buf = torch.zeros(4096, dtype=torch.bfloat16, device=dev)
+    if rank > 0:
+        ev = torch.cuda.Event()
+        ev.record()
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            work = dist.irecv(buf, rank - 1)
+    if rank + 1 < world:
+        sw = dist.isend(torch.full((4096,), float(rank % 64), dtype=torch.bfloat16, device=dev), rank + 1)
+    if work is not None:
+        work.wait()                    # the compute stream waits for the transfer
+        y = buf.float() + 1            # consumer on the compute stream
+        _sync(dev)
+        ok = bool((y == float((rank - 1) % 64) + 1).all())
+    if sw is not None:
+        sw.wait()
+    _sync(dev)
+    return ok, "" if ok else "side-stream receive not ordered before its consumer"
+
+
+def _capture(fn: Callable[[], None], dev) -> Optional[torch.cuda.CUDAGraph]:
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        fn()                       # warm-up outside capture
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    return g
+
+
+def check_graph_collective(rank: int, world: int, vote: Callable[[bool], bool]) -> tuple:
+    dev = _dev()
+    if dev.type != "cuda":
+        vote(True)
+        return None, "needs RCCL"
+    x = torch.zeros(2048, device=dev)
+    err = ""
+    try:
+        g = _capture(lambda: dist.all_reduce(x), dev)
+    except Exception as e:  # noqa: BLE001 — a capture failure is an outcome, not an error
+        g, err = None, f"capture raised {e!r}"[:300]
+    if not vote(g is not None):          # replay only if EVERY rank captured
+        return False, err or "capture failed on another rank"
+    for it in range(2):
+        x.fill_(float(rank + it))
+        g.replay()
+        _sync(dev)
+        want = sum(range(world)) + world * it
+        if not bool((x == want).all()):
+            return False, f"replay {it}: got {float(x[0])}, want {want}"
+    return True, ""
+
+
+def check_native_rccl(rank: int, world: int, vote: Callable[[bool], bool]) -> tuple:
+    dev = _dev()
+    if dev.type != "cuda":
+        vote(True)
+        return None, "needs RCCL"
+    from .rccl import RcclComm
+
+    wc = sub = None
+    try:
+        wc = RcclComm.world()
+        x = torch.full((1024,), float(rank + 1), device=dev)
+        wc.all_reduce_(x)
+        _sync(dev)
+        if not bool((x == world * (world + 1) / 2).all()):
+            raise RuntimeError("all_reduce")
+        g = torch.empty(world * 4, device=dev)
+        wc.all_gather(torch.full((4,), float(rank), device=dev), g)
+        a = torch.tensor([float(rank * 100 + j) for j in range(world)], device=dev)
+        b = torch.empty_like(a)
+        wc.all_to_all(a, b)
+        _sync(dev)
+        if g.view(world, 4)[:, 0].tolist() != [float(r) for r in range(world)]:
+            raise RuntimeError("all_gather")
+        if b.tolist() != [float(j * 100 + rank) for j in range(world)]:
+            raise RuntimeError("all_to_all")
+        # grouped point-to-point ring (the PP boundary transfer)
+        nxt, prv = (rank + 1) % world, (rank - 1) % world
+        snd = torch.full((512,), float(rank), device=dev)
+        rcv = torch.empty(512, device=dev)
+        RcclComm.group_start()
+        wc.send(snd, nxt)
+        wc.recv(rcv, prv)
+        RcclComm.group_end()
+        _sync(dev)
+        if not bool((rcv == float(prv)).all()):
+            raise RuntimeError("send/recv")
+        # split (one communicator per mesh axis): pairs of ranks
+        if world % 2 == 0:
+            sub = wc.split(rank // 2, rank % 2)
+            y = torch.full((64,), float(rank), device=dev)
+            sub.all_reduce_(y)
+            _sync(dev)
+            if not bool((y == float(2 * (rank // 2) * 2 + 1)).all()):
+                raise RuntimeError("split all_reduce")
+        ok, err = True, ""
+    except Exception as e:  # noqa: BLE001
+        ok, err = False, f"{e!r}"[:300]
+    if not vote(ok):
+        _close(wc, sub)
+        return False, err or "failed on another rank"
+    # capture + replay (graph-captured decode steps issue their collectives this way)
+    z = torch.zeros(1024, device=dev)
+    try:
+        gr = _capture(lambda: wc.all_reduce_(z), dev)
+    except Exception as e:  # noqa: BLE001
+        gr, err = None, f"capture raised {e!r}"[:300]
+    if not vote(gr is not None):
+        _close(wc, sub)
+        return False, err or "capture failed on another rank"
+    z.fill_(float(rank))
+    gr.replay()
+    _sync(dev)
+    ok = bool((z == float(sum(range(world)))).all())
+    _close(wc, sub)
+    return ok, "" if ok else "captured all_reduce replayed wrong"
+
+
+def _close(*comms) -> None:
+    for c in comms:
+        if c is not None:
+            try:
+                c.close()
+            except Exception:  # noqa: BLE001
+                pass
+
+
+def check_custom_ar(rank: int, world: int, pgs: dict, vote: Callable[[bool], bool]) -> tuple:
+    dev = _dev()
+    if dev.type != "cuda":
+        for n in (2, 4, 8):
+            if n <= world and world % n == 0:
+                vote(True)
+                vote(True)
+        return None, "needs GPUs"
+    from .custom_allreduce import CustomAllReduce
+
+    details = []
+    all_ok = True
+    for n in (2, 4, 8):
+        if n > world or world % n:
+            continue
+        pg = pgs.get(n) if n < world else dist.group.WORLD
+        ranks = list(range((rank // n) * n, (rank // n) * n + n))
+        car = None
+        ok = True
+        try:
+            car = CustomAllReduce(ranks, rank % n, pg, max_bytes=8 << 20, device=dev)
+            ok = car.ok
+            if ok:
+                for two in ([False, True] if n >= 4 else [False]):
+                    x = (torch.arange(64 * 8192, device=dev, dtype=torch.float32).view(64, 8192) % 13 + rank)
+                    x = x.to(torch.bfloat16)
+                    y = x.clone()
+                    car.all_reduce_(y, two_shot=two)
+                    r = x.clone()
+                    dist.all_reduce(r, group=pg)
+                    _sync(dev)
+                    if not torch.equal(y, r) or car.error():
+                        ok = False
+                        details.append(f"n={n} {'two' if two else 'one'}-shot differs from RCCL")
+            else:
+                details.append(f"n={n} self-test failed")
+        except Exception as e:  # noqa: BLE001
+            ok = False
+            details.append(f"n={n} raised {e!r}"[:200])
+        ok = vote(ok)
+        gr = None
+        if ok:   # captured inside a decode graph: capture on every rank, then replay
+            buf = torch.zeros(16, 8192, dtype=torch.bfloat16, device=dev)
+            try:
+                gr = _capture(lambda: car.all_reduce_(buf), dev)
+            except Exception as e:  # noqa: BLE001
+                details.append(f"n={n} capture raised {e!r}"[:200])
+        if vote(gr is not None) and gr is not None:
+            try:
+                for it in range(2):
+                    buf.fill_(float(rank + it))
+                    gr.replay()
+                    _sync(dev)
+                    if not bool((buf.float() == float(sum(ranks) + n * it)).all()) or car.error():
+                        ok = False
+                        details.append(f"n={n} replay {it} wrong")
+            except Exception as e:  # noqa: BLE001
+                ok = False
+                details.append(f"n={n} replay raised {e!r}"[:200])
+        elif ok:
+            ok = False
+        all_ok = all_ok and ok
+        if car is not None:
+            car.close()
+    return all_ok, "; ".join(details)
+
+
+# ---------------------------------------------------------------------------------------------
+# driver
+# ---------------------------------------------------------------------------------------------
+def run_preflight(timeout_s: Optional[float] = None, exit_fn: Callable[[int], None] = os._exit,
+                  apply: bool = True) -> PreflightReport:
+    """Collective over the world (every rank calls it once, after init_process_group). Returns
+    the report; with `apply` the fallbacks are written to os.environ. Raises PreflightError
+    when a mandatory check failed on any rank."""
+    rep = PreflightReport()
+    if not dist.is_initialized() or dist.get_world_size() < 2:
+        return rep
+    t_all = time.perf_counter()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    timeout_s = float(timeout_s or os.environ.get("BFLY_PREFLIGHT_TIMEOUT_S") or 90.0)
+    inject = _injections(rank)
+    wd = _Watchdog(rank, exit_fn)
+    wd.arm("control_group", timeout_s)
+    ctrl = dist.new_group(list(range(world)), backend="gloo")   # votes survive a broken RCCL
+    wd.disarm()
+
+    def vote(ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=ctrl)
+        return bool(t.item())
+
+    # sub-groups are created collectively up front (every rank, every group, same order)
+    pgs = {}
+    wd.arm("new_group", timeout_s)
+    for n in (2, 4, 8):
+        if n < world and world % n == 0:
+            groups = [list(range(i, i + n)) for i in range(0, world, n)]
+            made = [dist.new_group(g) for g in groups]
+            pgs[n] = made[rank // n]
+    wd.disarm()
+
+    def run(name: str, fn: Callable[[], tuple]) -> bool:
+        kind = inject.get(name)
+        t0 = time.perf_counter()
+        wd.arm(name, timeout_s)
+        try:
+            if kind == "hang":
+                while True:
+                    time.sleep(3600)
+            # injected fail / raise: the check still runs (its internal votes must line up
+            # with the other ranks'), with those votes forced to "failed" (voting())
+            ok, detail = fn()
+            if kind == "raise":
+                raise RuntimeError(f"injected failure in {name}")
+            if kind == "fail":
+                ok, detail = False, f"injected failure in {name}"
+        except Exception as e:  # noqa: BLE001 — an exception is a failed check
+            ok, detail = False, f"{e!r}"[:300]
+        wd.disarm()
+        # the check's own votes are done; the outcome vote decides for every rank
+        wd.arm(name + ":vote", timeout_s)
+        agreed = vote(ok is not False)
+        wd.disarm()
+        if ok is None and agreed:
+            rep.results[name] = {"ok": None, "ms": (time.perf_counter() - t0) * 1e3, "detail": detail}
+            return False
+        if not agreed and ok is not False:
+            detail = detail or "failed on another rank"
+        rep.results[name] = {"ok": bool(agreed), "ms": (time.perf_counter() - t0) * 1e3, "detail": detail}
+        return agreed
+
+    def voting(name: str) -> Callable[[bool], bool]:
+        # votes inside a check (capture-before-replay agreement) honour injected failures
+        def v(ok: bool) -> bool:
+            return vote(ok and inject.get(name) not in ("fail", "raise"))
+        return v
+
+    try:
+        for name, fn in (("world_collectives", lambda: check_world_collectives(rank, world)),
+                         ("p2p_all_pairs", lambda: check_p2p_all_pairs(rank, world))):
+            if not run(name, fn):
+                raise PreflightError(f"preflight: mandatory check '{name}' failed: "
+                                     f"{rep.results[name]['detail'] or 'on another rank'}")
+        rep.allow_tp = run("subgroups", lambda: check_subgroups(rank, world, pgs)) or not pgs
+        env = {}
+        if not run("comm_stream_recv", lambda: check_comm_stream_recv(rank, world)) \
+                and rep.results["comm_stream_recv"]["ok"] is False:
+            env["BFLY_PP_PREPOST"] = "0"
+            rep.disabled.append("pp_prepost")
+        graph_pg = run("graph_collective", lambda: check_graph_collective(rank, world, voting("graph_collective")))
+        native = run("native_rccl", lambda: check_native_rccl(rank, world, voting("native_rccl")))
+        user_native = os.environ.get("BFLY_NATIVE_RCCL")
+        if native and user_native not in ("0", "false", "off"):
+            env["BFLY_NATIVE_RCCL"] = "1"
+            rep.enabled.append("native_rccl")
+        elif rep.results["native_rccl"]["ok"] is False:
+            env["BFLY_NATIVE_RCCL"] = "0"
+            rep.disabled.append("native_rccl")
+        car = run("custom_ar", lambda: check_custom_ar(rank, world, pgs, voting("custom_ar")))
+        if not car and rep.results["custom_ar"]["ok"] is False:
+            env["BFLY_CUSTOM_AR"] = "0"
+            rep.disabled.append("custom_ar")
+        captured_ok = graph_pg or native or rep.results["graph_collective"]["ok"] is None
+        if not captured_ok:
+            env["BFLY_DISABLE_GRAPHS"] = "1"
+            rep.disabled.append("hipgraph_decode")
+        rep.env = env
+        if apply:
+            os.environ.update(env)
+    finally:
+        wd.close()
+    rep.seconds = time.perf_counter() - t_all
+    return rep
+
+
+def main(argv=None) -> int:
+    """Standalone: `torchrun --nproc-per-node N -m butterfly_amd.parallel.preflight` (or
+    tools/multigpu_preflight.py) prints rank 0's report as one JSON line."""
+    from .comm import init_distributed
+
+    rank, world, local = init_distributed()
+    if torch.cuda.is_available() and dist.get_backend() == "nccl":
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    try:
+        rep = run_preflight(apply=False)
+    except PreflightError as e:
+        print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
+        return 3
+    if rank == 0:
+        print(json.dumps({"preflight": rep.summary(), "world_size": world, "backend": dist.get_backend()}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -71,6 +71,10 @@ define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout 
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
 define("BFLY_STEP_TIMEOUT_S", 0.0, float, "engine step watchdog: terminate a rank whose step exceeds this (0 = off)")
 define("BFLY_FAULT", "", str, "fault injection 'rank:step:kind' (kind: hang|exit|nan) for tests")
+define("BFLY_PREFLIGHT", True, _bool, "multi-rank jobs (bench.py): run the bounded-time multi-GPU preflight "
+       "(parallel/preflight.py) before partitioning; failed features fall back, a hang exits 75")
+define("BFLY_PREFLIGHT_TIMEOUT_S", 90.0, float, "deadline of each preflight check (seconds)")
+define("BFLY_PREFLIGHT_INJECT", "", str, "preflight fault injection 'check:kind[:rank],...' (kind: fail|raise|hang)")
 define("BFLY_NAN_CHECK", True, _bool, "check the logits of every sampled step for NaN/Inf and fail the step "
        "(one reduction over the local vocab shard per step)")
 define("BFLY_TRACE", "", str, "write a chrome-trace JSON of engine steps to this path")

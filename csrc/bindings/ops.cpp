@@ -226,6 +226,65 @@ void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
                       out_scores.data_ptr<float>(), cur_stream(), thp, check_finite ? 1 : 0);
 }
 
+// Exact top-k / top-p radix select (sample.hip). `ws` is one zeroed f32 buffer holding
+// state [rows, 8] | smax [rows] (int32 bits) | hist [rows, 512].
+struct TkpViews { float* state; int* smax; float* hist; };
+TkpViews tkp_views(Tensor& ws, int rows) {
+  CHECK_GPU(ws);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && ws.numel() >= (long)rows * (8 + 1 + 512),
+              "tkp: workspace must be f32 [rows * 521] contiguous");
+  float* b = ws.data_ptr<float>();
+  return {b, reinterpret_cast<int*>(b + rows * 8), b + rows * 9};
+}
+
+void check_tkp_logits(const Tensor& logits, const Tensor& temps) {
+  CHECK_GPU(logits); CHECK_BF16(logits); CHECK_ALIGN16(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0, "tkp: logits");
+  TORCH_CHECK(temps.scalar_type() == at::kFloat && temps.is_contiguous() && temps.numel() == logits.size(0),
+              "tkp: temps [rows] f32");
+}
+
+void tkp_begin(const Tensor& logits, const Tensor& temps, const Tensor& top_k, const Tensor& top_p, Tensor& ws) {
+  check_tkp_logits(logits, temps);
+  const int rows = logits.size(0);
+  CHECK_I32(top_k);
+  TORCH_CHECK(top_k.numel() == rows && top_k.is_contiguous(), "tkp_begin: top_k [rows] int32");
+  TORCH_CHECK(top_p.scalar_type() == at::kFloat && top_p.numel() == rows && top_p.is_contiguous(),
+              "tkp_begin: top_p [rows] f32");
+  TkpViews v = tkp_views(ws, rows);
+  c10::DeviceGuard g(logits.device());
+  bfly::launch_tkp_begin(bf(logits), logits.stride(0), rows, logits.size(1), temps.data_ptr<float>(),
+                         top_k.data_ptr<int>(), top_p.data_ptr<float>(), v.state, v.smax, cur_stream());
+}
+
+void tkp_pass(const Tensor& logits, const Tensor& temps, Tensor& ws, int64_t pass, int64_t phase) {
+  check_tkp_logits(logits, temps);
+  TORCH_CHECK(pass >= 0 && pass < 4 && (phase == 0 || phase == 1), "tkp_pass: pass 0-3, phase 0/1");
+  const int rows = logits.size(0);
+  TkpViews v = tkp_views(ws, rows);
+  c10::DeviceGuard g(logits.device());
+  bfly::launch_tkp_pass(bf(logits), logits.stride(0), rows, logits.size(1), temps.data_ptr<float>(), v.state,
+                        v.smax, v.hist, (int)pass, (int)phase, cur_stream());
+}
+
+void tkp_select(const Tensor& top_p, Tensor& ws, int64_t rows, int64_t pass, int64_t phase) {
+  CHECK_GPU(top_p);
+  TORCH_CHECK(top_p.scalar_type() == at::kFloat && top_p.numel() == rows && top_p.is_contiguous(),
+              "tkp_select: top_p [rows] f32");
+  TORCH_CHECK(pass >= 0 && pass < 4 && (phase == 0 || phase == 1), "tkp_select: pass 0-3, phase 0/1");
+  TkpViews v = tkp_views(ws, rows);
+  c10::DeviceGuard g(top_p.device());
+  bfly::launch_tkp_select(top_p.data_ptr<float>(), v.state, v.hist, rows, (int)pass, (int)phase, cur_stream());
+}
+
+void tkp_final(Tensor& ws, int64_t rows, Tensor& thresh) {
+  TORCH_CHECK(thresh.scalar_type() == at::kFloat && thresh.numel() == rows && thresh.is_contiguous(),
+              "tkp_final: thresh [rows] f32");
+  TkpViews v = tkp_views(ws, rows);
+  c10::DeviceGuard g(ws.device());
+  bfly::launch_tkp_final(v.state, rows, thresh.data_ptr<float>(), cur_stream());
+}
+
 int64_t gemm_workspace_size(int64_t M, int64_t N, int64_t K) {
   return (int64_t)bfly::gemm_workspace_bytes(M, N, K);
 }
@@ -763,6 +822,10 @@ TORCH_LIBRARY(bfly, m) {
         "Tensor(f!)? counters) -> ()");
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
         "Tensor(b!) out_scores, Tensor(c!) workspace, Tensor? thresh=None, bool check_finite=False) -> ()");
+  m.def("tkp_begin(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor(a!) ws) -> ()");
+  m.def("tkp_pass(Tensor logits, Tensor temps, Tensor(a!) ws, int pass_, int phase) -> ()");
+  m.def("tkp_select(Tensor top_p, Tensor(a!) ws, int rows, int pass_, int phase) -> ()");
+  m.def("tkp_final(Tensor(a!) ws, int rows, Tensor(b!) thresh) -> ()");
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace, "
         "Tensor? bias=None) -> ()");
@@ -815,6 +878,10 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("embed", &embed);
   m.impl("init_hash", &init_hash);
   m.impl("sample", &sample);
+  m.impl("tkp_begin", &tkp_begin);
+  m.impl("tkp_pass", &tkp_pass);
+  m.impl("tkp_select", &tkp_select);
+  m.impl("tkp_final", &tkp_final);
   m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("gemm", &gemm);
   m.impl("gemm_with_plan", &gemm_with_plan);

@@ -56,6 +56,15 @@ void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vst
                    const float* temps, const long* seeds, uint64_t* workspace, int* out_ids,
                    float* out_scores, hipStream_t stream, const float* thresh = nullptr,
                    int check_finite = 0);
+// exact top-k / top-p thresholds by radix select (sample.hip): state [rows, 8] f32 bits,
+// smax [rows] int32 (zeroed), hist [rows, 512] f32 (zeroed); see the kernel comment
+void launch_tkp_begin(const bf16* logits, long row_stride, int rows, int V, const float* temps,
+                      const int* top_k, const float* top_p, float* state, int* smax, hipStream_t stream);
+void launch_tkp_pass(const bf16* logits, long row_stride, int rows, int V, const float* temps,
+                     float* state, const int* smax, float* hist, int pass, int phase, hipStream_t stream);
+void launch_tkp_select(const float* top_p, float* state, float* hist, int rows, int pass, int phase,
+                       hipStream_t stream);
+void launch_tkp_final(const float* state, int rows, float* thresh, hipStream_t stream);
 
 // gemm.hip
 GemmPlan plan_gemm(int M, int N, int K);

@@ -116,7 +116,7 @@ sample_partial_kernel(const bf16* __restrict__ logits, long row_stride, int V, i
   }
 }
 
-__global__ void sample_final_kernel(const uint64_t* __restrict__ partial, int chunks,
+__global__ void sample_final_kernel(const uint64_t* __restrict__ partial, int chunks, int vstart,
                                     int* __restrict__ out_ids, float* __restrict__ out_scores) {
   const int row = blockIdx.x;
   uint64_t b = 0;
@@ -124,9 +124,265 @@ __global__ void sample_final_kernel(const uint64_t* __restrict__ partial, int ch
   b = wave_max_u64(b);
   if (threadIdx.x == 0) {
     const bool bad = b == ~0ULL;
-    out_ids[row] = bad ? -1 : (int)(~(uint32_t)b);
-    if (out_scores) out_scores[row] = bad ? INFINITY : unordered_f32((uint32_t)(b >> 32));
+    // b == 0: every token of this shard lies below the row's top-k / top-p threshold (common
+    // with vocab-parallel shards). No candidate: score -inf (loses the TP merge to any real
+    // candidate), id kept in range.
+    const bool none = b == 0;
+    out_ids[row] = bad ? -1 : (none ? vstart : (int)(~(uint32_t)b));
+    if (out_scores) out_scores[row] = bad ? INFINITY : (none ? -INFINITY : unordered_f32((uint32_t)(b >> 32)));
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Exact top-k / top-p thresholds by radix select (A17/K10). The filter of a row is one
+// threshold on s = logit * (1 / temperature): top-k keeps the k largest s (ties included),
+// top-p then keeps, in descending order, every token whose preceding probability mass (under
+// the top-k-renormalised distribution) is <= p. Both thresholds are exact token values found
+// by a most-significant-digit-first radix select over the 32-bit order-preserving key of s:
+// 4 passes of 8 bits per filter, each a 256-bin histogram of the keys that still match the
+// selected prefix. Under tensor parallelism the caller SUM-all-reduces every histogram (and
+// MAX-all-reduces the row maximum), so each vocab shard contributes its tokens and all ranks
+// select the same digits; no candidate cap, no sort, fixed shapes (graph-capturable).
+//
+// Workspace per row (f32 bits; int32 fields stored through __float_as_int):
+//   state[8] : 0 top-k prefix (u32)  1 k remaining  2 top-p prefix (u32)  3 mass above prefix
+//              4 Z (mass of the top-k set)  5 flags (1 = top-k active, 2 = top-p active)
+//   smax[1]  : row max of s as a signed-comparable ordered int (MAX-reducible as int32)
+//   hist[512]: 256 counts + 256 masses exp(s - max) (SUM-reducible as f32; counts exact < 2^24)
+// ---------------------------------------------------------------------------------------
+constexpr int kTkpThreads = 256;
+
+__device__ __forceinline__ int signed_ordered(float f) { return (int)(ordered_f32(f) ^ 0x80000000u); }
+__device__ __forceinline__ float from_signed_ordered(int v) { return unordered_f32((uint32_t)v ^ 0x80000000u); }
+
+// Row maximum of s over this shard (atomicMax into smax, zeroed by the caller) and the row's
+// initial select state.
+__global__ void __launch_bounds__(kTkpThreads)
+tkp_begin_kernel(const bf16* __restrict__ logits, long row_stride, int V, int chunk,
+                 const float* __restrict__ temps, const int* __restrict__ top_k,
+                 const float* __restrict__ top_p, float* __restrict__ state, int* __restrict__ smax) {
+  __shared__ float red[kTkpThreads / 64];
+  const int row = blockIdx.x, c = blockIdx.y;
+  const float temp = temps[row];
+  const float inv_t = temp > 0.f ? 1.f / temp : 1.f;
+  const bf16* lr = logits + (long)row * row_stride;
+  const int begin = c * chunk, end = min(V, begin + chunk);
+  float m = -INFINITY;
+  for (int i = begin + threadIdx.x * 8; i < end; i += kTkpThreads * 8) {
+    if (i + 8 <= end) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lr + i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, bf2f(v[j]) * inv_t);
+    } else {
+      for (int j = 0; i + j < end; ++j) m = fmaxf(m, bf2f(lr[i + j]) * inv_t);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kTkpThreads / 64; ++w) m = fmaxf(m, red[w]);
+    atomicMax(smax + row, signed_ordered(m));
+    if (c == 0) {
+      float* st = state + row * 8;
+      const int k = temp > 0.f ? top_k[row] : 0;
+      const int flags = (k > 0 ? 1 : 0) | (temp > 0.f && top_p[row] < 1.f ? 2 : 0);
+      st[0] = __int_as_float(0);
+      st[1] = __int_as_float(k);
+      st[2] = __int_as_float(0);
+      st[3] = 0.f;
+      st[4] = 0.f;
+      st[5] = __int_as_float(flags);
+    }
+  }
+}
+
+// One radix pass: histogram of digit `pass` (bits 31-8*pass .. 24-8*pass) of the keys whose
+// higher digits equal the selected prefix. phase 0 = top-k (counts), 1 = top-p (counts and
+// masses, restricted to keys >= the top-k threshold key).
+__global__ void __launch_bounds__(kTkpThreads)
+tkp_hist_kernel(const bf16* __restrict__ logits, long row_stride, int V, int chunk,
+                const float* __restrict__ temps, const float* __restrict__ state,
+                const int* __restrict__ smax, float* __restrict__ hist, int pass, int phase) {
+  __shared__ float h[512];
+  const int row = blockIdx.x, c = blockIdx.y;
+  const float* st = state + row * 8;
+  const int flags = __float_as_int(st[5]);
+  if (!(flags & (phase == 0 ? 1 : 2))) return;   // block-uniform
+  for (int i = threadIdx.x; i < 512; i += kTkpThreads) h[i] = 0.f;
+  __syncthreads();
+  const float inv_t = 1.f / temps[row];
+  const uint32_t prefix = (uint32_t)__float_as_int(st[phase == 0 ? 0 : 2]);
+  const uint32_t kmin = (phase == 1 && (flags & 1)) ? (uint32_t)__float_as_int(st[0]) : 0u;
+  const float mx = from_signed_ordered(smax[row]);
+  const int shift = 24 - 8 * pass;
+  const bf16* lr = logits + (long)row * row_stride;
+  const int begin = c * chunk, end = min(V, begin + chunk);
+  auto add = [&](float s) {
+    const uint32_t key = ordered_f32(s);
+    if (key < kmin) return;
+    if (pass > 0 && (key >> (shift + 8)) != prefix) return;
+    const int d = (key >> shift) & 255;
+    atomicAdd(&h[d], 1.f);
+    if (phase == 1) atomicAdd(&h[256 + d], __expf(s - mx));
+  };
+  for (int i = begin + threadIdx.x * 8; i < end; i += kTkpThreads * 8) {
+    if (i + 8 <= end) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lr + i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) add(bf2f(v[j]) * inv_t);
+    } else {
+      for (int j = 0; i + j < end; ++j) add(bf2f(lr[i + j]) * inv_t);
+    }
+  }
+  __syncthreads();
+  float* hr = hist + (long)row * 512;
+  for (int i = threadIdx.x; i < (phase == 1 ? 512 : 256); i += kTkpThreads)
+    if (h[i] != 0.f) atomicAdd(hr + i, h[i]);
+}
+
+// Pick this pass's digit from the (reduced) histogram and clear it for the next pass. One
+// wave per row; lane l owns bins 4l .. 4l+3, and the scan runs from the top bin down.
+__global__ void __launch_bounds__(64)
+tkp_select_kernel(const float* __restrict__ top_p, float* __restrict__ state,
+                  float* __restrict__ hist, int pass, int phase) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  float* st = state + row * 8;
+  const int flags = __float_as_int(st[5]);
+  float* hr = hist + (long)row * 512;
+  if (!(flags & (phase == 0 ? 1 : 2))) return;
+  // lanes in DESCENDING bin order: lane l holds bins 255-4l .. 252-4l
+  float cnt[4], mass[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    cnt[j] = hr[255 - 4 * lane - j];
+    mass[j] = phase == 1 ? hr[256 + 255 - 4 * lane - j] : 0.f;
+  }
+  // inclusive prefix sums over the descending order: per-lane, then across lanes
+  float cs = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+  float ms = mass[0] + mass[1] + mass[2] + mass[3];
+  float cex = cs, mex = ms;   // becomes the exclusive prefix of the lane
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float a = __shfl_up(cex, o, 64), b = __shfl_up(mex, o, 64);
+    if (lane >= o) { cex += a; mex += b; }
+  }
+  const float ctot = __shfl(cex, 63, 64), mtot = __shfl(mex, 63, 64);
+  cex -= cs;
+  mex -= ms;
+  int choice = -1;   // digit chosen by this lane (the wave takes the max / min below)
+  if (phase == 0) {
+    const int k_rem = __float_as_int(st[1]);
+    if (pass == 0 && ctot < (float)k_rem) {   // k >= tokens: keep everything
+      if (lane == 0) st[5] = __int_as_float(flags & ~1);
+    } else {
+      // first bin (descending) where the inclusive count reaches k_rem
+      float run = cex;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float before = run;
+        run += cnt[j];
+        if (choice < 0 && before < (float)k_rem && run >= (float)k_rem) choice = 255 - 4 * lane - j;
+      }
+      // exactly one lane holds the crossing bin
+      int d = choice;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) d = max(d, __shfl_xor(d, o, 64));
+      float above = 0.f;   // count of bins strictly above d
+      run = cex;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (255 - 4 * lane - j == d) above = run;
+        run += cnt[j];
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) above += __shfl_xor(above, o, 64);
+      if (lane == 0) {
+        st[0] = __int_as_float((int)(((uint32_t)__float_as_int(st[0]) << 8) | (uint32_t)d));
+        st[1] = __int_as_float(k_rem - (int)above);
+      }
+    }
+  } else {
+    float z = st[4], mabove = st[3];
+    if (pass == 0) { z = mtot; mabove = 0.f; }
+    const float lim = top_p[row] * z;
+    // lowest non-empty bin whose mass strictly above it (within the prefix) keeps
+    // mabove + that <= lim; scanning descending, that is the LAST qualifying bin
+    float run = mex, keep_above = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (cnt[j] > 0.f && mabove + run <= lim) { choice = 255 - 4 * lane - j; keep_above = run; }
+      run += mass[j];
+    }
+    // smallest digit among lanes' choices (descending order: the largest lane index wins)
+    int d = choice < 0 ? 256 : choice;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = min(d, __shfl_xor(d, o, 64));
+    float ka = (choice == d) ? keep_above : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ka += __shfl_xor(ka, o, 64);
+    if (lane == 0) {
+      if (d == 256) d = 255;   // unreachable with a consistent histogram (the top bin qualifies)
+      st[2] = __int_as_float((int)(((uint32_t)__float_as_int(st[2]) << 8) | (uint32_t)d));
+      st[3] = mabove + ka;
+      st[4] = z;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hr[255 - 4 * lane - j] = 0.f;
+    hr[256 + 255 - 4 * lane - j] = 0.f;
+  }
+}
+
+// Final per-row threshold on s (-inf = no filter), as read by sample_partial_kernel.
+__global__ void tkp_final_kernel(const float* __restrict__ state, int rows, float* __restrict__ thresh) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  const float* st = state + row * 8;
+  const int flags = __float_as_int(st[5]);
+  uint32_t key = 0;
+  if (flags & 1) key = (uint32_t)__float_as_int(st[0]);
+  if (flags & 2) key = max(key, (uint32_t)__float_as_int(st[2]));
+  thresh[row] = flags ? unordered_f32(key) : -INFINITY;
+}
+
+static void tkp_chunks(int V, int& chunks, int& chunk) {
+  chunks = (V + 8191) / 8192;
+  if (chunks > 64) chunks = 64;
+  chunk = (V + chunks - 1) / chunks;
+  chunk = (chunk + 7) / 8 * 8;
+  chunks = (V + chunk - 1) / chunk;
+}
+
+void launch_tkp_begin(const bf16* logits, long row_stride, int rows, int V, const float* temps,
+                      const int* top_k, const float* top_p, float* state, int* smax, hipStream_t stream) {
+  if (rows <= 0) return;
+  int chunks, chunk;
+  tkp_chunks(V, chunks, chunk);
+  tkp_begin_kernel<<<dim3(rows, chunks), kTkpThreads, 0, stream>>>(logits, row_stride, V, chunk, temps, top_k,
+                                                                    top_p, state, smax);
+}
+
+void launch_tkp_pass(const bf16* logits, long row_stride, int rows, int V, const float* temps,
+                     float* state, const int* smax, float* hist, int pass, int phase, hipStream_t stream) {
+  if (rows <= 0) return;
+  int chunks, chunk;
+  tkp_chunks(V, chunks, chunk);
+  tkp_hist_kernel<<<dim3(rows, chunks), kTkpThreads, 0, stream>>>(logits, row_stride, V, chunk, temps, state,
+                                                                   smax, hist, pass, phase);
+}
+
+void launch_tkp_select(const float* top_p, float* state, float* hist, int rows, int pass, int phase,
+                       hipStream_t stream) {
+  if (rows <= 0) return;
+  tkp_select_kernel<<<rows, 64, 0, stream>>>(top_p, state, hist, pass, phase);
+}
+
+void launch_tkp_final(const float* state, int rows, float* thresh, hipStream_t stream) {
+  if (rows <= 0) return;
+  tkp_final_kernel<<<(rows + 63) / 64, 64, 0, stream>>>(state, rows, thresh);
 }
 
 void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vstart,
@@ -141,7 +397,7 @@ void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vst
   dim3 g1(rows, chunks);
   sample_partial_kernel<<<g1, kSampleThreads, 0, stream>>>(logits, row_stride, V, chunk, vstart,
                                                            temps, seeds, thresh, workspace, check_finite);
-  sample_final_kernel<<<rows, 64, 0, stream>>>(workspace, chunks, out_ids, out_scores);
+  sample_final_kernel<<<rows, 64, 0, stream>>>(workspace, chunks, vstart, out_ids, out_scores);
 }
 
 }  // namespace bfly

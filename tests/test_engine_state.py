@@ -121,3 +121,21 @@ def test_launcher_restart_resumes_from_snapshot(tmp_path):
     got, log = run({"BFLY_FAULT": "1:7:exit"}, ["--max-restarts", "1"], tmp_path)
     assert "restart 1/1" in log and "resumed 3 requests" in log, log[-3000:]
     assert got == want and len(want) == 3 and all(len(t) == 12 for t in want)
+
+
+def test_snapshot_job_identity(tmp_path):
+    """A restarted job resumes only a snapshot carrying its own job fingerprint (ADVICE r2:
+    a stale snapshot of an earlier job in the same directory must never be replayed)."""
+    p1 = SamplingParams(max_tokens=4, temperature=0.7, seed=5)
+    job_a = state.job_fingerprint("llama-tiny", ["abc", "x"], p1)
+    assert job_a == state.job_fingerprint("llama-tiny", ["abc", "x"], SamplingParams(max_tokens=4, temperature=0.7, seed=5))
+    assert job_a != state.job_fingerprint("llama-tiny", ["abc", "y"], p1)
+    assert job_a != state.job_fingerprint("llama-tiny", ["abc", "x"], SamplingParams(max_tokens=5, temperature=0.7, seed=5))
+    eng = _engine(False)
+    eng.job_id = job_a
+    eng.add_request([1, 2], SamplingParams(max_tokens=2))
+    path = state.save(eng, state.replica_path(tmp_path, 0))
+    assert state.snapshot_job(path) == job_a
+    with pytest.raises(ValueError):
+        state.restore(_engine(False), state.load(path), job="some-other-job")
+    assert state.restore(_engine(False), state.load(path), job=job_a) == [0]

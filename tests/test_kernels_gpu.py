@@ -117,28 +117,65 @@ def test_sample_gumbel_matches_reference():
 
 
 def test_sample_topk_topp_on_device():
-    """Filtered sampling (top-k / top-p thresholds + the thresholded Gumbel kernel) on the GPU
-    picks exactly what the fp32 reference picks with the same thresholds, and every pick lies
-    in the exact truncated set."""
+    """Filtered sampling on the GPU: the radix-select thresholds (tkp_* kernels) equal the
+    tie-aware exact ones on a 128k vocabulary with high-entropy rows (nuclei of thousands of
+    tokens), equal the CPU reference's, and the thresholded Gumbel kernel then picks exactly
+    what the fp32 reference picks."""
     from butterfly_amd.engine.sampler import Sampler, SamplingParams
+    from tests.test_sampler import value_threshold
 
-    V = 4096
-    logits = _bf(4, V, scale=3.0, seed=17)
-    params = [SamplingParams(temperature=0.8, top_k=20), SamplingParams(temperature=1.0, top_p=0.4),
-              SamplingParams(temperature=0.6, top_k=50, top_p=0.7), SamplingParams(temperature=0.0)]
+    V = 128256
+    params = [SamplingParams(temperature=0.8, top_k=20), SamplingParams(temperature=1.0, top_p=0.9),
+              SamplingParams(temperature=0.6, top_k=5000, top_p=0.95), SamplingParams(temperature=0.0),
+              SamplingParams(temperature=1.2, top_p=0.3), SamplingParams(temperature=1.0, top_k=1)]
+    logits = _bf(len(params), V, scale=0.6, seed=17)
     temps = torch.tensor([p.temperature for p in params], device=DEV)
-    seeds = torch.tensor([3, 5, 7, 9], dtype=torch.int64, device=DEV)
+    seeds = torch.arange(3, 3 + len(params), dtype=torch.int64, device=DEV)
     smp = Sampler(None, V, 0, 1)
     thr = smp.thresholds(logits, temps, params)
+    thr_cpu = Sampler(None, V, 0, 1).thresholds(logits.cpu(), temps.cpu(), params)
+    for r, p in enumerate(params):
+        if p.temperature <= 0:
+            assert float(thr[r]) == float("-inf")
+            continue
+        want = value_threshold(logits[r].cpu(), p.temperature, p.top_k, p.top_p)
+        assert float(thr[r]) == want, (r, float(thr[r]), want)
+        assert float(thr_cpu[r]) == want
     ids, _ = ops.sample(logits, temps, seeds, vstart=0, thresh=thr)
     ids_ref, _ = ref.sample(logits.cpu(), temps.cpu(), seeds.cpu(), vstart=0, thresh=thr.cpu())
     assert ids.cpu().tolist() == ids_ref.tolist()
     got = smp.sample(logits, temps, seeds, params)
     assert torch.equal(got.cpu(), ids.cpu())
-    for r, p in enumerate(params[:3]):
-        s = logits[r].float() / p.temperature
-        assert s[int(ids[r])] >= thr[r]
     assert int(ids[3]) == int(logits[3].float().argmax())
+    assert int(ids[5]) == int(logits[5].float().argmax())
+
+
+@pytest.mark.parametrize("tp", [2, 4])
+def test_sample_filtered_vocab_parallel_on_device(tp):
+    """Vocab-parallel shards on the GPU (loopback TP ranks sharing the device): histograms are
+    summed across shards, shards left without a candidate (top_k = 1, tiny top_p) score -inf,
+    and the merged ids equal the single-shard ids."""
+    from butterfly_amd.engine.sampler import Sampler, SamplingParams
+    from butterfly_amd.parallel.fake import FakeWorld
+    from butterfly_amd.parallel.mesh import Mesh
+
+    V = 32768
+    params = [SamplingParams(temperature=1.0, top_k=1), SamplingParams(temperature=0.8, top_p=0.02),
+              SamplingParams(temperature=1.1, top_k=3000, top_p=0.9), SamplingParams(temperature=0.0)]
+    logits = _bf(len(params), V, scale=2.0, seed=23)
+    temps = torch.tensor([p.temperature for p in params], device=DEV)
+    seeds = torch.arange(5, 5 + len(params), dtype=torch.int64, device=DEV)
+    one = Sampler(None, V, 0, 1).sample(logits, temps, seeds, params, check_finite=True)
+    assert int(one[0]) == int(logits[0].float().argmax())
+    world = FakeWorld(Mesh(tp=tp))
+
+    def body(rank, comm):
+        Vl = V // tp
+        return Sampler(comm, V, rank * Vl, tp).sample(logits[:, rank * Vl:(rank + 1) * Vl].contiguous(), temps,
+                                                      seeds, params, check_finite=True)
+
+    for ids in world.run(body):
+        assert ids.cpu().tolist() == one.cpu().tolist()
 
 
 GEMM_SHAPES = [

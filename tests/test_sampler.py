@@ -1,6 +1,7 @@
-"""Device top-k / top-p (engine/sampler.py): one threshold per row on logit / temperature,
-Gumbel-max over the kept set. Checked against an exact sort-based reference of the truncated
-set, across TP splits of the vocabulary (loopback ranks), and end to end."""
+"""Device top-k / top-p (engine/sampler.py): one exact radix-selected threshold per row on
+logit * (1 / temperature), Gumbel-max over the kept set. Checked against an exact sort-based
+reference of the truncated set (including 128k-vocab, high-entropy rows whose nucleus holds
+thousands of tokens), across TP splits of the vocabulary (loopback ranks), and end to end."""
 import pytest
 import torch
 
@@ -11,7 +12,7 @@ from butterfly_amd.parallel.mesh import Mesh
 
 def exact_keep(row: torch.Tensor, temp: float, top_k: int, top_p: float) -> torch.Tensor:
     """The kept token set by sorting (top-k first, then the nucleus of the renormalised rest)."""
-    s = row.float() / temp
+    s = row.float() * (1.0 / torch.tensor(temp, dtype=torch.float32))   # the kernels' f32 scaling
     order = torch.argsort(s, descending=True)
     sv = s[order]
     n = len(sv) if top_k <= 0 else min(top_k, len(sv))
@@ -22,6 +23,25 @@ def exact_keep(row: torch.Tensor, temp: float, top_k: int, top_p: float) -> torc
     m = int((before <= top_p).sum()) if top_p < 1.0 else n
     keep[order[:max(1, m)]] = True
     return keep
+
+
+def value_threshold(row: torch.Tensor, temp: float, top_k: int, top_p: float) -> float:
+    """Tie-aware exact threshold (a value filter keeps whole tie groups): top-k keeps every
+    token >= the k-th largest value; top-p then keeps each value whose strictly larger tokens
+    hold <= p of the (top-k renormalised) mass."""
+    s = row.float() * (1.0 / torch.tensor(temp, dtype=torch.float32))
+    sv = torch.sort(s, descending=True).values.double()
+    t = float("-inf")
+    if top_k > 0:
+        t = float(sv[min(top_k, len(sv)) - 1])
+        sv = sv[sv >= t]
+    if top_p < 1.0:
+        vals, counts = torch.unique_consecutive(sv, return_counts=True)
+        mass = torch.exp(vals - vals[0]) * counts
+        above = torch.cumsum(mass, 0) - mass               # mass strictly above each value
+        ok = above <= top_p * mass.sum()
+        t = max(t, float(vals[ok].min()))
+    return t
 
 
 CASES = [SamplingParams(temperature=0.8, top_k=5), SamplingParams(temperature=1.0, top_p=0.3),
@@ -37,7 +57,7 @@ def test_thresholds_match_exact_sets():
     temps = torch.tensor([p.temperature for p in CASES])
     thr = smp.thresholds(logits, temps, CASES)
     for r, p in enumerate(CASES):
-        got = (logits[r].float() / p.temperature) >= thr[r]
+        got = (logits[r].float() * (1.0 / torch.tensor(p.temperature))) >= thr[r]
         assert torch.equal(got, exact_keep(logits[r], p.temperature, p.top_k, p.top_p)), r
 
 
@@ -74,6 +94,48 @@ def test_filtered_sampling_stays_in_set_and_is_tp_invariant():
         smp = Sampler(comm, V, rank * V // 2, 2)
         return smp.sample(logits[:, rank * V // 2:(rank + 1) * V // 2],
                           torch.tensor([p.temperature for p in CASES]), seeds, CASES)
+
+    for ids in world.run(body):
+        assert torch.equal(ids, one)
+
+
+def test_wide_nucleus_128k_vocab_is_exact():
+    """High-entropy rows over a Llama-3-sized vocabulary: the nucleus holds far more than the
+    1,024 candidates the previous top-C scheme could see; the radix select stays exact."""
+    torch.manual_seed(3)
+    V = 128256
+    params = [SamplingParams(temperature=1.0, top_p=0.9), SamplingParams(temperature=1.5, top_k=5000, top_p=0.95),
+              SamplingParams(temperature=0.9, top_k=3000), SamplingParams(temperature=1.0, top_p=0.5)]
+    logits = (torch.randn(len(params), V) * 0.5).to(torch.bfloat16)
+    temps = torch.tensor([p.temperature for p in params])
+    thr = Sampler(None, V, 0, 1).thresholds(logits, temps, params)
+    for r, p in enumerate(params):
+        keep = exact_keep(logits[r], p.temperature, p.top_k, p.top_p)
+        got = (logits[r].float() * (1.0 / torch.tensor(p.temperature))) >= thr[r]
+        assert int(keep.sum()) > 1024
+        # bf16 logits tie: a value threshold keeps whole tie groups (value_threshold)
+        assert float(thr[r]) == value_threshold(logits[r], p.temperature, p.top_k, p.top_p), r
+
+
+@pytest.mark.parametrize("tp", [2, 4])
+def test_narrow_filters_with_empty_shards(tp):
+    """top_k=1 / tiny top_p leave most vocab shards with no candidate: the merged id must be
+    the single-rank id (an empty shard scores -inf, never NaN / id -1)."""
+    torch.manual_seed(4)
+    V = 1024
+    params = [SamplingParams(temperature=1.0, top_k=1), SamplingParams(temperature=0.8, top_p=0.01),
+              SamplingParams(temperature=1.2, top_k=2, top_p=0.5)]
+    logits = torch.randn(len(params), V) * 4
+    temps = torch.tensor([p.temperature for p in params])
+    seeds = torch.tensor([11, 12, 13], dtype=torch.int64)
+    one = Sampler(None, V, 0, 1).sample(logits, temps, seeds, params, check_finite=True)
+    assert int(one[0]) == int(logits[0].argmax())
+    world = FakeWorld(Mesh(tp=tp))
+
+    def body(rank, comm):
+        Vl = V // tp
+        return Sampler(comm, V, rank * Vl, tp).sample(logits[:, rank * Vl:(rank + 1) * Vl], temps, seeds, params,
+                                                      check_finite=True)
 
     for ids in world.run(body):
         assert torch.equal(ids, one)

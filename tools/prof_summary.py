@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals for the decode phase (every
-dispatch after the last prefill-attention dispatch) and per decode step.
+"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals for the decode phase and per
+decode step.
 
-usage: python tools/prof_summary.py gpurun_out/prof_x/run_kernel_trace.csv|run_results.db [--steps K] [--md out.md]
+The decode window is cut from the trace itself: it starts after the first sampling dispatch
+that follows the LAST prefill kernel (flash-prefill attention, big-tile GEMM or a hipBLASLt
+`Cijk` GEMM), so the prefill step's own tail (norm, LM head, sampling) is outside it, and it
+ends with the last sampling dispatch. Every decode step samples exactly once
+(sample_final_kernel), so the number of decode steps in the window is the number of sampling
+dispatches in it; with --layers the count of decode-attention dispatches / layers is printed
+as a cross-check.
+
+usage: python tools/prof_summary.py gpurun_out/prof_x/run_kernel_trace.csv|run_results.db [--layers 80] [--md out.md]
 """
 import argparse
 import csv
@@ -34,15 +42,19 @@ def load_rows(path: str) -> list:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--steps", type=int, default=0, help="decode steps in the window (for per-step numbers)")
+    ap.add_argument("--layers", type=int, default=0, help="model layers (cross-check: attention calls / layers)")
     ap.add_argument("--md", default=None)
     a = ap.parse_args()
     rows = load_rows(a.trace)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # the decode window starts after the prefill's last attention AND its trailing big-tile GEMMs
-    last_prefill = max((i for i, r in enumerate(rows) if "attn_prefill" in r["Kernel_Name"]
-                        or "gemm_big_kernel" in r["Kernel_Name"]), default=-1)
-    dec = rows[last_prefill + 1:]
+    is_prefill = lambda n: "attn_prefill" in n or "gemm_big" in n or "Cijk" in n   # noqa: E731
+    is_sample = lambda n: "sample_final" in n                                          # noqa: E731
+    last_prefill = max((i for i, r in enumerate(rows) if is_prefill(r["Kernel_Name"])), default=-1)
+    samples = [i for i, r in enumerate(rows) if is_sample(r["Kernel_Name"]) and i > last_prefill]
+    if len(samples) < 2:
+        raise SystemExit("trace holds fewer than two decode steps after the last prefill kernel")
+    dec = rows[samples[0] + 1:samples[-1] + 1]
+    steps = len(samples) - 1
     agg = defaultdict(lambda: [0, 0.0])
     for r in dec:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
@@ -55,9 +67,13 @@ def main():
              "", "| kernel | calls | total ms | % | avg us |", "|---|---|---|---|---|"]
     for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         lines.append(f"| {k} | {c} | {t / 1e3:.3f} | {100 * t / tot:.1f} | {t / c:.1f} |")
-    if a.steps:
-        lines.append("")
-        lines.append(f"per decode step (/{a.steps}): kernel time {tot / a.steps / 1e3:.3f} ms")
+    lines.append("")
+    lines.append(f"decode steps in the window: {steps} (sampling dispatches); per step: kernel time "
+                 f"{tot / steps / 1e3:.3f} ms, wall span {span / steps / 1e3:.3f} ms, "
+                 f"{len(dec) / steps:.1f} dispatches")
+    if a.layers:
+        n_attn = sum(c for k, (c, _) in agg.items() if "attn_decode" in k)
+        lines.append(f"cross-check: {n_attn} decode-attention dispatches / {a.layers} layers = {n_attn / a.layers:.2f} steps")
     text = "\n".join(lines)
     print(text)
     if a.md:
