@@ -300,7 +300,7 @@ def run(a) -> int:
         "rccl_ranks_seen": ranks_seen,
         "plan": {"name": plan.name, "dp": mesh.dp, "tp": mesh.tp, "pp": mesh.pp, "ep": mesh.ep,
                  "estimate_tokens_per_s": round(plan.estimate["tokens_per_second"], 1)},
-        "graphs_captured": sorted(runner.graphs),
+        "graphs_captured": runner.captured_buckets,
         "graphs_failed": sorted(runner.eager_buckets),
         "custom_ar_active": comm.custom_ar is not None,
         "comm_probe": probe or None,
@@ -309,7 +309,7 @@ def run(a) -> int:
         "config": {"model": MODEL_NAMES.get(a.model, a.model),
                    "global_batch": a.batch_per_gpu * a.gpus, "seq_len": a.prompt_len,
                    "parallelism": plan.name, "stages": [list(s) for s in plan.stages],
-                   "hipgraph": bool(runner.graphs) and not runner.eager_buckets,
+                   "hipgraph": bool(runner.captured_buckets) and not runner.eager_buckets,
                    "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""),
                    "pp_async_groups": groups if groups > 1 else None,
                    "async_decode": bool(eng.async_pp and mesh.pp == 1)},

@@ -35,7 +35,7 @@ import torch
 from .. import ops
 from ..config import EngineConfig, ModelConfig
 from ..models import Shard, build_model
-from ..parallel.comm import Communicator
+from ..parallel.comm import Communicator, NativeWork
 from ..parallel.mesh import Mesh
 from ..utils import flags, trace
 from ..utils.health import FaultInjector, StepWatchdog
@@ -155,6 +155,12 @@ class LLMEngine:
         self._bbufs: list = []
         self._bslot = 0
         self._bevents: list = [None, None]
+        # native RCCL pipeline edges: a non-first stage's decode graph receives the boundary
+        # rows itself (model_runner.set_pipeline_io) and stages send their graphs' static
+        # outputs on the communicator's send stream — no pre-posted buffers, no copies
+        self._native_pp = bool(self.async_pp and mesh.pp > 1 and getattr(self.comm, "native_p2p", False))
+        if self._native_pp:
+            self._prepost = False
         self._comm_stream = (torch.cuda.Stream(self.device)
                              if self._prepost and self.device.type == "cuda" else None)
         d = self.model.dims
@@ -169,6 +175,9 @@ class LLMEngine:
             buckets.append(self.scheduler.group_batch)    # a full group replays one graph
         self.runner = ModelRunner(self.model, self.kv, engine_cfg.max_seq_len, engine_cfg.use_graphs,
                                   buckets, max_batch=engine_cfg.max_batch)
+        if self._native_pp:
+            self.runner.set_pipeline_io(recv_fn=None if coord.pp == 0 else self.comm.recv_native,
+                                        sends=coord.pp < mesh.pp - 1)
         self.requests: dict[int, Request] = {}
         self._ids = itertools.count()
         self.metrics = Metrics()
@@ -659,12 +668,13 @@ class LLMEngine:
     def _pp_stage_work(self, p: PipePlan) -> None:
         """recv the residual stream (stage > 0) -> run this stage -> isend (not last) or sample
         (last stage: ids kept on the plan for the broadcast)."""
+        native_dec = self._native_pp and p.plan.kind == 2   # the decode graph receives itself
         h, posted = None, self._posted.pop(p.tick, None)
         if posted is not None:
             h, work, slot = posted
             work.wait()          # RCCL: the compute stream waits for the transfer, the host does not
             self.metrics.inc("pp_preposted_recvs")
-        elif not self.pp_first:
+        elif not self.pp_first and not native_dec:
             h = torch.empty(p.tokens, self.cfg.hidden_size, dtype=self.model.dtype, device=self.device)
             self.comm.recv(h, self.mesh.prev_stage(self.rank))
         if p.cow:
@@ -680,8 +690,19 @@ class LLMEngine:
             ev.record()          # after every kernel that reads the boundary buffer
             self._bevents[posted[2]] = ev
         if not self.pp_last:
-            snd = out.clone() if p.plan.kind == 2 else out   # graph outputs are reused by the next replay
-            self._sends.append(self.comm.isend(self._maybe_poison(snd), self.mesh.next_stage(self.rank)))
+            nxt = self.mesh.next_stage(self.rank)
+            if native_dec:
+                # the whole bucket of the instance just replayed, straight from its static output;
+                # the runner replays that instance again only after this send completed
+                g = self.runner.last_instance
+                w = self.comm.isend(self._maybe_poison(g.output), nxt)
+                g.send_done = w.event
+                self.metrics.inc("pp_native_graph_sends")
+            else:
+                snd = out.clone() if p.plan.kind == 2 else out   # graph outputs are reused by the next replay
+                w = self.comm.isend(self._maybe_poison(snd), nxt)
+                if not isinstance(w, NativeWork):   # native sends keep their tensor alive themselves
+                    self._sends.append(w)
         else:
             p.ids = self._sample(out, p.rids)
 

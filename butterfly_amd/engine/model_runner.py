@@ -6,6 +6,15 @@ inputs into the bucket's buffers (padding rows: slot -1 = no cache write, ctx_le
 replays. Everything inside — GEMMs, RoPE/KV append, paged attention, norms, TP all-reduces
 (RCCL or the one-shot P2P kernel), the LM head and the TP sampling all-gather — is captured,
 so the host cost per token is one replay.
+
+Pipeline stages on native RCCL (`set_pipeline_io`): a non-first stage's decode graph starts
+with the receive of the previous stage's boundary rows (Communicator.recv_native, captured in
+the graph), landing them directly in the graph's static `hidden_in`; the full bucket is on the
+wire, so sender and receiver agree on the shape whatever each replays. A stage that sends keeps
+TWO instances per bucket and alternates them: the send of one instance's static output (issued
+by the engine on the communicator's send stream, no copy) may still be in flight while the
+other instance computes the next tick; an instance is replayed again only after its send-done
+event (`_DecodeGraph.send_done`).
 """
 from __future__ import annotations
 
@@ -39,6 +48,7 @@ class _DecodeGraph:
         self.hidden_in = None if first else torch.zeros(bucket, hidden, dtype=torch.bfloat16, device=device)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.output: Optional[torch.Tensor] = None
+        self.send_done = None        # event: the send of `output` has completed (pipeline stages)
 
 
 class ModelRunner:
@@ -63,6 +73,21 @@ class ModelRunner:
         hb = max(self.buckets + [max_batch])
         self._tables_host = np.zeros((hb, self.max_blocks), dtype=np.int32)
         self._ctx_host = np.zeros((hb,), dtype=np.int32)
+        # native pipeline I/O (set_pipeline_io)
+        self.recv_fn = None
+        self.instances = 1
+        self._flip: dict = {}          # bucket -> index of the instance replayed next
+        self.last_instance: Optional[_DecodeGraph] = None
+
+    def set_pipeline_io(self, recv_fn=None, sends: bool = False) -> None:
+        """`recv_fn(t)`: receive the previous stage's rows into `t` on the current stream
+        (captured at the head of every decode graph); `sends`: the stage's outputs are sent,
+        so each bucket gets two alternating instances (module doc)."""
+        self.recv_fn = recv_fn
+        self.instances = 2 if sends else 1
+
+    def bucket_of(self, n: int) -> int:
+        return self.buckets[bisect.bisect_left(self.buckets, n)]
 
     # ------------------------------------------------------------------------------------
     def prefill_batch(self, plan, tokens_of) -> ForwardBatch:
@@ -162,6 +187,10 @@ class ModelRunner:
         shape; steps where some EP rank is prefilling run eagerly (graphs_ok=False)."""
         B = len(inp["ids"])
         need = max(B, ep_tokens)
+        if self.recv_fn is not None or self.instances > 1:
+            if need > self.buckets[-1]:
+                raise RuntimeError(f"pipeline decode of {need} rows exceeds the largest bucket {self.buckets[-1]}")
+            return self._run_pipeline_decode(self.bucket_of(need), inp, hidden_in)
         if not self.use_graphs or not graphs_ok or need > self.buckets[-1] or ep_alltoall:
             fb = self.decode_batch(inp, ep_tokens)
             fb.ep_alltoall = ep_alltoall
@@ -182,6 +211,48 @@ class ModelRunner:
                 return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
         self._stage(g, inp, hidden_in)
         g.graph.replay()
+        return g.output[:B]
+
+    def _run_pipeline_decode(self, bucket: int, inp: dict, hidden_in):
+        """Decode of a pipeline stage with native I/O: alternate the bucket's instances, wait
+        for the instance's previous send, receive (inside the graph, or eagerly into the same
+        static buffer on the eager fallback) and run over the whole bucket. The instance is
+        left in `last_instance` (its full-bucket `output` is what the engine sends)."""
+        B = len(inp["ids"])
+        insts = self.graphs.get(bucket)
+        if insts is None:
+            insts = []
+            for i in range(self.instances):
+                g = None
+                if self.use_graphs and bucket not in self.eager_buckets:
+                    try:
+                        g = self._capture(bucket, register=False)
+                    except Exception as e:  # noqa: BLE001 — eager on the same static buffers
+                        import warnings
+
+                        warnings.warn(f"hipGraph capture of decode bucket {bucket} failed ({e!r}); "
+                                      "running eagerly")
+                        self.eager_buckets.add(bucket)
+                        torch.cuda.synchronize(self.device)
+                if g is None:
+                    m = self.model
+                    g = _DecodeGraph(bucket, self.max_blocks, self.device, m.cfg.hidden_size, m.first)
+                insts.append(g)
+            self.graphs[bucket] = insts
+        i = self._flip.get(bucket, 0)
+        self._flip[bucket] = (i + 1) % len(insts)
+        g = insts[i]
+        if g.send_done is not None:
+            torch.cuda.current_stream(self.device).wait_event(g.send_done)
+            g.send_done = None
+        self._stage(g, inp, None if self.recv_fn is not None else hidden_in)
+        if g.graph is not None:
+            g.graph.replay()
+        else:
+            if self.recv_fn is not None:
+                self.recv_fn(g.hidden_in)
+            g.output = self.run(self._graph_batch(g), g.hidden_in)
+        self.last_instance = g
         return g.output[:B]
 
     def _stage(self, g: _DecodeGraph, inp: dict, hidden_in) -> None:
@@ -206,27 +277,35 @@ class ModelRunner:
                             is_prefill=False, block_tables=g.block_tables, ctx_lens=g.ctx_lens,
                             max_ctx=self.max_seq_len, logits_idx=None, ep_tokens=g.bucket)
 
-    def _capture(self, bucket: int) -> _DecodeGraph:
+    def _capture(self, bucket: int, register: bool = True) -> _DecodeGraph:
         m = self.model
         g = _DecodeGraph(bucket, self.max_blocks, self.device, m.cfg.hidden_size, m.first)
         fb = self._graph_batch(g)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(2):   # warm up allocator / workspaces outside capture
-                self.run(fb, g.hidden_in)
+            for _ in range(2):   # warm up allocator / workspaces outside capture (no receive:
+                self.run(fb, g.hidden_in)   # a transfer would consume a real message)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, pool=self.pool):
+            if self.recv_fn is not None and g.hidden_in is not None:
+                self.recv_fn(g.hidden_in)       # the boundary receive is the graph's first node
             g.output = self.run(fb, g.hidden_in)
         g.graph = graph
-        self.graphs[bucket] = g
+        if register:
+            self.graphs[bucket] = g
         return g
 
     def capture_all(self, max_batch: int) -> None:
         for b in self.buckets:
             if b <= max_batch and b not in self.graphs:
                 self._capture(b)
+
+    @property
+    def captured_buckets(self) -> list:
+        return sorted(b for b, g in self.graphs.items()
+                      if (g.graph is not None if isinstance(g, _DecodeGraph) else all(x.graph is not None for x in g)))

@@ -97,10 +97,6 @@ class TransformerLM:
                                                  cfg.rope_scaling, device=self.device)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.seq_parallel = self.tp > 1 and self.ep == 1 and flags.get("BFLY_SEQ_PARALLEL")
-        # decode: RoPE + KV append fused into the attention kernel (bf16 caches; the cache
-        # dtype is only known per call, so the check happens there)
-        self.fused_decode_rope = (self.device.type == "cuda" and cfg.pos_emb == "rope"
-                                  and flags.get("BFLY_FUSED_DECODE_ROPE"))
         self.sp_min_tokens = flags.get("BFLY_SEQ_PARALLEL_MIN_TOKENS")
 
     # ------------------------------------------------------------------------------------
@@ -357,11 +353,6 @@ class TransformerLM:
         qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
         kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
         slots = fb.slots if kc is not None else None
-        if (not fb.is_prefill and self.fused_decode_rope and kc is not None and kc.dtype == torch.bfloat16):
-            attn = ops.attn_decode_rope(qkv, fb.positions, self.cos, self.sin, fb.slots, kc, vc, fb.block_tables,
-                                        fb.ctx_lens, d.hq, self.scale, fb.max_ctx)
-            o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
-            return ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce)
         if c.pos_emb == "rope":
             qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
         elif kc is not None:

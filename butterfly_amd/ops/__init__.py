@@ -25,12 +25,7 @@ _loaded = False
 _load_error: str | None = None
 
 EPILOGUES = {"none": 0, "bias": 1, "silu": 2}
-DECODE_PART_TOKENS = 0
-# Split combine inside the decode kernel (last-arriver merge) instead of the combine kernel.
-# Off: measured 2x slower on MI355X (B=64 ctx 1024: 104 vs 53 us; B=1 ctx 8192: 168 vs 47 us)
-# — the per-workgroup agent-scope release (L2 write-back) and the serial merge in one
-# workgroup cost more than the separate, fully parallel combine launch.
-FUSED_DECODE_COMBINE = False   # 0 = pick the context split per call (attn_decode_part_tokens)
+DECODE_PART_TOKENS = 0   # 0 = pick the context split per call (attn_decode_part_tokens)
 
 
 def load_library(path: str | os.PathLike | None = None) -> bool:
@@ -127,7 +122,6 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
                  for b in range(1, max_batch + 1))
         _arena.get(device, "attn_o", max_batch * num_kv_heads * ns * 16 * head_dim, torch.float32)
         _arena.get(device, "attn_ml", max_batch * num_kv_heads * ns * 16 * 2, torch.float32)
-        _arena.get(device, "attn_cnt", max_batch * num_kv_heads, torch.int32, zero=True)
     _arena.get(device, "sample", max(max_batch, max_tokens, 1) * 64, torch.int64)
     _arena.get(device, "tkp", max(max_batch, max_tokens, 1) * 521, torch.float32)
 
@@ -355,7 +349,7 @@ def _linear_library(x, w, epilogue: str, out):
 def gemm_plan(M: int, N: int, K: int) -> dict:
     load_library()
     k, mt, nt, bm, bn, sk, wk = torch.ops.bfly.gemm_plan(M, N, K)
-    return {"kind": ("skinny", "tile", "big", "dec")[k], "mt": mt, "nt": nt, "wk": wk, "bm": bm, "bn": bn,
+    return {"kind": ("skinny", "tile", "big", "dec", "big8")[k], "mt": mt, "nt": nt, "wk": wk, "bm": bm, "bn": bn,
             "splitk": sk}
 
 
@@ -397,47 +391,12 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_c
     if part_tokens <= 0:
         part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
     ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
-    po = pml = cnt = None
+    po = pml = None
     if ns > 1:
         po = _arena.get(q.device, "attn_o", B * Hkv * ns * 16 * D, torch.float32)
         pml = _arena.get(q.device, "attn_ml", B * Hkv * ns * 16 * 2, torch.float32)
-        if FUSED_DECODE_COMBINE:
-            # zeroed once; the kernel's last-arriving split re-arms every counter it used
-            cnt = _arena.get(q.device, "attn_cnt", B * Hkv, torch.int32, zero=True)
     torch.ops.bfly.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx,
-                               part_tokens, out, po, pml, cnt)
-    return out
-
-
-def attn_decode_rope(qkv, positions, cos, sin, slots, k_cache, v_cache, block_tables, ctx_lens,
-                     n_q: int, scale: float, max_ctx: int, part_tokens: int = DECODE_PART_TOKENS, out=None):
-    """rope_kv + attn_decode in one kernel for a decode step: `qkv` [B, (Hq + 2 Hkv) D] is the
-    QKV projection output (or a deferred split-K `Partial` of it, reduced in the kernel); the
-    new token's K/V are written at `slots` and attention runs over the cached positions plus
-    the new token. Returns attention out [B, Hq, D]. bf16 caches only."""
-    if isinstance(qkv, Partial):
-        rows, slabs = qkv.out, qkv.slabs
-    else:
-        rows, slabs = qkv, None
-    if not _gpu(rows):
-        rows = ref.rope_kv(rows, positions, cos, sin, n_q, k_cache.shape[1], slots, k_cache, v_cache)
-        B, D = rows.shape[0], k_cache.shape[3]
-        q = rows[:, : n_q * D].view(B, n_q, D)
-        return ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx, part_tokens, out)
-    B, Hkv, D = rows.shape[0], k_cache.shape[1], k_cache.shape[3]
-    if out is None:
-        out = torch.empty(B, n_q, D, dtype=rows.dtype, device=rows.device)
-    if part_tokens <= 0:
-        part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
-    ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
-    po = pml = cnt = None
-    if ns > 1:
-        po = _arena.get(rows.device, "attn_o", B * Hkv * ns * 16 * D, torch.float32)
-        pml = _arena.get(rows.device, "attn_ml", B * Hkv * ns * 16 * 2, torch.float32)
-        if FUSED_DECODE_COMBINE:
-            cnt = _arena.get(rows.device, "attn_cnt", B * Hkv, torch.int32, zero=True)
-    torch.ops.bfly.attn_decode_rope(rows, slabs, positions, cos, sin, slots, k_cache, v_cache, block_tables,
-                                    ctx_lens, n_q, scale, max_ctx, part_tokens, out, po, pml, cnt)
+                               part_tokens, out, po, pml)
     return out
 
 

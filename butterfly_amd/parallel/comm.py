@@ -34,6 +34,21 @@ import torch.distributed as dist
 from .mesh import Mesh
 
 
+class NativeWork:
+    """Completion handle of a native RCCL point-to-point transfer issued on a side stream:
+    `wait()` makes the CURRENT stream wait for it (torch Work semantics), `event` lets a
+    caller order later work on it directly."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
+    def is_completed(self) -> bool:
+        return self.event.query()
+
+
 @dataclass
 class GroupHandle:
     ranks: list
@@ -53,6 +68,11 @@ class Communicator:
         self.groups = groups
         self.custom_ar = None            # optional CustomAllReduce for the tp group
         self.stats = {"all_reduce_bytes": 0, "send_bytes": 0, "recv_bytes": 0, "calls": 0}
+        # native RCCL pipeline edges (parallel/rccl.pp_edges): to the next / from the previous
+        # stage; sends run on their own stream so a send never blocks the compute stream
+        self.pp_native_send = None
+        self.pp_native_recv = None
+        self._send_stream = None
 
     # -- construction ---------------------------------------------------------------------
     @classmethod
@@ -167,14 +187,36 @@ class Communicator:
         """Create the rank's native RCCL communicators (collective over the world): the world
         one from a broadcast unique id, then one ncclCommSplit per mesh axis. Returns
         {axis: RcclComm} for the groups that now use them."""
-        from .rccl import RcclComm, split_mesh
+        from .rccl import RcclComm, pp_edges, split_mesh
 
         world = RcclComm.world()
         natives = split_mesh(world, self.mesh, self.rank)
         for axis, nc in natives.items():
             self.groups[axis].native = nc
         self.groups["world"].native = world
+        self.pp_native_send, self.pp_native_recv = pp_edges(world, self.mesh, self.rank)
         return natives
+
+    @property
+    def native_p2p(self) -> bool:
+        """Pipeline boundary transfers run on native RCCL edge communicators."""
+        return self.pp_native_send is not None or self.pp_native_recv is not None
+
+    def _edge(self, peer: int, sending: bool):
+        if sending:
+            return self.pp_native_send if peer == self.mesh.next_stage(self.rank) else None
+        return self.pp_native_recv if peer == self.mesh.prev_stage(self.rank) else None
+
+    def send_stream(self, device) -> "torch.cuda.Stream":
+        if self._send_stream is None:
+            self._send_stream = torch.cuda.Stream(device)
+        return self._send_stream
+
+    def recv_native(self, t: torch.Tensor) -> torch.Tensor:
+        """Receive from the previous stage on the CURRENT stream (capturable: a stage's decode
+        graph starts with it, landing the boundary rows in the graph's static input)."""
+        self.pp_native_recv.recv(t, 0)
+        return t
 
     def check_health(self) -> None:
         """Raise if the IPC all-reduce recorded a peer-wait timeout (a rank stopped arriving:
@@ -298,6 +340,10 @@ class Communicator:
 
     def send(self, t: torch.Tensor, dst: int) -> None:
         self.stats["send_bytes"] += t.numel() * t.element_size()
+        nc = self._edge(dst, True)
+        if nc is not None:
+            nc.send(t.contiguous(), 1)          # stream-ordered on the current stream
+            return
         if t.is_cuda and not self._world_nccl():   # gloo point-to-point needs host memory
             dist.send(t.detach().cpu().contiguous(), dst)
             return
@@ -305,6 +351,10 @@ class Communicator:
 
     def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
         self.stats["recv_bytes"] += t.numel() * t.element_size()
+        nc = self._edge(src, False)
+        if nc is not None:
+            nc.recv(t, 0)
+            return t
         if t.is_cuda and not self._world_nccl():
             h = torch.empty(t.shape, dtype=t.dtype)
             dist.recv(h, src)
@@ -315,12 +365,31 @@ class Communicator:
 
     def isend(self, t: torch.Tensor, dst: int):
         self.stats["send_bytes"] += t.numel() * t.element_size()
+        nc = self._edge(dst, True)
+        if nc is not None:
+            # on the send stream, after everything the current stream has queued (the producer);
+            # the allocator keeps `t` alive until the send stream is past it
+            s = self.send_stream(t.device)
+            s.wait_stream(torch.cuda.current_stream(t.device))
+            t = t.contiguous()
+            with torch.cuda.stream(s):
+                nc.send(t, 1)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            t.record_stream(s)
+            return NativeWork(ev)
         if t.is_cuda and not self._world_nccl():
             return dist.isend(t.detach().cpu().contiguous(), dst)
         return dist.isend(t.contiguous(), dst)
 
     def irecv(self, t: torch.Tensor, src: int):
         self.stats["recv_bytes"] += t.numel() * t.element_size()
+        nc = self._edge(src, False)
+        if nc is not None:
+            nc.recv(t, 0)                      # on the current stream (a pre-poster's comm stream)
+            ev = torch.cuda.Event()
+            ev.record()
+            return NativeWork(ev)
         return dist.irecv(t, src)
 
     def broadcast_(self, t: torch.Tensor, src_in_group: int = 0, group: str = "world") -> torch.Tensor:

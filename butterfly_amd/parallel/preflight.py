@@ -354,12 +354,14 @@ def check_native_rccl(rank: int, world: int, vote: Callable[[bool], bool]) -> tu
 
 
 def _close(*comms) -> None:
-    for c in comms:
-        if c is not None:
-            try:
-                c.close()
-            except Exception:  # noqa: BLE001
-                pass
+    """Check communicators are left alive (a few MB each): ncclCommDestroy of a communicator
+    that ran point-to-point transfers, or whose captured graph still exists, can block forever
+    (seen on a one-rank communicator on MI355X), and a blocked destroy here would cost the
+    whole job. They are never used again."""
+    _LEAKED.extend(c for c in comms if c is not None)
+
+
+_LEAKED: list = []
 
 
 def check_custom_ar(rank: int, world: int, pgs: dict, vote: Callable[[bool], bool]) -> tuple:

@@ -125,6 +125,43 @@ class RcclComm:
             _lib().rccl_release(self.handle, abort)
 
 
+def pp_edges(world: RcclComm, mesh, rank: int) -> tuple:
+    """Two-rank communicators for this rank's pipeline edges (collective: every rank calls it
+    with the same mesh): (to the next stage, from the previous stage), each None at the ends.
+    Edge s -> s+1 of a pipeline gets its own communicator (sender = rank 0, receiver = rank 1),
+    split from `world` in two calls (even edges, then odd ones: a rank sits on at most one edge
+    of each parity). Separate communicators per direction keep a stage's receive (captured in
+    its decode graph) and its send (eager, on the send stream) on different RCCL objects.
+    The connections are set up here with one tiny transfer per edge, so no later (captured)
+    transfer has to run a connection handshake."""
+    if mesh.pp <= 1:
+        return None, None
+    groups = mesh.all_groups("pp")
+    g = next(i for i, grp in enumerate(groups) if rank in grp)
+    s = groups[g].index(rank)
+    pp = mesh.pp
+    send = recv = None
+    for parity in (0, 1):
+        if s % 2 == parity and s + 1 < pp:
+            c = world.split(g * pp + s, 0, [rank, groups[g][s + 1]])
+            send = c
+        elif s % 2 != parity and s >= 1:
+            c = world.split(g * pp + s - 1, 1, [groups[g][s - 1], rank])
+            recv = c
+        else:
+            world.split(-1, 0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.zeros(16, dtype=torch.float32, device=dev)
+    # warm-up in stage order (first edges first) so no pair waits on another
+    for parity in (0, 1):
+        if send is not None and s % 2 == parity:
+            send.send(t, 1)
+        if recv is not None and (s - 1) % 2 == parity:
+            recv.recv(t, 0)
+    torch.cuda.synchronize(dev)
+    return send, recv
+
+
 def split_mesh(world: RcclComm, mesh, rank: int) -> dict:
     """One communicator per mesh axis with more than one rank, split from `world` (collective:
     every rank calls this with the same mesh). Returns {axis: RcclComm}."""

@@ -26,6 +26,11 @@ vocab-parallel sampling all-gather) — written down ahead of time so that it ca
 Stream assignment follows the engine: TP all-reduces run on the compute stream (one-shot IPC
 kernel when BFLY_CUSTOM_AR is active, else RCCL, both stream-ordered), PP sends are `isend` on
 RCCL's stream (they overlap the next group's compute), the token broadcast ends the step.
+With native RCCL pipeline edges (`native_pp=True`, parallel/rccl.pp_edges) the boundary receive
+is the FIRST node of the stage's captured decode graph (stream "graph": it lands in the graph's
+static input), and the send leaves the graph's static output on the communicator's send stream
+(stream "send"); both move the whole graph bucket (`bucket` rows), which is what the engine
+puts on the wire.
 """
 from __future__ import annotations
 
@@ -77,7 +82,7 @@ class RankProgram:
 
 
 def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int = 1,
-                 dtype_bytes: int = BF16) -> RankProgram:
+                 dtype_bytes: int = BF16, native_pp: bool = False, bucket: Optional[int] = None) -> RankProgram:
     """The decode-step program of `rank` for `tokens` sequences. With the asynchronous pipeline
     (default) a step is one tick carrying one request group (`tokens` = the group's size, one
     microbatch); the synchronous pipeline (engine._pipeline_decode) cuts the step's batch into
@@ -89,14 +94,15 @@ def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int 
     bounds = [tokens * i // M for i in range(M + 1)]
     for m in range(M):
         _microbatch(plan, rank, bounds[m + 1] - bounds[m], prog.instrs.append, ep_sync=(m == 0),
-                    dtype_bytes=dtype_bytes)
+                    dtype_bytes=dtype_bytes, native_pp=native_pp, bucket=bucket)
     if plan.mesh.pp > 1:
         prog.instrs.append(Instr("broadcast", tuple(plan.mesh.pp_group(rank)), tokens * 4, "comm",
                                  "sampled ids from the last stage"))
     return prog
 
 
-def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool, dtype_bytes: int = BF16) -> None:
+def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool, dtype_bytes: int = BF16,
+                native_pp: bool = False, bucket: Optional[int] = None) -> None:
     cfg: ModelConfig = plan.model
     mesh = plan.mesh
     c = mesh.coord(rank)
@@ -116,6 +122,10 @@ def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool,
         add(Instr("compute", note="embedding gather (vocab shard)"))
         if tp > 1:
             add(Instr("all_reduce", tp_g, act, "compute", "vocab-parallel embedding"))
+    elif native_pp:
+        wire = (bucket or tokens) * h * dtype_bytes
+        add(Instr("recv", (mesh.prev_stage(rank), rank), wire, "graph",
+                  "residual stream from previous stage: first node of the captured decode graph"))
     else:
         add(Instr("recv", (mesh.prev_stage(rank), rank), act, "comm", "residual stream from previous stage"))
     for layer in range(a, b):
@@ -143,6 +153,10 @@ def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool,
         add(Instr("compute", note="final norm, LM head (vocab shard), sampling"))
         if tp > 1:
             add(Instr("all_gather", tp_g, R * 2 * 4, "compute", "vocab-parallel argmax: (score, id) pairs"))
+    elif native_pp:
+        wire = (bucket or tokens) * h * dtype_bytes
+        add(Instr("send", (rank, mesh.next_stage(rank)), wire, "send",
+                  "residual stream to next stage: the graph's static output (A/B instance), send stream"))
     else:
         add(Instr("send", (rank, mesh.next_stage(rank)), act, "comm", "residual stream to next stage"))
 
@@ -213,7 +227,8 @@ def link_bytes(plan: PartitionPlan, progs: dict) -> dict:
     return out
 
 
-def programs(plan: PartitionPlan, tokens: int, microbatches: int = 1, dtype_bytes: int = BF16) -> dict:
+def programs(plan: PartitionPlan, tokens: int, microbatches: int = 1, dtype_bytes: int = BF16,
+             native_pp: bool = False, bucket: Optional[int] = None) -> dict:
     """rank_program for every rank (each DP replica decodes `tokens` sequences); activations
     are `dtype_bytes` wide (bf16 on the GPU, fp32 on the CPU reference path)."""
-    return {r: rank_program(plan, r, tokens, microbatches, dtype_bytes) for r in range(plan.n_gpus)}
+    return {r: rank_program(plan, r, tokens, microbatches, dtype_bytes, native_pp, bucket) for r in range(plan.n_gpus)}

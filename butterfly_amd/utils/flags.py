@@ -42,15 +42,11 @@ define("BFLY_CUSTOM_AR_2SHOT_BYTES", 512 << 10, int, "IPC all-reduces of at leas
 define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0: heuristic plans only; read by the kernel library)")
 define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
-define("BFLY_GEMM_SLAB_WT", False, _bool, "write split-K partial slabs write-through (sc1); measured slower in the decode step, off (read by the kernel library)")
 define("BFLY_GEMM_LIBRARY_MIN_M", 6144, int, "plain (epilogue-free) GEMMs with at least this many rows (prefill "
        "QKV / O / down) run on hipBLASLt; fused GEMMs (SwiGLU, bias) always run the HIP kernels; 0 = never")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
-define("BFLY_FUSED_DECODE_ROPE", False, _bool, "decode steps: RoPE and the new token's KV-cache append inside the "
-       "decode attention kernel (one launch instead of rope_kv + attn_decode; bf16 caches). Off: measured 1 % "
-       "slower on the 70B B=64 step (every workgroup's serial prologue costs more than the launch it saves)")
 define("BFLY_NATIVE_RCCL", False, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "
        "all-to-all) on the rank's own RCCL communicators (world init + ncclCommSplit per mesh axis, "
        "parallel/rccl.py) instead of torch ProcessGroups; multi-rank path needs a multi-GPU node")

@@ -417,8 +417,7 @@ int64_t attn_decode_part_tokens(int64_t B, int64_t Hkv, int64_t max_ctx) {
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& block_tables, const Tensor& ctx_lens, double scale,
                  int64_t max_ctx, int64_t part_tokens, Tensor& out,
-                 const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml,
-                 const c10::optional<Tensor>& counters) {
+                 const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml) {
   CHECK_GPU(q); CHECK_BF16(q); CHECK_KV(k_cache, v_cache); CHECK_BF16(out);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "attn_decode: q [B, Hq, D]");
   const int B = q.size(0), Hq = q.size(1), D = q.size(2);
@@ -441,75 +440,13 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
     po = part_o->data_ptr<float>();
     pml = part_ml->data_ptr<float>();
   }
-  int* cnt = nullptr;
-  if (counters.has_value()) {
-    CHECK_I32(*counters);
-    TORCH_CHECK(counters->numel() >= (long)B * Hkv && counters->is_contiguous(), "attn_decode: counters [B*Hkv] (zeroed)");
-    cnt = counters->data_ptr<int>();
-  }
   c10::DeviceGuard g(q.device());
   const int rc = bfly::launch_attn_decode(bf(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                           block_tables.data_ptr<int>(), block_tables.stride(0),
                                           ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale,
-                                          max_ctx, part_tokens, bf(out), po, pml, cur_stream(), cnt,
+                                          max_ctx, part_tokens, bf(out), po, pml, cur_stream(),
                                           k_cache.scalar_type() == at::kFloat8_e4m3fn);
   TORCH_CHECK(rc == 0, "attn_decode: unsupported configuration (rc=", rc, ")");
-}
-
-// Decode attention with the new token's RoPE + paged-cache append fused in: `qkv` [B, (Hq +
-// 2 Hkv) D] bf16 is the QKV projection output (or the destination of `part`, its split-K f32
-// slabs [sk, B, (Hq + 2 Hkv) D], reduced inside the kernel).
-void attn_decode_rope(const Tensor& qkv, const c10::optional<Tensor>& part, const Tensor& positions,
-                      const Tensor& cos_t, const Tensor& sin_t, const Tensor& slots, Tensor& k_cache,
-                      Tensor& v_cache, const Tensor& block_tables, const Tensor& ctx_lens, int64_t Hq,
-                      double scale, int64_t max_ctx, int64_t part_tokens, Tensor& out,
-                      const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml,
-                      const c10::optional<Tensor>& counters) {
-  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_KV(k_cache, v_cache); CHECK_BF16(out);
-  TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous(), "attn_decode_rope: qkv [B, (Hq+2Hkv)*D] contiguous");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "attn_decode_rope: caches");
-  TORCH_CHECK(k_cache.scalar_type() == at::kBFloat16, "attn_decode_rope: bf16 caches only");
-  const int B = qkv.size(0), Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
-  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "attn_decode_rope: qkv width");
-  TORCH_CHECK(v_cache.size(2) == D && v_cache.size(3) == BS, "attn_decode_rope: cache dims");
-  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)B * Hq * D, "attn_decode_rope: out");
-  CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_I32(positions); CHECK_I32(slots);
-  TORCH_CHECK(positions.numel() >= B && slots.numel() >= B && ctx_lens.numel() >= B, "attn_decode_rope: per-row inputs");
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1,
-              "attn_decode_rope: block_tables");
-  TORCH_CHECK((long)block_tables.size(1) * BS >= max_ctx, "attn_decode_rope: block table too narrow for max_ctx");
-  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
-                  sin_t.is_contiguous() && cos_t.size(1) == D / 2, "attn_decode_rope: f32 tables [max_pos, D/2]");
-  const float* pp = nullptr;
-  int sk = 1;
-  if (part.has_value()) {
-    TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() && part->dim() == 3 &&
-                    part->size(1) == B && part->size(2) == qkv.size(1), "attn_decode_rope: part [sk, B, N] f32");
-    pp = part->data_ptr<float>();
-    sk = part->size(0);
-  }
-  if (part_tokens <= 0) part_tokens = bfly::attn_decode_part_tokens(B, Hkv, max_ctx);
-  const int nsplit = bfly::attn_decode_splits(max_ctx, part_tokens);
-  float *po = nullptr, *pml = nullptr;
-  if (nsplit > 1) {
-    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "attn_decode_rope: partial buffers required");
-    TORCH_CHECK(part_o->numel() >= (long)B * Hkv * nsplit * 16 * D, "attn_decode_rope: part_o too small");
-    TORCH_CHECK(part_ml->numel() >= (long)B * Hkv * nsplit * 16 * 2, "attn_decode_rope: part_ml too small");
-    po = part_o->data_ptr<float>();
-    pml = part_ml->data_ptr<float>();
-  }
-  int* cnt = nullptr;
-  if (counters.has_value()) {
-    CHECK_I32(*counters);
-    cnt = counters->data_ptr<int>();
-  }
-  c10::DeviceGuard g(qkv.device());
-  const int rc = bfly::launch_attn_decode_rope(
-      bf(qkv), pp, sk, positions.data_ptr<int>(), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(),
-      slots.data_ptr<int>(), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr<int>(),
-      block_tables.stride(0), ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale, max_ctx, part_tokens,
-      bf(out), po, pml, cur_stream(), cnt, 0);
-  TORCH_CHECK(rc == 0, "attn_decode_rope: unsupported configuration (rc=", rc, ")");
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& cu_seqlens,
@@ -816,10 +753,6 @@ TORCH_LIBRARY(bfly, m) {
   m.def("add(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("init_hash(Tensor(a!) out, int grow0, int gcol0, int gcols, int seed, float amp) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vstart) -> ()");
-  m.def("attn_decode_rope(Tensor qkv, Tensor? part, Tensor positions, Tensor cos_t, Tensor sin_t, Tensor slots, "
-        "Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor ctx_lens, int Hq, float scale, "
-        "int max_ctx, int part_tokens, Tensor(c!) out, Tensor(d!)? part_o, Tensor(e!)? part_ml, "
-        "Tensor(f!)? counters) -> ()");
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
         "Tensor(b!) out_scores, Tensor(c!) workspace, Tensor? thresh=None, bool check_finite=False) -> ()");
   m.def("tkp_begin(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor(a!) ws) -> ()");
@@ -838,7 +771,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("attn_decode_part_tokens(int B, int Hkv, int max_ctx) -> int", &attn_decode_part_tokens);
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
         "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
-        "Tensor(c!)? part_ml, Tensor(d!)? counters=None) -> ()");
+        "Tensor(c!)? part_ml) -> ()");
   m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
   m.def("moe_max_tiles(int tk, int num_local, int bm=64) -> int", &moe_max_tiles);
@@ -882,7 +815,6 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("tkp_pass", &tkp_pass);
   m.impl("tkp_select", &tkp_select);
   m.impl("tkp_final", &tkp_final);
-  m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("gemm", &gemm);
   m.impl("gemm_with_plan", &gemm_with_plan);
   m.impl("gemm_deferred", &gemm_deferred);

@@ -12,7 +12,8 @@ typedef __bf16 bf16;
 enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_SILU = 2 };
 
 struct GemmPlan {
-  int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 2 = 256x256 big tile (prefill), 3 = decode ring
+  int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 2 = 256x256 big tile (prefill), 3 = decode ring,
+             // 4 = 256x256 8-phase big tile (BK 64)
   int mt, nt;
   int wk;    // skinny: waves splitting K inside a workgroup (1, 2, 4)
   int bm, bn;
@@ -93,16 +94,7 @@ int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const 
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
                        bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                       int* counters = nullptr,    // zeroed [B*Hkv]: fused split combine
-                       int kv_fp8 = 0, const struct DecRope* rope = nullptr);
-// Decode attention with the RoPE + KV-cache append of the new token fused in (attention.hip):
-// qkv = the QKV projection rows (bf16) or `part` = its split-K slabs [sk][B][(Hq+2Hkv)D].
-int launch_attn_decode_rope(const bf16* qkv, const float* part, int sk, const int* positions,
-                            const float* cos_t, const float* sin_t, const int* slots, void* k_cache,
-                            void* v_cache, const int* block_tables, int bt_stride, const int* ctx_lens,
-                            int B, int Hq, int Hkv, int D, int block_size, float scale, int max_ctx,
-                            int part_tokens, bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                            int* counters, int kv_fp8);            // caches hold FP8 e4m3 (bfly_kv.h)
+                       int kv_fp8 = 0);            // caches hold FP8 e4m3 (bfly_kv.h)
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,

@@ -15,7 +15,7 @@
 //   The cache may hold FP8 e4m3 instead of bf16 (bfly_kv.h): half the bytes per page, widened
 //   to bf16 in registers before the same MFMAs.
 //
-// Prefill (attn_prefill_kernel): causal varlen flash attention. Workgroup = 256 query rows
+// Prefill (attn_prefill_persist_kernel): causal varlen flash attention. Workgroup = 256 query rows
 // of one head (8 waves x 32 rows, 2 waves per SIMD), KV tiles of 64 keys staged by LDS-DMA
 // into a 4-deep ring of XOR-swizzled LDS images (cdna_hip_programming.md T10 image (b)): K is
 // read by ds_read_b128 as the 32x32x16 A operand of S^T = K . Q^T, V by ds_read_b64_tr_b16 as
@@ -37,105 +37,13 @@ constexpr float kNegInf = -INFINITY;
 // ---------------------------------------------------------------------------------------
 // Decode
 // ---------------------------------------------------------------------------------------
-// Split combine fused into the decode kernel: every split of a (sequence, kv head) publishes
-// its partial (O, m, l) and takes a ticket; the split that arrives last merges all partials
-// (fixed split order: deterministic) and writes the output, then re-arms the counter for the
-// next call. Hand-off per cdna_hip_programming.md §5 split-K item 2 (stores drained, barrier,
-// one agent-scope release + relaxed ticket; one agent-scope acquire in the last arriver). The
-// partials are 8 KiB per split, so the serial merge is short; it replaces a separate combine
-// launch and its kernel boundary.
-__device__ __forceinline__ void decode_split_done(const float* __restrict__ part_o,
-                                                  const float* __restrict__ part_ml,
-                                                  int* __restrict__ counters, int b, int h,
-                                                  int nsplit, int G, int Hq, int Hkv,
-                                                  bf16* __restrict__ out, int* s_last) {
-  constexpr int D = 128;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int* cnt = counters + b * Hkv + h;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == nsplit - 1;
-    if (last) {
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *s_last = last;
-  }
-  __syncthreads();
-  if (!*s_last) return;
-  const long base = (long)(b * Hkv + h) * nsplit;
-  for (int e = threadIdx.x; e < G * D; e += blockDim.x) {
-    const int qr = e / D, d = e % D;
-    float M = kNegInf;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[((base + s) * 16 + qr) * 2]);
-    const float Mb = M == kNegInf ? 0.f : M;
-    float L = 0.f, O = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-      const float ms = part_ml[((base + s) * 16 + qr) * 2];
-      if (ms == kNegInf) continue;
-      const float w = exp2f(ms - Mb);
-      L += w * part_ml[((base + s) * 16 + qr) * 2 + 1];
-      O += w * part_o[((base + s) * 16 + qr) * D + d];
-    }
-    out[((long)b * Hq + h * G + qr) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
-  }
-}
-
-// Fused decode prologue (FUSED): the kernel takes the QKV projection's row (bf16, or the f32
-// split-K slabs of the QKV GEMM, reduced here), applies RoPE to its query fragments in
-// registers (the rotate-half partner of every d the lane holds is in the lane's own fragments),
-// attends over the CACHED keys only (positions < ctx - 1), and the workgroup whose split holds
-// position ctx - 1 adds the new token's key/value analytically and writes them into their cache
-// page. That replaces the rope_kv launch before every decode attention (its kernel, its
-// boundary, and the round trip of q through memory). Numerics follow rope_kv exactly: the
-// row is rounded to bf16 before the rotation, the rotated values to bf16 after it.
-// Measured (profiles/r2_fused_decode_rope_ab.log, 70B B=64): 30.58 vs 30.26 ms per step
-// unfused, so it is off by default (BFLY_FUSED_DECODE_ROPE): each of the ~512 workgroups pays
-// the prologue's dependent loads (positions -> tables, slabs) and a barrier before its first
-// MFMA, more in sum than the rope_kv launch and boundary it removes.
-struct DecRope {
-  const bf16* qkv;          // [B, (Hq + 2 Hkv) D] bf16 (when part == nullptr)
-  const float* part;        // or the QKV GEMM's split-K slabs [sk][B][(Hq + 2 Hkv) D]
-  int sk;
-  long slab;
-  const int* positions;     // [B]
-  const float* cos_t;       // [max_pos, D/2]
-  const float* sin_t;
-  const int* slots;         // [B] cache slot of the new token (< 0: do not cache)
-  void* k_w;                // the caches (written at the new token's slot)
-  void* v_w;
-};
-
-// 8 consecutive values of one QKV row as floats, rounded to bf16 (the value rope_kv would see)
-__device__ __forceinline__ void dec_row8(const DecRope& rp, long row_off, int col, float (&x)[8]) {
-  if (rp.part) {
-    const float* pr = rp.part + row_off + col;
-    f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
-    for (int k = 1; k < rp.sk; ++k) {
-      lo += *reinterpret_cast<const f32x4*>(pr + k * rp.slab);
-      hi += *reinterpret_cast<const f32x4*>(pr + k * rp.slab + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { x[j] = bf2f(f2bf(lo[j])); x[j + 4] = bf2f(f2bf(hi[j])); }
-  } else {
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(rp.qkv + row_off + col);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = bf2f(v[j]);
-  }
-}
-
-template <int D, int BS, typename CT, bool FUSED = false>
+template <int D, int BS, typename CT>
 __global__ void __launch_bounds__(kAttnThreads)
 attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restrict__ k_cache,
                    const CT* __restrict__ v_cache, const int* __restrict__ block_tables,
                    int bt_stride, const int* __restrict__ ctx_lens, int Hq, int Hkv,
                    float scale_log2, int part_tokens, bf16* __restrict__ out,
-                   float* __restrict__ part_o, float* __restrict__ part_ml,
-                   int* __restrict__ counters, DecRope rp = DecRope{}) {
+                   float* __restrict__ part_o, float* __restrict__ part_ml) {
   static_assert(D == 128 && BS == 32, "decode kernel is specialised for D=128, BS=32");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -143,23 +51,17 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   const int G = Hq / Hkv;
   const int ctx = ctx_lens[b];
   const int tok0 = s * part_tokens;
-  // FUSED: the cache holds positions < ctx - 1; the new token (ctx - 1) is added separately
-  const int tok1 = min(FUSED ? ctx - 1 : ctx, tok0 + part_tokens);
-  const bool has_new = FUSED && ctx > 0 && ctx - 1 >= tok0 && ctx - 1 < tok0 + part_tokens;
+  const int tok1 = min(ctx, tok0 + part_tokens);
   const long part_base = ((long)(b * Hkv + h) * nsplit + s);
 
   __shared__ float s_o[4][8][4][64];
   __shared__ float s_m[4][16], s_l[4][16];
-  __shared__ float s_snew[16], s_vnew[D];
-  __shared__ __attribute__((aligned(16))) bf16 s_rows[FUSED ? 17 : 1][D];   // rotated q rows (+ new key)
-  __shared__ int s_last;
 
-  if (tok0 >= tok1 && !has_new) {  // empty split: mark it so the combine skips it
+  if (tok0 >= tok1) {  // empty split: mark it so the combine skips it
     if (nsplit > 1 && threadIdx.x < 16) {
       part_ml[(part_base * 16 + threadIdx.x) * 2 + 0] = kNegInf;
       part_ml[(part_base * 16 + threadIdx.x) * 2 + 1] = 0.f;
     }
-    if (nsplit > 1 && counters) decode_split_done(part_o, part_ml, counters, b, h, nsplit, G, Hq, Hkv, out, &s_last);
     return;
   }
 
@@ -173,7 +75,7 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   auto d_off = [&](int ds) { return kF8 ? 64 * (ds >> 1) + 16 * g + 8 * (ds & 1) : 32 * ds + 8 * g; };
   // Q^T fragment (B operand): lane holds Q[row r][d]; rows >= G are zero.
   bf16x8 qf[4];
-  if constexpr (!FUSED) {
+  {
     const int qr = r < G ? r : 0;
     const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D;
 #pragma unroll
@@ -265,69 +167,6 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   raw_t kA[2][4], vA[8], kB[2][4], vB[8];
   int p = p0 + wid;
   if (p < p1) load_page(p, kA, vA);
-  if constexpr (FUSED) {
-    // (the first KV page is already in flight) The workgroup's G query rows -- and, in the
-    // split that holds the new token, its key -- are rotated ONCE, spread over all threads
-    // (thread = one rotation pair of one row), staged in LDS as bf16, then read back as MFMA
-    // fragments; the value row goes to LDS and its cache page by 16 threads.
-    const long row_off = (long)b * (Hq + 2 * Hkv) * D;
-    const int pos = rp.positions[b];
-    const float* cr = rp.cos_t + (long)pos * (D / 2);
-    const float* sr = rp.sin_t + (long)pos * (D / 2);
-    const int nrows = G + (has_new ? 1 : 0);
-    for (int e = threadIdx.x; e < nrows * (D / 16); e += kAttnThreads) {
-      const int row = e / (D / 16), p0r = (e % (D / 16)) * 8;     // 8 pairs (d, d + 64)
-      const int head = row < G ? h * G + row : Hq + h;
-      float x[8], y[8];
-      dec_row8(rp, row_off, head * D + p0r, x);
-      dec_row8(rp, row_off, head * D + p0r + D / 2, y);
-      bf16x8 a, c2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float cs = cr[p0r + j], sn = sr[p0r + j];
-        a[j] = f2bf(x[j] * cs - y[j] * sn);
-        c2[j] = f2bf(y[j] * cs + x[j] * sn);
-      }
-      *reinterpret_cast<bf16x8*>(&s_rows[row][p0r]) = a;
-      *reinterpret_cast<bf16x8*>(&s_rows[row][p0r + D / 2]) = c2;
-    }
-    const int slot = rp.slots ? rp.slots[b] : -1;
-    if (has_new && threadIdx.x < D / 8) {   // the new token's value (transposed V page)
-      float x[8];
-      const int d0 = threadIdx.x * 8;
-      dec_row8(rp, row_off, (Hq + Hkv + h) * D + d0, x);
-      CT* vp = slot >= 0 ? static_cast<CT*>(rp.v_w) + ((long)(slot / BS) * Hkv + h) * D * BS + slot % BS : nullptr;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s_vnew[d0 + j] = x[j];
-        if (vp) KV<CT>::store1(vp + (long)(d0 + j) * BS, f2bf(x[j]));
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    {
-      const int qr = r < G ? r : 0;
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        qf[ds] = *reinterpret_cast<const bf16x8*>(&s_rows[qr][d_off(ds)]);
-        if (r >= G) qf[ds] = bf16x8{};
-      }
-    }
-    if (has_new && wid == 0) {
-      float dot = 0.f;
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        const bf16x8 kn = *reinterpret_cast<const bf16x8*>(&s_rows[G][d_off(ds)]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dot += bf2f(qf[ds][j]) * bf2f(kn[j]);
-        if (slot >= 0 && r == 0)   // lanes g = 0..3 hold all 128 d of the key
-          KV<CT>::store8(static_cast<CT*>(rp.k_w) + (((long)(slot / BS) * Hkv + h) * BS + slot % BS) * D + d_off(ds), kn);
-      }
-      dot += __shfl_xor(dot, 16, 64);
-      dot += __shfl_xor(dot, 32, 64);
-      if (g == 0) s_snew[r] = r < G ? dot * scale_log2 : kNegInf;
-    }
-  }
   if constexpr (sizeof(CT) == 2) {
     while (p < p1) {
       if (p + 4 < p1) load_page(p + 4, kB, vB);
@@ -377,7 +216,6 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
     float M = kNegInf;
 #pragma unroll
     for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][qr]);
-    if (has_new) M = fmaxf(M, s_snew[qr]);
     const float Mb = M == kNegInf ? 0.f : M;
     float L = 0.f, O = 0.f;
     const int dt = d >> 4, i = d & 3, ln = qr + 16 * ((d & 15) >> 2);
@@ -386,11 +224,6 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
       const float f = exp2f(s_m[w][qr] - Mb);
       L += f * s_l[w][qr];
       O += f * s_o[w][dt][i][ln];
-    }
-    if (has_new) {   // p of the new key, rounded to bf16 like every P that meets V
-      const float pn = bf2f(f2bf(exp2f(s_snew[qr] - Mb)));
-      L += pn;
-      O += pn * bf2f(f2bf(s_vnew[d]));
     }
     if (nsplit == 1) {
       out[((long)b * Hq + h * G + qr) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
@@ -402,7 +235,6 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
       }
     }
   }
-  if (nsplit > 1 && counters) decode_split_done(part_o, part_ml, counters, b, h, nsplit, G, Hq, Hkv, out, &s_last);
 }
 
 // One workgroup per (query row, kv head, sequence); thread = head dim element. The split
@@ -478,26 +310,6 @@ __device__ __forceinline__ void pf_wait_tiles(int after) {
   else pf_vm_wait<0>();
 }
 
-// Stage one 64-key K/V tile (2 x 16 KiB) by LDS-DMA: each wave-instruction writes 4 rows
-// (1 KiB) lane-linearly; the XOR image is produced by swizzling the per-lane SOURCE chunk.
-__device__ __forceinline__ void pf_stage(const bf16* __restrict__ k, long k_stride,
-                                         const bf16* __restrict__ v, long v_stride, int s0, int L,
-                                         int kh, int t, char* kb, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < kPfIters; ++i) {
-    const int piece = i * kPfWaves + wid;          // 16 pieces of 4 rows
-    const int row = piece * 4 + (lane >> 4);
-    const int ch = (lane & 15) ^ pf_swz(row);
-    int key = t * kPfBKV + row;
-    key = key < L ? key : L - 1;
-    const long ko = (long)(s0 + key);
-    __builtin_amdgcn_global_load_lds((pf_gbl_t)(k + ko * k_stride + (long)kh * 128 + ch * 8),
-                                     (pf_lds_t)(kb + piece * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((pf_gbl_t)(v + ko * v_stride + (long)kh * 128 + ch * 8),
-                                     (pf_lds_t)(kb + kPfBKV * 256 + piece * 1024), 16, 0, 0);
-  }
-}
-
 // S^T tiles of one 64-key tile: s[kt][r] = S[key = kv0 + 32kt + (r&3) + 8(r>>2) + 4hi][query c]
 __device__ __forceinline__ void pf_qk(const char* kb, const bf16x8 (&qf)[8], int lane,
                                       f32x16 (&s)[2]) {
@@ -559,18 +371,6 @@ __device__ __forceinline__ float pf_exp(const f32x16 (&s)[2], float scale_log2, 
         pb[kt][h][j] = f2bf(pv);
       }
   return ps;
-}
-
-// pf_exp without the row sum (MFSUM: the sum comes from the matrix core, below).
-__device__ __forceinline__ void pf_exp_nosum(const f32x16 (&s)[2], float scale_log2, float mb,
-                                             bf16x8 (&pb)[2][2]) {
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        pb[kt][h][j] = f2bf(__builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][8 * h + j], scale_log2, -mb)));
 }
 
 // O^T[d][q] += V^T[d][key] P^T[key][q]; the A operand comes from transposed LDS reads.
@@ -647,148 +447,6 @@ __device__ __forceinline__ void pf_stage_buf(const bf16* __restrict__ k, long k_
 // (cdna_hip_programming.md T13).
 constexpr float kPfRescaleThr = 8.f;
 
-// Causal varlen flash attention. Workgroup = kPfBQ query rows of one head (32 rows per wave,
-// two waves per SIMD); 64-key K/V tiles in an S-deep LDS-DMA ring (counted vmcnt, one raw
-// barrier per tile). Per wave: S^T = K Q^T on 32x32x16 MFMAs (the lane owns one query column:
-// row max/sum are lane-local plus one swap), P^T built in registers from the accumulator,
-// O^T += V^T P^T with V fed by transposed LDS reads (ds_read_b64_tr_b16).
-// The loop is VALU-bound next to its MFMAs (rocprofv3: ~10 VALU per MFMA), so the template
-// flags trim VALU: BUFDMA (scalar tile windows, above), DEFER (skip the O rescale), and PRIO
-// (waves 4-7, which lose VALU arbitration to their older SIMD partners, at s_setprio 1).
-// Measured and dropped (profiles/r2_attn_prefill_variants.log): a 5-stage ring (-7 % on
-// 16k tokens), waves 4-7 running PV one tile late (-15..-25 %), a one-tile software pipeline
-// of QK(t+1) beside softmax(t) (spills at 256 VGPRs, -35 %), and a 4-wave x 64-row layout
-// with K/V fragments shared by two subtiles, one wave per SIMD (-25..-35 %: nothing left to
-// hide the softmax -> PV chain; profiles/r2_attn_prefill_wide_variant.log).
-template <int D, int S, bool PRIO, bool DEFER, bool BUFDMA, bool MFSUM>
-__global__ void __launch_bounds__(kPfThreads)
-attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
-                    long k_stride, const bf16* __restrict__ v, long v_stride,
-                    const int* __restrict__ cu_seqlens, const int* __restrict__ cu_k, int Hq,
-                    int Hkv, float scale_log2, int causal, bf16* __restrict__ out, long o_stride,
-                    float* __restrict__ lse) {
-  static_assert(D == 128, "prefill kernel is specialised for D=128");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int STAGE_BYTES = 2 * kPfBKV * D * 2;  // K | V, 32 KiB
-  constexpr int V_OFF = kPfBKV * 256;
-  constexpr int AHEAD = S - 1;                      // tiles staged ahead of the one consumed
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int seq = blockIdx.y, h = blockIdx.z;
-  const int s0 = cu_seqlens[seq];
-  const int L = cu_seqlens[seq + 1] - s0;            // query rows of this sequence
-  // keys: the same rows (self-attention), or another chunk of the sequence (context-parallel
-  // ring steps: non-causal, a different length and offset)
-  const int sk0 = cu_k[seq];
-  const int Lk = cu_k[seq + 1] - sk0;
-  // heaviest (last, under the causal mask) query blocks first: the grid's tail is light work
-  const int q0 = (causal ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * kPfBQ;
-  if (q0 >= L) return;
-  const int kh = h / (Hq / Hkv);
-  const int hi = lane >> 5, c = lane & 31;
-  const bool cz = causal != 0;
-  if (PRIO && __builtin_amdgcn_readfirstlane(wid) >= kPfWaves / 2) __builtin_amdgcn_s_setprio(1);
-
-  // Q^T fragments (B operand of 32x32x16): lane holds Q[row c][d = 16ks + 8hi + j].
-  const int qrow = q0 + 32 * wid + c;
-  bf16x8 qf[8];
-  {
-    const int qr = qrow < L ? qrow : L - 1;
-    const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (long)(s0 + qr) * q_stride + (long)h * D + 8 * hi);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = qp[2 * ks];
-  }
-  PfDma dma{};
-  if (BUFDMA) dma = pf_dma_offsets(k_stride, v_stride, wid, lane);
-
-  f32x16 o[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
-  float m = kNegInf, lsum = 0.f;
-  // MFSUM: the softmax row sums as a fifth 32-row block of O^T whose A operand is all ones:
-  // 4 extra MFMAs per tile (the matrix pipe has slack) replace 32 f32 adds per lane (the VALU
-  // does not), and the sum is of the same bf16 P that multiplies V.
-  f32x16 osum = f32x16{};
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
-
-  const int kv_end = causal ? min(Lk, q0 + kPfBQ) : Lk;
-  const int ntiles = (kv_end + kPfBKV - 1) / kPfBKV;
-  const int wave_qmax = q0 + 32 * wid + 31;
-  // last visible key of this lane's query (causal) or of the chunk, for the masked tiles
-  const int last_key = cz ? min(qrow, Lk - 1) : Lk - 1;
-
-  auto stage = [&](int t, char* dst) {
-    if (BUFDMA) pf_stage_buf(k, k_stride, v, v_stride, sk0, Lk, kh, t, dst, wid, dma);
-    else pf_stage(k, k_stride, v, v_stride, sk0, Lk, kh, t, dst, wid, lane);
-  };
-#pragma unroll
-  for (int st = 0; st < AHEAD; ++st)
-    if (st < ntiles) stage(st, smem + st * STAGE_BYTES);
-  int buf = 0;
-  for (int t = 0; t < ntiles; ++t) {
-    // tile t landed; the (up to AHEAD - 1) tiles issued after it may still fly
-    pf_wait_tiles(min(ntiles - 1, t + AHEAD - 1) - t);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t + AHEAD < ntiles) {
-      int nb = buf + AHEAD;
-      if (nb >= S) nb -= S;
-      stage(t + AHEAD, smem + nb * STAGE_BYTES);
-    }
-    const int kv0 = t * kPfBKV;
-    const char* kb = smem + buf * STAGE_BYTES;
-    if (!(cz && kv0 > wave_qmax)) {
-      f32x16 sc[2];
-      pf_qk(kb, qf, lane, sc);
-      // masking only on the diagonal / ragged-end tiles (wave-uniform branch)
-      const bool need_mask = (cz && kv0 + kPfBKV - 1 > q0 + 32 * wid) || kv0 + kPfBKV > Lk;
-      const int lim = last_key - kv0 - 4 * hi;
-      const float tmax = need_mask ? pf_tile_max<true>(sc, lim, scale_log2) : pf_tile_max<false>(sc, lim, scale_log2);
-      float alpha = 1.f;
-      // (first tile: tmax - (-inf) = inf, or NaN on an all-masked row: both take the rescale)
-      if (!DEFER || !__all(tmax - m <= kPfRescaleThr)) {
-        const float mn = fmaxf(m, tmax);
-        const float mb = mn == kNegInf ? 0.f : mn;
-        alpha = __builtin_amdgcn_exp2f(m - mb);
-        m = mn;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-        if (MFSUM) osum *= alpha;
-      }
-      const float mb = m == kNegInf ? 0.f : m;
-      bf16x8 pb[2][2];
-      if (MFSUM) {
-        pf_exp_nosum(sc, scale_log2, mb, pb);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) osum = mfma32(ones, pb[kt][hh], osum);
-      } else {
-        lsum = lsum * alpha + pf_exp(sc, scale_log2, mb, pb);
-      }
-      pf_pv(kb + V_OFF, pb, lane, o);
-    }
-    if (++buf == S) buf = 0;
-  }
-  if (MFSUM) lsum = osum[0];   // every row of the ones block holds the full key sum
-  else lsum += __shfl_xor(lsum, 32, 64);
-  if (qrow >= L) return;
-  // natural-log sum of exp(score * scale) over the visible keys (-inf: none), for merging
-  // partial attention over key chunks (attn_lse_merge_kernel)
-  if (lse != nullptr && hi == 0)
-    lse[(long)(s0 + qrow) * Hq + h] = lsum > 0.f ? (m + __log2f(lsum)) * 0.69314718055994531f : kNegInf;
-  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-  bf16* op = out + (long)(s0 + qrow) * o_stride + (long)h * D;
-  // o[dt][r] = O[query c][d = 32dt + (r&3) + 8(r>>2) + 4hi]
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      bf16x4 w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = f2bf(o[dt][4 * a + j] * inv);
-      *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * a + 4 * hi) = w;
-    }
-}
 
 // ---------------------------------------------------------------------------------------
 // Persistent prefill: one workgroup per CU walks the (query block, sequence, head) items in
@@ -797,9 +455,20 @@ attn_prefill_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __res
 // The K/V ring runs ACROSS items: the tiles of the next item are staged while the current
 // item's last tiles are computed, and no workgroup launch, Q/ring prologue or grid tail sits
 // between items. Short prompts gain most (a 1024-token causal block is 4-16 tiles of work next
-// to a fixed per-workgroup start). Per tile the math is attn_prefill_kernel's (BUFDMA staging,
-// deferred rescale, wave priority); the wave-local vmcnt wait counts the tiles issued after the
-// consumed one (later stores and Q loads only make the wait conservative).
+// to a fixed per-workgroup start): 423 / 583 / 804 -> 663 / 862 / 925 TF/s at 16x1024 / 4x4096 /
+// 1x16384 tokens against one workgroup per item (profiles/r2_attn_prefill_persistent.log).
+// Per tile: S^T = K Q^T on 32x32x16 MFMAs (the lane owns one query column: row max/sum are
+// lane-local plus one swap), P^T built in registers from the accumulator, O^T += V^T P^T with V
+// fed by transposed LDS reads (ds_read_b64_tr_b16). The loop is VALU-bound next to its MFMAs, so
+// the VALU is trimmed: buffer-descriptor K/V staging (scalar tile windows), the deferred O
+// rescale, and s_setprio 1 for waves 4-7 (which lose VALU arbitration to their older SIMD
+// partners). The wave-local vmcnt wait counts the tiles issued after the consumed one (later
+// stores and Q loads only make the wait conservative).
+// Measured and dropped (profiles/r2_attn_prefill_variants*.log, r2_attn_prefill_wide_variant.log):
+// a 5-stage ring (-7 % on 16k tokens), waves 4-7 running PV one tile late (-15..-25 %), a
+// one-tile software pipeline of QK(t+1) beside softmax(t) (spills at 256 VGPRs, -35 %), a
+// 4-wave x 64-row layout sharing K/V fragments (-25..-35 %), row sums on the matrix core (+-1 %),
+// and the round-1 non-persistent kernel (one workgroup per item; 16-40 % slower).
 // ---------------------------------------------------------------------------------------
 struct PfItem {
   int valid, rows, ntiles;  // valid: item index in range; rows: query rows to write (q0 < L);
@@ -973,11 +642,9 @@ int attn_decode_part_tokens(int B, int Hkv, int max_ctx) {
 int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
-                       bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                       int* counters, int kv_fp8, const DecRope* rope) {
+                       bf16* out, float* part_o, float* part_ml, hipStream_t stream, int kv_fp8) {
   if (B <= 0) return 0;
   if (D != 128 || block_size != 32 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
-  if (rope != nullptr && kv_fp8) return -6;   // fused RoPE: bf16 caches only
   if (part_tokens <= 0) part_tokens = attn_decode_part_tokens(B, Hkv, max_ctx);
   if (part_tokens % block_size != 0) return -2;
   if (attn_decode_splits(max_ctx, part_tokens) > 256) return -4;
@@ -985,46 +652,23 @@ int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const 
   if (nsplit > 1 && (part_o == nullptr || part_ml == nullptr)) return -3;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(nsplit, Hkv, B);
-  int* cnt = nsplit > 1 ? counters : nullptr;
-  if (rope != nullptr)
-    attn_decode_kernel<128, 32, bf16, true><<<grid, kAttnThreads, 0, stream>>>(
-        q, q_stride, static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), block_tables,
-        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, cnt, *rope);
-  else if (kv_fp8)
+  if (kv_fp8)
     attn_decode_kernel<128, 32, fp8_t><<<grid, kAttnThreads, 0, stream>>>(
         q, q_stride, static_cast<const fp8_t*>(k_cache), static_cast<const fp8_t*>(v_cache), block_tables,
-        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, cnt);
+        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml);
   else
     attn_decode_kernel<128, 32, bf16><<<grid, kAttnThreads, 0, stream>>>(
         q, q_stride, static_cast<const bf16*>(k_cache), static_cast<const bf16*>(v_cache), block_tables,
-        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, cnt);
-  if (nsplit > 1 && counters == nullptr) {
+        bt_stride, ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml);
+  if (nsplit > 1) {
+    // Measured and dropped: merging the splits inside the decode kernel (last arriver, agent-
+    // scope release/acquire per workgroup) ran 2x slower than this parallel combine launch
+    // (B=64 ctx 1024: 104 vs 53 us); RoPE + KV append fused into the decode kernel ran 1 %
+    // slower per 70B step than rope_kv + attention (profiles/r2_fused_decode_rope_ab.log).
     dim3 g2(Hq / Hkv, Hkv, B);
     attn_decode_combine_kernel<128><<<g2, 128, 0, stream>>>(part_o, part_ml, nsplit, Hq, Hkv, out);
   }
   return 0;
-}
-
-int launch_attn_decode_rope(const bf16* qkv, const float* part, int sk, const int* positions,
-                            const float* cos_t, const float* sin_t, const int* slots, void* k_cache,
-                            void* v_cache, const int* block_tables, int bt_stride, const int* ctx_lens,
-                            int B, int Hq, int Hkv, int D, int block_size, float scale, int max_ctx,
-                            int part_tokens, bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                            int* counters, int kv_fp8) {
-  DecRope rp;
-  rp.qkv = qkv;
-  rp.part = part;
-  rp.sk = sk;
-  rp.slab = (long)B * (Hq + 2 * Hkv) * D;
-  rp.positions = positions;
-  rp.cos_t = cos_t;
-  rp.sin_t = sin_t;
-  rp.slots = slots;
-  rp.k_w = k_cache;
-  rp.v_w = v_cache;
-  return launch_attn_decode(qkv, 0, k_cache, v_cache, block_tables, bt_stride, ctx_lens, B, Hq, Hkv, D,
-                            block_size, scale, max_ctx, part_tokens, out, part_o, part_ml, stream, counters,
-                            kv_fp8, &rp);
 }
 
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
@@ -1034,16 +678,8 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   if (nseq <= 0 || max_seqlen <= 0) return 0;
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid((max_seqlen + kPfBQ - 1) / kPfBQ, nseq, Hq);
-  // variant (BFLY_ATTN_PF_VARIANT, A/B timing): ring depth, priority, deferred rescale, buffer DMA.
-  // 16x1024 / 4x4096 / 1x16384 tokens (64 q / 8 kv heads): 390 / 537 / 740 TF/s (variant 1) ->
-  // 471 / 610 / 800 (variant 0); profiles/r2_attn_prefill_variants.log
-  // variant 3 (default): the persistent item walk, 423 / 583 / 804 -> 663 / 862 / 925 TF/s at
-  // 16x1024 / 4x4096 / 1x16384 (profiles/r2_attn_prefill_persistent.log)
-  const char* ev = getenv("BFLY_ATTN_PF_VARIANT");
-  int var = ev ? atoi(ev) : 3;
   const int* cuk = cu_k != nullptr ? cu_k : cu_seqlens;
-  if (var == 3) {
+  {
     constexpr int S_ = 3;
     const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;
     static int ncu = 0;
@@ -1062,25 +698,6 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
         causal ? 1 : 0, out, o_stride, lse);
     return 0;
   }
-#define PF_VARIANT(ID, S_, PR_, DF_, BD_, MS_)                                                         \
-  if (var == ID) {                                                                                \
-    const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;                                           \
-    static bool attr = false;                                                                     \
-    if (!attr) {                                                                                  \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_kernel<128, S_, PR_, DF_, BD_, MS_>), \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
-      attr = true;                                                                                \
-    }                                                                                             \
-    attn_prefill_kernel<128, S_, PR_, DF_, BD_, MS_><<<grid, kPfThreads, lds, stream>>>(               \
-        q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cuk, Hq, Hkv, scale_log2, causal ? 1 : 0, \
-        out, o_stride, lse);                                                                      \
-    return 0;                                                                                     \
-  }
-  PF_VARIANT(0, 3, true, true, true, false)     // one workgroup per item (context-parallel ring steps)
-  PF_VARIANT(1, 4, false, false, false, false)  // round-1 kernel, for A/B
-  PF_VARIANT(2, 3, true, true, true, true)      // row sums on the matrix core: neutral (+-1 %)
-#undef PF_VARIANT
-  return -5;
 }
 
 // K16: merge a partial attention result over another key chunk into running accumulators

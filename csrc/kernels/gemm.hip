@@ -63,12 +63,10 @@ __device__ __forceinline__ void store_out4(bf16* out, long ldo, int m, int n, f3
 }
 
 // Split-K partial slabs: 16 B per lane through a buffer descriptor, plain (write-back) stores.
-// BFLY_GEMM_SLAB_WT=1 makes them write-through (`sc1`, aux 16), so a launch would not end with
-// MBs of dirty f32 lines to write back before its consumer starts (MI355X_MICROARCH.md
-// 'boundary': + B / 6 TB/s for B dirty bytes). Measured in the whole decode step it is SLOWER:
-// Llama-3-70B 30.28-30.32 vs 29.99-30.02 ms, Llama-3-8B 5.58 vs 5.49 ms
-// (profiles/r2_slab_writethrough_ab.log), so it stays off.
-__constant__ int g_slab_wt = 0;
+// Measured and dropped: write-through (`sc1`) slab stores, meant to spare the consumer the
+// write-back of MBs of dirty f32 lines (MI355X_MICROARCH.md 'boundary'), made the whole decode
+// step SLOWER: Llama-3-70B 30.28-30.32 vs 29.99-30.02 ms, Llama-3-8B 5.58 vs 5.49 ms
+// (profiles/r2_slab_writethrough_ab.log).
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(float* base, long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
@@ -76,10 +74,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(float* base, long by
 }
 
 __device__ __forceinline__ void store_slab4(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
-  if (g_slab_wt)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
-  else
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
 }
 
 // Reduce split-K partial slabs [SK][M][N] (f32) and apply the epilogue.
@@ -764,102 +759,201 @@ gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
                         part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
 }
 
-// Persistent variant of gemm_big_kernel (no split-K): one workgroup per CU walks its output
-// tiles (round j = the one-tile-per-workgroup grid's j-th wave of G workgroups, same XCD remap
-// and GROUP_M order), and the glds ring runs ACROSS tiles: the next tile's first
-// K-steps are staged while this tile's last ones are computed, and the epilogue (register ->
-// global stores, no barrier) sits between two K-steps of one flattened loop. The wave groups'
-// ping-pong stagger is set up once per launch instead of once per tile. (The same structure
-// took the prefill attention kernel from 423 to 663 TF/s at 16 x 1024 tokens.) Measured here it
-// is 13-19 % slower than one workgroup per tile (gate_up M = 8192: 6553 vs 5707 us; the tile
-// order matching the one-tile grid's and per-tile accumulator scopes did not change that), so
-// it is opt-in (BFLY_GEMM_BIG_PERSIST=1) and kept for A/B.
-template <int S>
-__global__ void __launch_bounds__(kBigThreads)
-gemm_big_persist_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
-                        int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                        bf16* __restrict__ out, long ldo) {
-  constexpr int BM = 256, BN = 256, TI = 8, TJ = 4;
-  constexpr int A_BYTES = BM * kBigBK * 2, STAGE_BYTES = 2 * A_BYTES;
-  constexpr int LPW = 4;   // glds per wave per stage (2 for X, 2 for W)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// ---------------------------------------------------------------------------------------
+// 8-phase big-tile GEMM (prefill): 256x256 tile, BK = 64, two K-tile LDS buffers (128 KiB),
+// 8 waves (2 along M x 4 along N, 128x64 outputs each) in two groups staggered by one barrier
+// (group wr = 1 starts one s_barrier later), so on every SIMD one wave runs a 16-MFMA segment
+// while its partner reads fragments and issues DMA (cdna_hip_programming.md §5 "The 256²
+// 8-phase template", T3+T4+T5).
+//
+// A K-tile is consumed in 4 phases, one C-quadrant of the wave's 128x64 block each:
+//   q0: rows 0-63 x cols 0-31   reads A-lo (8 ds_read_b128) + B-lo (4)
+//   q1: rows 0-63 x cols 32-63  reads B-hi (4)            (A-lo kept in registers)
+//   q2: rows 64-127 x cols 32-63 reads A-hi (8)           (B-hi kept)
+//   q3: rows 64-127 x cols 0-31  no reads                 (A-hi, B-lo kept)
+// so each of the K-tile's four half-tiles (A-lo = rows {0-63, 128-191}, A-hi = {64-127,
+// 192-255}, B-lo = cols {0-31, 64-95, ...}, B-hi = the other 32-column groups; 16 KiB each) is
+// read completely in ONE phase. Every phase issues one half-tile of DMA (2 glds per wave) into
+// a half that was fully read (and retired by lgkmcnt(0) before a barrier every reader passed)
+// in an earlier phase: K-tile k's halves go out at phases 4(k-2)+{2,3,4,5} (A-lo, B-lo, B-hi,
+// A-hi), i.e. one phase after the same half of K-tile k-2 was read. The counted wait is in
+// phase 4k only (the K-tile's last phase): vmcnt(6) leaves the 3 half-tiles issued after A-hi(k)
+// in flight and retires all of K-tile k, which is read from phase 4k+1 on (one phase after the
+// wait, behind a barrier both groups pass: the template's RAW rule). Raw s_barrier only: a
+// __syncthreads() would drain the DMA in flight (§5 "Pipelining across barriers").
+// ---------------------------------------------------------------------------------------
+constexpr int kB8Threads = 512;
+constexpr int kB8LdsBytes = 2 * 2 * 256 * 128;   // 2 buffers x (A, B) x 256 rows x 128 B
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-  const int ntile_all = mtiles * ntiles;
-  const int G = gridDim.x;
-  const int my_tiles = (int)blockIdx.x < ntile_all ? (ntile_all - (int)blockIdx.x + G - 1) / G : 0;
-  const int ktiles = K / kBigBK;
-  const int total = my_tiles * ktiles;   // flattened (tile, K-step) count of this workgroup
-  if (total == 0) return;
-  auto tile_mn = [&](int j, int& m0, int& n0) {
-    // round j does what the one-tile-per-workgroup grid dispatches j-th: workgroups
-    // j*G .. j*G+G-1 of it, through the same XCD remap and GROUP_M order
-    const int t = xcd_remap(j * G + (int)blockIdx.x, ntile_all);
-    const int per_group = kBigGroupM * ntiles;
-    const int g = t / per_group, first_m = g * kBigGroupM;
-    const int gsize = min(mtiles - first_m, kBigGroupM);
-    m0 = (first_m + (t % per_group) % gsize) * BM;
-    n0 = ((t % per_group) / gsize) * BN;
-  };
-  // stage cursor: the flattened step it stages next, as (tile, K-step) and that tile's origin
-  int sj = 0, skt = 0, sm0, sn0;
-  tile_mn(0, sm0, sn0);
-  auto stage_next = [&](char* b) {
-    big_stage(X, ldx, sm0, M, skt * kBigBK, b, wid, lane);
-    big_stage(W, ldw, sn0, N, skt * kBigBK, b + A_BYTES, wid, lane);
-    if (++skt == ktiles) {
-      skt = 0;
-      if (++sj < my_tiles) tile_mn(sj, sm0, sn0);
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < total) stage_next(smem + s * STAGE_BYTES);
-  big_wait<S, LPW>(min(S - 1, total) - 1);
-  __builtin_amdgcn_s_barrier();
-  if (wm == 1) __builtin_amdgcn_s_barrier();
-  int buf = 0;
-  for (int j = 0; j < my_tiles; ++j) {   // tiles; the K-step loop below is gemm_big_kernel's
-    int m0, n0;
-    tile_mn(j, m0, n0);
-    f32x4 acc[TI][TJ];
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int q = 0; q < TJ; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int g0 = j * ktiles;
-    for (int g = g0; g < g0 + ktiles; ++g) {
-      const char* As = smem + buf * STAGE_BYTES;
-      const char* Bs = As + A_BYTES;
-      bf16x8 bfr[TJ], af[TI];
-#pragma unroll
-      for (int q = 0; q < TJ; ++q) bfr[q] = big_frag(Bs, wn * 64 + 16 * q + (lane & 15), lane >> 4);
-#pragma unroll
-      for (int i = 0; i < TI; ++i) af[i] = big_frag(As, wm * 128 + 16 * i + (lane & 15), lane >> 4);
-      if (g + S - 1 < total) {
-        int nbuf = buf + S - 1;
-        if (nbuf >= S) nbuf -= S;
-        stage_next(smem + nbuf * STAGE_BYTES);
-      }
-      // step g+1 must have landed; steps g+2 .. g+S-1 (issued) may still fly
-      big_wait<S, LPW>(min(total - 1, g + S - 1) - (g + 1));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int q = 0; q < TJ; ++q) acc[i][q] = mfma16(bfr[q], af[i], acc[i][q]);   // C^T tile
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_s_barrier();
-      if (++buf == S) buf = 0;
-    }
-    tile_epilogue<TI, TJ>(acc, m0 + wm * 128, n0 + wn * 64, lane, M, N, epi, bias, out, ldo, nullptr, m0);
+// LDS row-block (8 rows x 128 B = 1 KiB) of the h-th DMA instruction of half-tile `half`
+// (0 A-lo / 1 B-lo / 2 B-hi / 3 A-hi; h in 0..15: instruction 2*wave + {0,1}).
+__device__ __forceinline__ int b8_block(int half, int h) {
+  if (half == 0 || half == 3) {            // A: rows {0-63,128-191} (lo) or {64-127,192-255} (hi)
+    const int base = half == 0 ? 0 : 8;
+    return (h < 8 ? base + h : 16 + base + (h - 8));
   }
-  if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
+  // B: 32-row groups g (0..3) at rows 64g + (hi ? 32 : 0); 4 blocks per group
+  const int g = h >> 2, b = h & 3;
+  return g * 8 + (half == 2 ? 4 : 0) + b;
+}
+
+__device__ __forceinline__ void b8_stage(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W,
+                                         long ldw, int m0, int M, int n0, int N, int k0, char* buf,
+                                         int half, int wid, int lane) {
+  const bool isA = half == 0 || half == 3;
+  const bf16* src = isA ? X : W;
+  const long ld = isA ? ldx : ldw;
+  const int r0 = isA ? m0 : n0, rmax = isA ? M : N;
+  char* lds = buf + (isA ? 0 : 256 * 128);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = b8_block(half, 2 * wid + i);
+    const int row = blk * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);   // lds_frag's swizzle, on the source
+    int gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;
+    const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 0);
+  }
+}
+
+template <bool EARLY>
+__global__ void __launch_bounds__(kB8Threads)
+gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
+                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
+                 bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+  constexpr int BM = 256, BN = 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int per_group = kBigGroupM * ntiles;
+  const int grp = t / per_group, first_m = grp * kBigGroupM;
+  const int gsize = min(mtiles - first_m, kBigGroupM);
+  const int m0 = (first_m + (t % per_group) % gsize) * BM;
+  const int n0 = ((t % per_group) / gsize) * BN;
+  const int ktiles = K / 64;
+  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
+  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
+  const int nk = kt1 - kt0;   // >= 2 (host check)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto bufp = [&](int k) -> char* { return smem + (k & 1) * (2 * 256 * 128); };
+  auto stage = [&](int k, int half) {
+    b8_stage(X, ldx, W, ldw, m0, M, n0, N, (kt0 + k) * 64, bufp(k), half, wid, lane);
+  };
+  // prologue: all of K-tile 0, then A-lo, B-lo, B-hi of K-tile 1 (the load stream's order)
+  stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
+  stage(1, 0); stage(1, 1); stage(1, 2);
+  vm_wait<6>();                          // K-tile 0 landed (this wave's part)
+  __builtin_amdgcn_s_barrier();          // every wave's part
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  const int ar = wr * 128 + (lane & 15);  // A fragment row of block i: ar + 16 i
+  const int bc = wc * 64 + (lane & 15);   // B fragment row (output column) of block j
+  bf16x8 a_lo[4][2], a_hi[4][2], b_lo[2][2], b_hi[2][2];
+  for (int k = 0; k < nk; ++k) {
+    const char* As = bufp(k);
+    const char* Bs = As + 256 * 128;
+    const bool more = k + 1 < nk, more2 = k + 2 < nk;
+    // ---- q0: read A-lo, B-lo; DMA A-hi(k+1)
+    // EARLY: A-lo is the one half restaged one phase after its read (q1 below), so only its
+    // reads must retire before this phase's barrier (lgkmcnt(4) after A first, B last); every
+    // other read completes inside the wave's own MFMA segment (compiler-placed waits), which
+    // releases the barrier earlier (guide §5 template: "lgkmcnt(8) retires the reads issued
+    // first"). Without EARLY every load segment drains its reads before the barrier.
+    if constexpr (EARLY) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) b_lo[j][ks] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
+      if (more) stage(k + 1, 3);
+      asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) b_lo[j][ks] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
+      if (more) stage(k + 1, 3);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b_lo[j][ks], a_lo[i][ks], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q1: read B-hi; DMA A-lo(k+2) (A-lo(k) was read in q0)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b_hi[j][ks] = lds_frag(Bs, bc + 32 + 16 * j, ks * 4 + (lane >> 4));
+    if (more2) stage(k + 2, 0);
+    if constexpr (!EARLY) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b_hi[j][ks], a_lo[i][ks], acc[i][2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q2: read A-hi; DMA B-lo(k+2) (B-lo(k) was read in q0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a_hi[i][ks] = lds_frag(As, ar + 64 + 16 * i, ks * 4 + (lane >> 4));
+    if (more2) stage(k + 2, 1);
+    if constexpr (!EARLY) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b_hi[j][ks], a_hi[i][ks], acc[4 + i][2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- q3: no reads; DMA B-hi(k+2) (B-hi(k) was read in q1); retire K-tile k+1
+    if (more2) stage(k + 2, 2);
+    if (more2) vm_wait<6>();   // A-hi(k+1) and older landed; A-lo/B-lo/B-hi(k+2) fly
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b_lo[j][ks], a_hi[i][ks], acc[4 + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    (void)more;
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
+  tile_epilogue<8, 4>(acc, m0 + wr * 128, n0 + wc * 64, lane, M, N, epi, bias, out, ldo,
+                      part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -900,9 +994,6 @@ static void init_nt_policy() {
   const int zero = 0;
   const char* e = getenv("BFLY_GEMM_NT_WEIGHTS");
   if (e && e[0] == '0') (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile_w_nt), &zero, sizeof(int));
-  const int one = 1;
-  e = getenv("BFLY_GEMM_SLAB_WT");
-  if (e && e[0] == '1') (void)hipMemcpyToSymbol(HIP_SYMBOL(g_slab_wt), &one, sizeof(int));
 }
 
 template <int BM, int BN, int WMW, int STAGES>
@@ -946,45 +1037,41 @@ static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
 static void run_big(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                     hipStream_t stream) {
+  // Measured and dropped (profiles/r2_gemm_big_persistent_ab.log): a persistent tile walk with
+  // the glds ring running across tiles, 13-19 % slower than one workgroup per tile; a 4-stage
+  // (128 KiB) ring, 1-2 % slower than 5.
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<kBigStages>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kBigStages * 2 * 256 * kBigBK * 2);
+    attr = true;
+  }
   const int tiles = ((M + 255) / 256) * (N / 256);
-  static int stages = 0;
-  if (!stages) {
-    const char* e = getenv("BFLY_BIG_STAGES");
-    stages = e && atoi(e) == 4 ? 4 : kBigStages;   // BFLY_BIG_STAGES=4: A/B against the 128 KiB ring
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<4>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 256 * kBigBK * 2);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<5>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 256 * kBigBK * 2);
-  }
-  const size_t lds = (size_t)stages * 2 * 256 * kBigBK * 2;
-  // BFLY_GEMM_BIG_PERSIST=1: the persistent tile walk (opt-in: measured 13-19 % SLOWER than one
-  // workgroup per tile on the 70B prefill shapes, profiles/r2_gemm_big_persistent_ab.log)
-  static int persist = -1;
-  if (persist < 0) {
-    const char* e = getenv("BFLY_GEMM_BIG_PERSIST");
-    persist = (e && e[0] == '1') ? 1 : 0;
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_persist_kernel<4>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 2 * 256 * kBigBK * 2);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_persist_kernel<5>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 2 * 256 * kBigBK * 2);
-  }
-  if (persist && sk == 1) {
-    const int g = tiles < num_cus() ? tiles : num_cus();
-    if (stages == 5)
-      gemm_big_persist_kernel<5><<<g, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo);
-    else
-      gemm_big_persist_kernel<4><<<g, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo);
-    return;
-  }
+  const size_t lds = (size_t)kBigStages * 2 * 256 * kBigBK * 2;
   dim3 grid(tiles, sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  if (stages == 5)
-    gemm_big_kernel<5><<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
-  else
-    gemm_big_kernel<4><<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  gemm_big_kernel<kBigStages><<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
-
+static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, int early,
+                     hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+    attr = true;
+  }
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  dim3 grid(tiles, sk);
+  float* part = sk > 1 ? splitk_part(ws) : nullptr;
+  if (early)
+    gemm_big8_kernel<true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  else
+    gemm_big8_kernel<false><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+}
 
 // Plan selection, from the tools/bench_gemm.py sweep on MI355X (Llama-3-70B TP1/TP8 shapes,
 // weights streamed from HBM): the LDS-tiled kernel with a small BM and split-K beats the
@@ -1121,6 +1208,10 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     if (N % 256 != 0 || K % kBigBK != 0) return -1;
     if (p.sk > 1 && (long)((M + 255) / 256) * (N / 256) > kSplitCounters) return -1;
     if (!dry) run_big(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+  } else if (p.kind == 4) {
+    // 8-phase big tile: every split needs >= 2 K-tiles of 64
+    if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
+    if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, p.mt, stream);   // mt: EARLY
   } else if (p.kind == 3) {
     // decode ring GEMM: plan {3, SW (weight ring depth), waves, waves along M, BM, BN, sk}
     if (N % p.bn != 0 || K % kBK != 0 || K / kBK < p.sk * 2) return -1;
@@ -1177,7 +1268,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind >= 2)) {   // big kernel: no fixup path
+  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind == 2 || p.kind == 4)) {   // big kernels: no fixup path
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);

@@ -226,10 +226,9 @@ def test_attn_prefill_non_causal():
     _close(o, ref.attn_prefill(q, k, v, cu, 130, 0.088, False), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("part_tokens", [0, 128, 256, 4096])
 @pytest.mark.parametrize("Hq,Hkv", [(16, 2), (8, 8), (64, 8)])
-def test_attn_decode_paged(part_tokens, Hq, Hkv, fused, monkeypatch):
+def test_attn_decode_paged(part_tokens, Hq, Hkv):
     D, BS = 128, 32
     lens = [1, 31, 32, 100, 700]
     B = len(lens)
@@ -241,11 +240,9 @@ def test_attn_decode_paged(part_tokens, Hq, Hkv, fused, monkeypatch):
     ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
     q = _bf(B, Hq, D, seed=26)
     scale = 1.0 / math.sqrt(D)
-    monkeypatch.setattr(ops, "FUSED_DECODE_COMBINE", fused)
     want = ref.attn_decode(q, kc, vc, perm, ctx, scale)
-    for _ in range(2):   # the fused combine must leave its split counters re-armed
-        o = ops.attn_decode(q, kc, vc, perm, ctx, scale, max(lens), part_tokens)
-        _close(o, want, 2e-2, 2e-2)
+    o = ops.attn_decode(q, kc, vc, perm, ctx, scale, max(lens), part_tokens)
+    _close(o, want, 2e-2, 2e-2)
 
 
 def test_attn_decode_strided_q():
@@ -664,39 +661,3 @@ def test_sample_check_finite():
     assert torch.equal(rid.cpu(), ids)
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(64, 8), (16, 2)])
-@pytest.mark.parametrize("part_tokens", [0, 128])
-@pytest.mark.parametrize("partial", [False, True])
-def test_attn_decode_rope_fused(Hq, Hkv, part_tokens, partial):
-    """Decode attention with RoPE + the new token's KV append fused in (attn_decode_rope) equals
-    rope_kv followed by attn_decode: same attention output, and the caches hold the same rotated
-    key / value at the new token's slot (bit for bit). Also from split-K slabs of the QKV GEMM,
-    and with the context split over several workgroups (the new token then lives in the last)."""
-    D, BS = 128, 32
-    lens = [1, 31, 32, 33, 100, 700]      # context incl. the new token at position len-1
-    B = len(lens)
-    mb = (max(lens) + BS - 1) // BS
-    nblk = B * mb + 3
-    kc = _bf(nblk, Hkv, BS, D, seed=101)
-    vc = _bf(nblk, Hkv, D, BS, seed=102)
-    bt = torch.randperm(nblk)[: B * mb].view(B, mb).to(torch.int32).to(DEV)
-    ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
-    pos = (ctx - 1).contiguous()
-    slots = torch.tensor([int(bt[i, (n - 1) // BS]) * BS + (n - 1) % BS for i, n in enumerate(lens)],
-                         dtype=torch.int32, device=DEV)
-    N = (Hq + 2 * Hkv) * D
-    cos, sin = ops.rope_tables(D, 2048, 500000.0, None, device=DEV)
-    if partial:
-        slabs = torch.randn(3, B, N, device=DEV) * 0.7
-        qkv_in = lambda: ops.Partial(slabs.clone(), torch.empty(B, N, dtype=torch.bfloat16, device=DEV))  # noqa: E731
-    else:
-        base = _bf(B, N, seed=103)
-        qkv_in = lambda: base.clone()  # noqa: E731
-    k1, v1 = kc.clone(), vc.clone()
-    rows = ops.rope_kv(qkv_in(), pos, cos, sin, Hq, Hkv, slots, k1, v1)
-    want = ops.attn_decode(rows[:, : Hq * D].view(B, Hq, D), k1, v1, bt, ctx, 0.0883, max(lens), part_tokens)
-    k2, v2 = kc.clone(), vc.clone()
-    got = ops.attn_decode_rope(qkv_in(), pos, cos, sin, slots, k2, v2, bt, ctx, Hq, 0.0883, max(lens), part_tokens)
-    torch.cuda.synchronize()
-    assert torch.equal(k1, k2) and torch.equal(v1, v2)
-    _close(got, want, 2e-2, 2e-2)

@@ -148,3 +148,25 @@ def test_async_pipeline_preposted_receives(preset, kw, monkeypatch):
         assert on == (not first)
         if not first:
             assert used > 0
+
+
+def test_native_pp_program_puts_recv_in_graph_and_send_on_send_stream():
+    """With native RCCL pipeline edges the boundary receive is the decode graph's first node
+    and the send leaves from the send stream, both moving the whole graph bucket; the programs
+    stay pairwise consistent."""
+    from butterfly_amd.partition import schedule as sch
+    from butterfly_amd.partition.plan import PartitionPlan  # noqa: F401
+    from butterfly_amd.partition import partition
+    from butterfly_amd.config import ModelConfig
+
+    plan = partition(ModelConfig.from_preset("llama-tiny"), 4, {"tp": 2, "pp": 2}, batch_per_gpu=8, ctx=128)
+    progs = sch.programs(plan, 6, native_pp=True, bucket=8)
+    sch.check_programs(progs)
+    h = plan.model.hidden_size
+    for r, p in progs.items():
+        c = plan.mesh.coord(r)
+        p2p = [i for i in p.comm() if i.op in ("send", "recv")]
+        assert len(p2p) == 1
+        i = p2p[0]
+        assert i.nbytes == 8 * h * 2
+        assert (i.op, i.stream) == (("recv", "graph") if c.pp == 1 else ("send", "send"))

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Paged decode-attention microbenchmark (KV bytes streamed per call -> TB/s)."""
+"""Attention microbenchmark: causal flash prefill (TFLOP/s of useful causal FLOPs) and paged
+decode (KV bytes streamed per call -> TB/s)."""
 import argparse
 import json
 import os
@@ -18,15 +19,9 @@ def main():
                     help="prefill cases seqs:len:Hq:Hkv ('' to skip)")
     ap.add_argument("--parts", default="0", help="decode split sizes to try (0 = auto)")
     ap.add_argument("--kv-dtype", default="bf16,fp8", help="decode cache element types to time")
-    ap.add_argument("--variants", default="", help="prefill kernel variants to time (BFLY_ATTN_PF_VARIANT)")
     a = ap.parse_args()
     ops.load_library()
-    cases = [(c, None) for c in filter(None, a.prefill.split(","))]
-    if a.variants:
-        cases = [(c, v) for v in a.variants.split(",") for c, _ in cases]
-    for case, var in cases:
-        if var is not None:
-            os.environ["BFLY_ATTN_PF_VARIANT"] = var
+    for case in filter(None, a.prefill.split(",")):
         n, Ls, Hq, Hkv = map(int, case.split(":"))
         D, T = 128, n * Ls
         q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16)
@@ -47,7 +42,7 @@ def main():
         torch.cuda.synchronize()
         us = st.elapsed_time(en) / it * 1e3
         flops = 4.0 * n * Ls * Ls / 2 * Hq * D          # causal useful FLOPs
-        print(json.dumps({"prefill": case, "variant": var, "us": round(us, 1),
+        print(json.dumps({"prefill": case, "us": round(us, 1),
                           "TFLOPs": round(flops / us / 1e6, 1)}), flush=True)
     for case, kvd in [(c, k) for c in a.cases.split(",") for k in a.kv_dtype.split(",")]:
         B, ctx, Hq, Hkv = map(int, case.split(":"))

@@ -5,7 +5,7 @@
 #
 # STEP forms (each runs under its own `timeout -k 10`, output under gpurun_out/; the first
 # failing step ends the run with its exit code):
-#   tests[=PYTEST_ARGS]      pytest -m gpu (default: the whole GPU suite)        -> pytest_gpu.log
+#   tests[=PATHS]            pytest -m gpu (default: the whole GPU suite)        -> pytest_gpu_<n>.log
 #   smoke                    __graft_entry__.smoke()                             -> smoke.log
 #   bench[=BENCH_ARGS]       python bench.py BENCH_ARGS                          -> bench_<n>.log
 #   prof=TAG[=BENCH_ARGS]    rocprofv3 kernel trace of bench.py + prof_summary   -> prof_TAG/, prof_TAG.md
@@ -22,8 +22,9 @@ for step in "$@"; do
   [[ "$step" == *=* ]] && arg=${step#*=}
   case "$kind" in
     tests)
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread $arg \
-        > gpurun_out/pytest_gpu.log 2>&1 ;;
+      # tests=PATHS runs those files / node ids instead of the whole GPU suite
+      timeout -k 10 1000 python -u -m pytest ${arg:-tests} -m gpu -x -q --timeout 120 --timeout-method thread \
+        > gpurun_out/pytest_gpu_$n.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench)
