@@ -2,13 +2,15 @@
 """Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals for the decode phase and per
 decode step.
 
-The decode window is cut from the trace itself: it starts after the first sampling dispatch
-that follows the LAST prefill kernel (flash-prefill attention, big-tile GEMM or a hipBLASLt
-`Cijk` GEMM), so the prefill step's own tail (norm, LM head, sampling) is outside it, and it
-ends with the last sampling dispatch. Every decode step samples exactly once
-(sample_final_kernel), so the number of decode steps in the window is the number of sampling
-dispatches in it; with --layers the count of decode-attention dispatches / layers is printed
-as a cross-check.
+The decode window is cut from the trace itself. Every decode step samples exactly once
+(sample_final_kernel) after one forward pass; the segments between consecutive sampling
+dispatches after the LAST prefill kernel (flash-prefill attention, big-tile GEMM or a hipBLASLt
+`Cijk` GEMM) are decode steps. A segment that holds more forward passes than a step (the
+hipGraph capture's eager warm-up runs before the first replay) is skipped: the window starts
+after the first segment whose decode-attention count is the per-step count (the most common
+one, i.e. the layer count) and ends with the last sampling dispatch. The number of decode steps
+is the number of sampling dispatches in the window; decode-attention dispatches / layers is
+printed as a cross-check.
 
 usage: python tools/prof_summary.py gpurun_out/prof_x/run_kernel_trace.csv|run_results.db [--layers 80] [--md out.md]
 """
@@ -51,10 +53,14 @@ def main():
     is_sample = lambda n: "sample_final" in n                                          # noqa: E731
     last_prefill = max((i for i, r in enumerate(rows) if is_prefill(r["Kernel_Name"])), default=-1)
     samples = [i for i, r in enumerate(rows) if is_sample(r["Kernel_Name"]) and i > last_prefill]
-    if len(samples) < 2:
+    if len(samples) < 3:
         raise SystemExit("trace holds fewer than two decode steps after the last prefill kernel")
-    dec = rows[samples[0] + 1:samples[-1] + 1]
-    steps = len(samples) - 1
+    attn = [sum(1 for j in range(a + 1, b) if "attn_decode" in rows[j]["Kernel_Name"])
+            for a, b in zip(samples, samples[1:])]
+    per_step = a.layers or max(set(attn), key=attn.count)
+    first = next(i for i, n in enumerate(attn) if n == per_step)     # segment samples[i] -> samples[i+1]
+    dec = rows[samples[first] + 1:samples[-1] + 1]
+    steps = len(samples) - 1 - first
     agg = defaultdict(lambda: [0, 0.0])
     for r in dec:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
