@@ -288,9 +288,6 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     epilogue): when the plan splits K, return a `Partial` whose reduce the consumer fuses."""
     if not _gpu(x):
         return ref.linear(x, w, bias, epilogue, out)
-    if (bias is None and epilogue == "none" and x.shape[0] >= _library_min_m()
-            and not torch.cuda.is_current_stream_capturing()):
-        return _linear_library(x, w, epilogue, out)
     if defer and bias is None and epilogue == "none":
         M, N = x.shape[0], w.shape[0]
         if out is None:
@@ -315,35 +312,6 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True) if need else None
     torch.ops.bfly.gemm(x, w, out, bias, epi, ws)
     return out
-
-
-_LIB_MIN_M = None
-
-
-def _library_min_m() -> int:
-    global _LIB_MIN_M
-    if _LIB_MIN_M is None:
-        from ..utils import flags
-
-        _LIB_MIN_M = int(flags.get("BFLY_GEMM_LIBRARY_MIN_M")) or (1 << 62)
-    return _LIB_MIN_M
-
-
-def _linear_library(x, w, epilogue: str, out):
-    """Plain (epilogue-free) prefill GEMM on hipBLASLt (torch.matmul): at M >= 6144 it runs
-    1.50-1.59 PF/s against 1.20-1.30 for gemm_big_kernel on the Llama-3-70B QKV / O / down
-    projections (profiles/r2_gemm_prefill_vs_hipblaslt.log). Fused ops stay on our kernels:
-    the SwiGLU gate/up GEMM (linear(..., epilogue="silu")) always runs gemm_big_kernel with the
-    activation in its epilogue, as do bias epilogues, split-K-deferred decode GEMMs and the MoE
-    grouped GEMMs. (`epilogue="silu"` here = hipBLASLt + our interleaved silu_mul, for A/B.)"""
-    M, N = x.shape[0], w.shape[0]
-    if epilogue == "none":
-        if out is None:
-            out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-        return torch.matmul(x, w.t(), out=out)
-    if epilogue != "silu":
-        raise ValueError(epilogue)
-    return silu_mul(torch.matmul(x, w.t()), out, interleave=SILU_INTERLEAVE)
 
 
 def gemm_plan(M: int, N: int, K: int) -> dict:

@@ -613,151 +613,9 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
                         part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
 }
 
-// ---------------------------------------------------------------------------------------
-// Big-tile GEMM (prefill / large M): 256x256 tile, 8 waves (2 along M x 4 along N, each
-// owning a 128x64 output block = 8x4 MFMA 16x16x32 accumulators), BK = 32, 5-stage ring of
-// glds-staged K-tiles (5 x 32 KiB = the whole 160 KiB LDS, one workgroup per CU). Per K-step a wave
-// issues 12 ds_read_b128 and 32 MFMAs (half the LDS bytes per MFMA of the 128x128 tile), waits
-// for its K-tile with a counted vmcnt (up to three K-tiles stay in flight across the raw barrier),
-// and runs the MFMA cluster at raised priority (cdna_hip_programming.md T3/T4 + setprio).
-// LDS rows are 64 B; the big_swz permutation makes every 16-lane ds_read_b128 group hit 16
-// distinct 16-B slots of the bank line (the DMA writes lane-linearly, so the swizzle is
-// applied on the per-lane SOURCE address). Tiles are walked in GROUP_M super-rows inside each
-// XCD's contiguous range, so the 32 CUs of an XCD share X and W panels in their L2.
-// Measured and dropped (profiles/r2_gemm_big_variants.log, M = 8192): splitting each K-step
-// into two 16-MFMA phases (finer ping-pong, each with half the fragment reads and DMA) -12..-16 %;
-// one static s_setprio 1 for the second wave group instead of the per-cluster flips -12..-17 %.
-// ---------------------------------------------------------------------------------------
-constexpr int kBigThreads = 512;
-constexpr int kBigBK = 32;
-constexpr int kBigStages = 5;   // 5 x 32 KiB = the whole 160 KiB LDS (1-2 % over 4 stages)
+// Prefill tiles are walked in GROUP_M super-rows inside each XCD's contiguous range, so the
+// 32 CUs of an XCD share X and W panels in their L2.
 constexpr int kBigGroupM = 8;
-
-// 64-B rows put 4 rows on one 256-B bank line; the 16-B slot of (row, chunk) is
-// (row % 4) * 4 + (chunk ^ big_swz(row)). ds_read_b128 serves a wave in the lane groups
-// {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): for a fragment read (row = lane & 15,
-// chunk = lane >> 4) each group holds rows {q, q+4, q+8, q+12} of one q = row % 4 with chunks
-// {c, c^1, c^1, c}, and the permutation 0,2,3,1 over (row >> 2) & 3 sends those to 4 distinct
-// slots: conflict-free (a plain XOR with (row >> 2) & 3 is 2-way in every group).
-__device__ __forceinline__ int big_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
-
-__device__ __forceinline__ void big_stage(const bf16* __restrict__ src, long ld, int row0,
-                                          int row_max, int k0, char* lds, int wid, int lane) {
-  // 256 rows x 32 bf16 = 16 KiB = 16 wave-instructions of 16 rows (4 lanes x 16 B per row)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int blk = i * 8 + wid;
-    const int row = blk * 16 + (lane >> 2);
-    const int slot = lane & 3;
-    const int chunk = slot ^ big_swz(row);
-    int gr = row0 + row;
-    gr = gr < row_max ? gr : row_max - 1;
-    const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ bf16x8 big_frag(const char* lds, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(lds + row * 64 + ((chunk ^ big_swz(row)) << 4));
-}
-
-// s_waitcnt vmcnt(n * LPW) for a runtime n in [0, S-2] (vmcnt takes an immediate).
-template <int S, int LPW>
-__device__ __forceinline__ void big_wait(int n) {
-  if (S > 4 && n >= 3) vm_wait<3 * LPW>();
-  else if (n >= 2) vm_wait<2 * LPW>();
-  else if (n == 1) vm_wait<LPW>();
-  else vm_wait<0>();
-}
-
-template <int S>
-__global__ void __launch_bounds__(kBigThreads)
-gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
-                int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                bf16* __restrict__ out, long ldo, float* __restrict__ part) {
-  constexpr int BM = 256, BN = 256, TI = 8, TJ = 4;
-  constexpr int A_BYTES = BM * kBigBK * 2, STAGE_BYTES = 2 * A_BYTES;
-  constexpr int LPW = 4;   // glds per wave per stage (2 for X, 2 for W)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-  const int ntile_all = mtiles * ntiles;
-  const int t = xcd_remap(blockIdx.x, ntile_all);
-  // GROUP_M ordering: consecutive tiles walk GROUP_M row-tiles of one column, then the next
-  const int per_group = kBigGroupM * ntiles;
-  const int g = t / per_group, first_m = g * kBigGroupM;
-  const int gsize = min(mtiles - first_m, kBigGroupM);
-  const int tm = first_m + (t % per_group) % gsize;
-  const int tn = (t % per_group) / gsize;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int ktiles = K / kBigBK;
-  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
-  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
-
-  f32x4 acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // Ping-pong schedule: the two wave groups (wm = 0 / 1, one wave of each per SIMD) run
-  // staggered by one barrier, so one group's MFMA cluster overlaps the other group's
-  // ds_read + glds phase. Barrier b splits group 0 as load(k) | 2k | mfma(k) | 2k+1 and
-  // group 1 as load(k) | 2k+1 | mfma(k) | 2k+2. Each load(k) waits (counted vmcnt) for
-  // stage k+1, reads stage k (waited one step earlier by BOTH groups, before a barrier the
-  // reader has passed), refills the buffer of stage k-1 (read by both groups before barriers
-  // they passed, lgkmcnt(0) retired) with stage k+3, and retires its ds_reads before the
-  // barrier that ends the phase.
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s) {
-    if (kt0 + s < kt1) {
-      char* b = smem + s * STAGE_BYTES;
-      big_stage(X, ldx, m0, M, (kt0 + s) * kBigBK, b, wid, lane);
-      big_stage(W, ldw, n0, N, (kt0 + s) * kBigBK, b + A_BYTES, wid, lane);
-    }
-  }
-  // stage 0 must land; the (issued - 1) later stages may still fly
-  big_wait<S, LPW>(min(S - 1, kt1 - kt0) - 1);
-  __builtin_amdgcn_s_barrier();
-  if (wm == 1) __builtin_amdgcn_s_barrier();
-  int buf = 0;
-  for (int kt = kt0; kt < kt1; ++kt) {
-    // load phase
-    const char* As = smem + buf * STAGE_BYTES;
-    const char* Bs = As + A_BYTES;
-    bf16x8 bfr[TJ], af[TI];
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) bfr[j] = big_frag(Bs, wn * 64 + 16 * j + (lane & 15), lane >> 4);
-#pragma unroll
-    for (int i = 0; i < TI; ++i) af[i] = big_frag(As, wm * 128 + 16 * i + (lane & 15), lane >> 4);
-    if (kt + S - 1 < kt1) {
-      int nbuf = buf + S - 1;
-      if (nbuf >= S) nbuf -= S;
-      char* nb = smem + nbuf * STAGE_BYTES;
-      big_stage(X, ldx, m0, M, (kt + S - 1) * kBigBK, nb, wid, lane);
-      big_stage(W, ldw, n0, N, (kt + S - 1) * kBigBK, nb + A_BYTES, wid, lane);
-    }
-    // stage kt+1 must have landed; stages kt+2 .. kt+S-1 (issued) may still fly
-    big_wait<S, LPW>(min(kt1 - 1, kt + S - 1) - (kt + 1));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // MFMA phase
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);   // C^T tile
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
-    if (++buf == S) buf = 0;
-  }
-  if (wm == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
-  tile_epilogue<TI, TJ>(acc, m0 + wm * 128, n0 + wn * 64, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
-}
 
 // ---------------------------------------------------------------------------------------
 // 8-phase big-tile GEMM (prefill): 256x256 tile, BK = 64, two K-tile LDS buffers (128 KiB),
@@ -781,6 +639,15 @@ gemm_big_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
 // in flight and retires all of K-tile k, which is read from phase 4k+1 on (one phase after the
 // wait, behind a barrier both groups pass: the template's RAW rule). Raw s_barrier only: a
 // __syncthreads() would drain the DMA in flight (§5 "Pipelining across barriers").
+// The prefill kernel for every M > 256 (plan kind 4; EARLY = plan mt 1).
+// Measured and dropped (profiles/r3_gemm_prefill_pmc.md, M = 8192, 70B projections):
+//  - the round-2 5-slot BK-32 ring kernel (8 waves, one 16x16x32 K-step per barrier):
+//    2-7 % slower at M = 8192, within -3..+32 % at M = 256/512;
+//  - one wave per SIMD, 4 waves x 128x128 per wave (hipBLASLt's shape: MT256x256x64, 256
+//    threads): 32x32x16 with a 4/5-slot BK-32 glds ring 1.07-1.10 PF; 16x16x32 with buffer
+//    loads to LDS and the second MFMA half deferred behind the next K-tile's reads 1.13-1.23
+//    PF; the same with BK 64 in a 2-slot ring 1.00-1.12 PF (WAIT_ANY x3: one K-tile of lead
+//    does not cover HBM latency). All at 49-52 % MFMA-busy cycles against hipBLASLt's 87 %.
 // ---------------------------------------------------------------------------------------
 constexpr int kB8Threads = 512;
 constexpr int kB8LdsBytes = 2 * 2 * 256 * 128;   // 2 buffers x (A, B) x 256 rows x 128 B
@@ -1034,25 +901,6 @@ static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr);
 }
 
-static void run_big(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
-                    int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                    hipStream_t stream) {
-  // Measured and dropped (profiles/r2_gemm_big_persistent_ab.log): a persistent tile walk with
-  // the glds ring running across tiles, 13-19 % slower than one workgroup per tile; a 4-stage
-  // (128 KiB) ring, 1-2 % slower than 5.
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<kBigStages>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kBigStages * 2 * 256 * kBigBK * 2);
-    attr = true;
-  }
-  const int tiles = ((M + 255) / 256) * (N / 256);
-  const size_t lds = (size_t)kBigStages * 2 * 256 * kBigBK * 2;
-  dim3 grid(tiles, sk);
-  float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  gemm_big_kernel<kBigStages><<<grid, kBigThreads, lds, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
-}
-
 static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, int early,
                      hipStream_t stream) {
@@ -1163,14 +1011,17 @@ static GemmPlan plan_gemm_heuristic(int M, int N, int K) {
     p.sk = sk;
     return p;
   }
-  if (M > 256 && N % 256 == 0 && K % kBigBK == 0) {
-    // prefill / large batch: 256x256 ping-pong tile (~1.27 PF at M = 8192 on MI355X vs ~0.9 for
-    // the 128x128 tile); split K only when the tile grid cannot fill the 256 CUs
-    p.kind = 2;
+  if (M > 256 && N % 256 == 0 && K % 64 == 0) {
+    // prefill / large batch: 256x256 8-phase tile with early LDS release (gemm_big8_kernel
+    // <EARLY>: 1.36-1.39 PF at M = 8192 on the 70B projections, +2-7 % over the 5-slot ring
+    // kernel; profiles/r3_gemm_prefill_pmc.md); split K only when the tile grid cannot fill
+    // the 256 CUs
+    p.kind = 4;
+    p.mt = 1;
     p.bm = p.bn = 256;
     const int tiles = ((M + 255) / 256) * (N / 256);
     int sk = 1;
-    while (tiles * sk < 256 && K / kBigBK >= sk * 2 * 8 && sk < 8) sk *= 2;
+    while (tiles * sk < 256 && K / 64 >= sk * 2 * 8 && sk < 8) sk *= 2;
     p.sk = sk;
     return p;
   }
@@ -1204,11 +1055,7 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                     hipStream_t stream, bool dry = false, bool defer = false) {
-  if (p.kind == 2) {
-    if (N % 256 != 0 || K % kBigBK != 0) return -1;
-    if (p.sk > 1 && (long)((M + 255) / 256) * (N / 256) > kSplitCounters) return -1;
-    if (!dry) run_big(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
-  } else if (p.kind == 4) {
+  if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
     if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, p.mt, stream);   // mt: EARLY
@@ -1268,7 +1115,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind == 2 || p.kind == 4)) {   // big kernels: no fixup path
+  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind == 4)) {   // big kernels: no fixup path
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);

@@ -281,24 +281,25 @@ def test_moe_route_and_gate_scale():
     _close(h, h2, 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(600, 512, 1024), (256, 768, 160), (77, 256, 96), (1000, 1280, 4096),
-                                   (300, 512, 64), (520, 512, 32)])
+@pytest.mark.parametrize("M,N,K", [(600, 512, 1024), (256, 768, 192), (77, 256, 128), (1000, 1280, 4096),
+                                   (300, 512, 256), (520, 512, 128)])
 @pytest.mark.parametrize("epi", ["none", "bias", "silu"])
-def test_gemm_big_tile(M, N, K, epi, kind=2):
-    """256x256 8-wave kernel (plan kind 2): ragged M, K-tile counts below / above the ring
-    depth, split-K, all epilogues, asymmetric operands."""
+def test_gemm_big_tile(M, N, K, epi):
+    """256x256 8-phase prefill kernel (plan kind 4, EARLY = plan mt in {0, 1}): ragged M,
+    the minimum of two 64-deep K-tiles per split, split-K, all epilogues, asymmetric operands."""
     x = _bf(M, K, seed=60)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=61)
     b = _bf(N, seed=62) if epi == "bias" else None
     nout = N // 2 if epi == "silu" else N
     want = ref.linear(x, w, b, "silu" if epi == "silu" else "none")
-    for sk in (1, 2, 3):
-        if K // 32 < sk:
-            continue
-        out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-        ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
-        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
-        _close(out, want, 2e-2, 2e-2)
+    for early in (0, 1):
+        for sk in (1, 2, 3):
+            if K // 64 < 2 * sk:
+                continue
+            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+            ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
+            torch.ops.bfly.gemm_with_plan(x, w, out, [4, early, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+            _close(out, want, 2e-2, 2e-2)
 
 
 TILE_CFGS = [(16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1), (64, 128, 1), (64, 128, 2),
@@ -628,19 +629,17 @@ def test_attn_prefill_long_vs_fp32(lens, Hq, Hkv, heads):
         assert err < 3e-2 and rel < 1e-2, (h, err, rel)
 
 
-@pytest.mark.parametrize("epi", ["none", "silu"])
-def test_linear_large_m_library_path(epi, monkeypatch):
-    """Plain prefill GEMMs at M >= BFLY_GEMM_LIBRARY_MIN_M go to hipBLASLt (the A/B form of the
-    SwiGLU one: hipBLASLt + our interleaved silu_mul); same result as the fp32 reference and as
-    our own big-tile kernel, which linear() keeps for the fused SwiGLU GEMM."""
-    monkeypatch.setattr(ops, "_LIB_MIN_M", 4096)
-    x, w = _bf(4096, 512, seed=90), _bf(1024, 512, seed=91, scale=0.05)
-    lib = ops._linear_library(x, w, epi, None)
-    monkeypatch.setattr(ops, "_LIB_MIN_M", 1 << 62)
-    own = ops.linear(x, w, epilogue=epi)
-    want = ref.linear(x.float(), w.float(), epilogue=epi)
-    _close(lib, want, 3e-2, 3e-2)
-    _close(lib, own, 3e-2, 3e-2)
+@pytest.mark.parametrize("epi", ["none", "silu", "bias"])
+def test_linear_large_m_prefill_path(epi):
+    """Prefill-sized GEMMs (M > 256, an M tail) run the 256x256 8-phase kernel for every
+    epilogue; there is no library fallback left in linear()."""
+    assert ops.gemm_plan(4100, 1024, 512)["kind"] == "big8"
+    x, w = _bf(4100, 512, seed=90), _bf(1024, 512, seed=91, scale=0.05)
+    b = _bf(1024, seed=92) if epi == "bias" else None
+    own = ops.linear(x, w, bias=b, epilogue="none" if epi == "bias" else epi)
+    want = ref.linear(x.float(), w.float(), b.float() if b is not None else None,
+                      epilogue="none" if epi == "bias" else epi)
+    _close(own, want, 3e-2, 3e-2)
 
 
 def test_sample_check_finite():

@@ -93,7 +93,7 @@ def main():
                 nout = N // 2 if epi == "silu" else N
                 out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
                 plan = ops.gemm_plan(M, N, K)
-                auto = [("skinny", "tile", "big", "dec").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
+                auto = [("skinny", "tile", "big", "dec", "big8").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
                         plan["bn"], plan["splitk"]]
                 t = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, Ws[i % copies], out, auto, ops.EPILOGUES[epi], ws),
                            tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": auto, "auto": True})
@@ -133,8 +133,8 @@ def main():
                                 cands.append([3, sw, nwm * nwn, nwm, bm, bn, sk])
                     if M >= 128 and N % 256 == 0:
                         for sk in (1, 2, 4):
-                            if K // 32 >= sk * 8:
-                                cands.append([2, 0, 0, 0, 256, 256, sk])
+                            if K // 64 >= sk * 4:
+                                cands.append([4, 1, 0, 0, 256, 256, sk])
                     for pl in cands:
                         try:
                             tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(

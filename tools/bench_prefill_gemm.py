@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Prefill GEMM A/B on the Llama-3-70B projections: gemm_big_kernel (plan kind 2, BK 32 ring)
-vs gemm_big8_kernel (kind 4, 8-phase BK 64; big8e = its early-release variant, plan mt = 1)
-vs torch.matmul (hipBLASLt, yardstick only).
+"""Prefill GEMM A/B on the Llama-3-70B projections: gemm_big8_kernel (plan kind 4, 8-phase
+BK 64; big8e = its early-release variant, plan mt = 1, the default) vs torch.matmul (hipBLASLt,
+yardstick only; not used by the framework). The round-3 variants that lost (the BK-32 ring
+kernel, three one-wave-per-SIMD kernels) are recorded in profiles/r3_gemm_prefill_pmc.md.
 
 Random uniform [-1, 1) operands (cdna_hip_programming.md §5.4 rule 25: zero-filled data clocks
 higher), interleaved rounds in one process (rule 24), median and min per variant. First checks
@@ -32,20 +33,20 @@ def uni(*shape):
 def check(ws):
     """kind 4 vs the fp32 reference: M tails, split-K, bias and SiLU epilogues."""
     bad = []
-    for M, N, K, epi, sk in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
+    for kind, M, N, K, epi, sk in [(k,) + c for k in (4,) for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
                              (1024, 1024, 2048, "silu", 1), (512, 1280, 4096, "none", 4), (777, 512, 1024, "bias", 1),
-                             (2048, 2560, 8192, "none", 2)]:
+                             (2048, 2560, 8192, "none", 2)]]:
         x = uni(M, K) * 0.5
         w = uni(N, K) * 0.05
         b = uni(N) if epi == "bias" else None
         nout = N // 2 if epi == "silu" else N
         out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
-        torch.ops.bfly.gemm_with_plan(x, w, out, [4, 1, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 1, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
         want = ref.linear(x.float(), w.float(), b.float() if b is not None else None,
                           "silu" if epi == "silu" else "none")
         err = ((out.float() - want).abs() / (want.abs() + 2e-2)).max().item()
         rel = ((out.float() - want).norm() / want.norm()).item()
-        row = {"M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
+        row = {"kind": kind, "M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
         print(json.dumps({"check": row}), flush=True)
         if rel > 1e-2:
             bad.append(row)
@@ -58,6 +59,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--check-only", action="store_true")
+    ap.add_argument("--sks", default="1", help="split-K factors tried per variant (best reported)")
+    ap.add_argument("--variants", default="", help="comma list (default: all)")
     a = ap.parse_args()
     assert ops.load_library(), ops._load_error
     ws = torch.zeros(256 << 20, dtype=torch.float32, device="cuda")
@@ -71,12 +74,19 @@ def main():
             nout = N // 2 if epi == "silu" else N
             out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
             e = ops.EPILOGUES[epi]
-            variants = {
-                "big": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [2, 0, 0, 0, 256, 256, 1], e, ws),
+            variants = {}
+            for sk in [int(v) for v in a.sks.split(",")]:
+                if (K // 64) < 2 * sk:
+                    continue
+                sfx = "" if a.sks == "1" else f"/sk{sk}"
+                variants["big8e" + sfx] = lambda sk=sk: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 1, 0, 0, 256, 256, sk], e, ws)
+            variants.update({
                 "big8": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, 1], e, ws),
-                "big8e": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 1, 0, 0, 256, 256, 1], e, ws),
-            }
-            if epi == "none":
+            })
+            if a.variants:
+                keep = a.variants.split(",")
+                variants = {k: v for k, v in variants.items() if k.split("/")[0] in keep}
+            if epi == "none" and (not a.variants or "hipblaslt" in a.variants):
                 variants["hipblaslt"] = lambda: torch.matmul(x, w.t(), out=out)
             times = {k: [] for k in variants}
             for fn in variants.values():     # warm-up

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals for the decode phase and per
-decode step.
+"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals for the prefill window (first to
+last prefill kernel), for the decode phase and per decode step.
 
 The decode window is cut from the trace itself. Every decode step samples exactly once
 (sample_final_kernel) after one forward pass; the segments between consecutive sampling
@@ -55,6 +55,22 @@ def main():
     samples = [i for i, r in enumerate(rows) if is_sample(r["Kernel_Name"]) and i > last_prefill]
     if len(samples) < 3:
         raise SystemExit("trace holds fewer than two decode steps after the last prefill kernel")
+    first_prefill = min((i for i, r in enumerate(rows) if is_prefill(r["Kernel_Name"])), default=-1)
+    pre_lines = []
+    if first_prefill >= 0:
+        pre = rows[first_prefill:last_prefill + 1]
+        pagg = defaultdict(lambda: [0, 0.0])
+        for r in pre:
+            pagg[short(r["Kernel_Name"])][0] += 1
+            pagg[short(r["Kernel_Name"])][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        ptot = sum(v[1] for v in pagg.values())
+        pspan = (int(pre[-1]["End_Timestamp"]) - int(pre[0]["Start_Timestamp"])) / 1e3
+        pre_lines = [f"prefill window (first to last prefill kernel; mixed steps include their decode rows): "
+                     f"{len(pre)} dispatches, kernel time {ptot / 1e3:.2f} ms, wall span {pspan / 1e3:.2f} ms",
+                     "", "| kernel | calls | total ms | % | avg us |", "|---|---|---|---|---|"]
+        for k, (c, t) in sorted(pagg.items(), key=lambda kv: -kv[1][1])[:15]:
+            pre_lines.append(f"| {k} | {c} | {t / 1e3:.3f} | {100 * t / ptot:.1f} | {t / c:.1f} |")
+        pre_lines += ["", ""]
     attn = [sum(1 for j in range(a + 1, b) if "attn_decode" in rows[j]["Kernel_Name"])
             for a, b in zip(samples, samples[1:])]
     per_step = a.layers or max(set(attn), key=attn.count)
@@ -80,7 +96,7 @@ def main():
     if a.layers:
         n_attn = sum(c for k, (c, _) in agg.items() if "attn_decode" in k)
         lines.append(f"cross-check: {n_attn} decode-attention dispatches / {a.layers} layers = {n_attn / a.layers:.2f} steps")
-    text = "\n".join(lines)
+    text = "\n".join(pre_lines + lines)
     print(text)
     if a.md:
         with open(a.md, "w") as f:
