@@ -175,6 +175,12 @@ class LLMEngine:
             buckets.append(self.scheduler.group_batch)    # a full group replays one graph
         self.runner = ModelRunner(self.model, self.kv, engine_cfg.max_seq_len, engine_cfg.use_graphs,
                                   buckets, max_batch=engine_cfg.max_batch)
+        # byte-minimal EP dispatch for the decode MoE layer (collective over the EP group, so
+        # every EP rank sets it up here, eagerly, before any graph capture)
+        self.ep_ipc = False
+        if mesh.ep > 1 and cfg.is_moe and flags.get("BFLY_EP_IPC"):
+            self.ep_ipc = self.comm.enable_ep_ipc(max(self.runner.buckets[-1], engine_cfg.max_batch),
+                                                  cfg.hidden_size, cfg.experts_per_token)
         if self._native_pp:
             self.runner.set_pipeline_io(recv_fn=None if coord.pp == 0 else self.comm.recv_native,
                                         sends=coord.pp < mesh.pp - 1)

@@ -572,8 +572,9 @@ class TransformerLM:
         destination: a token goes once to each rank owning one of its top-k experts, at the
         position given by a running count over the tokens bound there, so no capacity can
         overflow and no token is dropped. Shapes are static and nothing waits on the host,
-        so the layer replays inside the decode hipGraph. Packing (ep_pack_kernel: positions,
-        row copies, metadata) and the return combine (ep_combine_kernel) are one kernel each.
+        so the layer replays inside the decode hipGraph. The exchange is comm.ep_dispatch /
+        comm.ep_combine: byte-minimal over peer IPC buffers when enabled (parallel/ep_ipc.py:
+        only routed rows travel, once each way), else ep_pack + all-to-all + ep_combine.
         The receiver computes ONLY routed rows (moe_align + grouped GEMMs skip padding, whose
         expert ids are -1); a second all-to-all brings each rank's weighted partial sums
         back, summed in f32 at the source.
@@ -581,15 +582,10 @@ class TransformerLM:
         of every local expert to the rows actually routed to it."""
         d = self.dims
         k = topk_ids.shape[1]
-        El, ep = d.experts, self.ep
-        send, meta, slot = ops.ep_pack(x, topk_ids, topk_w, slots, El, ep, cap)
-        xr = self.comm.all_to_all(send, "ep")
-        mr = self.comm.all_to_all(meta, "ep")
-        ids_r = mr[:, :k].contiguous().view(torch.int32)     # int32 bits travel in the f32 block
-        yr = ops.moe_sparse_ffn(xr, ids_r, mr[:, k:].contiguous(),
-                                self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"], d.expert0, El, d.ffn,
-                                expected_slots=cap * k)     # on average T x k routed slots per rank
-        return ops.ep_combine(self.comm.all_to_all(yr, "ep"), slot)
+        r = self.comm.ep_dispatch(x, topk_ids, topk_w, slots, d.experts, cap)
+        yr = ops.moe_sparse_ffn(r.x, r.ids, r.w, self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"], d.expert0,
+                                d.experts, d.ffn, expected_slots=cap * k)   # on average T x k routed slots per rank
+        return self.comm.ep_combine(yr, r)
 
     # ------------------------------------------------------------------------------------
     # KV cache layout helpers

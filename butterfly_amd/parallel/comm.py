@@ -67,6 +67,7 @@ class Communicator:
         self.rank = rank
         self.groups = groups
         self.custom_ar = None            # optional CustomAllReduce for the tp group
+        self.ep_ipc = None               # optional byte-minimal EP dispatch (parallel/ep_ipc.py)
         self.stats = {"all_reduce_bytes": 0, "send_bytes": 0, "recv_bytes": 0, "calls": 0}
         # native RCCL pipeline edges (parallel/rccl.pp_edges): to the next / from the previous
         # stage; sends run on their own stream so a send never blocks the compute stream
@@ -183,6 +184,48 @@ class Communicator:
             car.close()
         return self.custom_ar is not None
 
+    def enable_ep_ipc(self, capmax: int, hidden: int, top_k: int) -> bool:
+        """Set up the byte-minimal IPC EP dispatch for the decode MoE layer (collective over the
+        EP group; eager, before any graph capture). True when it passed its self-test."""
+        g = self.groups["ep"]
+        if g.size not in (2, 4, 8) or not torch.cuda.is_available() or g.pg is None:
+            return False
+        from .ep_ipc import EpIpc
+
+        ipc = EpIpc(g.ranks, g.rank_in_group, g.pg, capmax, hidden, top_k)
+        self.ep_ipc = ipc if ipc.ok else None
+        if not ipc.ok:
+            ipc.close()
+        return self.ep_ipc is not None
+
+    def ep_dispatch(self, x: torch.Tensor, ids: torch.Tensor, w: torch.Tensor, slots, experts_per_rank: int,
+                    cap: int):
+        """Fixed-capacity EP token dispatch (decode): every token goes once to each EP rank
+        owning one of its top-k experts. Returns an ep_ipc.EpRoute: this rank's routed rows,
+        their local expert ids / weights, and the slots to combine the returned rows. Byte-
+        minimal IPC path when enabled, else ep_pack + two all-to-alls (bitwise the same)."""
+        from .. import ops
+        from .ep_ipc import EpRoute
+
+        ipc = self.ep_ipc
+        if ipc is not None and ipc.fits(x, ids, cap):
+            return ipc.dispatch(x, ids, w, slots, experts_per_rank, cap)
+        k = ids.shape[1]
+        send, meta, slot = ops.ep_pack(x, ids, w, slots, experts_per_rank, self.size("ep"), cap)
+        xr = self.all_to_all(send, "ep")
+        mr = self.all_to_all(meta, "ep")
+        return EpRoute(xr, mr[:, :k].contiguous().view(torch.int32), mr[:, k:].contiguous(), slot,
+                       x.shape[0], "a2a")
+
+    def ep_combine(self, y: torch.Tensor, route) -> torch.Tensor:
+        """Return every routed row's expert output to its source and sum each token's rows (f32,
+        fixed rank order)."""
+        from .. import ops
+
+        if route.path != "a2a":
+            return self.ep_ipc.combine(y, route)
+        return ops.ep_combine(self.all_to_all(y, "ep"), route.slot)
+
     def enable_native_rccl(self) -> dict:
         """Create the rank's native RCCL communicators (collective over the world): the world
         one from a broadcast unique id, then one ncclCommSplit per mesh axis. Returns
@@ -224,6 +267,8 @@ class Communicator:
         asynchronous error. Cheap: one 4-byte device read plus host queries."""
         if self.custom_ar is not None and self.custom_ar.error():
             raise RuntimeError(f"rank {self.rank}: custom all-reduce peer wait timed out")
+        if self.ep_ipc is not None and self.ep_ipc.error():
+            raise RuntimeError(f"rank {self.rank}: EP IPC dispatch peer wait timed out")
         for name, g in self.groups.items():
             if g is not None and g.native is not None:
                 err = g.native.async_error()

@@ -270,5 +270,14 @@ class FakeComm(Communicator):
         # the engine's pre-post ordering (the matching send happened earlier in that tick)
         return True
 
+    def enable_ep_ipc(self, capmax: int, hidden: int, top_k: int) -> bool:
+        """The IPC dispatch's protocol in shared CPU memory (parallel/ep_ipc.EpLoopback)."""
+        if self.groups["ep"].size not in (2, 4, 8):
+            return False
+        from .ep_ipc import EpLoopback
+
+        self.ep_ipc = EpLoopback(self, capmax, hidden, top_k)
+        return True
+
     def check_health(self):
         return None

@@ -42,8 +42,6 @@ define("BFLY_CUSTOM_AR_2SHOT_BYTES", 512 << 10, int, "IPC all-reduces of at leas
 define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0: heuristic plans only; read by the kernel library)")
 define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
-define("BFLY_GEMM_LIBRARY_MIN_M", 6144, int, "plain (epilogue-free) GEMMs with at least this many rows (prefill "
-       "QKV / O / down) run on hipBLASLt; fused GEMMs (SwiGLU, bias) always run the HIP kernels; 0 = never")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
@@ -56,6 +54,8 @@ define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on p
 define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped expert GEMMs instead of the dense path")
 define("BFLY_EP_DECODE_A2A", True, _bool, "EP MoE on decode (and idle) steps: fixed-capacity all-to-all dispatch with "
        "routed-rows-only expert GEMMs, graph-capturable (0: all-gather + dense local experts + reduce-scatter)")
+define("BFLY_EP_IPC", True, _bool, "EP MoE on decode: byte-minimal dispatch / return over peer IPC buffers "
+       "(only routed rows travel; self-tested at start-up, else the fixed-capacity all-to-all)")
 define("BFLY_EP_ALLTOALL", True, _bool, "EP MoE on prefill steps: dispatch tokens by all-to-all (else all-gather / reduce-scatter)")
 define("BFLY_PP_ASYNC", True, _bool, "pipeline parallelism: keep pp decode groups in flight across steps "
        "(one group per stage per tick, no fill/drain bubble) instead of per-step microbatching")

@@ -736,6 +736,86 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tenso
   TORCH_CHECK(rc == 0, "custom_all_reduce: launch rejected (", rc, ")");
 }
 
+// ---- byte-minimal EP dispatch over peer IPC buffers (allocated with car_alloc) ------------
+static bfly::ArPeers ep_peers(at::IntArrayRef bases) {
+  TORCH_CHECK(bases.size() == 2 || bases.size() == 4 || bases.size() == 8, "ep_ipc: 2, 4 or 8 ranks");
+  bfly::ArPeers peers{};
+  for (size_t i = 0; i < bases.size(); ++i) {
+    TORCH_CHECK(bases[i] != 0, "ep_ipc: null peer buffer");
+    peers.base[i] = reinterpret_cast<char*>(bases[i]);
+  }
+  return peers;
+}
+
+std::vector<int64_t> ep_ipc_layout(int64_t ep, int64_t capmax, int64_t H, int64_t K) {
+  const bfly::EpLayout L = bfly::ep_ipc_layout((int)ep, (int)capmax, (int)H, (int)K);
+  return {L.x, L.ids, L.w, L.back, L.total};
+}
+
+// a [rows, cols] view of a region of this rank's IPC buffer (no ownership: the buffer lives as
+// long as the EpIpc object that allocated it)
+Tensor ep_ipc_view(int64_t ptr, int64_t offset, int64_t rows, int64_t cols, int64_t dtype, int64_t device) {
+  const at::ScalarType st = dtype == 0 ? at::kBFloat16 : dtype == 1 ? at::kInt : at::kFloat;
+  return at::from_blob(reinterpret_cast<char*>(ptr) + offset, {rows, cols},
+                       at::TensorOptions().dtype(st).device(at::kCUDA, (int)device));
+}
+
+void ep_ipc_dispatch(const Tensor& x, const Tensor& ids, const Tensor& w, const c10::optional<Tensor>& slots,
+                     int64_t experts_per_rank, int64_t capmax, at::IntArrayRef bases, int64_t rank, Tensor& slot) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_I32(ids); CHECK_I32(slot);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "ep_ipc_dispatch: x [T, H] contiguous");
+  const int T = x.size(0), H = x.size(1), ep = (int)bases.size();
+  TORCH_CHECK(ids.dim() == 2 && ids.size(0) == T && ids.is_contiguous(), "ep_ipc_dispatch: ids [T, k]");
+  const int K = ids.size(1);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == (long)T * K, "ep_ipc_dispatch: w");
+  TORCH_CHECK(capmax >= T, "ep_ipc_dispatch: more tokens than the buffer's capacity");
+  TORCH_CHECK(slot.is_contiguous() && slot.numel() == (long)T * ep, "ep_ipc_dispatch: slot [T, ep]");
+  const int* sp = nullptr;
+  if (slots.has_value()) {
+    CHECK_I32(*slots);
+    TORCH_CHECK(slots->numel() == T, "ep_ipc_dispatch: slots [T]");
+    sp = slots->data_ptr<int>();
+  }
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_ep_ipc_dispatch(bf(x), ids.data_ptr<int>(), w.data_ptr<float>(), sp, T, K, H,
+                                              (int)experts_per_rank, ep, (int)capmax, ep_peers(bases), (int)rank,
+                                              slot.data_ptr<int>(), cur_stream());
+  TORCH_CHECK(rc == 0, "ep_ipc_dispatch: rejected (", rc, ")");
+}
+
+void ep_ipc_wait(const Tensor& like, at::IntArrayRef bases, int64_t rank) {
+  CHECK_GPU(like);
+  c10::DeviceGuard g(like.device());
+  const int rc = bfly::launch_ep_ipc_wait(ep_peers(bases), (int)bases.size(), (int)rank, cur_stream());
+  TORCH_CHECK(rc == 0, "ep_ipc_wait: rejected (", rc, ")");
+}
+
+void ep_ipc_return(const Tensor& y, int64_t K, int64_t capmax, at::IntArrayRef bases, int64_t rank) {
+  CHECK_GPU(y); CHECK_BF16(y);
+  const int ep = (int)bases.size();
+  TORCH_CHECK(y.dim() == 2 && y.is_contiguous() && y.size(0) == ep * capmax, "ep_ipc_return: y [ep*capmax, H]");
+  c10::DeviceGuard g(y.device());
+  const int rc = bfly::launch_ep_ipc_return(bf(y), y.size(1), (int)K, ep, (int)capmax, ep_peers(bases), (int)rank,
+                                            cur_stream());
+  TORCH_CHECK(rc == 0, "ep_ipc_return: rejected (", rc, ")");
+}
+
+void ep_ipc_combine(const Tensor& slot, int64_t K, int64_t capmax, at::IntArrayRef bases, int64_t rank, Tensor& out) {
+  CHECK_GPU(out); CHECK_BF16(out); CHECK_I32(slot);
+  const int T = out.size(0), ep = (int)bases.size();
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && slot.numel() == (long)T * ep, "ep_ipc_combine: shapes");
+  c10::DeviceGuard g(out.device());
+  const int rc = bfly::launch_ep_ipc_combine(slot.data_ptr<int>(), T, out.size(1), (int)K, ep, (int)capmax,
+                                             ep_peers(bases), (int)rank, bf(out), cur_stream());
+  TORCH_CHECK(rc == 0, "ep_ipc_combine: rejected (", rc, ")");
+}
+
+std::vector<int64_t> ep_ipc_stats(int64_t p) {
+  long long v[2] = {0, 0};
+  TORCH_CHECK(bfly::ep_ipc_stats(reinterpret_cast<const void*>(p), v) == 0, "ep_ipc_stats: hipMemcpy failed");
+  return {v[0], v[1]};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(bfly, m) {
@@ -795,6 +875,15 @@ TORCH_LIBRARY(bfly, m) {
   m.def("car_buffer_bytes(int cap) -> int", [](int64_t cap) -> int64_t { return bfly::car_buffer_bytes(cap); });
   m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, Tensor(b!)? residual, Tensor? w, float eps, "
         "int[] bases, int rank, int cap, Tensor? slabs=None, bool two_shot=False) -> ()");
+  m.def("ep_ipc_layout(int ep, int capmax, int H, int K) -> int[]", &ep_ipc_layout);
+  m.def("ep_ipc_view(int ptr, int offset, int rows, int cols, int dtype, int device) -> Tensor", &ep_ipc_view);
+  m.def("ep_ipc_dispatch(Tensor x, Tensor ids, Tensor w, Tensor? slots, int experts_per_rank, int capmax, "
+        "int[] bases, int rank, Tensor(a!) slot) -> ()");
+  m.def("ep_ipc_wait(Tensor like, int[] bases, int rank) -> ()");
+  m.def("ep_ipc_return(Tensor y, int k, int capmax, int[] bases, int rank) -> ()");
+  m.def("ep_ipc_combine(Tensor slot, int k, int capmax, int[] bases, int rank, Tensor(a!) out) -> ()");
+  m.def("ep_ipc_stats(int ptr) -> int[]", &ep_ipc_stats);
+  m.def("ep_ipc_error(int ptr) -> int", [](int64_t p) -> int64_t { return bfly::ep_ipc_error(reinterpret_cast<const void*>(p)); });
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
         "bool causal, Tensor(a!) out, Tensor? cu_seqlens_k=None, Tensor(b!)? lse=None) -> ()");
   m.def("attn_lse_merge(Tensor(a!) acc_o, Tensor(b!) acc_lse, Tensor o, Tensor lse) -> ()");
@@ -833,4 +922,8 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("moe_combine_slabs", &moe_combine_slabs);
   m.impl("ep_pack", &ep_pack);
   m.impl("ep_combine", &ep_combine);
+  m.impl("ep_ipc_dispatch", &ep_ipc_dispatch);
+  m.impl("ep_ipc_wait", &ep_ipc_wait);
+  m.impl("ep_ipc_return", &ep_ipc_return);
+  m.impl("ep_ipc_combine", &ep_ipc_combine);
 }

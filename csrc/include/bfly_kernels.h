@@ -124,6 +124,21 @@ void car_ipc_close(void* p);
 int car_clear_error(void* base);
 int car_error(const void* base);
 
+// ep_ipc.hip — byte-minimal EP dispatch / return over peer IPC buffers (decode MoE)
+constexpr long kEpHeaderBytes = 65536;
+struct EpLayout { long x, ids, w, back, total; };   // byte offsets in a rank's buffer
+EpLayout ep_ipc_layout(int ep, int capmax, int H, int K);
+int launch_ep_ipc_dispatch(const bf16* x, const int* ids, const float* w, const int* slots, int T, int K,
+                           int H, int El, int ep, int capmax, const ArPeers& peers, int rank, int* slot_out,
+                           hipStream_t stream);
+int launch_ep_ipc_wait(const ArPeers& peers, int ep, int rank, hipStream_t stream);
+int launch_ep_ipc_return(const bf16* y, int H, int K, int ep, int capmax, const ArPeers& peers, int rank,
+                         hipStream_t stream);
+int launch_ep_ipc_combine(const int* slot, int T, int H, int K, int ep, int capmax, const ArPeers& peers,
+                          int rank, bf16* out, hipStream_t stream);
+int ep_ipc_stats(const void* base, long long* out2);
+int ep_ipc_error(const void* base);
+
 // moe.hip
 int launch_moe_route(const bf16* x, long x_stride, const bf16* wr, int T, int H, int E, int K,
                      float* gates, int* topk_ids, float* topk_w, hipStream_t stream);
