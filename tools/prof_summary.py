@@ -21,7 +21,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
+    n = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))
     n = n.replace("void ", "")
     m = re.match(r"_ZN4bfly\d+(\w+?)I", n)
     if m:
