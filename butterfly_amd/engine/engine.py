@@ -37,6 +37,8 @@ from ..config import EngineConfig, ModelConfig
 from ..models import Shard, build_model
 from ..parallel.comm import Communicator, NativeWork
 from ..parallel.mesh import Mesh
+from ..partition.plan import PartitionPlan
+from ..partition.schedule import exec_program
 from ..utils import flags, trace
 from ..utils.health import FaultInjector, StepWatchdog
 from ..utils.metrics import Metrics
@@ -97,6 +99,12 @@ class LLMEngine:
         if mesh.ep > 1 and mesh.pp > 1:
             raise ValueError("expert parallelism with pipeline stages is not a supported layout "
                              "(EP collectives span DP replicas of one stage)")
+        # the rank's step program (partition/schedule.py) drives the stage execution below:
+        # boundary receives / sends, stage runs, sampling and the id broadcast, with their peers
+        self.plan = PartitionPlan(model=cfg, n_gpus=mesh.world_size, dp=mesh.dp, tp=mesh.tp, pp=mesh.pp,
+                                  ep=mesh.ep, stages=[tuple(x) for x in stage_layers],
+                                  placement=list(range(mesh.world_size)))
+        self._exec_ops: dict = {}
         a, b = stage_layers[coord.pp]
         shard = Shard(tp_rank=coord.tp, tp_size=mesh.tp, layer_start=a, layer_end=b,
                       ep_rank=coord.dp if mesh.ep > 1 else 0, ep_size=mesh.ep)
@@ -454,57 +462,103 @@ class LLMEngine:
         self.metrics.observe_step(kind, len(rids), dt)
         return StepOutput(kind, rids, new, finished, dt)
 
+    def _ops(self, microbatches: int, native_pp: bool = False) -> list:
+        """Engine-level instructions of this rank's step program (schedule.exec_program)."""
+        key = (microbatches, native_pp)
+        ops = self._exec_ops.get(key)
+        if ops is None:
+            ops = self._exec_ops[key] = exec_program(self.plan, self.rank, microbatches, native_pp)
+        return ops
+
+    @staticmethod
+    def _execute(ops, recv, run, send, sample, broadcast=None) -> None:
+        """Interpret a step program: each engine-level instruction calls its hook with the
+        instruction (peers, stream, microbatch) — the order and the peers come from the program."""
+        h: dict = {}
+        out: dict = {}
+        for ins in ops:
+            e = ins.exec
+            if e == "recv":
+                h[ins.mb] = recv(ins)
+            elif e == "stage":
+                out[ins.mb] = run(ins.mb, h.get(ins.mb))
+            elif e == "send":
+                send(ins, out[ins.mb])
+            elif e == "sample":
+                sample(ins.mb, out[ins.mb])
+            elif e == "broadcast" and broadcast is not None:
+                broadcast(ins)
+
     def _run_stages(self, fn, T: int, R: int, rids) -> torch.Tensor:
         """Run this rank's pipeline stage on one batch; return sampled ids [R] (int32, on
-        every rank of the replica)."""
-        m = self.model
+        every rank of the replica). pp > 1: recv residual stream -> stage -> send, or sample
+        on the last stage; then the ids broadcast — as the step program lists them."""
         if self.mesh.pp == 1:
             return self._sample(fn(None), rids)
-        # pipeline: recv residual stream -> compute -> send; last stage samples + broadcasts
-        h = None
-        if not self.pp_first:
+        m, res = self.model, {}
+
+        def recv(ins):
             h = torch.empty(T, self.cfg.hidden_size, dtype=m.dtype, device=self.device)
-            self.comm.recv(h, self.mesh.prev_stage(self.rank))
-        out = fn(h)
-        ids = torch.empty(R, dtype=torch.int32, device=self.device)
-        if not self.pp_last:
-            self.comm.send(self._maybe_poison(out), self.mesh.next_stage(self.rank))
-        else:
-            ids = self._sample(out, rids)
-        self.comm.broadcast_(ids, src_in_group=self.mesh.pp - 1, group="pp")
-        return ids
+            self.comm.recv(h, ins.group[0])
+            return h
+
+        def send(ins, out):
+            self.comm.send(self._maybe_poison(out), ins.group[1])
+
+        def sample(mb, out):
+            res["ids"] = self._sample(out, rids)
+
+        def broadcast(ins):
+            ids = res.get("ids")
+            if ids is None:
+                ids = torch.empty(R, dtype=torch.int32, device=self.device)
+            self.comm.broadcast_(ids, src_in_group=len(ins.group) - 1, group="pp")
+            res["ids"] = ids
+
+        self._execute(self._ops(1), recv, lambda mb, h: fn(h), send, sample, broadcast)
+        return res["ids"]
 
     def _pipeline_decode(self, inp: dict, rids) -> torch.Tensor:
         """Synchronous pipeline decode (BFLY_PP_ASYNC=0, and EP layouts): the batch is cut
         into M = pp microbatches; stage s
         works on microbatch m while stage s+1 works on m-1 (RCCL send/recv of the residual
         stream over xGMI is stream-ordered, so the overlap needs no host synchronisation).
-        Each microbatch replays its own hipGraph bucket."""
+        Each microbatch replays its own hipGraph bucket. The order of receives, stage runs,
+        sends and the final broadcast is the step program's (M microbatches)."""
         B = len(rids)
         M = max(1, min(self.mesh.pp, B))
         bounds = [B * i // M for i in range(M + 1)]
         H = self.cfg.hidden_size
-        reqs, outs = [], []
-        for i in range(M):
-            a, b = bounds[i], bounds[i + 1]
-            sub = {k: v[a:b] for k, v in inp.items()}
-            h = None
-            if not self.pp_first:
-                h = torch.empty(b - a, H, dtype=self.model.dtype, device=self.device)
-                self.comm.recv(h, self.mesh.prev_stage(self.rank))
-            out = self.runner.run_decode(sub, h)
-            if not self.pp_last:
-                # copy out of the graph's static output before the next replay can reuse it
-                snd = self._maybe_poison(out.clone())
-                reqs.append(self.comm.isend(snd, self.mesh.next_stage(self.rank)))
-                outs.append(snd)
-            else:
-                outs.append(self._sample(out, rids[a:b]))
-        for r in reqs:
-            r.wait()
-        ids = torch.cat(outs) if self.pp_last else torch.empty(B, dtype=torch.int32, device=self.device)
-        self.comm.broadcast_(ids, src_in_group=self.mesh.pp - 1, group="pp")
-        return ids
+        reqs, keep, ids_mb, res = [], [], {}, {}
+
+        def recv(ins):
+            h = torch.empty(bounds[ins.mb + 1] - bounds[ins.mb], H, dtype=self.model.dtype, device=self.device)
+            self.comm.recv(h, ins.group[0])
+            return h
+
+        def run(mb, h):
+            a, b = bounds[mb], bounds[mb + 1]
+            return self.runner.run_decode({k: v[a:b] for k, v in inp.items()}, h)
+
+        def send(ins, out):
+            # copy out of the graph's static output before the next replay can reuse it
+            snd = self._maybe_poison(out.clone())
+            reqs.append(self.comm.isend(snd, ins.group[1]))
+            keep.append(snd)
+
+        def sample(mb, out):
+            ids_mb[mb] = self._sample(out, rids[bounds[mb]:bounds[mb + 1]])
+
+        def broadcast(ins):
+            for r in reqs:
+                r.wait()
+            ids = torch.cat([ids_mb[i] for i in range(M)]) if ids_mb else \
+                torch.empty(B, dtype=torch.int32, device=self.device)
+            self.comm.broadcast_(ids, src_in_group=len(ins.group) - 1, group="pp")
+            res["ids"] = ids
+
+        self._execute(self._ops(M), recv, run, send, sample, broadcast)
+        return res["ids"]
 
     # ------------------------------------------------------------------------------------
     # asynchronous pipeline (engine/pipeline.py): one tick = every stage advances one group
@@ -673,44 +727,58 @@ class LLMEngine:
 
     def _pp_stage_work(self, p: PipePlan) -> None:
         """recv the residual stream (stage > 0) -> run this stage -> isend (not last) or sample
-        (last stage: ids kept on the plan for the broadcast)."""
+        (last stage: ids kept on the plan for the broadcast, which the tick issues when the plan
+        leaves the pipeline) — the step program's instructions of one microbatch."""
         native_dec = self._native_pp and p.plan.kind == 2   # the decode graph receives itself
-        h, posted = None, self._posted.pop(p.tick, None)
-        if posted is not None:
-            h, work, slot = posted
-            work.wait()          # RCCL: the compute stream waits for the transfer, the host does not
-            self.metrics.inc("pp_preposted_recvs")
-        elif not self.pp_first and not native_dec:
+        state: dict = {}
+
+        def recv(ins):
+            posted = self._posted.pop(p.tick, None)
+            if posted is not None:
+                h, work, _ = posted
+                work.wait()      # RCCL: the compute stream waits for the transfer, the host does not
+                self.metrics.inc("pp_preposted_recvs")
+                state["posted"] = posted
+                return h
+            if ins.stream == "graph":
+                return None
             h = torch.empty(p.tokens, self.cfg.hidden_size, dtype=self.model.dtype, device=self.device)
-            self.comm.recv(h, self.mesh.prev_stage(self.rank))
-        if p.cow:
-            self.kv.copy_blocks(p.cow)
-        if p.plan.kind == 1:
-            out = self.runner.run(self.runner.prefill_batch(p.plan, lambda r: self.requests[r].tokens), h)
-        else:
-            ids = self._first_stage_ids(p) if self.pp_first else np.zeros(len(p.rids), dtype=np.int32)
-            inp = self.runner.decode_inputs(p.plan, ids)
-            out = self.runner.run_decode(inp, h)
-        if posted is not None and self._comm_stream is not None:
-            ev = torch.cuda.Event()
-            ev.record()          # after every kernel that reads the boundary buffer
-            self._bevents[posted[2]] = ev
-        if not self.pp_last:
-            nxt = self.mesh.next_stage(self.rank)
-            if native_dec:
+            self.comm.recv(h, ins.group[0])
+            return h
+
+        def run(mb, h):
+            if p.cow:
+                self.kv.copy_blocks(p.cow)
+            if p.plan.kind == 1:
+                out = self.runner.run(self.runner.prefill_batch(p.plan, lambda r: self.requests[r].tokens), h)
+            else:
+                ids = self._first_stage_ids(p) if self.pp_first else np.zeros(len(p.rids), dtype=np.int32)
+                out = self.runner.run_decode(self.runner.decode_inputs(p.plan, ids), h)
+            posted = state.get("posted")
+            if posted is not None and self._comm_stream is not None:
+                ev = torch.cuda.Event()
+                ev.record()          # after every kernel that reads the boundary buffer
+                self._bevents[posted[2]] = ev
+            return out
+
+        def send(ins, out):
+            if ins.stream == "send":
                 # the whole bucket of the instance just replayed, straight from its static output;
                 # the runner replays that instance again only after this send completed
                 g = self.runner.last_instance
-                w = self.comm.isend(self._maybe_poison(g.output), nxt)
+                w = self.comm.isend(self._maybe_poison(g.output), ins.group[1])
                 g.send_done = w.event
                 self.metrics.inc("pp_native_graph_sends")
             else:
                 snd = out.clone() if p.plan.kind == 2 else out   # graph outputs are reused by the next replay
-                w = self.comm.isend(self._maybe_poison(snd), nxt)
+                w = self.comm.isend(self._maybe_poison(snd), ins.group[1])
                 if not isinstance(w, NativeWork):   # native sends keep their tensor alive themselves
                     self._sends.append(w)
-        else:
+
+        def sample(mb, out):
             p.ids = self._sample(out, p.rids)
+
+        self._execute(self._ops(1, native_dec), recv, run, send, sample)
 
     # ------------------------------------------------------------------------------------
     def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list:

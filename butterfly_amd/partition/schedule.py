@@ -7,7 +7,8 @@ communication instructions between them, with group, peer and payload. It is the
 engine runs — `engine/engine.py:_run_stages` / `_pipe_stage` (recv residual stream -> stage
 -> isend, or sample + broadcast ids) and `models/transformer.py` (vocab-parallel embedding
 all-reduce, two TP all-reduces per layer, EP fixed-capacity all-to-all dispatch and return,
-vocab-parallel sampling all-gather) — written down ahead of time so that it can be
+vocab-parallel sampling all-gather; with the IPC EP exchange, dispatch and return of the
+routed rows) — written down ahead of time so that it can be
 
   * checked for cross-rank consistency without running anything (`check_programs`: every
     group collective is issued by all members in the same order with the same payload, every
@@ -21,7 +22,11 @@ vocab-parallel sampling all-gather) — written down ahead of time so that it ca
     to choose among layouts whose estimated throughput is within 2 % (`search.select`); the
     cut points themselves come from the time/memory DP;
   * compared with what the engine actually issued (tests/test_schedule.py replays a decode
-    step through the loopback backend, parallel/fake.py, and diffs its log against this).
+    step through the loopback backend, parallel/fake.py, and diffs its log against this);
+  * EXECUTED: the engine-level instructions (`exec`: recv / stage / send / sample / broadcast,
+    per microbatch; `exec_program`) are what engine._execute interprets for every pipelined or
+    single-stage step — the peers, streams and order of the boundary transfers come from here,
+    not from code in the engine.
 
 Stream assignment follows the engine: TP all-reduces run on the compute stream (one-shot IPC
 kernel when BFLY_CUSTOM_AR is active, else RCCL, both stream-ordered), PP sends are `isend` on
@@ -45,11 +50,15 @@ BF16 = 2
 
 @dataclass(frozen=True)
 class Instr:
-    op: str                      # compute | all_reduce | all_gather | reduce_scatter | all_to_all | send | recv | broadcast
+    op: str                      # compute | all_reduce | all_gather | reduce_scatter | all_to_all | ep_dispatch |
+                                 # ep_return | send | recv | broadcast
     group: tuple = ()            # global ranks taking part (send/recv: (src, dst))
     nbytes: int = 0              # payload this rank contributes (all_gather: its own slice)
-    stream: str = "compute"      # compute | comm
+    stream: str = "compute"      # compute | comm | graph | send
     note: str = ""
+    exec: str = ""               # engine-level step: recv | stage | send | sample | broadcast ("" = issued
+                                 # inside the stage's model forward / sampler, or before the step)
+    mb: int = 0                  # microbatch the engine-level step belongs to
 
     def key(self) -> tuple:
         """What must agree between the members of a collective (or a send/recv pair)."""
@@ -82,7 +91,8 @@ class RankProgram:
 
 
 def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int = 1,
-                 dtype_bytes: int = BF16, native_pp: bool = False, bucket: Optional[int] = None) -> RankProgram:
+                 dtype_bytes: int = BF16, native_pp: bool = False, bucket: Optional[int] = None,
+                 ep_ipc: bool = False) -> RankProgram:
     """The decode-step program of `rank` for `tokens` sequences. With the asynchronous pipeline
     (default) a step is one tick carrying one request group (`tokens` = the group's size, one
     microbatch); the synchronous pipeline (engine._pipeline_decode) cuts the step's batch into
@@ -94,15 +104,23 @@ def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int 
     bounds = [tokens * i // M for i in range(M + 1)]
     for m in range(M):
         _microbatch(plan, rank, bounds[m + 1] - bounds[m], prog.instrs.append, ep_sync=(m == 0),
-                    dtype_bytes=dtype_bytes, native_pp=native_pp, bucket=bucket)
+                    dtype_bytes=dtype_bytes, native_pp=native_pp, bucket=bucket, ep_ipc=ep_ipc, mb=m)
     if plan.mesh.pp > 1:
         prog.instrs.append(Instr("broadcast", tuple(plan.mesh.pp_group(rank)), tokens * 4, "comm",
-                                 "sampled ids from the last stage"))
+                                 "sampled ids from the last stage", exec="broadcast"))
     return prog
 
 
+def exec_program(plan: PartitionPlan, rank: int, microbatches: int = 1, native_pp: bool = False) -> list:
+    """The engine-level steps of `rank`'s program (instructions with `exec` set), in issue order:
+    what engine._execute runs for a step of `microbatches` microbatches. They do not depend on
+    the token count (only the payloads do), so the engine builds them once per shape."""
+    prog = rank_program(plan, rank, max(1, microbatches), max(1, microbatches), native_pp=native_pp)
+    return [i for i in prog.instrs if i.exec]
+
+
 def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool, dtype_bytes: int = BF16,
-                native_pp: bool = False, bucket: Optional[int] = None) -> None:
+                native_pp: bool = False, bucket: Optional[int] = None, ep_ipc: bool = False, mb: int = 0) -> None:
     cfg: ModelConfig = plan.model
     mesh = plan.mesh
     c = mesh.coord(rank)
@@ -118,21 +136,37 @@ def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool,
     if ep > 1 and ep_sync:
         # all EP ranks agree on the padded row count, on prefill vs decode and on idling
         add(Instr("max_int", ep_g, 3 * 8, "compute", "EP step agreement (rows, prefill?, work?)"))
+    if not first and native_pp:
+        wire = (bucket or tokens) * h * dtype_bytes
+        add(Instr("recv", (mesh.prev_stage(rank), rank), wire, "graph",
+                  "residual stream from previous stage: first node of the captured decode graph",
+                  exec="recv", mb=mb))
+    elif not first:
+        add(Instr("recv", (mesh.prev_stage(rank), rank), act, "comm", "residual stream from previous stage",
+                  exec="recv", mb=mb))
+    # the stage's model forward: every instruction up to the send / sampling is issued inside it
+    add(Instr("compute", note=f"stage: layers {a}..{b - 1}", exec="stage", mb=mb))
     if first:
         add(Instr("compute", note="embedding gather (vocab shard)"))
         if tp > 1:
             add(Instr("all_reduce", tp_g, act, "compute", "vocab-parallel embedding"))
-    elif native_pp:
-        wire = (bucket or tokens) * h * dtype_bytes
-        add(Instr("recv", (mesh.prev_stage(rank), rank), wire, "graph",
-                  "residual stream from previous stage: first node of the captured decode graph"))
-    else:
-        add(Instr("recv", (mesh.prev_stage(rank), rank), act, "comm", "residual stream from previous stage"))
     for layer in range(a, b):
         add(Instr("compute", note=f"layer {layer}: norm, QKV, RoPE+KV append, attention, O"))
         if tp > 1:
             add(Instr("all_reduce", tp_g, act, "compute", f"layer {layer} attention output (+ add, RMSNorm)"))
-        if moe and ep > 1:
+        if moe and ep > 1 and ep_ipc:
+            # byte-minimal IPC exchange (parallel/ep_ipc.py): each token row travels once to
+            # each rank owning one of its experts, and its output once back. The bytes depend
+            # on the routing: the payload here is the bound, min(k, ep) ranks per token.
+            k = cfg.experts_per_token
+            hits = tokens * min(k, ep)
+            add(Instr("compute", note=f"layer {layer}: router"))
+            add(Instr("ep_dispatch", ep_g, hits * (h * dtype_bytes + 8 * k), "compute",
+                      f"layer {layer} EP: routed rows + expert ids / weights into the owners' IPC blocks"))
+            add(Instr("compute", note=f"layer {layer}: local experts on routed rows only"))
+            add(Instr("ep_return", ep_g, hits * h * dtype_bytes, "compute",
+                      f"layer {layer} EP: routed rows' expert outputs back into the sources' IPC blocks"))
+        elif moe and ep > 1:
             # fixed-capacity dispatch (models/transformer.py _moe_alltoall_fixed): `tokens`
             # rows reserved per destination, expert ids + gate weights (f32) alongside
             k = cfg.experts_per_token
@@ -150,15 +184,17 @@ def _microbatch(plan: PartitionPlan, rank: int, tokens: int, add, ep_sync: bool,
                 nb = R * h * dtype_bytes if (last and layer == b - 1) else act
                 add(Instr("all_reduce", tp_g, nb, "compute", f"layer {layer} FFN output"))
     if last:
-        add(Instr("compute", note="final norm, LM head (vocab shard), sampling"))
+        add(Instr("compute", note="final norm, LM head (vocab shard) in the stage; sampling", exec="sample", mb=mb))
         if tp > 1:
             add(Instr("all_gather", tp_g, R * 2 * 4, "compute", "vocab-parallel argmax: (score, id) pairs"))
     elif native_pp:
         wire = (bucket or tokens) * h * dtype_bytes
         add(Instr("send", (rank, mesh.next_stage(rank)), wire, "send",
-                  "residual stream to next stage: the graph's static output (A/B instance), send stream"))
+                  "residual stream to next stage: the graph's static output (A/B instance), send stream",
+                  exec="send", mb=mb))
     else:
-        add(Instr("send", (rank, mesh.next_stage(rank)), act, "comm", "residual stream to next stage"))
+        add(Instr("send", (rank, mesh.next_stage(rank)), act, "comm", "residual stream to next stage",
+                  exec="send", mb=mb))
 
 
 def check_programs(progs: dict) -> None:
@@ -203,7 +239,7 @@ def link_bytes(plan: PartitionPlan, progs: dict) -> dict:
             n = len(i.group)
             if i.op == "send":
                 put(i.group[0], i.group[1], i.nbytes)
-            elif i.op == "all_to_all" and n > 1:
+            elif i.op in ("all_to_all", "ep_dispatch", "ep_return") and n > 1:
                 me = i.group.index(r)
                 for j, peer in enumerate(i.group):      # direct: block j to member j
                     if j != me:
@@ -228,7 +264,8 @@ def link_bytes(plan: PartitionPlan, progs: dict) -> dict:
 
 
 def programs(plan: PartitionPlan, tokens: int, microbatches: int = 1, dtype_bytes: int = BF16,
-             native_pp: bool = False, bucket: Optional[int] = None) -> dict:
+             native_pp: bool = False, bucket: Optional[int] = None, ep_ipc: bool = False) -> dict:
     """rank_program for every rank (each DP replica decodes `tokens` sequences); activations
     are `dtype_bytes` wide (bf16 on the GPU, fp32 on the CPU reference path)."""
-    return {r: rank_program(plan, r, tokens, microbatches, dtype_bytes, native_pp, bucket) for r in range(plan.n_gpus)}
+    return {r: rank_program(plan, r, tokens, microbatches, dtype_bytes, native_pp, bucket, ep_ipc)
+            for r in range(plan.n_gpus)}

@@ -75,7 +75,7 @@ def _decode_window(rank, comm, preset, mesh, stages):
     comm.barrier()
     out = eng.step()
     comm.barrier()
-    return out.kind, eng.async_pp
+    return out.kind, eng.async_pp, eng.ep_ipc
 
 
 @pytest.mark.parametrize("pp_async", ["1", "0"])
@@ -91,7 +91,7 @@ def test_program_matches_engine(preset, kw, pp_async, monkeypatch):
     mesh = plan.mesh
     world = FakeWorld(mesh, timeout_s=60)
     outs = world.run(lambda r, c: _decode_window(r, c, preset, mesh, plan.stages))
-    assert all(k == "decode" for k, _ in outs)
+    assert all(k == "decode" for k, _, _ in outs)
     if outs[0][1]:   # asynchronous pipeline: a step is one tick carrying one request group
         tokens, mb = len(PROMPTS) // mesh.pp, 1
     else:            # synchronous: the whole batch in pp microbatches
@@ -100,12 +100,16 @@ def test_program_matches_engine(preset, kw, pp_async, monkeypatch):
         mine = [(op, grp, nb) for rk, op, grp, shape, nb in world.log if rk == r]
         bars = [i for i, e in enumerate(mine) if e[0] == "barrier"]
         got = [e for e in mine[bars[-2] + 1: bars[-1]]]
-        want = [i for i in programs(plan, tokens, mb, dtype_bytes=4)[r].comm() if i.op != "recv"]   # CPU: fp32
+        want = [i for i in programs(plan, tokens, mb, dtype_bytes=4, ep_ipc=outs[r][2])[r].comm()
+                if i.op != "recv"]   # CPU: fp32
         # the loopback log names broadcasts by source ("broadcast<src>") and records sends
         assert [("broadcast" if op.startswith("broadcast") else op, grp) for op, grp, _ in got] == \
             [(i.op, i.group) for i in want], (r, got, [(i.op, i.group) for i in want])
         for (op, _, nb), i in zip(got, want):
-            # every payload, EP dispatch / sampling gather / broadcast included
+            # every payload, EP dispatch / sampling gather / broadcast included; the IPC EP
+            # exchange logs its rendezvous (the program carries the routed-bytes bound)
+            if op in ("ep_dispatch", "ep_return"):
+                continue
             assert nb == i.nbytes, (r, op, nb, i)
 
 
@@ -170,3 +174,47 @@ def test_native_pp_program_puts_recv_in_graph_and_send_on_send_stream():
         i = p2p[0]
         assert i.nbytes == 8 * h * 2
         assert (i.op, i.stream) == (("recv", "graph") if c.pp == 1 else ("send", "send"))
+
+
+@pytest.mark.parametrize("pp_async", ["1", "0"])
+@pytest.mark.parametrize("kw", [dict(pp=2), dict(tp=2, pp=2), dict(tp=2)])
+def test_engine_executes_rank_program(kw, pp_async, monkeypatch):
+    """The rank program drives the engine: every boundary receive, stage run,
+    send, sampling and id broadcast the engine performs is an instruction of
+    schedule.exec_program, executed in the program's order with the program's peers."""
+    from butterfly_amd.engine.engine import LLMEngine as Eng
+    from butterfly_amd.partition.schedule import exec_program
+
+    monkeypatch.setenv("BFLY_PP_ASYNC", pp_async)
+    torch.set_num_threads(1)
+    n = kw.get("tp", 1) * kw.get("pp", 1)
+    plan = partition(ModelConfig.from_preset("llama-tiny"), n, kw, batch_per_gpu=4)
+    mesh = plan.mesh
+    ran: dict = {}
+    orig = Eng._execute
+
+    def spy(ops, recv, run, send, sample, broadcast=None):
+        import threading
+
+        ran.setdefault(threading.current_thread().name, []).append(list(ops))
+        return orig(ops, recv, run, send, sample, broadcast)
+
+    monkeypatch.setattr(Eng, "_execute", staticmethod(spy))
+    world = FakeWorld(mesh, timeout_s=60)
+    outs = world.run(lambda r, c: _decode_window(r, c, "llama-tiny", mesh, plan.stages))
+    assert all(k == "decode" for k, _, _ in outs)
+    if mesh.pp == 1:
+        assert not ran        # single stage: the stage run and sampling need no program walk
+        return
+    assert len(ran) == mesh.world_size
+    progs = {(m, nat): {r: exec_program(plan, r, m, nat) for r in range(n)} for m in (1, mesh.pp) for nat in (False,)}
+    for calls in ran.values():
+        for ops in calls:
+            assert any(ops == p[r] for p in progs.values() for r in p), ops
+    # sends and receives go to the program's peers: next / previous stage
+    for r in range(n):
+        for ins in exec_program(plan, r, 1):
+            if ins.exec == "send":
+                assert ins.group == (r, mesh.next_stage(r))
+            if ins.exec == "recv":
+                assert ins.group == (mesh.prev_stage(r), r)
