@@ -14,8 +14,8 @@ exposes the handful of collectives the rank programs need:
   broadcast_    control-plane metadata
 
 Small TP all-reduces (decode) can be routed to a one-shot peer-to-peer kernel
-(parallel/custom_allreduce.py) instead of RCCL; everything else stays on RCCL. With
-BFLY_NATIVE_RCCL=1 the data-path collectives of every multi-rank group go to the rank's own
+(parallel/custom_allreduce.py) instead of RCCL; everything else stays on RCCL. On RCCL
+(BFLY_NATIVE_RCCL, on by default) the data-path collectives of every multi-rank group go to the rank's own
 RCCL communicators (parallel/rccl.py: world init + one ncclCommSplit per mesh axis) instead of
 torch's ProcessGroups; control-plane ops (host integers, barriers) stay on torch.
 Every op is stream-ordered and allocation-free when given outputs, so it can be captured

@@ -8,7 +8,7 @@ bootstrap. The data-path collectives are single stream-ordered RCCL calls on tor
 stream: no work objects, watchdog events or allocator stream records, so they capture into
 the decode hipGraph like the kernels around them.
 
-Enabled by BFLY_NATIVE_RCCL=1 (parallel/comm.py routes all-reduce / all-gather /
+Enabled whenever the backend is RCCL (BFLY_NATIVE_RCCL, default on; parallel/comm.py routes all-reduce / all-gather /
 reduce-scatter / all-to-all of groups larger than one rank here). RCCL refuses two ranks on
 one device, so on a one-GPU box only nranks = 1 communicators can be exercised; the multi-rank
 path needs a multi-GPU node.

@@ -45,9 +45,10 @@ define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
-define("BFLY_NATIVE_RCCL", False, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "
-       "all-to-all) on the rank's own RCCL communicators (world init + ncclCommSplit per mesh axis, "
-       "parallel/rccl.py) instead of torch ProcessGroups; multi-rank path needs a multi-GPU node")
+define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "
+       "all-to-all) and pipeline edges on the rank's own RCCL communicators (world init + ncclCommSplit "
+       "per mesh axis, parallel/rccl.py) instead of torch ProcessGroups, whenever the backend is RCCL "
+       "(the multi-GPU preflight turns it off if its native check fails); 0 = torch ProcessGroups")
 define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism: the residual stream and the norms are "
        "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
 define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")

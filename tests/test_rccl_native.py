@@ -28,8 +28,9 @@ def test_unique_id_and_version():
     assert v >= 22000, v                   # NCCL-API 2.20+ (ncclCommSplit)
 
 
-def test_flag_registered_off_by_default():
-    assert flags.get("BFLY_NATIVE_RCCL") is False
+def test_flag_registered_on_by_default(monkeypatch):
+    monkeypatch.delenv("BFLY_NATIVE_RCCL", raising=False)
+    assert flags.get("BFLY_NATIVE_RCCL") is True
 
 
 class _RecordingWorld:
