@@ -303,6 +303,8 @@ def run(a) -> int:
         "graphs_captured": runner.captured_buckets,
         "graphs_failed": sorted(runner.eager_buckets),
         "custom_ar_active": comm.custom_ar is not None,
+        "ep_ipc_active": comm.ep_ipc is not None,
+        "ep_ipc_link_bytes_rank0": comm.ep_ipc.stats() if comm.ep_ipc is not None else None,
         "comm_probe": probe or None,
         "preflight": preflight,
         "native_rccl": any(g is not None and g.native is not None for g in comm.groups.values()),
