@@ -37,14 +37,28 @@ def _to_dev(a, dev) -> torch.Tensor:
 
 
 class _DecodeGraph:
+    """Static inputs / output of one decode graph (bucket). The int32 inputs are views of ONE
+    device buffer [ids | positions | slots | ctx_lens | block tables], so a step stages them
+    with a single host-to-device copy from a pinned buffer (two, alternating, each reused only
+    after the event of its previous copy)."""
+
     def __init__(self, bucket: int, max_blocks: int, device, hidden: int, first: bool):
-        i32 = dict(dtype=torch.int32, device=device)
+        b = bucket
         self.bucket = bucket
-        self.input_ids = torch.zeros(bucket, **i32)
-        self.positions = torch.zeros(bucket, **i32)
-        self.slots = torch.full((bucket,), -1, **i32)
-        self.block_tables = torch.zeros(bucket, max_blocks, **i32)
-        self.ctx_lens = torch.ones(bucket, **i32)
+        self.max_blocks = max_blocks
+        self.inbuf = torch.zeros(b * (4 + max_blocks), dtype=torch.int32, device=device)
+        self.input_ids = self.inbuf[0:b]
+        self.positions = self.inbuf[b:2 * b]
+        self.slots = self.inbuf[2 * b:3 * b]
+        self.ctx_lens = self.inbuf[3 * b:4 * b]
+        self.block_tables = self.inbuf[4 * b:].view(b, max_blocks)
+        self.slots.fill_(-1)
+        self.ctx_lens.fill_(1)
+        pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
+        self.host = [torch.zeros(self.inbuf.numel(), dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.host_np = [h.numpy() for h in self.host]
+        self.host_events = [None, None]
+        self.host_flip = 0
         self.hidden_in = None if first else torch.zeros(bucket, hidden, dtype=torch.bfloat16, device=device)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.output: Optional[torch.Tensor] = None
@@ -256,19 +270,40 @@ class ModelRunner:
         return g.output[:B]
 
     def _stage(self, g: _DecodeGraph, inp: dict, hidden_in) -> None:
-        B = len(inp["ids"])
-        dev = self.device
-        t = lambda a: _to_dev(a, dev)  # noqa: E731
-        g.input_ids[:B].copy_(t(inp["ids"]))
-        g.positions[:B].copy_(t(inp["pos"]))
-        g.slots[:B].copy_(t(inp["slots"]))
-        g.block_tables[:B].copy_(t(inp["tables"]))
-        g.ctx_lens[:B].copy_(t(inp["ctx"]))
-        if B < g.bucket:
-            g.input_ids[B:].zero_()
-            g.positions[B:].zero_()
-            g.slots[B:].fill_(-1)
-            g.ctx_lens[B:].fill_(1)
+        """Fill the graph's static inputs: the host arrays (padding rows included: position 0,
+        no cache slot, context 1, page 0) go into a pinned buffer and reach the device in one
+        copy; input ids already on the device (gathered from the previous step's sampled ids)
+        are copied device to device."""
+        B, b = len(inp["ids"]), g.bucket
+        k = g.host_flip
+        g.host_flip ^= 1
+        if g.host_events[k] is not None:
+            g.host_events[k].synchronize()        # its previous copy has read the buffer
+        h = g.host_np[k]
+        ids = inp["ids"]
+        ids_dev = isinstance(ids, torch.Tensor) and ids.device.type != "cpu"
+        if not ids_dev:
+            h[0:B] = ids.numpy() if isinstance(ids, torch.Tensor) else ids
+            h[B:b] = 0
+        h[b:b + B] = inp["pos"]
+        h[b + B:2 * b] = 0
+        h[2 * b:2 * b + B] = inp["slots"]
+        h[2 * b + B:3 * b] = -1
+        h[3 * b:3 * b + B] = inp["ctx"]
+        h[3 * b + B:4 * b] = 1
+        tab = h[4 * b:].reshape(b, g.max_blocks)
+        tab[:B] = inp["tables"]
+        tab[B:] = 0
+        start = b if ids_dev else 0
+        g.inbuf[start:].copy_(g.host[k][start:], non_blocking=True)
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            g.host_events[k] = ev
+        if ids_dev:
+            g.input_ids[:B].copy_(ids)
+            if B < b:
+                g.input_ids[B:].zero_()
         if g.hidden_in is not None and hidden_in is not None:
             g.hidden_in[:B].copy_(hidden_in)
 

@@ -12,8 +12,8 @@ typedef __bf16 bf16;
 enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_SILU = 2 };
 
 struct GemmPlan {
-  int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 2 = 256x256 big tile (prefill), 3 = decode ring,
-             // 4 = 256x256 8-phase big tile (BK 64)
+  int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 3 = decode ring,
+             // 4 = 256x256 8-phase big tile (BK 64, prefill; kind 2 was the removed ring kernel)
   int mt, nt;
   int wk;    // skinny: waves splitting K inside a workgroup (1, 2, 4)
   int bm, bn;
