@@ -21,6 +21,8 @@
 // read by ds_read_b128 as the 32x32x16 A operand of S^T = K . Q^T, V by ds_read_b64_tr_b16 as
 // the A operand of O^T = V^T . P^T; the S^T accumulator is converted in registers into the
 // P^T B operand (§3 "An accumulator tile as the next MFMA's operand").
+#include <type_traits>
+
 #include "bfly_common.h"
 #include "bfly_kernels.h"
 #include "bfly_kv.h"
@@ -469,6 +471,13 @@ constexpr float kPfRescaleThr = 8.f;
 // one-tile software pipeline of QK(t+1) beside softmax(t) (spills at 256 VGPRs, -35 %), a
 // 4-wave x 64-row layout sharing K/V fragments (-25..-35 %), row sums on the matrix core (+-1 %),
 // and the round-1 non-persistent kernel (one workgroup per item; 16-40 % slower).
+// Round 3 (profiles/r3_attn_prefill_variants.log): the XCD-aware item walk (+5..10 %; the 8
+// query heads of a kv head had landed on 8 different L2s) and a wave-uniform wid (+1..3 %)
+// are kept; measured and dropped: 4 or 5 ring slots (equal), a one-wave-per-SIMD 4 x 64-row
+// kernel with two q-blocks pipelined inside the wave (-25..-65 %: the compiler puts every MFMA
+// result in AGPRs above 256 registers and serialises the LDS reads), K/V LDS-DMA as inline asm
+// (drops the compiler's per-tile vmcnt(0) before PV, yet -2 %), and Q rows staged by LDS-DMA
+// with position-counted vmcnt waits and fixed-count buffer stores (-1..-6 %).
 // ---------------------------------------------------------------------------------------
 struct PfItem {
   int valid, rows, ntiles;  // valid: item index in range; rows: query rows to write (q0 < L);
@@ -499,22 +508,24 @@ __device__ __forceinline__ PfItem pf_item(int i, int nqb, int nseq, int Hq, int 
   return it;
 }
 
-template <int D, int S>
+template <int D, int S, bool TR = false>
 __global__ void __launch_bounds__(kPfThreads)
 attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf16* __restrict__ k,
                             long k_stride, const bf16* __restrict__ v, long v_stride,
                             const int* __restrict__ cu_seqlens, const int* __restrict__ cu_k, int nseq,
                             int nqb, int Hq, int Hkv, float scale_log2, int causal,
-                            bf16* __restrict__ out, long o_stride, float* __restrict__ lse) {
+                            bf16* __restrict__ out, long o_stride, float* __restrict__ lse, int xr) {
   static_assert(D == 128 && S >= 2, "persistent prefill kernel is specialised for D=128");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = 2 * kPfBKV * D * 2;
   constexpr int AHEAD = S - 1;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid through readfirstlane: the compiler then knows every per-wave branch on it is
+  // wave-uniform (1-3 % faster: profiles/r3_attn_prefill_variants.log)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hi = lane >> 5, c = lane & 31;
   const bool cz = causal != 0;
   const int G = gridDim.x;
-  if (__builtin_amdgcn_readfirstlane(wid) >= kPfWaves / 2) __builtin_amdgcn_s_setprio(1);
+  if (wid >= kPfWaves / 2) __builtin_amdgcn_s_setprio(1);
   const PfDma dma = pf_dma_offsets(k_stride, v_stride, wid, lane);
 
   // consume cursor (C: the item being computed; items with query rows) and issue cursor
@@ -525,7 +536,10 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
       it = pf_item(idx, nqb, nseq, Hq, Hkv, cu_seqlens, cu_k, cz);
     } while (it.valid && (need_tiles ? it.ntiles == 0 : it.rows == 0));
   };
-  int ci = (int)blockIdx.x - G;
+  // XCD-aware walk: the dispatcher deals workgroups round-robin over the 8 XCDs (b % 8 share
+  // an L2); renumbered, each XCD's workgroups take consecutive items, i.e. the query heads
+  // of one kv head side by side, so their K/V tiles are fetched into ONE L2
+  int ci = (xr ? xcd_remap((int)blockIdx.x, G) : (int)blockIdx.x) - G;
   PfItem C{};
   next_item(ci, C, false);
   if (!C.valid) return;
@@ -533,6 +547,15 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
   PfItem I = C;
   if (I.ntiles == 0) next_item(ii, I, true);
   int issued = 0, consumed = 0, islot = 0, cslot = 0;
+  // TR (BFLY_ATTN_TRACE=1, tools/attn_trace.py): wave 0 stamps s_memtime at the item phases
+  // into the LSE buffer instead of writing LSE / O
+  int trj = 0;
+  auto trace = [&](int e) {
+    if constexpr (TR) {
+      if (wid == 0 && lane == 0 && trj < 32)
+        reinterpret_cast<long long*>(lse)[((long)blockIdx.x * 32 + trj) * 8 + e] = (long long)__builtin_amdgcn_s_memtime();
+    }
+  };
   auto issue_one = [&]() {
     if (!I.valid) return;
     pf_stage_buf(k, k_stride, v, v_stride, I.sk0, I.Lk, I.kh, it_t, smem + islot * STAGE_BYTES, wid, dma);
@@ -546,16 +569,26 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
 #pragma unroll
   for (int st = 0; st < AHEAD; ++st) issue_one();
 
+  // Q fragments of this lane's query row of item X (rows clamped into the sequence)
+  auto load_q = [&](const PfItem& X, bf16x8 (&qd)[8]) {
+    const int qrow = X.q0 + 32 * wid + c;
+    const int qr = qrow < X.L ? qrow : X.L - 1;
+    const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (long)(X.s0 + qr) * q_stride + (long)X.h * D + 8 * hi);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qd[ks] = qp[2 * ks];
+  };
   while (true) {
-    // ---- item start: Q fragments and softmax state of this lane's query row
+    // ---- item start: Q fragments and softmax state of this lane's query row. The next item
+    // is looked up (scalar loads of cu_seqlens) during this item's last tile, so that latency
+    // does not sit between two items. (Loading its Q there as well, into the dead qf, makes
+    // the allocator spill: measured and dropped.)
+    trace(0);
     const int qrow = C.q0 + 32 * wid + c;
     bf16x8 qf[8];
-    {
-      const int qr = qrow < C.L ? qrow : C.L - 1;
-      const bf16x8* qp = reinterpret_cast<const bf16x8*>(q + (long)(C.s0 + qr) * q_stride + (long)C.h * D + 8 * hi);
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) qf[ks] = qp[2 * ks];
-    }
+    load_q(C, qf);
+    int cin = ci;
+    PfItem Cn{};
+    auto prefetch_next = [&]() { next_item(cin, Cn, false); };
     f32x16 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
@@ -565,11 +598,15 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
     for (int t = 0; t < C.ntiles; ++t) {
       // this tile landed; the tiles issued after it may still fly
       pf_wait_tiles(min(issued - consumed - 1, AHEAD - 1));
+      if (t == 0) trace(1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      if (t == 0) trace(2);
+      if (t == C.ntiles - 1) trace(3);
       issue_one();                      // into the slot every wave finished reading last tile
       const char* kb = smem + cslot * STAGE_BYTES;
       const int kv0 = t * kPfBKV;
+      if (t == C.ntiles - 1) prefetch_next();
       if (!(cz && kv0 > wave_qmax)) {
         f32x16 sc[2];
         pf_qk(kb, qf, lane, sc);
@@ -593,10 +630,12 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
       if (++cslot == S) cslot = 0;
       ++consumed;
     }
+    if (C.ntiles == 0) prefetch_next();
     // ---- item end: normalise and store this lane's query row (no barrier: the next item's
     // first wait + barrier orders the ring; these stores only make that wait conservative)
+    trace(4);
     lsum += __shfl_xor(lsum, 32, 64);
-    if (qrow < C.L) {
+    if (!TR && qrow < C.L) {
       if (lse != nullptr && hi == 0)
         lse[(long)(C.s0 + qrow) * Hq + C.h] = lsum > 0.f ? (m + __log2f(lsum)) * 0.69314718055994531f : kNegInf;
       const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
@@ -611,7 +650,14 @@ attn_prefill_persist_kernel(const bf16* __restrict__ q, long q_stride, const bf1
           *reinterpret_cast<bf16x4*>(op + 32 * dt + 8 * a + 4 * hi) = w;
         }
     }
-    next_item(ci, C, false);
+    trace(5);
+    if constexpr (TR) {
+      if (wid == 0 && lane == 0 && trj < 32)
+        reinterpret_cast<long long*>(lse)[((long)blockIdx.x * 32 + trj) * 8 + 6] = C.ntiles;
+    }
+    ++trj;
+    ci = cin;
+    C = Cn;
     if (!C.valid) break;
   }
 }
@@ -679,25 +725,42 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
   if (D != 128 || Hq % Hkv != 0) return -1;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int* cuk = cu_k != nullptr ? cu_k : cu_seqlens;
-  {
-    constexpr int S_ = 3;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const int nqb = (max_seqlen + kPfBQ - 1) / kPfBQ;
+  const long items = (long)nqb * nseq * Hq;
+  const int g = (int)(items < ncu ? items : ncu);
+  static const bool tr = getenv("BFLY_ATTN_TRACE") != nullptr;
+  static const int xr = [] {
+    const char* e = getenv("BFLY_ATTN_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  auto launch = [&](auto sc) {
+    constexpr int S_ = decltype(sc)::value;
     const size_t lds = (size_t)S_ * 2 * kPfBKV * D * 2;
-    static int ncu = 0;
-    if (ncu == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    static bool attr = false;
+    if (!attr) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_persist_kernel<128, S_>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_prefill_persist_kernel<128, S_, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
     }
-    const int nqb = (max_seqlen + kPfBQ - 1) / kPfBQ;
-    const long items = (long)nqb * nseq * Hq;
-    const int g = (int)(items < ncu ? items : ncu);
-    attn_prefill_persist_kernel<128, S_><<<g, kPfThreads, lds, stream>>>(
-        q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cuk, nseq, nqb, Hq, Hkv, scale_log2,
-        causal ? 1 : 0, out, o_stride, lse);
-    return 0;
-  }
+    if (tr && lse != nullptr)
+      attn_prefill_persist_kernel<128, S_, true><<<g, kPfThreads, lds, stream>>>(
+          q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cuk, nseq, nqb, Hq, Hkv, scale_log2,
+          causal ? 1 : 0, out, o_stride, lse, xr);
+    else
+      attn_prefill_persist_kernel<128, S_><<<g, kPfThreads, lds, stream>>>(
+          q, q_stride, k, k_stride, v, v_stride, cu_seqlens, cuk, nseq, nqb, Hq, Hkv, scale_log2,
+          causal ? 1 : 0, out, o_stride, lse, xr);
+  };
+  launch(std::integral_constant<int, 3>{});   // 3 ring slots: 4 and 5 measured equal
+  return 0;
 }
 
 // K16: merge a partial attention result over another key chunk into running accumulators

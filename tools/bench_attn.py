@@ -12,11 +12,34 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from butterfly_amd import ops  # noqa: E402
 
 
+def timed(f, warm_ms=100.0, run_ms=200.0):
+    """Mean microseconds per call: calls run back to back for >= warm_ms (clocks and caches
+    settle; a handful of short calls is still on the idle clock) before >= run_ms are timed."""
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    f()
+    torch.cuda.synchronize()
+    st.record()
+    f()
+    en.record()
+    torch.cuda.synchronize()
+    one = max(st.elapsed_time(en), 1e-3)
+    for _ in range(max(2, int(warm_ms / one))):
+        f()
+    it = max(5, int(run_ms / one))
+    st.record()
+    for _ in range(it):
+        f()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / it * 1e3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="64:1024:64:8,64:1024:8:1,256:1024:64:8,1:8192:64:8,16:4096:64:8")
     ap.add_argument("--prefill", default="16:1024:64:8,4:4096:64:8,1:16384:64:8",
                     help="prefill cases seqs:len:Hq:Hkv ('' to skip)")
+    ap.add_argument("--noncausal", action="store_true", help="time the prefill cases without the causal mask")
     ap.add_argument("--parts", default="0", help="decode split sizes to try (0 = auto)")
     ap.add_argument("--kv-dtype", default="bf16,fp8", help="decode cache element types to time")
     a = ap.parse_args()
@@ -29,22 +52,13 @@ def main():
         v = torch.randn(T, Hkv, D, device="cuda", dtype=torch.bfloat16)
         cu = torch.arange(0, T + 1, Ls, dtype=torch.int32, device="cuda")
         out = torch.empty_like(q)
-        f = lambda: ops.attn_prefill(q, k, v, cu, Ls, 0.088, True, out=out)  # noqa: E731
-        for _ in range(2):
-            f()
-        torch.cuda.synchronize()
-        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        it = 5
-        st.record()
-        for _ in range(it):
-            f()
-        en.record()
-        torch.cuda.synchronize()
-        us = st.elapsed_time(en) / it * 1e3
-        flops = 4.0 * n * Ls * Ls / 2 * Hq * D          # causal useful FLOPs
-        print(json.dumps({"prefill": case, "us": round(us, 1),
+        causal = not a.noncausal
+        f = lambda: ops.attn_prefill(q, k, v, cu, Ls, 0.088, causal, out=out)  # noqa: E731
+        us = timed(f)
+        flops = 4.0 * n * Ls * Ls / (2 if causal else 1) * Hq * D   # useful FLOPs
+        print(json.dumps({"prefill": case, "causal": causal, "us": round(us, 1),
                           "TFLOPs": round(flops / us / 1e6, 1)}), flush=True)
-    for case, kvd in [(c, k) for c in a.cases.split(",") for k in a.kv_dtype.split(",")]:
+    for case, kvd in [(c, k) for c in filter(None, a.cases.split(",")) for k in filter(None, a.kv_dtype.split(","))]:
         B, ctx, Hq, Hkv = map(int, case.split(":"))
         cdt = torch.float8_e4m3fn if kvd == "fp8" else torch.bfloat16
         D, BS = 128, 32
@@ -57,17 +71,7 @@ def main():
         out = torch.empty_like(q)
         for pt in [int(x) for x in a.parts.split(",")]:
             f = lambda: ops.attn_decode(q, kc, vc, bt, cl, 0.088, ctx, part_tokens=pt, out=out)  # noqa: E731
-            for _ in range(3):
-                f()
-            torch.cuda.synchronize()
-            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            it = 20
-            st.record()
-            for _ in range(it):
-                f()
-            en.record()
-            torch.cuda.synchronize()
-            us = st.elapsed_time(en) / it * 1e3
+            us = timed(f)
             byts = 2 * B * ctx * Hkv * D * kc.element_size()
             used = pt if pt > 0 else torch.ops.bfly.attn_decode_part_tokens(B, Hkv, ctx)
             print(json.dumps({"B": B, "ctx": ctx, "Hq": Hq, "Hkv": Hkv, "kv": kvd, "us": round(us, 2),
