@@ -87,6 +87,12 @@ class TransformerLM:
         # (tp > 1: the IPC all-reduce takes the split-K slabs and reduces them in its publish)
         self.defer_reduce = defer and cfg.norm == "rms" and (
             self.tp == 1 or getattr(self.comm, "custom_ar", None) is not None)
+        # decode add+RMSNorm split over (row, column-chunk) workgroups with the 1/rms row scale
+        # applied by the consuming QKV / gate-up GEMM (ops.RowNormed); tp == 1 only (with TP the
+        # IPC all-reduce fuses the norm), dense FFNs (the MoE router reads the normed rows too)
+        self.rowscale_rows = (flags.get("BFLY_NORM_ROWSCALE_MAX_ROWS")
+                              if (self.device.type == "cuda" and cfg.norm == "rms" and self.tp == 1
+                                  and not cfg.is_moe and flags.get("BFLY_NORM_ROWSCALE")) else 0)
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
@@ -321,9 +327,11 @@ class TransformerLM:
             if delta is None:
                 x = self._norm(residual, self.p[pre + "in_w"], self.p.get(pre + "in_b"))
             else:
-                x = self._add_norm(delta, pre + "in", residual, partial)
+                x = self._add_norm(delta, pre + "in", residual, partial,
+                                   consumer=(pre + "qkv_w", "bias" if pre + "qkv_b" in self.p else "none"))
             o = self._attention_block(li, pre, x, fb, kv_caches)
-            x = self._add_norm(o, pre + "post", residual, self.tp > 1)
+            x = self._add_norm(o, pre + "post", residual, self.tp > 1,
+                               consumer=(pre + "gu_w", "silu") if self.cfg.act == "silu" else None)
             delta, partial = self._ffn(pre, x, fb)
         if not self.last:
             if delta is None:
@@ -474,10 +482,17 @@ class TransformerLM:
             k, v = k.to(dtype), v.to(dtype)
         return k.contiguous(), v.contiguous()
 
-    def _add_norm(self, t: torch.Tensor, prefix: str, residual: torch.Tensor, partial: bool) -> torch.Tensor:
+    def _add_norm(self, t: torch.Tensor, prefix: str, residual: torch.Tensor, partial: bool,
+                  consumer: Optional[tuple] = None) -> torch.Tensor:
         """residual += (all_reduce(t) if partial else t); return norm(residual). With TP the
-        all-reduce and the add+norm run as one fused kernel when the IPC all-reduce is on."""
+        all-reduce and the add+norm run as one fused kernel when the IPC all-reduce is on.
+        `consumer` (weight name, epilogue): the GEMM that reads the result; on decode-sized
+        batches whose plan takes a row scale, the norm returns an `ops.RowNormed`."""
         w, b = self.p[prefix + "_w"], self.p.get(prefix + "_b")
+        if consumer is not None and not partial and 0 < residual.shape[0] <= self.rowscale_rows:
+            cw = self.p[consumer[0]]
+            if ops.rowscale_ok(residual.shape[0], cw.shape[0], cw.shape[1], consumer[1]):
+                return ops.rms_norm(t, w, self.cfg.norm_eps, residual=residual, rows=True)
         if partial:
             if self.cfg.norm == "rms":
                 return self.comm.all_reduce_rms_norm_(t, w, self.cfg.norm_eps, residual, "tp")

@@ -153,10 +153,48 @@ def materialize(x):
     return x.materialize() if isinstance(x, Partial) else x
 
 
-def rms_norm(x, w, eps: float, out=None, residual=None):
+class RowNormed:
+    """RMSNorm output whose 1/rms row scale is left to the consuming GEMM (`rms_norm(...,
+    rows=True)`, norm.hip rmsnorm_rows_kernel): `y` [M, dim] bf16 = x * w, `ssp` [M, chunks] f32
+    partial sums of squares of x. `linear(RowNormed, ...)` scales row m of its result by
+    rsqrt(sum(ssp[m]) / dim + eps) in the GEMM epilogue (before bias / SiLU / split-K slabs)."""
+
+    __slots__ = ("y", "ssp", "eps")
+
+    def __init__(self, y: torch.Tensor, ssp: torch.Tensor, eps: float):
+        self.y, self.ssp, self.eps = y, ssp, eps
+
+    @property
+    def shape(self):
+        return self.y.shape
+
+
+_rowscale_ok: dict = {}
+
+
+def rowscale_ok(M: int, N: int, K: int, epilogue: str = "none") -> bool:
+    """True if the GEMM plan for this shape applies a RowScale (tile / decode-ring kernels)."""
+    key = (M, N, K, epilogue)
+    ok = _rowscale_ok.get(key)
+    if ok is None:
+        ok = load_library() and torch.ops.bfly.gemm_rowscale_check(M, N, K, EPILOGUES[epilogue]) == 0
+        _rowscale_ok[key] = ok
+    return ok
+
+
+def rms_norm(x, w, eps: float, out=None, residual=None, rows: bool = False):
     """y = x * rsqrt(mean(x^2) + eps) * w; with `residual`: residual += x first (in place)
     and y is the norm of the updated residual (the fused add+norm of every block). `x` may be
-    a deferred split-K GEMM output (`Partial`): its reduce is fused into this kernel."""
+    a deferred split-K GEMM output (`Partial`): its reduce is fused into this kernel.
+    `rows=True` (GPU): return a `RowNormed` for a row-scaling consumer GEMM instead."""
+    if rows and (isinstance(x, Partial) or _gpu(x)):
+        src = x.slabs if isinstance(x, Partial) else x
+        M, dim = src.shape[-2], src.shape[-1]
+        if out is None:
+            out = torch.empty(M, dim, dtype=w.dtype, device=w.device)
+        ssp = torch.empty(M, torch.ops.bfly.rms_norm_rows_chunks(dim), dtype=torch.float32, device=w.device)
+        torch.ops.bfly.rms_norm_rows(src, w, out, ssp, residual)
+        return RowNormed(out, ssp, eps)
     if isinstance(x, Partial):
         if out is None:
             out = torch.empty_like(x.out)
@@ -286,6 +324,9 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     """y = x @ w.T (+ bias) with optional fused SwiGLU epilogue ('silu': w rows gate/up
     interleaved in 16-row groups, output width w.shape[0] // 2). `defer=True` (no bias /
     epilogue): when the plan splits K, return a `Partial` whose reduce the consumer fuses."""
+    rn = None
+    if isinstance(x, RowNormed):   # consumer of a row-split RMSNorm: the GEMM applies 1/rms
+        rn, x = x, x.y
     if not _gpu(x):
         return ref.linear(x, w, bias, epilogue, out)
     if defer and bias is None and epilogue == "none":
@@ -294,7 +335,10 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
             out = torch.empty(M, N, dtype=x.dtype, device=x.device)
         need = torch.ops.bfly.gemm_workspace_size(M, N, x.shape[1])
         ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
-        sk = torch.ops.bfly.gemm_deferred(x, w, out, ws)
+        if rn is not None:
+            sk = torch.ops.bfly.gemm_deferred_rs(x, w, out, ws, rn.ssp, rn.eps)
+        else:
+            sk = torch.ops.bfly.gemm_deferred(x, w, out, ws)
         if sk == 1:
             return out
         off = torch.ops.bfly.gemm_slab_offset()
@@ -310,7 +354,10 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     # zero-initialised once: its head holds the split-K arrival counters, which every GEMM
     # leaves re-armed at zero
     ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True) if need else None
-    torch.ops.bfly.gemm(x, w, out, bias, epi, ws)
+    if rn is not None:
+        torch.ops.bfly.gemm_rs(x, w, out, bias, epi, ws, rn.ssp, rn.eps)
+    else:
+        torch.ops.bfly.gemm(x, w, out, bias, epi, ws)
     return out
 
 

@@ -43,6 +43,10 @@ define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0:
 define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
+define("BFLY_NORM_ROWSCALE", True, _bool, "decode add+RMSNorm split over (row, 1024-column) workgroups that write x * g "
+       "and partial sums of squares; the consuming QKV / gate-up GEMM applies the 1/rms row scale in its epilogue "
+       "(tp == 1, batches <= BFLY_NORM_ROWSCALE_MAX_ROWS; 0: one-workgroup-per-row add+RMSNorm)")
+define("BFLY_NORM_ROWSCALE_MAX_ROWS", 256, int, "largest batch that takes the row-split add+RMSNorm")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
 define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "

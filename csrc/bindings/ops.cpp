@@ -377,6 +377,99 @@ int64_t gemm_deferred(const Tensor& x, const Tensor& w, Tensor& out, Tensor& wor
   return rc;
 }
 
+// RMSNorm row scale of a consumer GEMM: ssp [M, chunks] f32 partial sums of squares written by
+// rms_norm_rows for X = x * g rows of width K.
+static bfly::RowScale row_scale(const Tensor& ssp, double eps, int M, int K) {
+  CHECK_GPU(ssp);
+  TORCH_CHECK(ssp.scalar_type() == at::kFloat && ssp.dim() == 2 && ssp.is_contiguous() && ssp.size(0) == M,
+              "row scale: ssp must be [M, chunks] f32");
+  return bfly::RowScale{ssp.data_ptr<float>(), (int)ssp.size(1), 1.f / (float)K, (float)eps};
+}
+
+// gemm() with the consumer RMSNorm row scale (X rows = x * g of rms_norm_rows)
+void gemm_rs(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& bias,
+             int64_t epilogue, const c10::optional<Tensor>& workspace, const Tensor& ssp, double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm_rs: 2-D operands");
+  CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 128 == 0, "gemm_rs: shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_rs: row strides % 8");
+  const int nout = epilogue == bfly::EPI_SILU ? N / 2 : N;
+  TORCH_CHECK(out.size(0) == M && out.size(1) == nout, "gemm_rs: out shape");
+  const bfly::bf16* bp = nullptr;
+  if (epilogue == bfly::EPI_BIAS) {
+    TORCH_CHECK(bias.has_value() && bias->numel() == N, "gemm_rs: bias required");
+    CHECK_BF16(*bias);
+    bp = bf(*bias);
+  }
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  if (workspace.has_value()) {
+    ws = reinterpret_cast<float*>(workspace->data_ptr());
+    ws_bytes = workspace->numel() * workspace->element_size();
+  }
+  const bfly::RowScale rs = row_scale(ssp, eps, M, K);
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_gemm(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, epilogue, bp,
+                                   bf(out), out.stride(0), ws, ws_bytes, cur_stream(), &rs);
+  TORCH_CHECK(rc == 0, "gemm_rs: unsupported plan M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
+}
+
+int64_t gemm_deferred_rs(const Tensor& x, const Tensor& w, Tensor& out, Tensor& workspace, const Tensor& ssp,
+                         double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm_deferred_rs: 2-D operands");
+  CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 128 == 0, "gemm_deferred_rs: shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_deferred_rs: row strides % 8");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.is_contiguous(), "gemm_deferred_rs: out");
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_contiguous(), "gemm_deferred_rs: workspace");
+  const bfly::RowScale rs = row_scale(ssp, eps, M, K);
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_gemm_deferred(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, bf(out),
+                                            out.stride(0), workspace.data_ptr<float>(),
+                                            workspace.numel() * 4, cur_stream(), &rs);
+  TORCH_CHECK(rc > 0, "gemm_deferred_rs: unsupported plan M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
+  return rc;
+}
+
+// Row-split add + RMSNorm for a row-scaling consumer GEMM: out = x * w (un-normalised),
+// ssp [rows, chunks] = per-chunk sums of squares. x: bf16 [rows, dim] or f32 slabs [sk, rows, dim].
+void rms_norm_rows(const Tensor& x, const Tensor& w, Tensor& out, Tensor& ssp,
+                   const c10::optional<Tensor>& residual) {
+  CHECK_GPU(x); CHECK_BF16(w); CHECK_BF16(out);
+  const bool slabs = x.scalar_type() == at::kFloat;
+  TORCH_CHECK(slabs ? (x.dim() == 3 && x.is_contiguous()) : (x.dim() == 2 && x.scalar_type() == at::kBFloat16),
+              "rms_norm_rows: x must be bf16 [rows, dim] or f32 slabs [sk, rows, dim]");
+  const int sk = slabs ? x.size(0) : 0;
+  const int rows = x.size(x.dim() - 2), dim = x.size(x.dim() - 1);
+  TORCH_CHECK(dim % 8 == 0 && w.numel() == dim && w.is_contiguous(), "rms_norm_rows: dim / weight");
+  if (!slabs) {
+    CHECK_INNER(x); CHECK_ALIGN16(x);
+    TORCH_CHECK(x.stride(0) % 8 == 0, "rms_norm_rows: row stride % 8");
+  }
+  TORCH_CHECK(out.is_contiguous() && out.size(0) == rows && out.size(1) == dim, "rms_norm_rows: out");
+  TORCH_CHECK(ssp.scalar_type() == at::kFloat && ssp.is_contiguous() && ssp.dim() == 2 && ssp.size(0) == rows &&
+                  ssp.size(1) == bfly::rmsnorm_rows_chunks(dim),
+              "rms_norm_rows: ssp must be [rows, ", bfly::rmsnorm_rows_chunks(dim), "] f32");
+  bfly::bf16* res = nullptr;
+  if (residual.has_value()) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) == rows && residual->size(1) == dim,
+                "rms_norm_rows: residual");
+    res = bf(*residual);
+  }
+  c10::DeviceGuard g(out.device());
+  const int rc = bfly::launch_rmsnorm_rows(slabs ? nullptr : bf(x), slabs ? 0 : x.stride(0), res, bf(w), bf(out),
+                                           ssp.data_ptr<float>(), rows, dim, res != nullptr, cur_stream(),
+                                           slabs ? x.data_ptr<float>() : nullptr, sk);
+  TORCH_CHECK(rc == 0, "rms_norm_rows: launch failed (rc=", rc, ")");
+}
+
 void splitk_reduce(const Tensor& slabs, Tensor& out) {
   CHECK_GPU(slabs);
   TORCH_CHECK(slabs.scalar_type() == at::kFloat && slabs.dim() == 3 && slabs.is_contiguous(), "splitk_reduce: slabs [sk, M, N] f32");
@@ -827,6 +920,13 @@ TORCH_LIBRARY(bfly, m) {
   m.def("splitk_reduce(Tensor slabs, Tensor(a!) out) -> ()");
   m.def("rms_norm_partial(Tensor slabs, Tensor w, float eps, Tensor(a!) out, Tensor(b!)? residual) -> ()");
   m.def("gemm_slab_offset() -> int", []() -> int64_t { return (int64_t)bfly::gemm_slab_offset_floats(); });
+  m.def("gemm_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace, "
+        "Tensor ssp, float eps) -> ()");
+  m.def("gemm_deferred_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) workspace, Tensor ssp, float eps) -> int");
+  m.def("rms_norm_rows(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) ssp, Tensor(c!)? residual) -> ()");
+  m.def("rms_norm_rows_chunks(int dim) -> int", [](int64_t dim) -> int64_t { return bfly::rmsnorm_rows_chunks(dim); });
+  m.def("gemm_rowscale_check(int M, int N, int K, int epilogue) -> int",
+        [](int64_t M, int64_t N, int64_t K, int64_t e) -> int64_t { return bfly::gemm_rowscale_check(M, N, K, e); });
   m.def("kv_append(Tensor k, Tensor v, Tensor slots, Tensor(a!) k_cache, Tensor(b!) v_cache) -> ()");
   m.def("silu_mul(Tensor gu, Tensor(a!) out, int interleave) -> ()");
   m.def("gelu(Tensor x, Tensor(a!) out) -> ()");
@@ -909,6 +1009,9 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("gemm_deferred", &gemm_deferred);
   m.impl("splitk_reduce", &splitk_reduce);
   m.impl("rms_norm_partial", &rms_norm_partial);
+  m.impl("gemm_rs", &gemm_rs);
+  m.impl("gemm_deferred_rs", &gemm_deferred_rs);
+  m.impl("rms_norm_rows", &rms_norm_rows);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("attn_lse_merge", &attn_lse_merge);

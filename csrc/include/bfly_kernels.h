@@ -11,6 +11,14 @@ typedef __bf16 bf16;
 
 enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_SILU = 2 };
 
+// Per-row output scale of a GEMM whose X rows are un-normalised RMSNorm inputs (x * g):
+// row m is multiplied by rsqrt(sum_c ss[m * chunks + c] * inv_dim + eps) before the epilogue.
+struct RowScale {
+  const float* ss;   // nullptr: no scaling
+  int chunks;
+  float inv_dim, eps;
+};
+
 struct GemmPlan {
   int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 3 = decode ring,
              // 4 = 256x256 8-phase big tile (BK 64, prefill; kind 2 was the removed ring kernel)
@@ -26,6 +34,13 @@ struct GemmPlan {
 void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y,
                     long y_stride, int rows, int dim, float eps, bool add_residual,
                     hipStream_t stream, const float* part = nullptr, int sk = 0);
+// Row-split add + RMSNorm whose consumer GEMM applies the row scale: writes y = x * w and the
+// partial sums of squares ssp[rows][rmsnorm_rows_chunks(dim)]; pass RowScale{ssp, chunks, 1/dim,
+// eps} to the GEMM that consumes y.
+int rmsnorm_rows_chunks(int dim);
+int launch_rmsnorm_rows(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y, float* ssp,
+                        int rows, int dim, bool add_residual, hipStream_t stream,
+                        const float* part = nullptr, int sk = 0);
 void launch_layernorm(const bf16* x, bf16* residual, const bf16* w, const bf16* b, bf16* y,
                       int rows, int dim, float eps, bool add_residual, hipStream_t stream);
 
@@ -74,18 +89,21 @@ int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, 
                      int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                      size_t ws_bytes, hipStream_t stream);
 int gemm_check(int M, int N, int K, int epi);
+// 0 if the auto plan for this shape takes a RowScale (tile and decode-ring kernels)
+int gemm_rowscale_check(int M, int N, int K, int epi);
 // Y = X W^T without epilogue; when the plan splits K, the f32 slabs are left in the workspace
 // (at gemm_slab_offset_floats(), layout [sk][M][N]) for the consumer kernel to reduce, and the
 // split count is returned; otherwise `out` is written and 1 is returned. < 0: error.
 int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
-                         bf16* out, long ldo, float* ws, size_t ws_bytes, hipStream_t stream);
+                         bf16* out, long ldo, float* ws, size_t ws_bytes, hipStream_t stream,
+                         const RowScale* rs = nullptr);
 size_t gemm_slab_offset_floats();
 void launch_splitk_reduce(const float* part, int sk, int M, int N, bf16* out, long ldo,
                           hipStream_t stream);
 void gemm_set_splitk_fixup(bool on);   // in-kernel split-K reduction (default: env / off)   // 0 if the auto plan can run this shape
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
-                hipStream_t stream);
+                hipStream_t stream, const RowScale* rs = nullptr);
 
 // attention.hip
 int attn_decode_splits(int max_ctx, int part_tokens);

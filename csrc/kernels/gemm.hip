@@ -352,14 +352,27 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int chunk) 
 // hold C^T: acc[i][j][r] = C[m = mw + 16i + (lane&15)][n = nw + 16j + 4(lane>>4) + r] — four
 // consecutive columns per lane, stored as one 16-B slab write or one 8-B bf16 write.
 // `pslab`: this workgroup's split-K slab from row m0 on (nullptr: apply the epilogue).
+// `rsc`: RMSNorm row scale of a consumer GEMM (RowScale, ss == nullptr: none), applied to the
+// accumulators first, so split-K slabs, the bias and the SiLU all see the normalised rows.
 template <int TI, int TJ>
 __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw, int nw, int lane,
                                               int M, int N, int epi, const bf16* __restrict__ bias,
                                               bf16* __restrict__ out, long ldo, float* __restrict__ pslab,
-                                              int m0) {
+                                              int m0, const RowScale& rsc) {
   const int lr = lane & 15, lc = 4 * (lane >> 4);
   const auto rs = slab_rsrc(pslab, pslab ? (long)(M - m0) * N * 4 : 0);
   const bool vec = (ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
+  float sc[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int m = mw + 16 * i + lr;
+    sc[i] = 1.f;
+    if (rsc.ss != nullptr && m < M) {
+      float t = 0.f;
+      for (int c = 0; c < rsc.chunks; ++c) t += rsc.ss[(long)m * rsc.chunks + c];
+      sc[i] = rsqrtf(t * rsc.inv_dim + rsc.eps);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const int m = mw + 16 * i + lr;
@@ -368,17 +381,17 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw
     for (int j = 0; j < TJ; ++j) {
       const int n = nw + 16 * j + lc;
       if (pslab) {
-        store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j]);
+        store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j] * sc[i]);
       } else if (epi == EPI_SILU) {
         if constexpr (TJ % 2 == 0) {   // gate/up 16-row groups pair up inside the wave
           if (j & 1) continue;
           f32x4 h;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) h[r] = silu(acc[i][j][r]) * acc[i][j + 1][r];
+          for (int r = 0; r < 4; ++r) h[r] = silu(acc[i][j][r] * sc[i]) * (acc[i][j + 1][r] * sc[i]);
           store_out4(out, ldo, m, nw / 2 + 16 * (j / 2) + lc, h, vec);
         }
       } else {
-        f32x4 v = acc[i][j];
+        f32x4 v = acc[i][j] * sc[i];
         if (epi == EPI_BIAS) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += bf2f(bias[n + r]);
@@ -406,7 +419,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
                  bf16* __restrict__ out, long ldo, float* __restrict__ part,
                  int* __restrict__ counters, const int* __restrict__ grows = nullptr,
                  const int4* __restrict__ gtiles = nullptr, const int* __restrict__ gcount = nullptr,
-                 long w_estride = 0) {
+                 long w_estride = 0, RowScale rsc = RowScale{nullptr, 0, 0.f, 0.f}) {
   constexpr int WNW = 4 / WMW;                // waves along M x waves along N
   constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
@@ -490,7 +503,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     if (++buf == STAGES) buf = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)blockIdx.y * m_slab * N + (long)m0 * N : nullptr, m0);
+                        part ? part + (long)blockIdx.y * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
   if (part && counters && splitk_arrive(counters + tile, gridDim.y, reinterpret_cast<int*>(smem)))
     splitk_fixup(part, gridDim.y, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
 }
@@ -542,7 +555,7 @@ template <int BM, int BN, int NWM, int NWN, int SW>
 __global__ void __launch_bounds__(kDecThreads)
 gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+                bf16* __restrict__ out, long ldo, float* __restrict__ part, RowScale rsc) {
   constexpr int SX = 3, NW = NWM * NWN;
   static_assert(NW * 64 <= kDecThreads && SW >= SX, "decode ring configuration");
   constexpr int WM = BM / NWM, WN = BN / NWN;   // per-wave output block
@@ -610,7 +623,7 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
     if (++wslot == SW) wslot = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
+                        part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0, rsc);
 }
 
 // Prefill tiles are walked in GROUP_M super-rows inside each XCD's contiguous range, so the
@@ -820,7 +833,8 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
   tile_epilogue<8, 4>(acc, m0 + wr * 128, n0 + wc * 64, lane, M, N, epi, bias, out, ldo,
-                      part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0);
+                      part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0,
+                      RowScale{nullptr, 0, 0.f, 0.f});
 }
 
 // ---------------------------------------------------------------------------------------
@@ -866,7 +880,7 @@ static void init_nt_policy() {
 template <int BM, int BN, int WMW, int STAGES>
 static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                     hipStream_t stream) {
+                     hipStream_t stream, const RowScale& rsc) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const size_t lds = (size_t)STAGES * (BM + BN) * kBK * 2;
@@ -879,13 +893,13 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   }
   gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
-      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr);
+      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr, nullptr, nullptr, nullptr, 0, rsc);
 }
 
 template <int BM, int BN, int NWM, int NWN, int SW>
 static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                    hipStream_t stream) {
+                    hipStream_t stream, const RowScale& rsc) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   constexpr size_t lds = (size_t)(3 * BM + SW * BN) * kBK * 2;
@@ -898,7 +912,7 @@ static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
   }
   dim3 grid(tiles, sk);
   gemm_dec_kernel<BM, BN, NWM, NWN, SW><<<grid, NWM * NWN * 64, lds, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr);
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, rsc);
 }
 
 static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
@@ -1054,7 +1068,10 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 // `dry`: validate only (the plan is supported for this shape/epilogue) without launching.
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
-                    hipStream_t stream, bool dry = false, bool defer = false) {
+                    hipStream_t stream, bool dry = false, bool defer = false,
+                    const RowScale* rs = nullptr) {
+  const RowScale rsc = rs ? *rs : RowScale{nullptr, 0, 0.f, 0.f};
+  if (rs != nullptr && p.kind != 1 && p.kind != 3) return -4;   // row scale: tile / ring epilogues only
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
@@ -1067,7 +1084,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     bool done = false;
 #define DEC_CASE(BM_, BN_, NWM_, NWN_, SW_)                                                      \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == NWM_ && p.nt == NWM_ * NWN_ && p.mt == SW_) { \
-    if (!dry) run_dec<BM_, BN_, NWM_, NWN_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream); \
+    if (!dry) run_dec<BM_, BN_, NWM_, NWN_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                 \
   }
     DEC_CASE(128, 224, 8, 1, 4) DEC_CASE(128, 224, 8, 1, 3) DEC_CASE(128, 256, 8, 1, 3)
@@ -1101,7 +1118,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     const int st = p.mt > 0 ? p.mt : 2;   // tile plans reuse `mt` as the pipeline depth
 #define TL_CASE(BM_, BN_, WMW_, ST_)                                                            \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_ && st == ST_) {                       \
-    if (!dry) run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream); \
+    if (!dry) run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                \
   }
 #define TL_ST(BM_, BN_, WMW_) TL_CASE(BM_, BN_, WMW_, 2) TL_CASE(BM_, BN_, WMW_, 3) TL_CASE(BM_, BN_, WMW_, 4)
@@ -1142,6 +1159,13 @@ static GemmPlan select_plan(int M, int N, int K, int epi) {
   if (run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true) != 0)
     p = plan_gemm_heuristic(M, N, K);
   return p;
+}
+
+int gemm_rowscale_check(int M, int N, int K, int epi) {
+  if (M <= 0) return 0;
+  const RowScale probe{nullptr, 0, 0.f, 0.f};
+  return run_plan(select_plan(M, N, K, epi), nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0,
+                  nullptr, nullptr, true, false, &probe);
 }
 
 // Grouped expert GEMM (MoE): BM x 128 tile (BM = 64 or 128 rows per expert tile, chosen by
@@ -1193,14 +1217,15 @@ int gemm_check(int M, int N, int K, int epi) {
 }
 
 int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
-                         bf16* out, long ldo, float* ws, size_t ws_bytes, hipStream_t stream) {
+                         bf16* out, long ldo, float* ws, size_t ws_bytes, hipStream_t stream,
+                         const RowScale* rs) {
   if (M <= 0) return 1;
   GemmPlan p = select_plan(M, N, K, EPI_NONE);
   if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
     p.sk = 1;
   const bool defer = p.sk > 1 && !(fixup_enabled() && p.kind < 2);
   const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, out, ldo, ws, stream,
-                          false, defer);
+                          false, defer, rs);
   if (rc != 0) return rc;
   return defer ? p.sk : 1;
 }
@@ -1217,12 +1242,12 @@ void launch_splitk_reduce(const float* part, int sk, int M, int N, bf16* out, lo
 
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
-                hipStream_t stream) {
+                hipStream_t stream, const RowScale* rs) {
   if (M <= 0) return 0;
   GemmPlan p = select_plan(M, N, K, epi);
   if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
     p.sk = 1;
-  return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream);
+  return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream, false, false, rs);
 }
 
 }  // namespace bfly

@@ -132,6 +132,80 @@ rmsnorm_partial_kernel(const float* __restrict__ part, int sk, long slab, bf16* 
   }
 }
 
+// Row-split add + RMSNorm for decode-sized batches whose consumer GEMM applies the row scale
+// (launch_gemm(..., rs)). The norm is linear in its row scale: norm(x) W^T = rsqrt(ms(x) + eps)
+// * ((x * g) W^T), so this kernel writes y = x * g and each (row, 1024-column chunk) workgroup
+// only its partial sum of squares ssp[row][chunk]; the GEMM epilogue sums the chunk partials
+// (the kernel boundary is the hand-off: no inter-workgroup protocol) and scales its rows.
+// Why: rmsnorm_partial_kernel gives a row (sk x dim x 4 bytes of slabs) to ONE workgroup, so at
+// a batch of 64 rows 64 CUs pull 8-16 MB while 192 idle; here rows x chunks workgroups share it.
+// x is the sum of `sk` f32 slabs [sk][rows][dim] (part != nullptr) or a bf16 [rows][dim] input.
+constexpr int kNormSplitThreads = 128;
+constexpr int kNormSplitCols = kNormSplitThreads * 8;
+
+__global__ void __launch_bounds__(kNormSplitThreads)
+rmsnorm_rows_kernel(const float* __restrict__ part, int sk, long slab, const bf16* __restrict__ x,
+                    long x_stride, bf16* __restrict__ residual, const bf16* __restrict__ w,
+                    bf16* __restrict__ y, float* __restrict__ ssp, int dim, int add_residual) {
+  __shared__ float red[4];
+  const long row = blockIdx.x;
+  const int col = blockIdx.y * kNormSplitCols + threadIdx.x * 8;
+  float ss = 0.f;
+  if (col < dim) {
+    bf16x8 a;
+    if (part != nullptr) {
+      const float* pr = part + row * (long)dim + col;
+      f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+#pragma unroll 8
+      for (int k = 1; k < sk; ++k) {
+        lo += *reinterpret_cast<const f32x4*>(pr + k * slab);
+        hi += *reinterpret_cast<const f32x4*>(pr + k * slab + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { a[j] = f2bf(lo[j]); a[j + 4] = f2bf(hi[j]); }
+    } else {
+      a = *reinterpret_cast<const bf16x8*>(x + row * x_stride + col);
+    }
+    float v[8];
+    if (add_residual) {
+      bf16x8* rp = reinterpret_cast<bf16x8*>(residual + row * (long)dim + col);
+      const bf16x8 r = *rp;
+      bf16x8 sm;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sm[j] = f2bf(bf2f(a[j]) + bf2f(r[j]));   // the stored bf16 residual is what is normalised
+        v[j] = bf2f(sm[j]);
+      }
+      *rp = sm;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+    }
+    const bf16x8 g = *reinterpret_cast<const bf16x8*>(w + col);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ss += v[j] * v[j];
+      o[j] = f2bf(v[j] * bf2f(g[j]));
+    }
+    *reinterpret_cast<bf16x8*>(y + row * (long)dim + col) = o;
+  }
+  ss = block_sum(ss, red);
+  if (threadIdx.x == 0) ssp[row * gridDim.y + blockIdx.y] = ss;
+}
+
+int rmsnorm_rows_chunks(int dim) { return (dim + kNormSplitCols - 1) / kNormSplitCols; }
+
+int launch_rmsnorm_rows(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y, float* ssp,
+                        int rows, int dim, bool add_residual, hipStream_t stream, const float* part, int sk) {
+  if (dim % 8 != 0) return -1;
+  if (rows <= 0) return 0;
+  dim3 grid(rows, rmsnorm_rows_chunks(dim));
+  rmsnorm_rows_kernel<<<grid, kNormSplitThreads, 0, stream>>>(part, sk, (long)rows * dim, x, x_stride, residual,
+                                                              w, y, ssp, dim, add_residual ? 1 : 0);
+  return 0;
+}
+
 template <int NV>
 __global__ void __launch_bounds__(kNormThreads)
 layernorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ residual,

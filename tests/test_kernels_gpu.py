@@ -416,6 +416,56 @@ def test_gemm_deferred_reduce_fusions(M, N, K):
         torch.testing.assert_close(vc[1], vc[0], atol=2e-2, rtol=2e-2)
 
 
+# (M, hidden, consumer N, epilogue, deferred): Llama-3-70B QKV (tile plan, split-K slabs) and
+# gate/up (tile, SiLU), Llama-3-8B QKV (decode-ring plan), a biased consumer, ragged row counts
+ROWSCALE_CASES = [(64, 8192, 10240, "none", True), (64, 8192, 57344, "silu", False),
+                  (64, 4096, 6144, "none", True), (61, 4096, 28672, "silu", False),
+                  (200, 8192, 1024, "bias", False), (33, 8192, 10240, "none", False)]
+
+
+@pytest.mark.parametrize("M,H,N,epi,defer", ROWSCALE_CASES)
+@pytest.mark.parametrize("src", ["slabs", "bf16"])
+def test_rms_norm_rows_with_rowscale_consumer(M, H, N, epi, defer, src):
+    """Row-split add + RMSNorm (y = x * g, partial sums of squares) followed by a GEMM that
+    applies the 1/rms row scale in its epilogue == fp32 add + RMSNorm + GEMM; the residual
+    update is bit-identical to the one-workgroup-per-row kernel's."""
+    if not ops.rowscale_ok(M, N, H, epi):
+        pytest.skip(f"plan for {M}x{N}x{H} takes no row scale")
+    K0 = 8192   # long enough that the producer GEMM splits K (slab input)
+    x0 = _bf(M, K0, seed=80)
+    w0 = _bf(H, K0, scale=1.0 / math.sqrt(K0), seed=81)
+    g = (1.0 + 0.5 * _bf(H, seed=82).float()).to(torch.bfloat16)
+    W = _bf(N, H, scale=1.0 / math.sqrt(H), seed=83)
+    b = _bf(N, seed=84) if epi == "bias" else None
+    r0 = _bf(M, H, seed=85)
+    delta = ops.linear(x0, w0)
+
+    def make_src():
+        if src == "bf16":
+            return delta
+        p = ops.linear(x0, w0, defer=True)
+        if not isinstance(p, ops.Partial):
+            pytest.skip("producer plan does not split K")
+        return p
+
+    ra, rb = r0.clone(), r0.clone()
+    ya = ops.rms_norm(make_src(), g, 1e-5, residual=ra)
+    rn = ops.rms_norm(make_src(), g, 1e-5, residual=rb, rows=True)
+    assert isinstance(rn, ops.RowNormed)
+    torch.testing.assert_close(rb, ra, atol=0, rtol=0)
+    got = ops.linear(rn, W, bias=b, epilogue="silu" if epi == "silu" else "none", defer=defer)
+    got = ops.materialize(got)
+    # fp32 reference from the stored bf16 residual
+    s = rb.float()
+    yn = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    want = ref.linear(yn.cpu(), W.float().cpu(), None if b is None else b.float().cpu(),
+                      "silu" if epi == "silu" else "none")
+    _close(got, want, 3e-2, 3e-2)
+    # and against the existing (normalise, then GEMM) path
+    base = ops.linear(ya, W, bias=b, epilogue="silu" if epi == "silu" else "none")
+    _close(got, base, 3e-2, 3e-2)
+
+
 @pytest.mark.parametrize("T,E,El,e0,k,H,F", [(300, 8, 8, 0, 2, 512, 256), (64, 8, 4, 4, 2, 256, 128),
                                            (1000, 8, 2, 2, 2, 256, 128), (5, 8, 8, 0, 2, 256, 128)])
 def test_moe_sparse_ffn(T, E, El, e0, k, H, F):

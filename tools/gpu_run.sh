@@ -17,6 +17,8 @@ mkdir -p gpurun_out
 n=0
 for step in "$@"; do
   n=$((n + 1))
+  # never overwrite an earlier invocation's logs in the same call (A/B runs chain invocations)
+  while compgen -G "gpurun_out/*_$n.log" > /dev/null; do n=$((n + 1)); done
   kind=${step%%=*}
   arg=""
   [[ "$step" == *=* ]] && arg=${step#*=}
