@@ -1092,7 +1092,6 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     DEC_CASE(128, 160, 8, 1, 4) DEC_CASE(128, 80, 8, 1, 6) DEC_CASE(128, 64, 8, 1, 8)
     DEC_CASE(128, 64, 4, 2, 8) DEC_CASE(64, 128, 4, 2, 6) DEC_CASE(64, 256, 4, 2, 4)
     DEC_CASE(64, 224, 4, 1, 4) DEC_CASE(64, 160, 4, 2, 5) DEC_CASE(64, 64, 4, 2, 8)
-    DEC_CASE(128, 128, 4, 2, 7) DEC_CASE(128, 128, 8, 1, 7) DEC_CASE(128, 64, 4, 2, 12)
 #undef DEC_CASE
     if (!done) return -2;
   } else if (p.kind == 0) {
