@@ -5,6 +5,8 @@
 # the IPC all-reduce and the IPC EP exchange; each run under its own time limit, the first
 # failure ends the script.
 #   tools/rehearse.sh [MODEL:N:PLAN ...]   -> gpurun_out/rehearse_<model>_<plan>.log
+# REHEARSE_ARGS replaces the default bench sizes (e.g. the real Llama-3-70B at its default batch:
+#   REHEARSE_ARGS="--steps 8 --warmup 2 --prompt-len 256" tools/rehearse.sh llama3-70b:2:tp2)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
@@ -16,7 +18,7 @@ for r in "${runs[@]}"; do
   IFS=: read -r model n plan <<< "$r"
   log=gpurun_out/rehearse_${model}_${n}_${plan}.log
   timeout -k 10 420 python -m butterfly_amd launch -n "$n" -- python bench.py --gpus "$n" --model "$model" \
-    --plan "$plan" --steps 8 --warmup 2 --batch-per-gpu 8 --prompt-len 64 --no-probe > "$log" 2>&1
+    --plan "$plan" ${REHEARSE_ARGS:---steps 8 --warmup 2 --batch-per-gpu 8 --prompt-len 64} --no-probe > "$log" 2>&1
   rc=$?
   grep -h '"metric"' "$log" | head -n 1 | cut -c1-220
   echo "[$rc] $model n=$n plan=$plan"
