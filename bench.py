@@ -151,6 +151,10 @@ def run(a) -> int:
     rank, world, local = init_distributed()
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    if world > 1:
+        # a multi-GPU step that hangs (wedged collective / peer) dumps every thread's stack and
+        # ends the rank with exit 75 instead of waiting for the driver's kill (utils/health.py)
+        os.environ.setdefault("BFLY_STEP_TIMEOUT_S", "300")
     if use_gpu:
         # one GPU per rank; ranks sharing a GPU (gloo test mode) all use device 0
         torch.cuda.set_device(local % torch.cuda.device_count())
