@@ -387,17 +387,20 @@ def check_custom_ar(rank: int, world: int, pgs: dict, vote: Callable[[bool], boo
             car = CustomAllReduce(ranks, rank % n, pg, max_bytes=8 << 20, device=dev)
             ok = car.ok
             if ok:
-                for two in ([False, True] if n >= 4 else [False]):
-                    x = (torch.arange(64 * 8192, device=dev, dtype=torch.float32).view(64, 8192) % 13 + rank)
-                    x = x.to(torch.bfloat16)
-                    y = x.clone()
-                    car.all_reduce_(y, two_shot=two)
-                    r = x.clone()
-                    dist.all_reduce(r, group=pg)
-                    _sync(dev)
-                    if not torch.equal(y, r) or car.error():
-                        ok = False
-                        details.append(f"n={n} {'two' if two else 'one'}-shot differs from RCCL")
+                # a decode-sized message and the largest the runtime routes here (8 MiB: the
+                # tp8 batch-512 all-reduce); integer-valued rows, so the sums are exact in bf16
+                for rows in (64, (8 << 20) // (8192 * 2)):
+                    for two in ([False, True] if n >= 4 else [False]):
+                        x = (torch.arange(rows * 8192, device=dev, dtype=torch.float32).view(rows, 8192) % 13 + rank)
+                        x = x.to(torch.bfloat16)
+                        y = x.clone()
+                        car.all_reduce_(y, two_shot=two)
+                        r = x.clone()
+                        dist.all_reduce(r, group=pg)
+                        _sync(dev)
+                        if not torch.equal(y, r) or car.error():
+                            ok = False
+                            details.append(f"n={n} {'two' if two else 'one'}-shot {rows}x8192 differs from RCCL")
             else:
                 details.append(f"n={n} self-test failed")
         except Exception as e:  # noqa: BLE001
