@@ -238,6 +238,9 @@ class Communicator:
             self.groups[axis].native = nc
         self.groups["world"].native = world
         self.pp_native_send, self.pp_native_recv = pp_edges(world, self.mesh, self.rank)
+        if getattr(self, "_rccl_poller", None) is None:
+            from .rccl import start_error_poller
+            self._rccl_poller = start_error_poller()
         return natives
 
     @property

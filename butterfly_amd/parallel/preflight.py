@@ -124,6 +124,10 @@ class _Watchdog:
                     traceback.print_stack(sys._current_frames().get(threading.main_thread().ident), file=sys.stderr)
                     sys.stderr.flush()
                 finally:
+                    # take the native RCCL communicators down first (a hung check is most often
+                    # a collective whose kernel waits on a peer), bounded, then exit
+                    from ..utils.health import run_abort_hooks
+                    run_abort_hooks()
                     self.exit_fn(HANG_EXIT_CODE)
                 return
 

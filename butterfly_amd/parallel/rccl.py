@@ -49,6 +49,10 @@ class RcclComm:
     def create(cls, uid: torch.Tensor, nranks: int, rank: int, ranks: Optional[list] = None) -> "RcclComm":
         """ncclCommInitRank on the current device with an id every member already holds."""
         h = _lib().rccl_init(uid.cpu().contiguous(), nranks, rank)
+        # the failure paths (health._default_failure, the preflight's hang exit) abort every
+        # native communicator before the process exits
+        from ..utils.health import register_abort_hook
+        register_abort_hook(abort_all)
         return cls(h, ranks if ranks is not None else list(range(nranks)))
 
     @classmethod
@@ -123,6 +127,42 @@ class RcclComm:
         if not self._closed:
             self._closed = True
             _lib().rccl_release(self.handle, abort)
+
+
+def live_handles() -> list:
+    """Handles of every live native communicator in this process."""
+    return [int(h) for h in _lib().rccl_live()]
+
+
+def abort_all() -> int:
+    """ncclCommAbort every live communicator (safe from any thread, also while another thread
+    is blocked in a collective): the failure-path hook. Returns how many were aborted."""
+    return int(_lib().rccl_abort_all())
+
+
+def async_errors() -> Optional[str]:
+    """None when every live communicator is healthy, else a description of the first
+    asynchronous error (the ErrorPoller check)."""
+    lib = _lib()
+    for h in lib.rccl_live():
+        try:
+            err = int(lib.rccl_async_error(h))
+        except RuntimeError:   # released between the listing and the query
+            continue
+        if err:
+            return f"RCCL communicator {int(h)} async error {err}"
+    return None
+
+
+def start_error_poller(period: Optional[float] = None, on_failure=None):
+    """Daemon thread polling `async_errors` every BFLY_RCCL_POLL_S seconds (0 = off): a peer
+    that died or a network error is acted on within a second even while the main thread is
+    stuck inside a collective; the failure handler aborts every communicator and exits 75."""
+    from ..utils import flags
+    from ..utils.health import ErrorPoller
+
+    period = flags.get("BFLY_RCCL_POLL_S") if period is None else period
+    return ErrorPoller(async_errors, period=period, on_failure=on_failure, name="bfly-rccl-poll").start()
 
 
 def pp_edges(world: RcclComm, mesh, rank: int) -> tuple:

@@ -68,6 +68,8 @@ define("BFLY_DIST_BACKEND", "", str, "torch.distributed backend override for ini
        "= RCCL with a GPU, gloo without; gloo lets several ranks share one GPU in tests)")
 define("BFLY_FORCE_CPU", False, _bool, "bench.py: run on the CPU reference path even when a GPU is visible "
        "(BASELINE config 1, the gloo plumbing configuration)")
+define("BFLY_RCCL_POLL_S", 1.0, float, "period of the thread polling native RCCL communicators for async errors "
+       "(on one: abort every communicator, exit 75); 0 = off")
 define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
 define("BFLY_STEP_TIMEOUT_S", 0.0, float, "engine step watchdog: terminate a rank whose step exceeds this (0 = off)")

@@ -8,6 +8,9 @@
 * StepWatchdog — arms a timer around each engine step; a step that outlives `timeout` (a hung
   collective, a GPU that stopped responding) dumps every thread's stack (faulthandler) and
   fires `on_failure`.
+* ErrorPoller — a daemon thread polling a check (the native RCCL communicators' async errors)
+  every second; on failure the registered abort hooks (`register_abort_hook`: abort every
+  native communicator) run, bounded, before the process exits with 75.
 * FaultInjector — BFLY_FAULT="rank:step:kind" (kind = hang | exit | nan) makes a chosen rank
   misbehave at a chosen step, so the detection paths are exercised by tests.
 """
@@ -26,11 +29,81 @@ from .logging import get_logger
 log = get_logger("health")
 
 
+_abort_hooks: list = []
+
+
+def register_abort_hook(fn: Callable[[], object]) -> None:
+    """Run `fn` on the failure path before the process exits (parallel/rccl.abort_all: take
+    the native RCCL communicators down so no kernel is left spinning on a dead peer)."""
+    if fn not in _abort_hooks:
+        _abort_hooks.append(fn)
+
+
+def run_abort_hooks(timeout: float = 5.0) -> None:
+    """Run the registered hooks on a daemon thread, bounded by `timeout`: an abort that itself
+    hangs must not keep the process from exiting."""
+    if not _abort_hooks:
+        return
+
+    def run():
+        for fn in list(_abort_hooks):
+            try:
+                fn()
+            except Exception as e:
+                log.warning(f"abort hook {getattr(fn, '__name__', fn)} failed: {e!r}")
+
+    t = threading.Thread(target=run, name="bfly-abort", daemon=True)
+    t.start()
+    t.join(timeout)
+    if t.is_alive():
+        log.error(f"abort hooks still running after {timeout}s; exiting anyway")
+
+
 def _default_failure(reason: str) -> None:
     log.error(f"fatal: {reason}; terminating")
     faulthandler.dump_traceback(all_threads=True)
     sys.stderr.flush()
+    run_abort_hooks()
     os._exit(75)
+
+
+class ErrorPoller:
+    """Polls `check() -> Optional[str]` every `period` seconds on a daemon thread and fires
+    `on_failure(reason)` on the first non-None answer. Used for the native RCCL communicators'
+    asynchronous errors (parallel/rccl.async_errors): the engine's own check_health runs only
+    every 256 steps and never while a step is stuck in a collective; this thread does."""
+
+    def __init__(self, check: Callable[[], Optional[str]], period: float = 1.0,
+                 on_failure: Optional[Callable[[str], None]] = None, name: str = "bfly-errpoll"):
+        self.check, self.period = check, period
+        self.on_failure = on_failure or _default_failure
+        self.name = name
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.failed: Optional[str] = None
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.period):
+            try:
+                reason = self.check()
+            except Exception as e:   # library gone = teardown
+                log.warning(f"{self.name} stopped: {e!r}")
+                return
+            if reason:
+                self.failed = reason
+                self.on_failure(reason)
+                return
+
+    def start(self) -> "ErrorPoller":
+        if self.period > 0:
+            self._thread = threading.Thread(target=self._run, name=self.name, daemon=True)
+            self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread:
+            self._thread.join(timeout=2 * self.period + 1)
 
 
 class HealthMonitor:

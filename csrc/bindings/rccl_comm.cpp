@@ -12,7 +12,9 @@
 //                                          on torch's current stream, in place or into `out`
 //   rccl_group_start / rccl_group_end      batch point-to-point calls (PP fan-out)
 //   rccl_async_error(h)                    ncclCommGetAsyncError, polled by the health monitor
-//   rccl_abort(h) / rccl_destroy(h)
+//   rccl_release(h, abort)                 ncclCommAbort / ncclCommDestroy of one communicator
+//   rccl_live() / rccl_abort_all()         live handles (polled by the async-error watcher);
+//                                          abort every one on the failure path
 //
 // Handles are indices into a process-wide table (a rank drives a few communicators at most).
 // This links the librccl.so torch itself loads, so there is exactly one RCCL in the process.
@@ -194,12 +196,45 @@ int64_t rccl_async_error(int64_t h) {
 }
 
 void rccl_release(int64_t h, bool abort) {
-  ncclComm_t c = comm_of(h);
+  ncclComm_t c = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_mu);
+    TORCH_CHECK(h >= 0 && h < (int64_t)g_comms.size(), "RCCL: bad communicator handle ", h);
+    c = g_comms[h];
     g_comms[h] = nullptr;
   }
+  if (c == nullptr) return;   // already released (or taken down by rccl_abort_all)
   RCCL_CHECK(abort ? ncclCommAbort(c) : ncclCommDestroy(c));
+}
+
+// Handles of the live communicators (the async-error watcher polls these from its own thread).
+std::vector<int64_t> rccl_live() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::vector<int64_t> out;
+  for (size_t i = 0; i < g_comms.size(); ++i)
+    if (g_comms[i] != nullptr) out.push_back((int64_t)i);
+  return out;
+}
+
+// Failure path: abort every live communicator. Communicators are created blocking, so a rank
+// whose peer died sits in a collective (a kernel spinning on a flag that never comes, or a host
+// wait on it); ncclCommAbort from another thread sets the abort flag those kernels poll, which
+// drains the stream and lets the process exit instead of wedging the GPU. The table entries are
+// cleared under the lock and aborted outside it, so a thread blocked in a collective that holds
+// a communicator pointer never deadlocks the abort. Errors are ignored: the process is going
+// down and every communicator must get its abort. Returns how many were aborted.
+int64_t rccl_abort_all() {
+  std::vector<ncclComm_t> victims;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& c : g_comms)
+      if (c != nullptr) {
+        victims.push_back(c);
+        c = nullptr;
+      }
+  }
+  for (ncclComm_t c : victims) (void)ncclCommAbort(c);
+  return (int64_t)victims.size();
 }
 
 }  // namespace
@@ -221,4 +256,6 @@ TORCH_LIBRARY_FRAGMENT(bfly, m) {
   m.def("rccl_group_end() -> ()", &rccl_group_end);
   m.def("rccl_async_error(int comm) -> int", &rccl_async_error);
   m.def("rccl_release(int comm, bool abort=False) -> ()", &rccl_release);
+  m.def("rccl_live() -> int[]", &rccl_live);
+  m.def("rccl_abort_all() -> int", &rccl_abort_all);
 }

@@ -132,6 +132,37 @@ def test_single_rank_communicator_collectives_and_graph():
 
 
 @pytest.mark.gpu
+def test_abort_all_and_error_poller():
+    """The failure path: the async-error poller sees a healthy communicator as healthy, and
+    abort_all takes every live communicator down (a later close of one is a no-op)."""
+    _lib_or_skip()
+    from butterfly_amd.parallel import rccl
+    from butterfly_amd.utils import health
+
+    c = rccl.RcclComm.create(torch.ops.bfly.rccl_unique_id(), 1, 0)
+    sub = c.split(0, 0, [0])
+    assert rccl.abort_all in health._abort_hooks
+    live = rccl.live_handles()
+    assert c.handle in live and sub.handle in live
+    assert rccl.async_errors() is None
+    fired = []
+    p = rccl.start_error_poller(period=0.05, on_failure=fired.append)
+    x = torch.ones(1 << 16, device="cuda")
+    c.all_reduce_(x)
+    torch.cuda.synchronize()
+    import time
+    time.sleep(0.3)
+    p.stop()
+    assert fired == [] and p.failed is None
+    assert rccl.abort_all() >= 2
+    assert c.handle not in rccl.live_handles() and sub.handle not in rccl.live_handles()
+    sub.close()
+    c.close()        # already aborted: no-op
+    with pytest.raises(RuntimeError):
+        c.all_reduce_(x)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,spec", [(2, "tp2"), (4, "dp2xtp2"), (8, "dp4xtp2")])
 def test_native_rccl_matches_torch_multi_gpu(n, spec):
     """Native world + split communicators vs torch.distributed RCCL, one GPU per rank."""

@@ -54,3 +54,49 @@ def test_health_monitor_detects_dead_rank():
     time.sleep(0.5)
     mon.stop()
     assert failures and "rank 1" in failures[0]
+
+
+def test_error_poller_fires_once_on_first_error():
+    import time
+
+    from butterfly_amd.utils.health import ErrorPoller
+
+    answers = [None, None, "comm 3 async error 6", "again"]
+    hits = []
+    p = ErrorPoller(lambda: answers.pop(0) if answers else None, period=0.02, on_failure=hits.append).start()
+    deadline = time.time() + 5
+    while not hits and time.time() < deadline:
+        time.sleep(0.01)
+    p.stop()
+    assert hits == ["comm 3 async error 6"] and p.failed == hits[0]
+    assert answers == ["again"]          # the thread stops after the first failure
+
+
+def test_abort_hooks_run_bounded(monkeypatch):
+    import threading
+    import time
+
+    from butterfly_amd.utils import health
+
+    monkeypatch.setattr(health, "_abort_hooks", [])
+    ran = []
+    block = threading.Event()
+    health.register_abort_hook(lambda: ran.append("a"))
+    health.register_abort_hook(lambda: block.wait(30))      # an abort that hangs
+    t0 = time.time()
+    health.run_abort_hooks(timeout=0.3)
+    assert ran == ["a"] and time.time() - t0 < 5
+    block.set()
+    f = health._abort_hooks[0]
+    health.register_abort_hook(f)                            # idempotent
+    assert len(health._abort_hooks) == 2
+
+
+def test_default_failure_runs_abort_hooks_before_exit(monkeypatch):
+    from butterfly_amd.utils import health
+
+    order = []
+    monkeypatch.setattr(health, "_abort_hooks", [lambda: order.append("abort")])
+    monkeypatch.setattr(health.os, "_exit", lambda code: order.append(("exit", code)))
+    health._default_failure("test")
+    assert order == ["abort", ("exit", 75)]
