@@ -83,3 +83,20 @@ def test_hung_check_exits_75_naming_rank_and_check():
     assert r.returncode == 75, log[-3000:]
     assert "PREFLIGHT-HANG rank=1 check=custom_ar" in log, log[-3000:]
     assert took < 120, took
+
+
+def test_watchdog_runs_abort_hooks_before_exit(monkeypatch):
+    """A hung check most often sits in a collective: the watchdog aborts the native RCCL
+    communicators (the registered abort hooks) before it exits."""
+    from butterfly_amd.parallel.preflight import HANG_EXIT_CODE, _Watchdog
+    from butterfly_amd.utils import health
+
+    order = []
+    monkeypatch.setattr(health, "_abort_hooks", [lambda: order.append("abort")])
+    wd = _Watchdog(rank=3, exit_fn=lambda code: order.append(("exit", code)))
+    wd.arm("native_rccl", 0.05)
+    deadline = time.monotonic() + 10
+    while len(order) < 2 and time.monotonic() < deadline:
+        time.sleep(0.02)
+    wd.close()
+    assert order == ["abort", ("exit", HANG_EXIT_CODE)]
