@@ -189,9 +189,13 @@ void rccl_group_start() { RCCL_CHECK(ncclGroupStart()); }
 void rccl_group_end() { RCCL_CHECK(ncclGroupEnd()); }
 
 // 0 = healthy; otherwise the ncclResult_t of an asynchronous failure (peer gone, timeout).
+// The query runs under the table lock (it is a non-blocking flag read), so the poller thread
+// can never race a concurrent rccl_release / rccl_abort_all into a destroyed communicator.
 int64_t rccl_async_error(int64_t h) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(h >= 0 && h < (int64_t)g_comms.size() && g_comms[h] != nullptr, "RCCL: bad communicator handle ", h);
   ncclResult_t st = ncclSuccess;
-  RCCL_CHECK(ncclCommGetAsyncError(comm_of(h), &st));
+  RCCL_CHECK(ncclCommGetAsyncError(g_comms[h], &st));
   return (int64_t)st;
 }
 
