@@ -220,6 +220,16 @@ def run(a) -> int:
                         use_graphs=not a.no_graphs,
                         graph_batch_sizes=[replica_batch],
                         kv_cache_dtype=a.kv_dtype, async_decode=not a.sync_decode)
+    health = None
+    if world > 1 and flags.get("BFLY_HEARTBEAT_S") > 0:
+        # rank heartbeats through the job's TCPStore (utils/health.py): a rank that dies or
+        # wedges OUTSIDE a step (where the step watchdog cannot see it) aborts the whole job,
+        # native communicators first, instead of leaving its peers in a collective
+        from butterfly_amd.utils.health import HealthMonitor
+
+        period = flags.get("BFLY_HEARTBEAT_S")
+        health = HealthMonitor(dist.distributed_c10d._get_default_store(), rank, world,
+                               period=period, timeout=max(60.0, 12 * period)).start()
     t0 = time.perf_counter()
     device = None if use_gpu else torch.device("cpu")
     eng = LLMEngine(cfg, mesh, ecfg, comm=comm, stage_layers=plan.stages, device=device)
@@ -326,6 +336,13 @@ def run(a) -> int:
         if a.out:
             with open(a.out, "w") as f:
                 f.write(line + "\n")
+    # orderly teardown: graphs, then IPC buffers and native RCCL communicators (bounded
+    # finalize-or-abort, never a hang), then the heartbeat and the process group
+    closed = eng.close()
+    if health is not None:
+        health.stop()
+    if closed:
+        log(f"teardown: {closed}", rank)
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -122,6 +122,14 @@ class LLM:
     def metrics(self) -> dict:
         return self.engine.metrics.summary()
 
+    def close(self) -> dict:
+        """Stop the heartbeat monitor and release the engine's graphs, IPC buffers and native
+        communicators (bounded; LLMEngine.close). Returns the teardown statuses."""
+        if self.health is not None:
+            self.health.stop()
+            self.health = None
+        return self.engine.close()
+
     # ---- request-state snapshots (engine/state.py, SURVEY.md §5.4) -------------------------
     def save_state(self, directory) -> Optional[Path]:
         """Write this replica's request state to <directory>/replica-<dp>.json (one rank per

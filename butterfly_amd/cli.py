@@ -76,26 +76,31 @@ def cmd_generate(a) -> int:
               tokenizer=a.tokenizer)
     prompts = a.prompt or ["Hello"]
     params = SamplingParams(max_tokens=a.max_tokens, temperature=a.temperature, seed=a.seed, ignore_eos=True)
-    restart = int(os.environ.get("BFLY_RESTART", "0") or 0)
-    # the snapshot carries this job's fingerprint: a restart resumes only its own job's state,
-    # never a stale snapshot an earlier, different job left in the directory
+    # a restart is BFLY_RESTART (launch --max-restarts) or torchrun's TORCHELASTIC_RESTART_COUNT
+    restart = max(int(os.environ.get("BFLY_RESTART", "0") or 0),
+                  int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0))
+    # the snapshot carries this job's fingerprint: a run resumes only its own job's state (a
+    # restart, or a manual re-run of the same job), never a stale snapshot an earlier, different
+    # job left in the directory — and only such a foreign snapshot is ever deleted
     job = state.job_fingerprint(a.model, prompts, params)
     llm.engine.job_id = job
     snap = state.replica_path(a.snapshot_dir, llm.dp_rank) if a.snapshot_dir else None
-    if snap is not None and restart == 0 and snap.exists() and llm.engine.coord.tp == 0 and llm.engine.coord.pp == 0:
-        snap.unlink()      # first attempt: whatever is there belongs to another run
-    if snap is not None and restart > 0 and snap.exists() and state.snapshot_job(snap) == job:
-        # restarted job: replay the request state of the failed attempt (engine/state.py)
+    ours = snap is not None and snap.exists() and state.snapshot_job(snap) == job
+    if snap is not None and snap.exists() and not ours:
+        print(f"ignoring {snap}: written by another job", file=sys.stderr)
+        if llm.engine.coord.tp == 0 and llm.engine.coord.pp == 0:
+            snap.unlink()
+    if ours:
+        # replay the request state of the interrupted attempt (engine/state.py)
         outs = llm.resume(a.snapshot_dir, job=job)
         print(f"resumed {len(outs)} requests from {a.snapshot_dir} (restart {restart})", file=sys.stderr)
     else:
-        if snap is not None and restart > 0 and snap.exists():
-            print(f"ignoring {snap}: written by another job", file=sys.stderr)
         outs = llm.generate(prompts, params)
     if llm.rank == 0:
         for o in outs:
             print(json.dumps({"prompt": o.prompt, "text": o.text, "token_ids": o.token_ids,
                               "ttft_s": o.ttft_s, "e2e_s": o.e2e_s}))
+    llm.close()
     return 0
 
 

@@ -192,6 +192,10 @@ class LLMEngine:
         if self._native_pp:
             self.runner.set_pipeline_io(recv_fn=None if coord.pp == 0 else self.comm.recv_native,
                                         sends=coord.pp < mesh.pp - 1)
+        if self.runner.use_graphs and not self.comm.graph_safe():
+            # a data-path collective on gloo (ranks sharing one GPU) cannot be captured: decode
+            # eagerly instead of attempting (and invalidating) a capture
+            self.runner.use_graphs = False
         self.requests: dict[int, Request] = {}
         self._ids = itertools.count()
         self.metrics = Metrics()
@@ -779,6 +783,18 @@ class LLMEngine:
             p.ids = self._sample(out, p.rids)
 
         self._execute(self._ops(1, native_dec), recv, run, send, sample)
+
+    def close(self) -> dict:
+        """Release the engine's device resources in dependency order: captured graphs first
+        (they hold the native communicators' kernels), then the communicator's IPC buffers and
+        native RCCL communicators (bounded finalize-or-abort). Returns the teardown statuses."""
+        # pipeline sends still in flight at shutdown may never be matched (the peer stopped
+        # stepping): they are dropped, not waited for
+        self._sends = []
+        self.runner.close()
+        if self.watchdog is not None:
+            self.watchdog.disarm()
+        return self.comm.close()
 
     # ------------------------------------------------------------------------------------
     def generate(self, prompts: list, params: Optional[SamplingParams] = None) -> list:

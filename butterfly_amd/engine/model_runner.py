@@ -36,6 +36,19 @@ def _to_dev(a, dev) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)
 
 
+def _recover_from_capture(device) -> None:
+    """After a failed capture: wait for the device and clear the sticky capture error, so the
+    eager fallback's first launch does not report it as its own."""
+    try:
+        torch.cuda.synchronize(device)
+    except Exception:  # noqa: BLE001 — the error being cleared may surface here first
+        pass
+    from .. import ops
+
+    if ops.load_library():
+        torch.ops.bfly.hip_clear_error()
+
+
 class _DecodeGraph:
     """Static inputs / output of one decode graph (bucket). The int32 inputs are views of ONE
     device buffer [ids | positions | slots | ctx_lens | block tables], so a step stages them
@@ -221,7 +234,7 @@ class ModelRunner:
 
                 warnings.warn(f"hipGraph capture of decode bucket {bucket} failed ({e!r}); running eagerly")
                 self.eager_buckets.add(bucket)
-                torch.cuda.synchronize(self.device)
+                _recover_from_capture(self.device)
                 return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
         self._stage(g, inp, hidden_in)
         g.graph.replay()
@@ -247,7 +260,7 @@ class ModelRunner:
                         warnings.warn(f"hipGraph capture of decode bucket {bucket} failed ({e!r}); "
                                       "running eagerly")
                         self.eager_buckets.add(bucket)
-                        torch.cuda.synchronize(self.device)
+                        _recover_from_capture(self.device)
                 if g is None:
                     m = self.model
                     g = _DecodeGraph(bucket, self.max_blocks, self.device, m.cfg.hidden_size, m.first)
@@ -334,6 +347,22 @@ class ModelRunner:
         if register:
             self.graphs[bucket] = g
         return g
+
+    def close(self) -> None:
+        """Drop every captured graph and the graph memory pool (before the communicators whose
+        kernels the graphs captured are torn down: parallel/rccl.py)."""
+        for v in self.graphs.values():
+            for g in (v if isinstance(v, list) else [v]):
+                g.graph = None
+                g.send_done = None
+        self.graphs.clear()
+        self.last_instance = None
+        self.pool = None
+        import gc
+
+        gc.collect()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     def capture_all(self, max_batch: int) -> None:
         for b in self.buckets:

@@ -303,6 +303,9 @@ def topkp_threshold(logits, temps, top_k, top_p, reduce_sum=None, reduce_max=Non
     L = torch.ops.bfly
     ws = _arena.get(logits.device, "tkp", R * 521, torch.float32)[: R * 521]
     ws.zero_()
+    # the row-max slot starts at the smallest ordered key (INT_MIN = below signed_ordered(-inf)):
+    # a zero would read as +0.0 and clamp the max of an all-negative row
+    ws[R * 8:R * 9].view(torch.int32).fill_(-2 ** 31)
     L.tkp_begin(logits, temps, top_k, top_p, ws)
     if reduce_max is not None:
         reduce_max(ws[R * 8:R * 9].view(torch.int32))

@@ -103,7 +103,15 @@ class Communicator:
         comm = cls(mesh, rank, groups)
         from ..utils import flags
 
-        if flags.get("BFLY_NATIVE_RCCL") and dist.get_backend() == "nccl" and torch.cuda.is_available():
+        gpu_rccl = dist.get_backend() == "nccl" and torch.cuda.is_available()
+        if gpu_rccl and flags.get("BFLY_PREFLIGHT"):
+            # every multi-GPU entry point (bench, CLI, LLM, server) gets the bounded-time
+            # preflight before the native communicators / IPC paths are switched on: a failed
+            # check turns its feature off here on every rank (collective, same point everywhere)
+            from .preflight import ensure_preflight
+
+            ensure_preflight()
+        if flags.get("BFLY_NATIVE_RCCL") and gpu_rccl:
             comm.enable_native_rccl()
         if flags.get("BFLY_CUSTOM_AR") and mesh.tp > 1 and torch.cuda.is_available():
             comm.enable_custom_all_reduce(flags.get("BFLY_CUSTOM_AR_MAX_BYTES"))
@@ -182,6 +190,8 @@ class Communicator:
         self.custom_ar = car if car.ok else None
         if not car.ok:
             car.close()
+        else:
+            self._start_poller()
         return self.custom_ar is not None
 
     def enable_ep_ipc(self, capmax: int, hidden: int, top_k: int) -> bool:
@@ -196,6 +206,8 @@ class Communicator:
         self.ep_ipc = ipc if ipc.ok else None
         if not ipc.ok:
             ipc.close()
+        else:
+            self._start_poller()
         return self.ep_ipc is not None
 
     def ep_dispatch(self, x: torch.Tensor, ids: torch.Tensor, w: torch.Tensor, slots, experts_per_rank: int,
@@ -238,10 +250,58 @@ class Communicator:
             self.groups[axis].native = nc
         self.groups["world"].native = world
         self.pp_native_send, self.pp_native_recv = pp_edges(world, self.mesh, self.rank)
+        self._start_poller()
+        return natives
+
+    def _start_poller(self) -> None:
+        """One error-poller thread per process (parallel/rccl.async_errors): native RCCL async
+        errors and the IPC kernels' host-mapped timeout words, checked every second even while
+        the main thread is stuck in a step."""
         if getattr(self, "_rccl_poller", None) is None:
             from .rccl import start_error_poller
             self._rccl_poller = start_error_poller()
-        return natives
+
+    def graph_safe(self) -> bool:
+        """True when every collective a decode step issues inside its graph is capturable:
+        single-rank groups, RCCL (native or ProcessGroup), or the IPC kernels. A gloo data-path
+        collective (ranks sharing one GPU in tests) is not: its host staging would invalidate
+        the capture, so such engines decode eagerly."""
+        for axis, ipc in (("tp", self.custom_ar), ("ep", self.ep_ipc), ("pp", None)):
+            g = self.groups.get(axis)
+            if g is None or g.size == 1 or g.native is not None or self._nccl(g) or ipc is not None:
+                continue
+            if axis == "pp" and not self.native_p2p:
+                continue      # pipeline transfers run outside the graph unless on native edges
+            return False
+        return True
+
+    def close(self) -> dict:
+        """Tear down this rank's native resources, bounded: the IPC buffers, then the native
+        RCCL communicators (edges, axes, world) through their finalize-or-abort close. Graphs
+        that captured any of them must be gone first (LLMEngine.close). Returns {name: status}."""
+        out = {}
+        if getattr(self, "_rccl_poller", None) is not None:
+            self._rccl_poller.stop()
+            self._rccl_poller = None
+        for name in ("custom_ar", "ep_ipc"):
+            obj = getattr(self, name)
+            if obj is not None:
+                obj.close()
+                setattr(self, name, None)
+                out[name] = "closed"
+        comms = [("pp_send", self.pp_native_send), ("pp_recv", self.pp_native_recv)]
+        comms += [(k, g.native) for k, g in self.groups.items() if g is not None and g.native is not None]
+        seen = set()
+        for name, c in comms:
+            if c is None or id(c) in seen:
+                continue
+            seen.add(id(c))
+            out[name] = c.close()
+        self.pp_native_send = self.pp_native_recv = None
+        for g in self.groups.values():
+            if g is not None:
+                g.native = None
+        return out
 
     @property
     def native_p2p(self) -> bool:
@@ -336,6 +396,8 @@ class Communicator:
         """Equal-split all-to-all along dim 0: block r of `t` (t.shape[0] / n rows) goes to group
         rank r; block r of the result came from group rank r. Fixed shapes and no host sync,
         so it is stream-ordered and hipGraph-capturable on RCCL (the EP decode dispatch)."""
+        from ..utils import flags
+
         g = self.groups[group]
         if g.size == 1:
             if out is not None:
@@ -345,7 +407,7 @@ class Communicator:
         if out is None:
             out = torch.empty_like(t)
         self.stats["calls"] += 1
-        if g.native is not None:
+        if g.native is not None and flags.get("BFLY_NATIVE_A2A"):
             return g.native.all_to_all(t, out)
         if self._nccl(g):
             dist.all_to_all_single(out, t.contiguous(), group=g.pg)

@@ -27,6 +27,30 @@ from .. import ops
 log = logging.getLogger("butterfly_amd.comm")
 
 
+def device_identity(index: int) -> str:
+    """Physical identity of a GPU (host + PCI domain/bus/device): equal for two ranks exactly
+    when they drive the same card, whatever each process's device numbering."""
+    import socket
+
+    p = torch.cuda.get_device_properties(index)
+    return f"{socket.gethostname()}:{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+
+
+def shared_device_refusal(idents: list, what: str) -> str | None:
+    """Reason to refuse an IPC group whose ranks share a GPU, or None. The flag-rendezvous
+    kernels spin while they wait for a peer's workgroups; on a shared GPU those spinning
+    workgroups of one rank can hold the CU resources a co-resident rank's kernel needs to reach
+    the rendezvous (co-residency starvation: the Llama-3-70B tp4 shared-GPU rehearsal stall,
+    profiles/r4_tp4_stall/). Tests opt in with BFLY_IPC_SHARED_DEVICE=1."""
+    from ..utils import flags
+
+    if len(set(idents)) == len(idents) or flags.get("BFLY_IPC_SHARED_DEVICE"):
+        return None
+    return (f"{what}: ranks of the group share a GPU ({idents}); spin-waiting IPC kernels can starve "
+            "each other's workgroups there, so the group keeps RCCL / the all-to-all "
+            "(BFLY_IPC_SHARED_DEVICE=1 allows it for tests)")
+
+
 class CustomAllReduce:
     def __init__(self, ranks: list, rank_in_group: int, pg, max_bytes: int = 8 << 20,
                  device: torch.device | None = None, two_shot_bytes: int | None = None):
@@ -43,6 +67,7 @@ class CustomAllReduce:
         if self.world not in (2, 4, 8):
             raise ValueError("custom all-reduce supports groups of 2, 4 or 8 ranks")
         L = torch.ops.bfly
+        L.health_init()          # host-mapped timeout words, allocated before any capture
         self._ptr = 0
         self._opened = []
         self.bases = []
@@ -58,10 +83,14 @@ class CustomAllReduce:
         # (xGMI). Ranks sharing one device (the 1-GPU test setup) need no peer mapping.
         me = self.device.index if self.device.index is not None else torch.cuda.current_device()
         handles: list = [None] * self.world
-        dist.all_gather_object(handles, (handle, me), group=pg)
-        devs = [d for _, d in handles]
-        handles = [h for h, _ in handles]
+        dist.all_gather_object(handles, (handle, me, device_identity(me)), group=pg)
+        devs = [d for _, d, _ in handles]
+        refusal = shared_device_refusal([i for _, _, i in handles], "custom all-reduce")
+        handles = [h for h, _, _ in handles]
         local_ok = all(h is not None for h in handles)
+        if refusal:
+            log.warning(refusal)
+            local_ok = False
         try:
             unreachable = [d for d in devs if d != me and not torch.cuda.can_device_access_peer(me, d)]
         except Exception as e:  # noqa: BLE001

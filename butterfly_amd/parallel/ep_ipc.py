@@ -60,6 +60,7 @@ class EpIpc:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         if self.ep not in (2, 4, 8):
             raise ValueError("EP IPC dispatch supports groups of 2, 4 or 8 ranks")
+        L.health_init()          # host-mapped timeout words, allocated before any capture
         lay = list(L.ep_ipc_layout(self.ep, self.capmax, self.H, self.K))
         self._off = dict(zip(("x", "ids", "w", "back", "total"), lay))
         self._ptr = 0
@@ -73,9 +74,15 @@ class EpIpc:
         except Exception as e:  # noqa: BLE001 — voted below
             log.warning("EP IPC: buffer export failed (%r)", e)
         me = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        from .custom_allreduce import device_identity, shared_device_refusal
+
         got: list = [None] * self.ep
-        dist.all_gather_object(got, (handle, me), group=pg)
-        local_ok = all(h is not None for h, _ in got)
+        dist.all_gather_object(got, (handle, me, device_identity(me)), group=pg)
+        refusal = shared_device_refusal([i for _, _, i in got], "EP IPC")
+        got = [(h, d) for h, d, _ in got]
+        local_ok = all(h is not None for h, _ in got) and refusal is None
+        if refusal:
+            log.warning(refusal)
         try:
             unreachable = [d for _, d in got if d != me and not torch.cuda.can_device_access_peer(me, d)]
         except Exception as e:  # noqa: BLE001
@@ -137,7 +144,7 @@ class EpIpc:
         once per rank it was sent to — bitwise. Every rank runs the same votes."""
         good = True
         El = 2
-        for T in (1, min(self.capmax, 37)):
+        for T in (0, 1, min(self.capmax, 37)):     # T = 0: an EP-idle rank still waits for returns
             g = torch.Generator().manual_seed(1000 + T)
             x = (torch.randn(T, self.H, generator=g) + self.rank).to(torch.bfloat16).to(self.device)
             ids = torch.randint(-1, self.ep * El, (T, self.K), generator=g, dtype=torch.int32).to(self.device)

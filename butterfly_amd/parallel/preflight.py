@@ -29,9 +29,27 @@ Checks, in order (G = needs a GPU and the RCCL backend; skipped on CPU / gloo):
                      the replay runs only if EVERY rank captured
   native_rccl        G: own RCCL communicators (parallel/rccl.py): world init, split, all_reduce,
                      all_gather, all_to_all, grouped send/recv, plus capture + replay
+  pp_edge_graph      G (after native_rccl): the native pipeline edges exactly as the engine
+                     drives them — parallel/rccl.pp_edges over a pp = world chain; every
+                     receiver captures recv + a consumer kernel as a graph (the receive is the
+                     graph's first node), every sender sends from two alternating static
+                     buffers on a side stream guarded by send-done events; 4 replays with
+                     changing payloads, bitwise. Fail -> BFLY_PP_NATIVE_EDGES=0 (torch-PG
+                     receives pre-posted on a comm stream)
+  native_a2a_graph   G (after native_rccl): a captured native all_to_all replayed with new
+                     payloads (the EP fixed-capacity decode dispatch). Fail -> BFLY_NATIVE_A2A=0
   custom_ar          G: the IPC one-shot / two-shot all-reduce (parallel/custom_allreduce.py)
                      for groups of 2, 4 and 8 ranks: its own self-test, then bitwise against
                      RCCL's all-reduce, then captured in a graph and replayed
+  ep_ipc             G: the byte-minimal EP exchange (parallel/ep_ipc.py) for groups of 2, 4
+                     and 8 ranks: its self-test, then dispatch + combine bitwise against the
+                     fixed-capacity all-to-all path, then captured and replayed.
+                     Fail -> BFLY_EP_IPC=0
+Communicators the checks create are closed at the end (graphs dropped first; bounded
+finalize-or-abort), never leaked.
+
+Every multi-GPU entry point runs this once per process: bench.py explicitly, and
+Communicator.from_mesh (CLI, LLM, server) through `ensure_preflight()`.
 
 Fault injection for tests: BFLY_PREFLIGHT_INJECT="check:kind[:rank],..." with kind fail
 (the check reports failure), raise (the check raises) or hang (the check never returns).
@@ -52,6 +70,7 @@ import torch.distributed as dist
 
 HANG_EXIT_CODE = 75
 MANDATORY = ("world_collectives", "p2p_all_pairs")
+_LAST_REPORT: Optional["PreflightReport"] = None
 
 
 class PreflightError(RuntimeError):
@@ -66,13 +85,15 @@ class PreflightReport:
     env: dict = field(default_factory=dict)         # environment flags set
     allow_tp: bool = True                           # sub-groups work (TP / PP plans allowed)
     seconds: float = 0.0
+    native_closed: dict = field(default_factory=dict)   # teardown status -> count of check communicators
 
     def summary(self) -> dict:
         return {"checks": {k: v["ok"] for k, v in self.results.items()},
                 "ms": {k: round(v["ms"], 1) for k, v in self.results.items()},
                 "failed_detail": {k: v["detail"] for k, v in self.results.items() if v["ok"] is False},
                 "disabled": self.disabled, "enabled": self.enabled, "env": self.env,
-                "allow_tp": self.allow_tp, "seconds": round(self.seconds, 2)}
+                "allow_tp": self.allow_tp, "seconds": round(self.seconds, 2),
+                "native_closed": self.native_closed}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -290,16 +311,45 @@ def check_graph_collective(rank: int, world: int, vote: Callable[[bool], bool]) 
     return True, ""
 
 
-def check_native_rccl(rank: int, world: int, vote: Callable[[bool], bool]) -> tuple:
+class _Natives:
+    """Communicators and graphs made by the native checks, shared between them (one world
+    init for all of them) and torn down together at the end: graphs first (a communicator
+    whose kernels a live graph captured cannot finish its finalize), then the communicators
+    through their bounded finalize-or-abort close."""
+
+    def __init__(self):
+        self.world = None
+        self.comms: list = []
+        self.graphs: list = []
+        self.closed: dict = {}
+
+    def add(self, *comms):
+        self.comms.extend(c for c in comms if c is not None)
+
+    def close(self) -> dict:
+        self.graphs.clear()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        for c in reversed(self.comms + ([self.world] if self.world is not None else [])):
+            try:
+                st = c.close()
+            except Exception as e:  # noqa: BLE001 — teardown reports, never raises
+                st = f"error {e!r}"[:120]
+            self.closed[st] = self.closed.get(st, 0) + 1
+        self.comms, self.world = [], None
+        return self.closed
+
+
+def check_native_rccl(rank: int, world: int, vote: Callable[[bool], bool], nat: _Natives) -> tuple:
     dev = _dev()
     if dev.type != "cuda":
         vote(True)
         return None, "needs RCCL"
     from .rccl import RcclComm
 
-    wc = sub = None
+    sub = None
     try:
-        wc = RcclComm.world()
+        wc = nat.world = RcclComm.world()
         x = torch.full((1024,), float(rank + 1), device=dev)
         wc.all_reduce_(x)
         _sync(dev)
@@ -329,6 +379,7 @@ def check_native_rccl(rank: int, world: int, vote: Callable[[bool], bool]) -> tu
         # split (one communicator per mesh axis): pairs of ranks
         if world % 2 == 0:
             sub = wc.split(rank // 2, rank % 2)
+            nat.add(sub)
             y = torch.full((64,), float(rank), device=dev)
             sub.all_reduce_(y)
             _sync(dev)
@@ -338,34 +389,121 @@ def check_native_rccl(rank: int, world: int, vote: Callable[[bool], bool]) -> tu
     except Exception as e:  # noqa: BLE001
         ok, err = False, f"{e!r}"[:300]
     if not vote(ok):
-        _close(wc, sub)
         return False, err or "failed on another rank"
     # capture + replay (graph-captured decode steps issue their collectives this way)
     z = torch.zeros(1024, device=dev)
     try:
         gr = _capture(lambda: wc.all_reduce_(z), dev)
+        nat.graphs.append(gr)
     except Exception as e:  # noqa: BLE001
         gr, err = None, f"capture raised {e!r}"[:300]
     if not vote(gr is not None):
-        _close(wc, sub)
         return False, err or "capture failed on another rank"
     z.fill_(float(rank))
     gr.replay()
     _sync(dev)
     ok = bool((z == float(sum(range(world)))).all())
-    _close(wc, sub)
     return ok, "" if ok else "captured all_reduce replayed wrong"
 
 
-def _close(*comms) -> None:
-    """Check communicators are left alive (a few MB each): ncclCommDestroy of a communicator
-    that ran point-to-point transfers, or whose captured graph still exists, can block forever
-    (seen on a one-rank communicator on MI355X), and a blocked destroy here would cost the
-    whole job. They are never used again."""
-    _LEAKED.extend(c for c in comms if c is not None)
+def check_pp_edge_graph(rank: int, world: int, vote: Callable[[bool], bool], nat: _Natives) -> tuple:
+    """The engine's native pipeline-edge pattern over a pp = world chain (module doc)."""
+    dev = _dev()
+    if dev.type != "cuda" or nat.world is None:
+        vote(True)
+        vote(True)
+        return None, "needs native RCCL"
+    from .mesh import Mesh
+    from .rccl import pp_edges
+
+    err = ""
+    send = recv = None
+    try:
+        send, recv = pp_edges(nat.world, Mesh(pp=world), rank, force=True)
+        nat.add(send, recv)
+        ok = True
+    except Exception as e:  # noqa: BLE001
+        ok, err = False, f"edge split raised {e!r}"[:300]
+    if not vote(ok):
+        return False, err or "edge split failed on another rank"
+    rows, cols = 16, 1024
+    inbuf = torch.zeros(rows, cols, device=dev)        # the graph's static hidden_in
+    y = torch.zeros(rows, cols, device=dev)
+    gr = None
+    if recv is not None:
+        # no eager warm-up: a transfer outside the graph would consume a real message; the
+        # body allocates nothing (in-place kernels on static buffers)
+        try:
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            _sync(dev)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                recv.recv(inbuf, 0)                  # the receive is the graph's first node
+                y.copy_(inbuf)
+                y.mul_(2.0)
+                y.add_(1.0)
+            nat.graphs.append(gr)
+        except Exception as e:  # noqa: BLE001
+            gr, err = None, f"receiver capture raised {e!r}"[:300]
+    if not vote(recv is None or gr is not None):
+        return False, err or "receiver capture failed on another rank"
+    side = torch.cuda.Stream(dev)
+    bufs = [torch.zeros(rows, cols, device=dev) for _ in range(2)]
+    done = [None, None]
+    ok = True
+    for it in range(4):
+        if gr is not None:
+            gr.replay()                              # waits for the previous stage's payload
+        if send is not None:
+            b = it % 2
+            cur = torch.cuda.current_stream(dev)
+            if done[b] is not None:
+                cur.wait_event(done[b])              # the A/B instance's previous send finished
+            bufs[b].fill_(float(rank * 1000 + it))   # producer on the compute stream
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                send.send(bufs[b], 1)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            done[b] = ev
+        if gr is not None:
+            _sync(dev)
+            want = float((rank - 1) * 1000 + it) * 2.0 + 1.0
+            if not bool((y == want).all()):
+                ok, err = False, f"replay {it}: got {float(y[0, 0])}, want {want}"
+                break
+    _sync(dev)
+    return ok, err
 
 
-_LEAKED: list = []
+def check_native_a2a_graph(rank: int, world: int, vote: Callable[[bool], bool], nat: _Natives) -> tuple:
+    dev = _dev()
+    if dev.type != "cuda" or nat.world is None:
+        vote(True)
+        return None, "needs native RCCL"
+    wc = nat.world
+    n = 64
+    src = torch.zeros(world * n, device=dev)
+    out = torch.zeros(world * n, device=dev)
+    err = ""
+    try:
+        gr = _capture(lambda: wc.all_to_all(src, out), dev)
+        nat.graphs.append(gr)
+    except Exception as e:  # noqa: BLE001
+        gr, err = None, f"capture raised {e!r}"[:300]
+    if not vote(gr is not None):
+        return False, err or "capture failed on another rank"
+    j = torch.arange(n, device=dev, dtype=torch.float32)
+    for it in range(3):
+        for d in range(world):          # block d goes to rank d: value encodes (src, dst, it, j)
+            src[d * n:(d + 1) * n] = rank * 1e5 + d * 1e3 + it * 100 + j
+        gr.replay()
+        _sync(dev)
+        want = torch.cat([s * 1e5 + rank * 1e3 + it * 100 + j for s in range(world)])
+        if not torch.equal(out, want):
+            return False, f"replay {it} wrong"
+    return True, ""
 
 
 def check_custom_ar(rank: int, world: int, pgs: dict, vote: Callable[[bool], bool]) -> tuple:
@@ -435,6 +573,99 @@ def check_custom_ar(rank: int, world: int, pgs: dict, vote: Callable[[bool], boo
         all_ok = all_ok and ok
         if car is not None:
             car.close()
+    return all_ok, "; ".join(details)
+
+
+def check_ep_ipc(rank: int, world: int, pgs: dict, vote: Callable[[bool], bool]) -> tuple:
+    """EpIpc for EP groups of 2, 4 and 8 ranks: self-test, then the decode dispatch + return
+    + combine bitwise against the fixed-capacity all-to-all path on the same routing, eager
+    and captured."""
+    dev = _dev()
+    sizes = [n for n in (2, 4, 8) if n <= world and world % n == 0]
+    if dev.type != "cuda":
+        for _ in sizes:
+            vote(True)
+            vote(True)
+        return None, "needs GPUs"
+    from .. import ops
+    from .ep_ipc import EpIpc
+
+    details, all_ok = [], True
+    H, K, El, cap = 512, 2, 2, 24
+    for n in sizes:
+        pg = pgs.get(n) if n < world else dist.group.WORLD
+        ipc, ok, gr = None, True, None
+        me = rank % n
+        try:
+            ipc = EpIpc(list(range((rank // n) * n, (rank // n) * n + n)), me, pg, cap, H, K, device=dev)
+            ok = ipc.ok
+            if ok:
+                g = torch.Generator().manual_seed(77 + rank)
+                T = 19
+                x = (torch.randn(T, H, generator=g) * 4).round().to(torch.bfloat16).to(dev)
+                ids = torch.randint(-1, n * El, (T, K), generator=g, dtype=torch.int32).to(dev)
+                w = torch.rand(T, K, generator=g).to(dev)
+                slots = torch.arange(T, dtype=torch.int32, device=dev)
+                slots[T - 1] = -1                                   # graph padding row
+                # path A: IPC exchange, identity "FFN" scaled by (rank + 1) on the expert side
+                r = ipc.dispatch(x, ids, w, slots, El, cap)
+                out_ipc = ipc.combine(r.x * float(me + 1), r)
+                # path B: ep_pack + all-to-all (torch process group) + ep_combine
+                send, meta, slot = ops.ep_pack(x, ids, w, slots, El, n, cap)
+                xr = torch.empty_like(send)
+                dist.all_to_all_single(xr, send, group=pg)
+                back = torch.empty_like(xr)
+                dist.all_to_all_single(back, (xr * float(me + 1)).contiguous(), group=pg)
+                out_a2a = ops.ep_combine(back, slot)
+                _sync(dev)
+                if not torch.equal(out_ipc, out_a2a) or ipc.error():
+                    ok = False
+                    details.append(f"n={n} IPC combine differs from the all-to-all path")
+            else:
+                details.append(f"n={n} self-test failed")
+        except Exception as e:  # noqa: BLE001
+            ok = False
+            details.append(f"n={n} raised {e!r}"[:200])
+        ok = vote(ok)
+        if ok:   # inside the decode graph: capture dispatch + combine on every rank, replay
+            xs = torch.zeros(8, H, dtype=torch.bfloat16, device=dev)
+            ids_s = torch.full((8, K), -1, dtype=torch.int32, device=dev)
+            w_s = torch.zeros(8, K, device=dev)
+            sl_s = torch.arange(8, dtype=torch.int32, device=dev)
+            res = {}
+
+            def body():
+                rr = ipc.dispatch(xs, ids_s, w_s, sl_s, El, cap)
+                res["out"] = ipc.combine(rr.x, rr)
+            try:
+                gr = _capture(body, dev)
+            except Exception as e:  # noqa: BLE001
+                details.append(f"n={n} capture raised {e!r}"[:200])
+        if vote(gr is not None) and gr is not None:
+            try:
+                for it in range(2):
+                    xs.fill_(float(rank + it))
+                    ids_s.copy_(((torch.arange(8 * K, device=dev).view(8, K) + it) % (n * El)).to(torch.int32))
+                    w_s.fill_(0.5)
+                    gr.replay()
+                    _sync(dev)
+                    hits = torch.zeros(8, dtype=torch.float32, device=dev)
+                    idc = ids_s.long() // El
+                    for t in range(8):
+                        hits[t] = len(set(idc[t].tolist()))
+                    want = (xs.float() * hits[:, None]).to(torch.bfloat16)
+                    if not torch.equal(res["out"], want) or ipc.error():
+                        ok = False
+                        details.append(f"n={n} replay {it} wrong")
+            except Exception as e:  # noqa: BLE001
+                ok = False
+                details.append(f"n={n} replay raised {e!r}"[:200])
+        elif ok:
+            ok = False
+        gr = None
+        all_ok = all_ok and ok
+        if ipc is not None:
+            ipc.close()
     return all_ok, "; ".join(details)
 
 
@@ -522,18 +753,37 @@ def run_preflight(timeout_s: Optional[float] = None, exit_fn: Callable[[int], No
             env["BFLY_PP_PREPOST"] = "0"
             rep.disabled.append("pp_prepost")
         graph_pg = run("graph_collective", lambda: check_graph_collective(rank, world, voting("graph_collective")))
-        native = run("native_rccl", lambda: check_native_rccl(rank, world, voting("native_rccl")))
-        user_native = os.environ.get("BFLY_NATIVE_RCCL")
-        if native and user_native not in ("0", "false", "off"):
-            env["BFLY_NATIVE_RCCL"] = "1"
-            rep.enabled.append("native_rccl")
-        elif rep.results["native_rccl"]["ok"] is False:
-            env["BFLY_NATIVE_RCCL"] = "0"
-            rep.disabled.append("native_rccl")
+        nat = _Natives()
+        try:
+            native = run("native_rccl", lambda: check_native_rccl(rank, world, voting("native_rccl"), nat))
+            user_native = os.environ.get("BFLY_NATIVE_RCCL")
+            if native and user_native not in ("0", "false", "off"):
+                env["BFLY_NATIVE_RCCL"] = "1"
+                rep.enabled.append("native_rccl")
+            elif rep.results["native_rccl"]["ok"] is False:
+                env["BFLY_NATIVE_RCCL"] = "0"
+                rep.disabled.append("native_rccl")
+            if not native:
+                nat.close()       # the follow-on native checks report "not applicable"
+            for name, fn, flag, feat in (
+                    ("pp_edge_graph", check_pp_edge_graph, "BFLY_PP_NATIVE_EDGES", "pp_native_edges"),
+                    ("native_a2a_graph", check_native_a2a_graph, "BFLY_NATIVE_A2A", "native_a2a")):
+                if not run(name, lambda fn=fn, name=name: fn(rank, world, voting(name), nat)) \
+                        and rep.results[name]["ok"] is False:
+                    env[flag] = "0"
+                    rep.disabled.append(feat)
+        finally:
+            wd.arm("native_close", timeout_s)
+            rep.native_closed = nat.close()
+            wd.disarm()
         car = run("custom_ar", lambda: check_custom_ar(rank, world, pgs, voting("custom_ar")))
         if not car and rep.results["custom_ar"]["ok"] is False:
             env["BFLY_CUSTOM_AR"] = "0"
             rep.disabled.append("custom_ar")
+        if not run("ep_ipc", lambda: check_ep_ipc(rank, world, pgs, voting("ep_ipc"))) \
+                and rep.results["ep_ipc"]["ok"] is False:
+            env["BFLY_EP_IPC"] = "0"
+            rep.disabled.append("ep_ipc")
         captured_ok = graph_pg or native or rep.results["graph_collective"]["ok"] is None
         if not captured_ok:
             env["BFLY_DISABLE_GRAPHS"] = "1"
@@ -544,7 +794,23 @@ def run_preflight(timeout_s: Optional[float] = None, exit_fn: Callable[[int], No
     finally:
         wd.close()
     rep.seconds = time.perf_counter() - t_all
+    global _LAST_REPORT
+    _LAST_REPORT = rep
     return rep
+
+
+def last_report() -> Optional[PreflightReport]:
+    """The report of this process's preflight, or None if it has not run."""
+    return _LAST_REPORT
+
+
+def ensure_preflight(exit_fn: Callable[[int], None] = os._exit) -> Optional[PreflightReport]:
+    """Run the preflight (applying its fallbacks) unless this process already did: the
+    Communicator.from_mesh gate, so the CLI / LLM / server paths get the same checks as
+    bench.py before any native communicator or IPC buffer is created. Collective."""
+    if _LAST_REPORT is not None or not dist.is_initialized() or dist.get_world_size() < 2:
+        return _LAST_REPORT
+    return run_preflight(exit_fn=exit_fn, apply=True)
 
 
 def main(argv=None) -> int:

@@ -12,6 +12,12 @@ Enabled whenever the backend is RCCL (BFLY_NATIVE_RCCL, default on; parallel/com
 reduce-scatter / all-to-all of groups larger than one rank here). RCCL refuses two ranks on
 one device, so on a one-GPU box only nranks = 1 communicators can be exercised; the multi-rank
 path needs a multi-GPU node.
+
+Communicators are NON-BLOCKING: init and split poll RCCL's background setup
+against BFLY_RCCL_INIT_TIMEOUT_S and raise TimeoutError (after aborting the half-built
+communicator) when a peer never joins; `close()` is a bounded ncclCommFinalize + destroy that
+falls back to an abort, so teardown never wedges. Graphs that captured a communicator's kernels
+must be dropped before it is closed (LLMEngine.close orders this).
 """
 from __future__ import annotations
 
@@ -31,6 +37,22 @@ def _lib():
     return torch.ops.bfly
 
 
+def _timeout(name: str, value: Optional[float]) -> float:
+    from ..utils import flags
+
+    return float(flags.get(name) if value is None else value)
+
+
+def _call(fn, *args):
+    """Native call; a deadline expiry (message 'RCCL-TIMEOUT') becomes TimeoutError."""
+    try:
+        return fn(*args)
+    except RuntimeError as e:
+        if "RCCL-TIMEOUT" in str(e):
+            raise TimeoutError(str(e).split("\n")[0]) from None
+        raise
+
+
 def version() -> int:
     """RCCL version code of the library torch loaded (e.g. 22606 = 2.26.6)."""
     return int(_lib().rccl_version())
@@ -46,9 +68,14 @@ class RcclComm:
 
     # -- construction ---------------------------------------------------------------------
     @classmethod
-    def create(cls, uid: torch.Tensor, nranks: int, rank: int, ranks: Optional[list] = None) -> "RcclComm":
-        """ncclCommInitRank on the current device with an id every member already holds."""
-        h = _lib().rccl_init(uid.cpu().contiguous(), nranks, rank)
+    def create(cls, uid: torch.Tensor, nranks: int, rank: int, ranks: Optional[list] = None,
+               timeout: Optional[float] = None) -> "RcclComm":
+        """Non-blocking ncclCommInitRankConfig on the current device with an id every member
+        already holds, polled until ready; TimeoutError after `timeout` seconds
+        (BFLY_RCCL_INIT_TIMEOUT_S) with the communicator aborted."""
+        lib = _lib()
+        lib.rccl_set_call_timeout(float(_timeout("BFLY_COMM_TIMEOUT_S", None)))
+        h = _call(lib.rccl_init, uid.cpu().contiguous(), nranks, rank, _timeout("BFLY_RCCL_INIT_TIMEOUT_S", timeout))
         # the failure paths (health._default_failure, the preflight's hang exit) abort every
         # native communicator before the process exits
         from ..utils.health import register_abort_hook
@@ -56,7 +83,7 @@ class RcclComm:
         return cls(h, ranks if ranks is not None else list(range(nranks)))
 
     @classmethod
-    def world(cls, pg=None) -> "RcclComm":
+    def world(cls, pg=None, timeout: Optional[float] = None) -> "RcclComm":
         """Collective over the torch.distributed world (or `pg`): rank 0's id is broadcast on
         the existing process group, then every rank joins."""
         lib = _lib()
@@ -65,12 +92,14 @@ class RcclComm:
         dev = "cuda" if dist.get_backend(pg) == "nccl" else "cpu"
         t = uid.to(dev)
         dist.broadcast(t, dist.get_global_rank(pg, 0) if pg is not None else 0, group=pg)
-        return cls.create(t.cpu(), n, r)
+        return cls.create(t.cpu(), n, r, timeout=timeout)
 
-    def split(self, color: int, key: int, ranks: Optional[list] = None) -> Optional["RcclComm"]:
+    def split(self, color: int, key: int, ranks: Optional[list] = None,
+              timeout: Optional[float] = None) -> Optional["RcclComm"]:
         """ncclCommSplit (collective over this communicator): ranks passing the same color form
-        one communicator ordered by key; color < 0 leaves the rank out (returns None)."""
-        h = _lib().rccl_split(self.handle, int(color), int(key))
+        one communicator ordered by key; color < 0 leaves the rank out (returns None). Bounded
+        like `create`."""
+        h = _call(_lib().rccl_split, self.handle, int(color), int(key), _timeout("BFLY_RCCL_INIT_TIMEOUT_S", timeout))
         return None if h < 0 else RcclComm(h, ranks if ranks is not None else [])
 
     # -- queries ----------------------------------------------------------------------------
@@ -123,10 +152,15 @@ class RcclComm:
     def group_end() -> None:
         _lib().rccl_group_end()
 
-    def close(self, abort: bool = False) -> None:
-        if not self._closed:
-            self._closed = True
-            _lib().rccl_release(self.handle, abort)
+    def close(self, abort: bool = False, timeout: Optional[float] = None) -> str:
+        """Tear down: 'clean' (finalize + destroy within `timeout`, BFLY_RCCL_CLOSE_TIMEOUT_S),
+        'aborted' (requested, or the finalize outlived its deadline) or 'released' (already
+        gone, e.g. taken down by abort_all). Never blocks past the deadline."""
+        if self._closed:
+            return "released"
+        self._closed = True
+        rc = int(_lib().rccl_release(self.handle, abort, _timeout("BFLY_RCCL_CLOSE_TIMEOUT_S", timeout)))
+        return {1: "clean", 0: "aborted"}.get(rc, "released")
 
 
 def live_handles() -> list:
@@ -141,9 +175,15 @@ def abort_all() -> int:
 
 
 def async_errors() -> Optional[str]:
-    """None when every live communicator is healthy, else a description of the first
-    asynchronous error (the ErrorPoller check)."""
+    """None when every live communicator is healthy and no IPC flag wait timed out, else a
+    description of the first failure (the ErrorPoller check). The IPC kernels' timeouts are
+    read from host-mapped health words (plain loads: safe while the stream is stuck)."""
     lib = _lib()
+    car, ep = (int(v) for v in lib.health_words())
+    if car:
+        return "custom all-reduce peer wait timed out (health word)"
+    if ep:
+        return "EP IPC dispatch peer wait timed out (health word)"
     for h in lib.rccl_live():
         try:
             err = int(lib.rccl_async_error(h))
@@ -165,7 +205,7 @@ def start_error_poller(period: Optional[float] = None, on_failure=None):
     return ErrorPoller(async_errors, period=period, on_failure=on_failure, name="bfly-rccl-poll").start()
 
 
-def pp_edges(world: RcclComm, mesh, rank: int) -> tuple:
+def pp_edges(world: RcclComm, mesh, rank: int, force: bool = False) -> tuple:
     """Two-rank communicators for this rank's pipeline edges (collective: every rank calls it
     with the same mesh): (to the next stage, from the previous stage), each None at the ends.
     Edge s -> s+1 of a pipeline gets its own communicator (sender = rank 0, receiver = rank 1),
@@ -174,7 +214,9 @@ def pp_edges(world: RcclComm, mesh, rank: int) -> tuple:
     its decode graph) and its send (eager, on the send stream) on different RCCL objects.
     The connections are set up here with one tiny transfer per edge, so no later (captured)
     transfer has to run a connection handshake."""
-    if mesh.pp <= 1:
+    from ..utils import flags
+
+    if mesh.pp <= 1 or not (force or flags.get("BFLY_PP_NATIVE_EDGES")):
         return None, None
     groups = mesh.all_groups("pp")
     g = next(i for i, grp in enumerate(groups) if rank in grp)

@@ -53,6 +53,17 @@ define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all
        "all-to-all) and pipeline edges on the rank's own RCCL communicators (world init + ncclCommSplit "
        "per mesh axis, parallel/rccl.py) instead of torch ProcessGroups, whenever the backend is RCCL "
        "(the multi-GPU preflight turns it off if its native check fails); 0 = torch ProcessGroups")
+define("BFLY_PP_NATIVE_EDGES", True, _bool, "with native RCCL: pipeline boundaries on two-rank edge communicators "
+       "(receive captured in the stage's decode graph, A/B sends on a side stream); 0 = torch ProcessGroup "
+       "send/recv with pre-posted receives (the preflight's pp_edge_graph check turns it off on failure)")
+define("BFLY_NATIVE_A2A", True, _bool, "with native RCCL: the EP all-to-all (fixed-capacity decode dispatch) on the "
+       "native communicator; 0 = torch ProcessGroup (the preflight's native_a2a_graph check turns it off)")
+define("BFLY_RCCL_INIT_TIMEOUT_S", 180.0, float, "deadline of a native RCCL communicator init / split (non-blocking "
+       "setup polled by the host); expiry aborts it and raises TimeoutError")
+define("BFLY_RCCL_CLOSE_TIMEOUT_S", 30.0, float, "deadline of a native RCCL communicator finalize at teardown; expiry "
+       "aborts it instead")
+define("BFLY_IPC_SHARED_DEVICE", False, _bool, "allow the IPC all-reduce / EP exchange for groups whose ranks share "
+       "one GPU (tests only: spin-waiting workgroups of one rank can starve a co-resident rank's kernels of CUs)")
 define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism: the residual stream and the norms are "
        "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
 define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")

@@ -799,6 +799,7 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tenso
     TORCH_CHECK(bases[i] != 0, "custom_all_reduce: null peer buffer");
     peers.base[i] = reinterpret_cast<char*>(bases[i]);
   }
+  peers.herr = bfly::health_words_device();
   bfly::bf16* res = nullptr;
   const bfly::bf16* wp = nullptr;
   if (residual.has_value()) {
@@ -837,8 +838,25 @@ static bfly::ArPeers ep_peers(at::IntArrayRef bases) {
     TORCH_CHECK(bases[i] != 0, "ep_ipc: null peer buffer");
     peers.base[i] = reinterpret_cast<char*>(bases[i]);
   }
+  peers.herr = bfly::health_words_device();
   return peers;
 }
+
+// Host-mapped health words (bfly_kernels.h): [kHealthCar] custom all-reduce and [kHealthEp]
+// EP IPC flag-wait timeouts. health_init allocates them (eagerly, before any graph capture);
+// reading them is a plain host load, safe from a poller thread while the GPU is busy or stuck.
+bool health_init() { return bfly::health_words_device() != nullptr; }
+
+// Read and reset the runtime's sticky last-error code: a failed stream capture leaves
+// hipErrorStreamCaptureInvalidated behind, which the next checked launch would report as
+// its own failure (ModelRunner clears it before falling back to eager decode).
+int64_t hip_clear_error() { return (int64_t)hipGetLastError(); }
+
+std::vector<int64_t> health_words() {
+  return {(int64_t)bfly::health_word(bfly::kHealthCar), (int64_t)bfly::health_word(bfly::kHealthEp)};
+}
+
+void health_clear() { bfly::health_clear(); }
 
 std::vector<int64_t> ep_ipc_layout(int64_t ep, int64_t capmax, int64_t H, int64_t K) {
   const bfly::EpLayout L = bfly::ep_ipc_layout((int)ep, (int)capmax, (int)H, (int)K);
@@ -981,6 +999,10 @@ TORCH_LIBRARY(bfly, m) {
         "int[] bases, int rank, Tensor(a!) slot) -> ()");
   m.def("ep_ipc_wait(Tensor like, int[] bases, int rank) -> ()");
   m.def("ep_ipc_return(Tensor y, int k, int capmax, int[] bases, int rank) -> ()");
+  m.def("health_init() -> bool", &health_init);
+  m.def("hip_clear_error() -> int", &hip_clear_error);
+  m.def("health_words() -> int[]", &health_words);
+  m.def("health_clear() -> ()", &health_clear);
   m.def("ep_ipc_combine(Tensor slot, int k, int capmax, int[] bases, int rank, Tensor(a!) out) -> ()");
   m.def("ep_ipc_stats(int ptr) -> int[]", &ep_ipc_stats);
   m.def("ep_ipc_error(int ptr) -> int", [](int64_t p) -> int64_t { return bfly::ep_ipc_error(reinterpret_cast<const void*>(p)); });

@@ -126,7 +126,14 @@ int launch_attn_lse_merge(float* acc_o, float* acc_lse, const bf16* o, long o_st
 constexpr int kArBlocks = 128;
 constexpr int kArMaxWorld = 8;
 constexpr long kArDataOff = 65536;
-struct ArPeers { char* base[kArMaxWorld]; };
+// herr: this process's host-mapped health words (health_words_device()); a flag wait that
+// times out also stores 1 into herr[kHealthCar] / herr[kHealthEp], which the host error
+// poller reads without any HIP call (so it sees a stuck peer while the stream is still busy)
+struct ArPeers { char* base[kArMaxWorld]; uint32_t* herr; };
+constexpr int kHealthCar = 0, kHealthEp = 1, kHealthWords = 16;
+uint32_t* health_words_device();        // lazily allocated pinned, mapped, coherent host memory
+uint32_t health_word(int i);            // host read (no HIP call once allocated)
+void health_clear();
 // flags/counters, two input buffers and two reduced-chunk buffers (two-shot), all double-buffered
 inline long car_buffer_bytes(long cap) { return kArDataOff + 4 * cap; }
 // `slabs` (optional): the input is split-K partials [sk][rows][dim] f32, reduced in the publish.

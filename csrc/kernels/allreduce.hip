@@ -41,6 +41,8 @@
 // after every peer started call e+2, so every peer finished call e's gather.
 #include <string.h>
 
+#include <mutex>
+
 #include "bfly_common.h"
 #include "bfly_kernels.h"
 
@@ -59,13 +61,15 @@ constexpr int kArThreads = 256;
 // a rank delayed by host work or by time-slicing (several ranks sharing one GPU) is waited for.
 constexpr long long kArSpinTimeoutTicks = 20LL * 100000000LL;   // 20 s
 
-__device__ __forceinline__ void spin_wait(const uint32_t* f, uint32_t e, uint32_t* err) {
+__device__ __forceinline__ void spin_wait(const uint32_t* f, uint32_t e, uint32_t* err, uint32_t* herr) {
   if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e) return;
   const long long t0 = wall_clock64();
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
     __builtin_amdgcn_s_sleep(2);
     if (wall_clock64() - t0 > kArSpinTimeoutTicks) {   // record and give up
       __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // host-visible copy for the error poller: a plain (vector) store, no host-memory atomic
+      if (herr != nullptr) __hip_atomic_store(herr + kHealthCar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
   }
@@ -80,7 +84,7 @@ __device__ __forceinline__ void rendezvous(const ArPeers& peers, char* my, long 
     uint32_t* pf = reinterpret_cast<uint32_t*>(peers.base[threadIdx.x] + off) + b * 8 + rank;
     __hip_atomic_store(pf, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t* f = reinterpret_cast<const uint32_t*>(my + off) + b * 8 + threadIdx.x;
-    spin_wait(f, e, reinterpret_cast<uint32_t*>(my + kArErrOff));
+    spin_wait(f, e, reinterpret_cast<uint32_t*>(my + kArErrOff), peers.herr);
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -409,6 +413,43 @@ void car_ipc_close(void* p) { (void)hipIpcCloseMemHandle(p); }
 
 int car_clear_error(void* base) {
   return hipMemset(static_cast<char*>(base) + kArErrOff, 0, 4) == hipSuccess ? 0 : -1;
+}
+
+namespace {
+std::mutex g_health_mu;
+uint32_t* g_health_host = nullptr;   // pinned, coherent, mapped into every device
+uint32_t* g_health_dev = nullptr;
+}  // namespace
+
+uint32_t* health_words_device() {
+  std::lock_guard<std::mutex> lk(g_health_mu);
+  if (g_health_dev == nullptr) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, kHealthWords * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent |
+                                                               hipHostMallocPortable) != hipSuccess)
+      return nullptr;
+    memset(h, 0, kHealthWords * sizeof(uint32_t));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return nullptr;
+    }
+    g_health_host = static_cast<uint32_t*>(h);
+    g_health_dev = static_cast<uint32_t*>(d);
+  }
+  return g_health_dev;
+}
+
+uint32_t health_word(int i) {
+  std::lock_guard<std::mutex> lk(g_health_mu);
+  if (g_health_host == nullptr || i < 0 || i >= kHealthWords) return 0;
+  return reinterpret_cast<volatile uint32_t*>(g_health_host)[i];
+}
+
+void health_clear() {
+  std::lock_guard<std::mutex> lk(g_health_mu);
+  if (g_health_host != nullptr)
+    for (int i = 0; i < kHealthWords; ++i) reinterpret_cast<volatile uint32_t*>(g_health_host)[i] = 0;
 }
 
 int car_error(const void* base) {

@@ -47,13 +47,15 @@ __device__ __forceinline__ uint32_t* ep_word(char* base, long off) {
   return reinterpret_cast<uint32_t*>(base + off);
 }
 
-__device__ __forceinline__ void ep_spin(const uint32_t* f, uint32_t e, uint32_t* err) {
+__device__ __forceinline__ void ep_spin(const uint32_t* f, uint32_t e, uint32_t* err, uint32_t* herr) {
   if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e) return;
   const long long t0 = wall_clock64();
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
     __builtin_amdgcn_s_sleep(2);
     if (wall_clock64() - t0 > kEpSpinTimeoutTicks) {
       __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // host-visible copy for the error poller (plain vector store into mapped host memory)
+      if (herr != nullptr) __hip_atomic_store(herr + kHealthEp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
   }
@@ -178,7 +180,7 @@ __global__ void __launch_bounds__(64)
 ep_ipc_wait_kernel(ArPeers peers, int rank) {
   char* my = peers.base[rank];
   const uint32_t e = __hip_atomic_load(ep_word(my, kEpCur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (threadIdx.x < EP) ep_spin(ep_word(my, kEpFlagsD) + threadIdx.x, e, ep_word(my, kEpErr));
+  if (threadIdx.x < EP) ep_spin(ep_word(my, kEpFlagsD) + threadIdx.x, e, ep_word(my, kEpErr), peers.herr);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
@@ -207,17 +209,21 @@ ep_ipc_return_kernel(const bf16* __restrict__ y, int H, int capmax, ArPeers peer
   }
 }
 
-// grid = T workgroups: out[t] = sum_d back[d][slot[t][d]] over the ranks t was sent to
+// grid = max(T, 1) workgroups: out[t] = sum_d back[d][slot[t][d]] over the ranks t was sent
+// to. A rank with no tokens (T == 0: EP-idle step) still runs one workgroup, whose only job is
+// the flag_r wait: without it the rank's next dispatch could overwrite peers' x / ids / counts
+// blocks before they finished this layer's FFN (the single-buffering invariant above).
 template <int EP>
 __global__ void __launch_bounds__(kEpThreads)
-ep_ipc_combine_kernel(const int* __restrict__ slot, int H, int capmax, ArPeers peers, int rank, EpLayout L,
+ep_ipc_combine_kernel(const int* __restrict__ slot, int T, int H, int capmax, ArPeers peers, int rank, EpLayout L,
                       bf16* __restrict__ out) {
   char* my = peers.base[rank];
   const uint32_t e = __hip_atomic_load(ep_word(my, kEpCur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (threadIdx.x < EP) ep_spin(ep_word(my, kEpFlagsR) + threadIdx.x, e, ep_word(my, kEpErr));
+  if (threadIdx.x < EP) ep_spin(ep_word(my, kEpFlagsR) + threadIdx.x, e, ep_word(my, kEpErr), peers.herr);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const long t = blockIdx.x;
+  if (t >= T) return;
   const bf16* back = reinterpret_cast<const bf16*>(my + L.back);
   int sl[EP];
 #pragma unroll
@@ -294,10 +300,10 @@ int launch_ep_ipc_return(const bf16* y, int H, int K, int ep, int capmax, const 
 int launch_ep_ipc_combine(const int* slot, int T, int H, int K, int ep, int capmax, const ArPeers& peers,
                           int rank, bf16* out, hipStream_t stream) {
   if (H % 8 != 0 || capmax <= 0 || rank < 0 || rank >= ep) return -1;
-  if (T <= 0) return 0;
+  if (T < 0) return -1;
   const EpLayout L = ep_ipc_layout(ep, capmax, H, K);
 #define EP_COMBINE(N) \
-  ep_ipc_combine_kernel<N><<<T, kEpThreads, 0, stream>>>(slot, H, capmax, peers, rank, L, out)
+  ep_ipc_combine_kernel<N><<<T > 0 ? T : 1, kEpThreads, 0, stream>>>(slot, T, H, capmax, peers, rank, L, out)
   EP_SWITCH(ep, EP_COMBINE)
 #undef EP_COMBINE
   return 0;

@@ -155,7 +155,7 @@ constexpr int kTkpThreads = 256;
 __device__ __forceinline__ int signed_ordered(float f) { return (int)(ordered_f32(f) ^ 0x80000000u); }
 __device__ __forceinline__ float from_signed_ordered(int v) { return unordered_f32((uint32_t)v ^ 0x80000000u); }
 
-// Row maximum of s over this shard (atomicMax into smax, zeroed by the caller) and the row's
+// Row maximum of s over this shard (atomicMax into smax, set to INT_MIN by the caller) and the row's
 // initial select state.
 __global__ void __launch_bounds__(kTkpThreads)
 tkp_begin_kernel(const bf16* __restrict__ logits, long row_stride, int V, int chunk,

@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# the multi-rank GPU tests run their ranks on ONE device: let the IPC all-reduce / EP exchange
+# run there (production refuses shared-GPU IPC groups: parallel/custom_allreduce.py)
+os.environ.setdefault("BFLY_IPC_SHARED_DEVICE", "1")
 
 
 def pytest_configure(config):

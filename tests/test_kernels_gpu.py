@@ -150,6 +150,27 @@ def test_sample_topk_topp_on_device():
     assert int(ids[5]) == int(logits[5].float().argmax())
 
 
+def test_topkp_all_negative_logits_low_temperature():
+    """Rows whose scaled logits are all far below zero: the radix select must start from the
+    true row maximum (not +0.0), or exp(s - 0) underflows, Z becomes 0 and top-p silently
+    keeps every token. GPU thresholds must equal the CPU reference's and the exact ones."""
+    from butterfly_amd.engine.sampler import Sampler, SamplingParams
+    from tests.test_sampler import value_threshold
+
+    V = 32000
+    params = [SamplingParams(temperature=0.05, top_p=0.9), SamplingParams(temperature=0.1, top_k=7, top_p=0.5),
+              SamplingParams(temperature=0.02, top_k=3)]
+    logits = (_bf(len(params), V, scale=0.5, seed=23).float() - 30.0).to(torch.bfloat16)
+    temps = torch.tensor([p.temperature for p in params], device=DEV)
+    thr = Sampler(None, V, 0, 1).thresholds(logits, temps, params)
+    thr_cpu = Sampler(None, V, 0, 1).thresholds(logits.cpu(), temps.cpu(), params)
+    for r, p in enumerate(params):
+        want = value_threshold(logits[r].cpu(), p.temperature, p.top_k, p.top_p)
+        assert float(thr[r]) == want, (r, float(thr[r]), want)
+        assert float(thr_cpu[r]) == want
+        assert want > float("-inf")   # the filter is active: not every token qualifies
+
+
 @pytest.mark.parametrize("tp", [2, 4])
 def test_sample_filtered_vocab_parallel_on_device(tp):
     """Vocab-parallel shards on the GPU (loopback TP ranks sharing the device): histograms are

@@ -6,7 +6,10 @@
   a captured stand-in copy from a static source), lands the rows in its static hidden_in, and
   a sending stage alternates two instances guarded by send-done events; every replay equals
   the eager stage forward over the same bucket-padded rows.
-(RCCL refuses two ranks on one device: the two-rank edge runs on the driver's 8-GPU node.)"""
+(RCCL refuses two ranks on one device: the two-rank edge runs on the driver's 8-GPU node, after
+the preflight's pp_edge_graph check has run exactly this pattern across the ranks.)"""
+import time
+
 import pytest
 import torch
 
@@ -55,13 +58,16 @@ def test_self_send_recv_captured_in_graph():
             torch.cuda.synchronize()
             torch.testing.assert_close(dst.float(), want.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
         assert c.async_error() == 0
+        # teardown in the engine's order: the graph that captured the transfer first, then a
+        # bounded finalize + destroy of the communicator (non-blocking: it cannot hang)
         del g
         torch.cuda.synchronize()
+        t0 = time.monotonic()
+        status = c.close(timeout=20.0)
+        assert status == "clean", status
+        assert time.monotonic() - t0 < 20.0
     finally:
-        # never destroyed: ncclCommDestroy of a communicator that ran (captured) point-to-point
-        # transfers waited forever on this image (the engine keeps its edges for the process'
-        # lifetime; the preflight leaks its check communicators the same way)
-        pass
+        c.close(abort=True)          # no-op after the clean close
 
 
 def _stage_model(first: bool):

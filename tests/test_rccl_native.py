@@ -126,9 +126,11 @@ def test_single_rank_communicator_collectives_and_graph():
         g.replay()
         torch.cuda.synchronize()
         assert torch.allclose(y, torch.full_like(y, 6.0))
-        sub.close()
+        del g
+        torch.cuda.synchronize()
+        assert sub.close() == "clean"
     finally:
-        c.close()
+        assert c.close() in ("clean", "released")
 
 
 @pytest.mark.gpu
@@ -160,6 +162,40 @@ def test_abort_all_and_error_poller():
     c.close()        # already aborted: no-op
     with pytest.raises(RuntimeError):
         c.all_reduce_(x)
+
+
+_INIT_HANG = """
+import time, torch
+from butterfly_amd import ops
+assert ops.load_library()
+from butterfly_amd.parallel.rccl import RcclComm, live_handles
+t0 = time.monotonic()
+try:
+    RcclComm.create(torch.ops.bfly.rccl_unique_id(), 2, 0, timeout=4.0)   # rank 1 never joins
+    print("NO-TIMEOUT")
+except TimeoutError as e:
+    print(f"TIMEOUT after {time.monotonic() - t0:.1f}s live={live_handles()}: {e}")
+"""
+
+
+@pytest.mark.gpu
+def test_init_deadline_aborts_instead_of_hanging():
+    """A communicator whose peer never joins (a 2-rank init with rank 1 absent) ends through the
+    non-blocking init's deadline: TimeoutError after ~4 s, the half-built communicator aborted,
+    nothing left in the handle table, the process exits normally (no watchdog os._exit)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _INIT_HANG], cwd=root, capture_output=True, text=True, timeout=90)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    line = next((ln for ln in r.stdout.splitlines() if ln.startswith("TIMEOUT")), None)
+    assert line is not None, out[-3000:]
+    took = float(line.split()[2].rstrip("s"))
+    assert 3.5 <= took < 30, line
+    assert "live=[]" in line, line
 
 
 @pytest.mark.gpu

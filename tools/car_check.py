@@ -8,6 +8,9 @@ and replay, and times the kernel.  On a multi-GPU node the same script runs one 
 usage: python -m butterfly_amd launch -n 2 -- python tools/car_check.py [--bench]"""
 import os
 import sys
+
+# ranks share cuda:0 here: opt in to shared-GPU IPC groups (refused in production)
+os.environ.setdefault("BFLY_IPC_SHARED_DEVICE", "1")
 import time
 
 import torch

@@ -12,6 +12,9 @@ script runs one rank per GPU.
 usage: python -m butterfly_amd launch -n 4 -- python tools/ep_ipc_check.py [--bench]"""
 import os
 import sys
+
+# ranks share cuda:0 here: opt in to shared-GPU IPC groups (refused in production)
+os.environ.setdefault("BFLY_IPC_SHARED_DEVICE", "1")
 import time
 
 import torch
