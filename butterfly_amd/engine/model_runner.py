@@ -172,11 +172,12 @@ class ModelRunner:
             for p in prefix:
                 pc.append(pc[-1] + p)
             pre_cu = t32(pc)
+            # every chunk's full table (prefix pages and the chunk's own): the paged prefill
+            # attention reads the chunk's keys from the cache too
             tab = np.zeros((len(chunk_sids), self.max_blocks), dtype=np.int32)
             for j, sid in enumerate(chunk_sids):
-                if prefix[j]:
-                    b = self.kv.manager.block_table(sid)
-                    tab[j, : len(b)] = b
+                b = self.kv.manager.block_table(sid)
+                tab[j, : len(b)] = b
             pre_tab = torch.from_numpy(tab).to(dev, non_blocking=True)
         fb = ForwardBatch(input_ids=t32(ids), positions=t32(pos), slots=t32(slots), is_prefill=True,
                           cu_seqlens=t32(cu), max_seqlen=max((cu[i + 1] - cu[i] for i in range(len(cu) - 1)), default=0),

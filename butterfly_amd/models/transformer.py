@@ -444,43 +444,22 @@ class TransformerLM:
         return ops.linear(self._norm(full, self.p["final_w"], self.p.get("final_b")), self.head_weight)
 
     def _mixed_attention(self, q, k, v, fb: ForwardBatch, kc, vc) -> torch.Tensor:
-        """Attention of a mixed step: paged decode for the first num_decode rows; for the
-        prompt-chunk rows, causal flash attention within the chunk, merged by log-sum-exp
-        (K16) with non-causal attention over the sequence's already-cached prefix."""
+        """Attention of a mixed step: paged decode for the first num_decode rows; the prompt-
+        chunk rows attend to their sequence's cached prefix and, causally, to the chunk itself.
+        With a cached prefix that is ONE pass over the paged cache (ops.attn_prefill_paged: the
+        chunk's K/V were appended by rope_kv just before), else flash attention over the chunk."""
         nd = fb.num_decode
         parts = []
         if nd:
             parts.append(ops.attn_decode(q[:nd], kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx))
         if q.shape[0] > nd:
-            qp, kp, vp = q[nd:], k[nd:], v[nd:]
+            qp = q[nd:]
             if fb.prefix_lens is not None and any(fb.prefix_lens):
-                o, lse = ops.attn_prefill(qp, kp, vp, fb.cu_seqlens, fb.max_seqlen, self.scale, True, return_lse=True)
-                kpre, vpre = self._gather_prefix(kc, vc, fb.prefix_tables, fb.prefix_lens, q.dtype)
-                o2, l2 = ops.attn_prefill(qp, kpre, vpre, fb.cu_seqlens, fb.max_seqlen, self.scale, False,
-                                          cu_seqlens_k=fb.prefix_cu, return_lse=True)
-                acc = o.float()
-                ops.attn_lse_merge_(acc, lse, o2, l2)
-                parts.append(acc.to(q.dtype))
+                parts.append(ops.attn_prefill_paged(qp, kc, vc, fb.prefix_tables, fb.cu_seqlens,
+                                                    fb.positions[nd:], fb.max_seqlen, self.scale))
             else:
-                parts.append(ops.attn_prefill(qp, kp, vp, fb.cu_seqlens, fb.max_seqlen, self.scale, True))
+                parts.append(ops.attn_prefill(qp, k[nd:], v[nd:], fb.cu_seqlens, fb.max_seqlen, self.scale, True))
         return parts[0] if len(parts) == 1 else torch.cat(parts)
-
-    @staticmethod
-    def _gather_prefix(kc, vc, tables, lens: list, dtype: Optional[torch.dtype] = None) -> tuple:
-        """Contiguous [sum(lens), Hkv, D] K and V of each sequence's first lens[i] cached tokens
-        (paged layouts: K [blocks, Hkv, BS, D], V [blocks, Hkv, D, BS])."""
-        BS = kc.shape[2]
-        ks, vs = [], []
-        for i, n in enumerate(lens):
-            if n == 0:
-                continue
-            blk = tables[i, : (n + BS - 1) // BS].long()
-            ks.append(kc.index_select(0, blk).permute(0, 2, 1, 3).reshape(-1, kc.shape[1], kc.shape[3])[:n])
-            vs.append(vc.index_select(0, blk).permute(0, 3, 1, 2).reshape(-1, vc.shape[1], vc.shape[2])[:n])
-        k, v = torch.cat(ks), torch.cat(vs)
-        if dtype is not None and k.dtype != dtype:     # FP8 cache: widen for flash attention
-            k, v = k.to(dtype), v.to(dtype)
-        return k.contiguous(), v.contiguous()
 
     def _add_norm(self, t: torch.Tensor, prefix: str, residual: torch.Tensor, partial: bool,
                   consumer: Optional[tuple] = None) -> torch.Tensor:

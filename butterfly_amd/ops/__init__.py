@@ -386,6 +386,19 @@ def attn_prefill(q, k, v, cu_seqlens, max_seqlen: int, scale: float, causal: boo
     return (out, lse) if return_lse else out
 
 
+def attn_prefill_paged(q, k_cache, v_cache, tables, cu_q, positions, max_q: int, scale: float, out=None):
+    """Chunked prefill attention over the paged cache (attention_paged.hip): query rows
+    [cu_q[s], cu_q[s+1]) of sequence s at `positions` attend causally to the sequence's cached
+    keys through tables[s] — the cached prefix and the chunk itself (already appended by
+    rope_kv) in one pass, no gather, no log-sum-exp merge. Caches bf16 or FP8."""
+    if not _gpu(q):
+        return ref.attn_prefill_paged(q, k_cache, v_cache, tables, cu_q, positions, max_q, scale, out)
+    if out is None:
+        out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+    torch.ops.bfly.attn_prefill_paged(q, k_cache, v_cache, tables, cu_q, positions, int(max_q), float(scale), out)
+    return out
+
+
 def attn_lse_merge_(acc_o, acc_lse, o, lse):
     """K16: fold a partial attention result (o bf16 [T, H, D], lse [T, H]) into running f32
     accumulators (acc_o [T, H, D], acc_lse [T, H]) in place."""

@@ -378,6 +378,35 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx=None
     return out
 
 
+def attn_prefill_paged(q, k_cache, v_cache, tables, cu_q, positions, max_q, scale, out=None):
+    """Chunked prefill over the paged cache: rows [cu_q[s], cu_q[s+1]) of sequence s (query
+    positions `positions[row]`) attend causally to keys [0, positions[row]] of the sequence,
+    read through tables[s] (the chunk's own K/V are already in the cache)."""
+    T, Hq, D = q.shape
+    Hkv, BS = k_cache.shape[1], k_cache.shape[2]
+    G = Hq // Hkv
+    res = torch.zeros(T, Hq, D, dtype=q.dtype, device=q.device)
+    cu = [int(x) for x in cu_q.tolist()]
+    pos = positions.long()
+    for s in range(len(cu) - 1):
+        a, b = cu[s], cu[s + 1]
+        if b <= a:
+            continue
+        n = int(pos[b - 1]) + 1
+        nblk = (n + BS - 1) // BS
+        blocks = tables[s, :nblk].long()
+        ks = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nblk * BS, D)[:, :n].float().repeat_interleave(G, 0)
+        vs = v_cache[blocks].permute(1, 0, 3, 2).reshape(Hkv, nblk * BS, D)[:, :n].float().repeat_interleave(G, 0)
+        sc = torch.einsum("thd,hnd->htn", q[a:b].float(), ks) * scale
+        mask = torch.arange(n, device=q.device)[None, :] > pos[a:b, None]
+        sc = sc.masked_fill(mask[None], float("-inf"))
+        res[a:b] = torch.einsum("htn,hnd->thd", torch.softmax(sc, -1), vs).to(q.dtype)
+    if out is None:
+        return res
+    out.copy_(res)
+    return out
+
+
 # ---------------------------------------------------------------------------------------
 # Deterministic init and MoE gating
 # ---------------------------------------------------------------------------------------

@@ -503,9 +503,16 @@ class Communicator:
         return dist.irecv(t, src)
 
     def broadcast_(self, t: torch.Tensor, src_in_group: int = 0, group: str = "world") -> torch.Tensor:
+        """In-place broadcast from group rank `src_in_group`. On the group's native RCCL
+        communicator (the pipeline's per-tick token-id feedback, group "pp") it is ONE
+        stream-ordered ncclBroadcast on the current stream: no ProcessGroup work object or
+        watchdog per tick, and the ids never leave the device."""
         g = self.groups[group]
         if g.size == 1:
             return t
+        self.stats["calls"] += 1
+        if g.native is not None and t.is_cuda:
+            return g.native.broadcast_(t, src_in_group)   # split keys = group order
         dist.broadcast(t, g.ranks[src_in_group], group=g.pg)
         return t
 

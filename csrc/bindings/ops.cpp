@@ -542,6 +542,32 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   TORCH_CHECK(rc == 0, "attn_decode: unsupported configuration (rc=", rc, ")");
 }
 
+// Chunked prefill over the paged cache (attention_paged.hip): q [T, Hq, D] rows grouped per
+// sequence by cu_q, positions [T] their absolute positions, tables [nseq, max_blocks].
+void attn_prefill_paged(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& tables,
+                        const Tensor& cu_q, const Tensor& positions, int64_t max_q, double scale, Tensor& out) {
+  CHECK_GPU(q); CHECK_BF16(q); CHECK_KV(k_cache, v_cache); CHECK_BF16(out);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "attn_prefill_paged: q [T, Hq, D]");
+  TORCH_CHECK(out.dim() == 3 && out.sizes() == q.sizes() && out.stride(2) == 1 && out.stride(1) == out.size(2),
+              "attn_prefill_paged: out like q");
+  const int Hq = q.size(1), D = q.size(2);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "attn_prefill_paged: caches");
+  const int Hkv = k_cache.size(1), BS = k_cache.size(2);
+  TORCH_CHECK(k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS, "attn_prefill_paged: cache dims");
+  CHECK_I32(tables); CHECK_I32(cu_q); CHECK_I32(positions);
+  const int nseq = cu_q.numel() - 1;
+  TORCH_CHECK(tables.dim() == 2 && tables.size(0) >= nseq && tables.stride(1) == 1, "attn_prefill_paged: tables");
+  TORCH_CHECK(positions.numel() >= q.size(0) && cu_q.is_contiguous() && positions.is_contiguous(),
+              "attn_prefill_paged: positions / cu_q");
+  c10::DeviceGuard g(q.device());
+  const int rc = bfly::launch_attn_prefill_paged(bf(q), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                                 tables.data_ptr<int>(), tables.stride(0), cu_q.data_ptr<int>(),
+                                                 positions.data_ptr<int>(), nseq, (int)max_q, Hq, Hkv, D, BS,
+                                                 (float)scale, bf(out), out.stride(0), cur_stream(),
+                                                 k_cache.scalar_type() == at::kFloat8_e4m3fn);
+  TORCH_CHECK(rc == 0, "attn_prefill_paged: unsupported configuration (rc=", rc, ")");
+}
+
 void attn_prefill(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& cu_seqlens,
                   int64_t max_seqlen, double scale, bool causal, Tensor& out,
                   const c10::optional<Tensor>& cu_seqlens_k, const c10::optional<Tensor>& lse) {
@@ -1006,6 +1032,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("ep_ipc_combine(Tensor slot, int k, int capmax, int[] bases, int rank, Tensor(a!) out) -> ()");
   m.def("ep_ipc_stats(int ptr) -> int[]", &ep_ipc_stats);
   m.def("ep_ipc_error(int ptr) -> int", [](int64_t p) -> int64_t { return bfly::ep_ipc_error(reinterpret_cast<const void*>(p)); });
+  m.def("attn_prefill_paged(Tensor q, Tensor k_cache, Tensor v_cache, Tensor tables, Tensor cu_q, "
+        "Tensor positions, int max_q, float scale, Tensor(a!) out) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens, int max_seqlen, float scale, "
         "bool causal, Tensor(a!) out, Tensor? cu_seqlens_k=None, Tensor(b!)? lse=None) -> ()");
   m.def("attn_lse_merge(Tensor(a!) acc_o, Tensor(b!) acc_lse, Tensor o, Tensor lse) -> ()");
@@ -1036,6 +1064,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("rms_norm_rows", &rms_norm_rows);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
+  m.impl("attn_prefill_paged", &attn_prefill_paged);
   m.impl("attn_lse_merge", &attn_lse_merge);
   m.impl("probe", &probe);
   m.impl("custom_all_reduce", &custom_all_reduce);

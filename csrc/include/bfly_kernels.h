@@ -118,6 +118,13 @@ int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stri
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,
                         hipStream_t stream, const int* cu_k = nullptr,
                         float* lse = nullptr);
+// attention_paged.hip — chunked prefill over the paged cache: query rows [cu_q[s], cu_q[s+1])
+// of sequence s at positions[row] attend causally to keys [0, positions[row]] read through
+// tables[s] (the chunk's own K/V already appended). G = Hq / Hkv <= 8.
+int launch_attn_prefill_paged(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
+                              const int* tables, int bt_stride, const int* cu_q, const int* positions,
+                              int nseq, int max_q, int Hq, int Hkv, int D, int block_size, float scale,
+                              bf16* out, long o_stride, hipStream_t stream, int kv_fp8 = 0);
 // K16 (context parallel): acc_o [T, H, 128] f32 / acc_lse [T, H] f32 absorb (o, lse).
 int launch_attn_lse_merge(float* acc_o, float* acc_lse, const bf16* o, long o_stride,
                           const float* lse, int T, int H, int D, hipStream_t stream);

@@ -75,3 +75,32 @@ def test_moe_sparse_reference_matches_dense():
     ref.moe_gate_scale(h, gates, e0, El)
     dense = ref.linear(h, dn)
     torch.testing.assert_close(sparse, dense, atol=1e-4, rtol=1e-4)
+
+
+def test_paged_prefill_reference_equals_flash_over_the_whole_prompt():
+    """ops.reference.attn_prefill_paged (the oracle of the paged chunked-prefill kernel): a chunk
+    at positions [st, st + n) over paged K/V equals the last n rows of causal attention over the
+    whole prompt's contiguous K/V."""
+    import math
+
+    from butterfly_amd.ops import reference as ref
+
+    torch.manual_seed(5)
+    D, BS, Hq, Hkv = 128, 32, 8, 2
+    L, st = 150, 97
+    k = torch.randn(L, Hkv, D)
+    v = torch.randn(L, Hkv, D)
+    q = torch.randn(L, Hq, D)
+    nb = (L + BS - 1) // BS
+    perm = torch.randperm(nb + 3)[:nb]
+    kc = torch.zeros(nb + 3, Hkv, BS, D)
+    vc = torch.zeros(nb + 3, Hkv, D, BS)
+    for t in range(L):
+        kc[perm[t // BS], :, t % BS] = k[t]
+        vc[perm[t // BS], :, :, t % BS] = v[t]
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32)  # noqa: E731
+    scale = 1 / math.sqrt(D)
+    got = ref.attn_prefill_paged(q[st:], kc, vc, perm.view(1, -1).to(torch.int32), i32([0, L - st]),
+                                 i32(list(range(st, L))), L - st, scale)
+    want = ref.attn_prefill(q, k, v, i32([0, L]), L, scale, True)[st:]
+    torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-5)
