@@ -185,10 +185,16 @@ class LLMEngine:
                                   buckets, max_batch=engine_cfg.max_batch)
         # byte-minimal EP dispatch for the decode MoE layer (collective over the EP group, so
         # every EP rank sets it up here, eagerly, before any graph capture)
-        self.ep_ipc = False
+        self.ep_ipc = self.ep_ipc_prefill = False
         if mesh.ep > 1 and cfg.is_moe and flags.get("BFLY_EP_IPC"):
             self.ep_ipc = self.comm.enable_ep_ipc(max(self.runner.buckets[-1], engine_cfg.max_batch),
                                                   cfg.hidden_size, cfg.experts_per_token)
+            if flags.get("BFLY_EP_IPC_PREFILL"):
+                # prefill steps (and decode steps beside an EP peer's prefill): the same exchange
+                # sized for the prefill budget, bounded by device-resident counts (no host sync)
+                self.ep_ipc_prefill = self.comm.enable_ep_ipc_prefill(
+                    max(engine_cfg.max_prefill_tokens, engine_cfg.max_batch, self.runner.buckets[-1]),
+                    cfg.hidden_size, cfg.experts_per_token)
         if self._native_pp:
             self.runner.set_pipeline_io(recv_fn=None if coord.pp == 0 else self.comm.recv_native,
                                         sends=coord.pp < mesh.pp - 1)

@@ -454,12 +454,20 @@ def moe_route(x, wr, top_k: int, gates=None, topk_ids=None, topk_w=None):
 
 
 def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, ffn: int,
-                   expected_slots: Optional[int] = None):
+                   expected_slots: Optional[int] = None, block_counts: Optional[tuple] = None):
     """Routed expert FFN: permute the (token, k) pairs of the local experts into per-expert
     row slots (moe_align), grouped gate/up GEMM with fused SiLU over gathered token rows,
     grouped down GEMM, weighted combine back to token order. Only routed rows are computed
-    (the dense path computes every local expert for every token)."""
+    (the dense path computes every local expert for every token).
+    `block_counts` = (counts [nblk] int32 on the device, cap): the rows are nblk blocks of `cap`
+    rows of which only the first counts[b] are valid (the EP IPC prefill receive buffer, sized
+    for the worst case): the other rows get no expert work and no output row."""
     if not _gpu(x):
+        if block_counts is not None:
+            cnt, cap = block_counts
+            r = torch.arange(x.shape[0]) % cap
+            ok = r < cnt.cpu().long()[torch.arange(x.shape[0]) // cap]
+            topk_ids = topk_ids.masked_fill(~ok.unsqueeze(1), -1)
         return ref.moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0, num_local, ffn)
     T, H = x.shape
     k = topk_ids.shape[1]
@@ -468,6 +476,7 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
         return torch.zeros(T, H, dtype=x.dtype, device=x.device)
     L = torch.ops.bfly
     dev = x.device
+    bcnt, bcap = block_counts if block_counts is not None else (None, 0)
     # tile rows from the expected rows per expert (all slots are local in the EP dispatch):
     # one 128-row tile reads each expert's weights once where two 64-row tiles would twice
     # `expected_slots`: (token, k) pairs expected to be local (the EP dispatch pads with
@@ -479,7 +488,7 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
     nt = L.moe_max_tiles(TK, num_local, bm)
     tiles = _arena.get(dev, "moe_tiles", nt * 4, torch.int32)[:nt * 4].view(nt, 4)
     count = _arena.get(dev, "moe_count", 1, torch.int32)[:1]
-    L.moe_align(topk_ids, e0, num_local, rows, slot_of, tiles, count, bm)
+    L.moe_align(topk_ids, e0, num_local, rows, slot_of, tiles, count, bm, bcnt, bcap)
     hmid = torch.empty(TK, ffn, dtype=x.dtype, device=dev)
     L.moe_grouped_gemm(x, gu_w, hmid, rows, tiles, count, 2 * ffn * H, 2 * ffn, H, num_local, EPILOGUES["silu"], bm)
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
@@ -490,11 +499,11 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
         part = _arena.get(dev, "moe_part", sk * TK * H, torch.float32)[: sk * TK * H].view(sk, TK, H)
         L.moe_grouped_gemm(hmid, down_w, hmid.new_empty(TK, H), None, tiles, count, ffn, H, ffn, num_local,
                            EPILOGUES["none"], bm, part)
-        L.moe_combine_slabs(part, slot_of, topk_w, out)
+        L.moe_combine_slabs(part, slot_of, topk_w, out, bcnt, bcap)
         return out
     y = torch.empty(TK, H, dtype=x.dtype, device=dev)
     L.moe_grouped_gemm(hmid, down_w, y, None, tiles, count, ffn, H, ffn, num_local, EPILOGUES["none"], bm)
-    L.moe_combine(y, slot_of, topk_w, out)
+    L.moe_combine(y, slot_of, topk_w, out, bcnt, bcap)
     return out
 
 

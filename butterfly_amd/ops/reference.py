@@ -508,6 +508,8 @@ def ep_pack(x, ids, w, slots, experts_per_rank: int, ep: int, cap: int):
 def ep_combine(back, slot):
     """out[t] = sum of back[slot[t, d]] over the ranks d token t was sent to (f32 sum)."""
     T, ep = slot.shape
+    if T == 0:
+        return back.new_zeros(0, back.shape[1])
     ext = torch.cat([back.float(), back.new_zeros(1, back.shape[1]).float()])
     idx = torch.where(slot >= 0, slot.long(), back.shape[0])
     return ext.index_select(0, idx.view(-1)).view(T, ep, -1).sum(1).to(back.dtype)

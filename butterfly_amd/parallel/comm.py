@@ -68,6 +68,7 @@ class Communicator:
         self.groups = groups
         self.custom_ar = None            # optional CustomAllReduce for the tp group
         self.ep_ipc = None               # optional byte-minimal EP dispatch (parallel/ep_ipc.py)
+        self.ep_ipc_prefill = None       # the same exchange sized for prefill steps (no host sync)
         self.stats = {"all_reduce_bytes": 0, "send_bytes": 0, "recv_bytes": 0, "calls": 0}
         # native RCCL pipeline edges (parallel/rccl.pp_edges): to the next / from the previous
         # stage; sends run on their own stream so a send never blocks the compute stream
@@ -210,6 +211,23 @@ class Communicator:
             self._start_poller()
         return self.ep_ipc is not None
 
+    def enable_ep_ipc_prefill(self, capmax: int, hidden: int, top_k: int) -> bool:
+        """A second IPC exchange sized for prefill steps (`capmax` tokens per source: the
+        engine's prefill budget). Its receive blocks are bounded by device-resident row counts,
+        so an EP prefill MoE layer needs no host synchronisation (ep_ipc.EpIpc.dispatch_prefill)."""
+        g = self.groups["ep"]
+        if g.size not in (2, 4, 8) or not torch.cuda.is_available() or g.pg is None:
+            return False
+        from .ep_ipc import EpIpc
+
+        ipc = EpIpc(g.ranks, g.rank_in_group, g.pg, capmax, hidden, top_k)
+        self.ep_ipc_prefill = ipc if ipc.ok else None
+        if not ipc.ok:
+            ipc.close()
+        else:
+            self._start_poller()
+        return self.ep_ipc_prefill is not None
+
     def ep_dispatch(self, x: torch.Tensor, ids: torch.Tensor, w: torch.Tensor, slots, experts_per_rank: int,
                     cap: int):
         """Fixed-capacity EP token dispatch (decode): every token goes once to each EP rank
@@ -283,7 +301,7 @@ class Communicator:
         if getattr(self, "_rccl_poller", None) is not None:
             self._rccl_poller.stop()
             self._rccl_poller = None
-        for name in ("custom_ar", "ep_ipc"):
+        for name in ("custom_ar", "ep_ipc", "ep_ipc_prefill"):
             obj = getattr(self, name)
             if obj is not None:
                 obj.close()

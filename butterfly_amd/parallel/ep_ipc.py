@@ -24,6 +24,7 @@ from __future__ import annotations
 import logging
 import threading
 from dataclasses import dataclass
+from typing import Optional
 
 import torch
 import torch.distributed as dist
@@ -45,6 +46,8 @@ class EpRoute:
     slot: torch.Tensor
     T: int
     path: str
+    counts: Optional[torch.Tensor] = None   # prefill: rows per source block [ep] (device int32)
+    cap: int = 0                            # rows per source block of x / ids / w
 
 
 class EpIpc:
@@ -107,6 +110,7 @@ class EpIpc:
             self.xv = L.ep_ipc_view(self._ptr, self._off["x"], rows, self.H, 0, dev)
             self.idv = L.ep_ipc_view(self._ptr, self._off["ids"], rows, self.K, 1, dev)
             self.wv = L.ep_ipc_view(self._ptr, self._off["w"], rows, self.K, 2, dev)
+            self.countsv = L.ep_ipc_view(self._ptr, L.ep_ipc_counts_offset(), 1, self.ep, 1, dev).view(self.ep)
             self.ok = self._self_test(pg)
 
     def fits(self, x: torch.Tensor, ids: torch.Tensor, cap: int) -> bool:
@@ -121,6 +125,20 @@ class EpIpc:
                           self.capmax, self.bases, self.rank, slot)
         L.ep_ipc_wait(x, self.bases, self.rank)
         return EpRoute(self.xv, self.idv, self.wv, slot, T, "ipc")
+
+    def dispatch_prefill(self, x, ids, w, experts_per_rank: int) -> EpRoute:
+        """Prefill-sized dispatch (any T <= capmax, no host sync): a device scan routes the
+        tokens, each routed row is stored once into its owners' blocks, and the per-source row
+        counts land in every receiver's header. The receive blocks are NOT marked empty row by
+        row: the route carries the device-resident counts, and the expert FFN bounds each block
+        by them (ops.moe_sparse_ffn block_counts)."""
+        T = x.shape[0]
+        slot = torch.empty(T, self.ep, dtype=torch.int32, device=x.device)
+        L = torch.ops.bfly
+        L.ep_ipc_dispatch_prefill(x.contiguous(), ids.contiguous(), w.contiguous(), experts_per_rank,
+                                  self.capmax, self.bases, self.rank, slot)
+        L.ep_ipc_wait(x, self.bases, self.rank)
+        return EpRoute(self.xv, self.idv, self.wv, slot, T, "ipc", self.countsv, self.capmax)
 
     def combine(self, y: torch.Tensor, route: EpRoute) -> torch.Tensor:
         L = torch.ops.bfly
@@ -214,22 +232,30 @@ class EpLoopback:
     stores only routed rows into the peers' blocks, meets the peers at a checked rendezvous
     where the GPU path spins on flags, returns only the counted rows."""
 
-    def __init__(self, comm, capmax: int, hidden: int, top_k: int, dtype=torch.bfloat16):
+    def __init__(self, comm, capmax: int, hidden: int, top_k: int, dtype=None, name: str = "ep_ipc"):
         self.comm = comm
         g = comm.groups["ep"]
         self.ep, self.rank = g.size, g.rank_in_group
         self.capmax, self.H, self.K = int(capmax), int(hidden), int(top_k)
-        world = comm.world
-        key = ("ep_ipc", tuple(g.ranks))
-        with world.cv:
-            sh = getattr(world, "shared", None)
-            if sh is None:
-                sh = world.shared = {}
-            if key not in sh:
-                sh[key] = _LoopbackShared(self.ep, self.capmax, self.H, self.K, dtype)
-            self.sh = sh[key]
+        self._key = (name, tuple(g.ranks))
+        self._sh = None
+        self._dtype = dtype          # None: the activations' dtype at the first dispatch
         self.rows_out = self.rows_back = 0
         self.ok = True
+
+    @property
+    def sh(self) -> "_LoopbackShared":
+        if self._sh is None:
+            world = self.comm.world
+            with world.cv:
+                shared = getattr(world, "shared", None)
+                if shared is None:
+                    shared = world.shared = {}
+                key = self._key + (self._dtype,)
+                if key not in shared:
+                    shared[key] = _LoopbackShared(self.ep, self.capmax, self.H, self.K, self._dtype)
+                self._sh = shared[key]
+        return self._sh
 
     def fits(self, x, ids, cap: int) -> bool:
         return x.shape[1] == self.H and ids.shape[1] == self.K and cap <= self.capmax and x.shape[0] <= cap
@@ -241,6 +267,8 @@ class EpLoopback:
     def dispatch(self, x, ids, w, slots, experts_per_rank: int, cap: int) -> EpRoute:
         from ..ops import reference as ref
 
+        if self._dtype is None:
+            self._dtype = x.dtype         # the receive buffers hold rows exactly as sent
         T = x.shape[0]
         C, s, sh = self.capmax, self.rank, self.sh
         send, meta, gslot = ref.ep_pack(x.cpu(), ids.cpu(), w.cpu().float(), None if slots is None else slots.cpu(),
@@ -258,6 +286,14 @@ class EpLoopback:
                 self.rows_out += n
         self._rendezvous("ep_dispatch")
         return EpRoute(sh.x[s].clone(), sh.ids[s].clone(), sh.w[s].clone(), slot, T, "loopback")
+
+    def dispatch_prefill(self, x, ids, w, experts_per_rank: int) -> EpRoute:
+        """The prefill dispatch of EpIpc: the same rows and slots; the counts travel with the
+        route (the emulation also marks empty rows, which the block counts make unnecessary)."""
+        r = self.dispatch(x, ids, w, None, experts_per_rank, x.shape[0])
+        r.counts = torch.tensor([self.sh.counts[self.rank][s] for s in range(self.ep)], dtype=torch.int32)
+        r.cap = self.capmax
+        return r
 
     def combine(self, y: torch.Tensor, route: EpRoute) -> torch.Tensor:
         C, me, sh = self.capmax, self.rank, self.sh

@@ -279,5 +279,14 @@ class FakeComm(Communicator):
         self.ep_ipc = EpLoopback(self, capmax, hidden, top_k)
         return True
 
+    def enable_ep_ipc_prefill(self, capmax: int, hidden: int, top_k: int) -> bool:
+        """The prefill-sized IPC exchange, emulated on its own shared buffers."""
+        if self.groups["ep"].size not in (2, 4, 8):
+            return False
+        from .ep_ipc import EpLoopback
+
+        self.ep_ipc_prefill = EpLoopback(self, capmax, hidden, top_k, name="ep_ipc_prefill")
+        return True
+
     def check_health(self):
         return None

@@ -72,6 +72,9 @@ define("BFLY_EP_DECODE_A2A", True, _bool, "EP MoE on decode (and idle) steps: fi
        "routed-rows-only expert GEMMs, graph-capturable (0: all-gather + dense local experts + reduce-scatter)")
 define("BFLY_EP_IPC", True, _bool, "EP MoE on decode: byte-minimal dispatch / return over peer IPC buffers "
        "(only routed rows travel; self-tested at start-up, else the fixed-capacity all-to-all)")
+define("BFLY_EP_IPC_PREFILL", True, _bool, "EP MoE on prefill steps (with BFLY_EP_IPC): the byte-minimal IPC exchange "
+       "sized for the prefill budget, routed by a device scan and bounded by device-resident row counts (no host "
+       "sync per layer; else the host-split variable all-to-all)")
 define("BFLY_EP_ALLTOALL", True, _bool, "EP MoE on prefill steps: dispatch tokens by all-to-all (else all-gather / reduce-scatter)")
 define("BFLY_PP_ASYNC", True, _bool, "pipeline parallelism: keep pp decode groups in flight across steps "
        "(one group per stage per tick, no fill/drain bubble) instead of per-step microbatching")

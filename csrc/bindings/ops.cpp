@@ -637,8 +637,17 @@ void moe_route(const Tensor& x, const Tensor& wr, int64_t top_k, Tensor& gates, 
 
 int64_t moe_max_tiles(int64_t TK, int64_t El, int64_t bm) { return bfly::moe_max_tiles(TK, El, (int)bm); }
 
+// block counts (EP IPC receive buffer): rows form blocks of `bcap`; only the first bcnt[b] rows of
+// block b are valid (device-resident counts, so no host sync)
+static const int* block_counts(const c10::optional<Tensor>& bcnt, int64_t bcap, long rows, const char* what) {
+  if (!bcnt.has_value()) return nullptr;
+  CHECK_I32(*bcnt);
+  TORCH_CHECK(bcap > 0 && rows % bcap == 0 && bcnt->numel() >= rows / bcap, what, ": block counts");
+  return bcnt->data_ptr<int>();
+}
+
 void moe_align(const Tensor& topk_ids, int64_t e0, int64_t num_local, Tensor& rows, Tensor& slot_of,
-               Tensor& tiles, Tensor& count, int64_t bm) {
+               Tensor& tiles, Tensor& count, int64_t bm, const c10::optional<Tensor>& bcnt, int64_t bcap) {
   TORCH_CHECK(bm == 64 || bm == 128, "moe_align: tile rows 64 or 128");
   CHECK_GPU(topk_ids); CHECK_I32(topk_ids); CHECK_I32(rows); CHECK_I32(slot_of); CHECK_I32(tiles); CHECK_I32(count);
   TORCH_CHECK(topk_ids.dim() == 2 && topk_ids.is_contiguous(), "moe_align: topk_ids [T, k]");
@@ -649,9 +658,11 @@ void moe_align(const Tensor& topk_ids, int64_t e0, int64_t num_local, Tensor& ro
                   tiles.size(0) >= bfly::moe_max_tiles(T * K, num_local, (int)bm), "moe_align: tiles [max_tiles, 4]");
   TORCH_CHECK(count.numel() == 1, "moe_align: count");
   c10::DeviceGuard g(topk_ids.device());
+  const int* bc = block_counts(bcnt, bcap, T, "moe_align");
   const int rc = bfly::launch_moe_align(topk_ids.data_ptr<int>(), T, K, e0, num_local, (int)bm,
                                         rows.data_ptr<int>(), slot_of.data_ptr<int>(),
-                                        reinterpret_cast<int4*>(tiles.data_ptr<int>()), count.data_ptr<int>(), cur_stream());
+                                        reinterpret_cast<int4*>(tiles.data_ptr<int>()), count.data_ptr<int>(), cur_stream(),
+                                        bc, (int)bcap);
   TORCH_CHECK(rc == 0, "moe_align: rejected (", rc, ")");
 }
 
@@ -694,7 +705,8 @@ void moe_grouped_gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::
   TORCH_CHECK(rc == 0, "moe_grouped_gemm: rejected (", rc, ")");
 }
 
-void moe_combine(const Tensor& y, const Tensor& slot_of, const Tensor& topk_w, Tensor& out) {
+void moe_combine(const Tensor& y, const Tensor& slot_of, const Tensor& topk_w, Tensor& out,
+                 const c10::optional<Tensor>& bcnt, int64_t bcap) {
   CHECK_GPU(y); CHECK_BF16(y); CHECK_I32(slot_of); CHECK_BF16(out);
   TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.dim() == 2 && topk_w.is_contiguous(), "moe_combine: topk_w");
   const int T = topk_w.size(0), K = topk_w.size(1), H = out.size(1);
@@ -702,11 +714,12 @@ void moe_combine(const Tensor& y, const Tensor& slot_of, const Tensor& topk_w, T
                   y.size(1) == H, "moe_combine: shapes");
   c10::DeviceGuard g(y.device());
   const int rc = bfly::launch_moe_combine(bf(y), slot_of.data_ptr<int>(), topk_w.data_ptr<float>(), T, K, H, bf(out),
-                                          cur_stream());
+                                          cur_stream(), block_counts(bcnt, bcap, T, "moe_combine"), (int)bcap);
   TORCH_CHECK(rc == 0, "moe_combine: H % 8");
 }
 
-void moe_combine_slabs(const Tensor& part, const Tensor& slot_of, const Tensor& topk_w, Tensor& out) {
+void moe_combine_slabs(const Tensor& part, const Tensor& slot_of, const Tensor& topk_w, Tensor& out,
+                       const c10::optional<Tensor>& bcnt, int64_t bcap) {
   CHECK_GPU(part); CHECK_I32(slot_of); CHECK_BF16(out);
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.dim() == 3 && part.is_contiguous(), "moe_combine_slabs: part");
   TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.dim() == 2 && topk_w.is_contiguous(), "moe_combine_slabs: topk_w");
@@ -716,7 +729,7 @@ void moe_combine_slabs(const Tensor& part, const Tensor& slot_of, const Tensor& 
   c10::DeviceGuard g(part.device());
   const int rc = bfly::launch_moe_combine_slabs(part.data_ptr<float>(), (int)part.size(0), part.size(1) * (long)H,
                                                 slot_of.data_ptr<int>(), topk_w.data_ptr<float>(), T, K, H, bf(out),
-                                                cur_stream());
+                                                cur_stream(), block_counts(bcnt, bcap, T, "moe_combine_slabs"), (int)bcap);
   TORCH_CHECK(rc == 0, "moe_combine_slabs: H % 4");
 }
 
@@ -920,6 +933,27 @@ void ep_ipc_dispatch(const Tensor& x, const Tensor& ids, const Tensor& w, const 
   TORCH_CHECK(rc == 0, "ep_ipc_dispatch: rejected (", rc, ")");
 }
 
+// Prefill-sized dispatch (T up to capmax; ep_ipc.hip launch_ep_ipc_dispatch_prefill)
+void ep_ipc_dispatch_prefill(const Tensor& x, const Tensor& ids, const Tensor& w, int64_t experts_per_rank,
+                             int64_t capmax, at::IntArrayRef bases, int64_t rank, Tensor& slot) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_I32(ids); CHECK_I32(slot);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "ep_ipc_dispatch_prefill: x [T, H] contiguous");
+  const int T = x.size(0), H = x.size(1), ep = (int)bases.size();
+  TORCH_CHECK(ids.dim() == 2 && ids.size(0) == T && ids.is_contiguous(), "ep_ipc_dispatch_prefill: ids [T, k]");
+  const int K = ids.size(1);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == (long)T * K,
+              "ep_ipc_dispatch_prefill: w");
+  TORCH_CHECK(capmax >= T, "ep_ipc_dispatch_prefill: more tokens than the buffer's capacity");
+  TORCH_CHECK(slot.is_contiguous() && slot.numel() == (long)T * ep, "ep_ipc_dispatch_prefill: slot [T, ep]");
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_ep_ipc_dispatch_prefill(bf(x), ids.data_ptr<int>(), w.data_ptr<float>(), T, K, H,
+                                                      (int)experts_per_rank, ep, (int)capmax, ep_peers(bases),
+                                                      (int)rank, slot.data_ptr<int>(), cur_stream());
+  TORCH_CHECK(rc == 0, "ep_ipc_dispatch_prefill: rejected (", rc, ")");
+}
+
+int64_t ep_ipc_counts_offset() { return bfly::ep_ipc_counts_offset(); }
+
 void ep_ipc_wait(const Tensor& like, at::IntArrayRef bases, int64_t rank) {
   CHECK_GPU(like);
   c10::DeviceGuard g(like.device());
@@ -1000,11 +1034,15 @@ TORCH_LIBRARY(bfly, m) {
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
   m.def("moe_max_tiles(int tk, int num_local, int bm=64) -> int", &moe_max_tiles);
   m.def("moe_align(Tensor topk_ids, int e0, int num_local, Tensor(a!) rows, Tensor(b!) slot_of, Tensor(c!) tiles, "
-        "Tensor(d!) count, int bm=64) -> ()");
+        "Tensor(d!) count, int bm=64, Tensor? bcnt=None, int bcap=0) -> ()");
   m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? rows, Tensor tiles, Tensor count, int w_estride, "
         "int n, int k, int num_experts, int epilogue, int bm=64, Tensor(b!)? part=None) -> ()");
-  m.def("moe_combine(Tensor y, Tensor slot_of, Tensor topk_w, Tensor(a!) out) -> ()");
-  m.def("moe_combine_slabs(Tensor part, Tensor slot_of, Tensor topk_w, Tensor(a!) out) -> ()");
+  m.def("moe_combine(Tensor y, Tensor slot_of, Tensor topk_w, Tensor(a!) out, Tensor? bcnt=None, int bcap=0) -> ()");
+  m.def("moe_combine_slabs(Tensor part, Tensor slot_of, Tensor topk_w, Tensor(a!) out, Tensor? bcnt=None, "
+        "int bcap=0) -> ()");
+  m.def("ep_ipc_dispatch_prefill(Tensor x, Tensor ids, Tensor w, int experts_per_rank, int capmax, int[] bases, "
+        "int rank, Tensor(a!) slot) -> ()");
+  m.def("ep_ipc_counts_offset() -> int", &ep_ipc_counts_offset);
   m.def("ep_pack(Tensor x, Tensor ids, Tensor w, Tensor? slots, int experts_per_rank, int ep, int cap, "
         "Tensor(a!) send, Tensor(b!) meta, Tensor(c!) slot) -> ()");
   m.def("ep_combine(Tensor back, Tensor slot, Tensor(a!) out) -> ()");
@@ -1074,6 +1112,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("moe_grouped_gemm", &moe_grouped_gemm);
   m.impl("moe_combine", &moe_combine);
   m.impl("moe_combine_slabs", &moe_combine_slabs);
+  m.impl("ep_ipc_dispatch_prefill", &ep_ipc_dispatch_prefill);
   m.impl("ep_pack", &ep_pack);
   m.impl("ep_combine", &ep_combine);
   m.impl("ep_ipc_dispatch", &ep_ipc_dispatch);

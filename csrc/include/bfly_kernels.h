@@ -168,6 +168,15 @@ int launch_ep_ipc_return(const bf16* y, int H, int K, int ep, int capmax, const 
                          hipStream_t stream);
 int launch_ep_ipc_combine(const int* slot, int T, int H, int K, int ep, int capmax, const ArPeers& peers,
                           int rank, bf16* out, hipStream_t stream);
+// Prefill-sized dispatch (any T <= capmax): a one-workgroup scan routes the tokens (slot_out,
+// per-destination totals), then one workgroup per token stores its row once into each owning
+// rank's block; the last arriver publishes the row counts and raises the dispatch flags. The
+// receive blocks are not marked row by row: consumers bound each block by its count
+// (ep_ipc_counts_offset / launch_moe_align bcnt).
+int launch_ep_ipc_dispatch_prefill(const bf16* x, const int* ids, const float* w, int T, int K, int H, int El,
+                                   int ep, int capmax, const ArPeers& peers, int rank, int* slot_out,
+                                   hipStream_t stream);
+long ep_ipc_counts_offset();
 int ep_ipc_stats(const void* base, long long* out2);
 int ep_ipc_error(const void* base);
 
@@ -179,10 +188,13 @@ void launch_moe_gate_scale(bf16* h, const float* gates, long T, int E, int e0, i
 
 // sparse MoE (moe.hip + gemm.hip grouped tiles)
 int moe_max_tiles(int TK, int El, int BM);
+// bcnt / bcap (optional): rows are blocks of bcap rows, of which the first bcnt[block] are
+// valid (EP IPC receive buffer): other rows get no slot and no combined output
 int launch_moe_align(const int* topk_ids, int T, int K, int e0, int El, int BM, int* rows,
-                     int* slot_of, int4* tiles, int* count, hipStream_t stream);
+                     int* slot_of, int4* tiles, int* count, hipStream_t stream,
+                     const int* bcnt = nullptr, int bcap = 0);
 int launch_moe_combine(const bf16* y, const int* slot_of, const float* w, int T, int K, int H,
-                       bf16* out, hipStream_t stream);
+                       bf16* out, hipStream_t stream, const int* bcnt = nullptr, int bcap = 0);
 constexpr int kMoeGroupBM = 64;
 int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w_estride, int N,
                         int K, int epi, const int* rows, const int4* tiles, const int* count,
@@ -192,7 +204,8 @@ int launch_ep_pack(const bf16* x, const int* ids, const float* w, const int* slo
                    int El, int ep, int cap, bf16* send, float* meta, int* slot, hipStream_t stream);
 int launch_ep_combine(const bf16* back, const int* slot, int T, int H, int ep, bf16* out, hipStream_t stream);
 int launch_moe_combine_slabs(const float* part, int sk, long slab, const int* slot_of, const float* w,
-                             int T, int K, int H, bf16* out, hipStream_t stream);
+                             int T, int K, int H, bf16* out, hipStream_t stream,
+                             const int* bcnt = nullptr, int bcap = 0);
 
 // probe.hip
 void launch_probe(int which, float* out, hipStream_t stream);

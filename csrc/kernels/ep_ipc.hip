@@ -40,6 +40,7 @@ namespace {
 
 constexpr long kEpCur = 0, kEpArriveD = 64, kEpArriveR = 128, kEpErr = 192;
 constexpr long kEpFlagsD = 256, kEpFlagsR = 512, kEpCounts = 768, kEpStats = 1024;
+constexpr long kEpTotals = 2048;   // prefill dispatch: this rank's per-destination row totals
 constexpr int kEpThreads = 256;
 constexpr long long kEpSpinTimeoutTicks = 20LL * 100000000LL;   // 20 s of the 100 MHz clock
 
@@ -244,6 +245,114 @@ ep_ipc_combine_kernel(const int* __restrict__ slot, int T, int H, int capmax, Ar
   }
 }
 
+// ---- prefill-sized dispatch (T up to capmax: thousands of tokens) ----------------------
+// The decode dispatch above recomputes every prefix count in every workgroup (O(T^2): fine
+// for a 64-row batch, not for a 16k-token prefill). Here one 1024-thread workgroup routes all
+// tokens with an exclusive scan: each thread counts its contiguous token chunk per destination,
+// the counts are scanned across the workgroup (wave shuffles, then the 16 wave totals), and a
+// second pass over the chunk writes slot[t][d] = rows of d before t (-1: not sent). Stable and
+// deterministic: the same slots as the decode dispatch.
+constexpr int kEpRouteThreads = 1024;
+
+template <int EP>
+__global__ void __launch_bounds__(kEpRouteThreads)
+ep_route_kernel(const int* __restrict__ ids, int T, int K, int El, int* __restrict__ slot_out,
+                int* __restrict__ totals) {
+  __shared__ int wsum[EP][kEpRouteThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int chunk = (T + kEpRouteThreads - 1) / kEpRouteThreads;
+  const int t0 = min(T, tid * chunk), t1 = min(T, t0 + chunk);
+  int cnt[EP];
+#pragma unroll
+  for (int d = 0; d < EP; ++d) cnt[d] = 0;
+  for (int t = t0; t < t1; ++t) {
+    bool h[EP];
+    ep_ipc_hits<EP>(ids, t, K, El, nullptr, h);
+#pragma unroll
+    for (int d = 0; d < EP; ++d) cnt[d] += h[d];
+  }
+  int excl[EP];
+#pragma unroll
+  for (int d = 0; d < EP; ++d) {
+    int v = cnt[d];                                  // inclusive scan inside the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o, 64);
+      if (lane >= o) v += u;
+    }
+    excl[d] = v - cnt[d];
+    if (lane == 63) wsum[d][wv] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int d = 0; d < EP; ++d) {
+    int before = 0, total = 0;
+    for (int w = 0; w < kEpRouteThreads / 64; ++w) {
+      before += w < wv ? wsum[d][w] : 0;
+      total += wsum[d][w];
+    }
+    excl[d] += before;
+    if (tid == 0) totals[d] = total;
+  }
+  for (int t = t0; t < t1; ++t) {
+    bool h[EP];
+    ep_ipc_hits<EP>(ids, t, K, El, nullptr, h);
+#pragma unroll
+    for (int d = 0; d < EP; ++d) slot_out[t * EP + d] = h[d] ? excl[d]++ : -1;
+  }
+}
+
+// grid = max(T, 1) workgroups: block t stores row t (ids / weights local to each destination)
+// once into every owning rank's block at its routed position; the last arriver publishes this
+// rank's row count at every destination and raises the dispatch flags (as the decode dispatch).
+template <int EP>
+__global__ void __launch_bounds__(kEpThreads)
+ep_ipc_scatter_kernel(const bf16* __restrict__ x, const int* __restrict__ ids, const float* __restrict__ w,
+                      int T, int K, int H, int El, int capmax, ArPeers peers, int rank, EpLayout L,
+                      const int* __restrict__ slot) {
+  __shared__ uint32_t s_e;
+  char* my = peers.base[rank];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) s_e = __hip_atomic_load(ep_word(my, kEpCur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  const uint32_t e = s_e;
+  if (b < T) {
+#pragma unroll
+    for (int d = 0; d < EP; ++d) {
+      const int pos = slot[b * EP + d];
+      if (pos < 0) continue;
+      const long row = (long)rank * capmax + pos;
+      char* pd = peers.base[d];
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(x + (long)b * H);
+      bf16x8* dst = reinterpret_cast<bf16x8*>(pd + L.x) + row * (H / 8);
+      for (int c = tid; c < H / 8; c += kEpThreads) dst[c] = src[c];
+      if (tid < K) {
+        const int ex = ids[b * K + tid];
+        const bool mine = ex >= 0 && ex / El == d;
+        reinterpret_cast<int*>(pd + L.ids)[row * K + tid] = mine ? ex : -1;
+        reinterpret_cast<float*>(pd + L.w)[row * K + tid] = mine ? w[b * K + tid] : 0.f;
+      }
+    }
+  }
+  if (ep_last_block(my, kEpArriveD)) {
+    if (tid == 0) {
+      const int* totals = reinterpret_cast<const int*>(my + kEpTotals);
+      long remote = 0;
+      for (int d = 0; d < EP; ++d) {
+        __hip_atomic_store(ep_word(peers.base[d], kEpCounts) + rank, (uint32_t)totals[d], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        if (d != rank) remote += totals[d];
+      }
+      reinterpret_cast<unsigned long long*>(my + kEpStats)[0] += (unsigned long long)remote;
+      __hip_atomic_store(ep_word(my, kEpCur), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __threadfence_system();     // the counts before the flags
+    __syncthreads();
+    if (tid < EP)
+      __hip_atomic_store(ep_word(peers.base[tid], kEpFlagsD) + rank, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
 
 EpLayout ep_ipc_layout(int ep, int capmax, int H, int K) {
@@ -278,6 +387,26 @@ int launch_ep_ipc_dispatch(const bf16* x, const int* ids, const float* w, const 
 #undef EP_DISPATCH
   return 0;
 }
+
+int launch_ep_ipc_dispatch_prefill(const bf16* x, const int* ids, const float* w, int T, int K, int H, int El,
+                                   int ep, int capmax, const ArPeers& peers, int rank, int* slot_out,
+                                   hipStream_t stream) {
+  if (H % 8 != 0 || K > kEpThreads || T < 0 || capmax < T || capmax <= 0 || El <= 0 || rank < 0 || rank >= ep)
+    return -1;
+  const EpLayout L = ep_ipc_layout(ep, capmax, H, K);
+  int* totals = reinterpret_cast<int*>(peers.base[rank] + kEpTotals);
+#define EP_PREFILL(N)                                                                                  \
+  do {                                                                                                 \
+    ep_route_kernel<N><<<1, kEpRouteThreads, 0, stream>>>(ids, T, K, El, slot_out, totals);            \
+    ep_ipc_scatter_kernel<N><<<T > 0 ? T : 1, kEpThreads, 0, stream>>>(x, ids, w, T, K, H, El, capmax,  \
+                                                                        peers, rank, L, slot_out);     \
+  } while (0)
+  EP_SWITCH(ep, EP_PREFILL)
+#undef EP_PREFILL
+  return 0;
+}
+
+long ep_ipc_counts_offset() { return kEpCounts; }
 
 int launch_ep_ipc_wait(const ArPeers& peers, int ep, int rank, hipStream_t stream) {
   if (rank < 0 || rank >= ep) return -1;

@@ -119,16 +119,24 @@ __global__ void moe_gate_scale_kernel(bf16* __restrict__ h, const float* __restr
   }
 }
 
+// `bcnt` (optional): the rows are ep blocks of `bcap` rows (the EP IPC receive buffer) of which
+// only the first bcnt[block] are valid this call; pairs of the other rows are skipped (slot -1),
+// so a receive buffer sized for the worst case costs work only for the rows that arrived.
 __global__ void __launch_bounds__(1024)
 moe_align_kernel(const int* __restrict__ topk_ids, int TK, int K, int e0, int El, int BM,
                  int* __restrict__ rows, int* __restrict__ slot_of, int4* __restrict__ tiles,
-                 int* __restrict__ count) {
+                 int* __restrict__ count, const int* __restrict__ bcnt, int bcap) {
   __shared__ int cnt[kMaxExperts], cur[kMaxExperts];
+  auto valid = [&](int i) {
+    if (bcnt == nullptr) return true;
+    const int row = i / K;
+    return row % bcap < bcnt[row / bcap];
+  };
   for (int e = threadIdx.x; e < El; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
   for (int i = threadIdx.x; i < TK; i += blockDim.x) {
     const int e = topk_ids[i] - e0;
-    if (e >= 0 && e < El) atomicAdd(&cnt[e], 1);
+    if (e >= 0 && e < El && valid(i)) atomicAdd(&cnt[e], 1);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -145,7 +153,7 @@ moe_align_kernel(const int* __restrict__ topk_ids, int TK, int K, int e0, int El
   __syncthreads();
   for (int i = threadIdx.x; i < TK; i += blockDim.x) {
     const int e = topk_ids[i] - e0;
-    if (e >= 0 && e < El) {
+    if (e >= 0 && e < El && valid(i)) {
       const int pos = atomicAdd(&cur[e], 1);
       rows[pos] = i / K;
       slot_of[i] = pos;
@@ -157,8 +165,10 @@ moe_align_kernel(const int* __restrict__ topk_ids, int TK, int K, int e0, int El
 
 __global__ void __launch_bounds__(256)
 moe_combine_kernel(const bf16* __restrict__ y, const int* __restrict__ slot_of,
-                   const float* __restrict__ w, int K, int H, bf16* __restrict__ out) {
+                   const float* __restrict__ w, int K, int H, bf16* __restrict__ out,
+                   const int* __restrict__ bcnt, int bcap) {
   const long t = blockIdx.x;
+  if (bcnt != nullptr && t % bcap >= bcnt[t / bcap]) return;   // row did not arrive: not written
   for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int j = 0; j < K; ++j) {
@@ -180,8 +190,10 @@ moe_combine_kernel(const bf16* __restrict__ y, const int* __restrict__ slot_of,
 // grouped down GEMM's split-K reduce folded in (f32 throughout, one bf16 rounding)
 __global__ void __launch_bounds__(256)
 moe_combine_slabs_kernel(const float* __restrict__ part, int sk, long slab, const int* __restrict__ slot_of,
-                         const float* __restrict__ w, int K, int H, bf16* __restrict__ out) {
+                         const float* __restrict__ w, int K, int H, bf16* __restrict__ out,
+                         const int* __restrict__ bcnt, int bcap) {
   const long t = blockIdx.x;
+  if (bcnt != nullptr && t % bcap >= bcnt[t / bcap]) return;
   for (int c = threadIdx.x * 4; c < H; c += 256 * 4) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int j = 0; j < K; ++j) {
@@ -198,10 +210,10 @@ moe_combine_slabs_kernel(const float* __restrict__ part, int sk, long slab, cons
 }
 
 int launch_moe_combine_slabs(const float* part, int sk, long slab, const int* slot_of, const float* w,
-                             int T, int K, int H, bf16* out, hipStream_t stream) {
-  if (H % 4 != 0 || sk < 1) return -1;
+                             int T, int K, int H, bf16* out, hipStream_t stream, const int* bcnt, int bcap) {
+  if (H % 4 != 0 || sk < 1 || (bcnt != nullptr && bcap <= 0)) return -1;
   if (T <= 0) return 0;
-  moe_combine_slabs_kernel<<<T, 256, 0, stream>>>(part, sk, slab, slot_of, w, K, H, out);
+  moe_combine_slabs_kernel<<<T, 256, 0, stream>>>(part, sk, slab, slot_of, w, K, H, out, bcnt, bcap);
   return 0;
 }
 
@@ -340,18 +352,18 @@ int launch_ep_combine(const bf16* back, const int* slot, int T, int H, int ep, b
 int moe_max_tiles(int TK, int El, int BM) { return (TK + BM - 1) / BM + El; }
 
 int launch_moe_align(const int* topk_ids, int T, int K, int e0, int El, int BM, int* rows,
-                     int* slot_of, int4* tiles, int* count, hipStream_t stream) {
-  if (El <= 0 || El > kMaxExperts || BM <= 0) return -1;
+                     int* slot_of, int4* tiles, int* count, hipStream_t stream, const int* bcnt, int bcap) {
+  if (El <= 0 || El > kMaxExperts || BM <= 0 || (bcnt != nullptr && (bcap <= 0 || T % bcap != 0))) return -1;
   if (T <= 0) return (int)hipMemsetAsync(count, 0, sizeof(int), stream);   // no tiles
-  moe_align_kernel<<<1, 1024, 0, stream>>>(topk_ids, T * K, K, e0, El, BM, rows, slot_of, tiles, count);
+  moe_align_kernel<<<1, 1024, 0, stream>>>(topk_ids, T * K, K, e0, El, BM, rows, slot_of, tiles, count, bcnt, bcap);
   return 0;
 }
 
 int launch_moe_combine(const bf16* y, const int* slot_of, const float* w, int T, int K, int H,
-                       bf16* out, hipStream_t stream) {
-  if (H % 8 != 0) return -1;
+                       bf16* out, hipStream_t stream, const int* bcnt, int bcap) {
+  if (H % 8 != 0 || (bcnt != nullptr && bcap <= 0)) return -1;
   if (T <= 0) return 0;
-  moe_combine_kernel<<<T, 256, 0, stream>>>(y, slot_of, w, K, H, out);
+  moe_combine_kernel<<<T, 256, 0, stream>>>(y, slot_of, w, K, H, out, bcnt, bcap);
   return 0;
 }
 

@@ -74,3 +74,32 @@ def test_expert_parallel_engine_ipc_on_off(ipc, monkeypatch):
     assert (outs[0][1] is not None) == (ipc == "1")
     if ipc == "1":
         assert outs[0][1].stats()["rows_out"] > 0
+
+
+@pytest.mark.parametrize("ep", [2, 4])
+def test_prefill_ipc_moe_equals_all_to_all(ep):
+    """The EP prefill MoE layer over the IPC exchange (device scan route, block-count-bounded
+    receiver; loopback emulation) is bitwise the host-split all-to-all path, with different
+    token counts per rank (one rank idle)."""
+    from butterfly_amd import ops
+    from butterfly_amd.config import ModelConfig
+    from butterfly_amd.models import Shard, build_model
+
+    torch.set_num_threads(1)
+    mesh = Mesh(dp=ep, ep=ep)
+    world = FakeWorld(mesh, timeout_s=60)
+    cfg = ModelConfig.from_preset("mixtral-tiny")
+
+    def run(r, comm):
+        me = comm.rank_in("ep")
+        m = build_model(cfg, Shard(ep_rank=me, ep_size=ep), device="cpu", dtype=torch.float32, comm=comm)
+        m.init_random(0)
+        assert comm.enable_ep_ipc_prefill(64, cfg.hidden_size, cfg.experts_per_token)
+        T = 0 if me == ep - 1 else 9 + 5 * me
+        x = torch.randn(T, cfg.hidden_size, generator=torch.Generator().manual_seed(me))
+        _, ids, w = ops.moe_route(x, m.p["l0.router_w"], cfg.experts_per_token)
+        a = m._moe_ipc_prefill("l0.", x, ids, w, comm.ep_ipc_prefill)
+        b = m._moe_alltoall("l0.", x, ids, w)
+        return torch.equal(a, b) and a.shape == (T, cfg.hidden_size)
+
+    assert all(world.run(run))

@@ -548,6 +548,27 @@ def test_moe_sparse_ffn(T, E, El, e0, k, H, F):
     _close(got, dense, 3e-2, 3e-2)
 
 
+@pytest.mark.parametrize("cap,counts,El", [(96, [0, 37, 96, 5], 1), (256, [200, 3, 0, 17, 250, 1, 90, 64], 2)])
+def test_moe_sparse_ffn_block_counts(cap, counts, El):
+    """EP prefill receive buffer: blocks of `cap` rows of which only the first counts[b] are
+    valid (device-resident counts, rows beyond hold stale garbage with live expert ids). The
+    valid rows must equal the fp32 reference over exactly those rows; nothing else is computed
+    or written (the invalid output rows keep their poison)."""
+    H, F, E, k = 512, 1024, 8, 2
+    nb = len(counts)
+    T = nb * cap
+    x = _bf(T, H, seed=95)
+    _, ids, w = ops.moe_route(x, _bf(E, H, seed=96), k)
+    gu = _bf(El * 2 * F, H, scale=1.0 / math.sqrt(H), seed=97)
+    dn = _bf(H, El * F, scale=1.0 / math.sqrt(F), seed=98)
+    cnt = torch.tensor(counts, dtype=torch.int32, device=DEV)
+    got = ops.moe_sparse_ffn(x, ids, w, gu, dn, 1, El, F, block_counts=(cnt, cap))
+    valid = torch.cat([torch.arange(cap) < c for c in counts])
+    want = ref.moe_sparse_ffn(x.cpu().float()[valid], ids.cpu()[valid], w.cpu()[valid], gu.cpu().float(),
+                              dn.cpu().float(), 1, El, F)
+    _close(got[valid.to(DEV)], want, 3e-2, 3e-2)
+
+
 @pytest.mark.parametrize("T,El,e0,H,F,pad,expect", [(64, 1, 3, 1024, 4096, 0, None),     # bm 128, split-K
                                                     (200, 2, 2, 512, 2048, 0, None),     # bm 128, 2 experts
                                                     (512, 1, 5, 1024, 4096, 384, 256),   # EP dispatch padding

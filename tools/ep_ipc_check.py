@@ -135,6 +135,46 @@ for it in range(3):
 if ipc.error():
     fails.append(f"device error word {ipc.error()}")
 
+# 4. prefill-sized dispatch (device scan route, counts in the receivers' headers, no empty-row
+#    markers): ranks send different token counts (one sends none); received rows, counts,
+#    slots and the combined output against the all-to-all layout at the prefill capacity
+PCAP = 1536
+pipc = EpIpc(list(range(world)), rank, dist.group.WORLD, PCAP, H, K, device=dev)
+if not pipc.ok:
+    fails.append("prefill EP IPC self-test failed")
+else:
+    for salt, base_t in ((400, 1200), (401, 7)):
+        Ts = [0 if (r == world - 1 and salt == 400) else base_t + 37 * r for r in range(world)]
+        ins = [inputs(r, Ts[r], salt) for r in range(world)]
+        packs = [ref.ep_pack(x_, i_, w_, None, El, world, PCAP) for x_, i_, w_, _ in ins]
+        x, ids, w, _ = (t.to(dev) for t in ins[rank])
+        r = pipc.dispatch_prefill(x, ids, w, El)
+        counts = r.counts.cpu().tolist()
+        want_counts = [int((packs[s_][2][:, rank] >= 0).sum()) for s_ in range(world)]
+        if counts != want_counts:
+            fails.append(f"prefill T={Ts}: counts {counts} != {want_counts}")
+        gx, gi = r.x.cpu(), r.ids.cpu()
+        for s_ in range(world):
+            n = want_counts[s_]
+            blk = slice(s_ * PCAP, s_ * PCAP + n)
+            if not torch.equal(gx[blk], packs[s_][0][rank * PCAP:rank * PCAP + n]):
+                fails.append(f"prefill T={Ts}: rows from rank {s_} differ")
+            if not torch.equal(gi[blk], packs[s_][1][rank * PCAP:rank * PCAP + n, :K].contiguous().view(torch.int32)):
+                fails.append(f"prefill T={Ts}: ids from rank {s_} differ")
+        send, meta, slot = packs[rank]
+        pos = torch.where(slot >= 0, slot - torch.arange(world, dtype=torch.int32) * PCAP, slot)
+        if not torch.equal(r.slot.cpu(), pos):
+            fails.append(f"prefill T={Ts}: slot map differs")
+        y = (r.x.float() * (rank + 1)).to(torch.bfloat16)
+        out = pipc.combine(y, r)
+        torch.cuda.synchronize()
+        back = torch.cat([(send[d * PCAP:(d + 1) * PCAP].float() * (d + 1)).to(torch.bfloat16) for d in range(world)])
+        if not torch.equal(out.cpu(), ref.ep_combine(back, slot)):
+            fails.append(f"prefill T={Ts}: combined output differs")
+    if pipc.error():
+        fails.append(f"prefill device error word {pipc.error()}")
+    pipc.close()
+
 # 3. timing: one decode-sized exchange (dispatch + wait + return + combine), expert step elided
 if "--bench" in sys.argv:
     for T in (16, 64):
