@@ -43,6 +43,7 @@ constexpr long kEpFlagsD = 256, kEpFlagsR = 512, kEpCounts = 768, kEpStats = 102
 constexpr long kEpTotals = 2048;   // prefill dispatch: this rank's per-destination row totals
 constexpr int kEpThreads = 256;
 constexpr long long kEpSpinTimeoutTicks = 20LL * 100000000LL;   // 20 s of the 100 MHz clock
+constexpr int kEpSpinCombineMaxRows = 256;   // combines of more rows wait in a separate one-WG kernel
 
 __device__ __forceinline__ uint32_t* ep_word(char* base, long off) {
   return reinterpret_cast<uint32_t*>(base + off);
@@ -214,14 +215,18 @@ ep_ipc_return_kernel(const bf16* __restrict__ y, int H, int capmax, ArPeers peer
 // to. A rank with no tokens (T == 0: EP-idle step) still runs one workgroup, whose only job is
 // the flag_r wait: without it the rank's next dispatch could overwrite peers' x / ids / counts
 // blocks before they finished this layer's FFN (the single-buffering invariant above).
-template <int EP>
+// SPIN = false: a one-workgroup ep_ipc_wait_return_kernel already waited (prefill-sized T:
+// thousands of workgroups spinning would only hold CUs a co-resident peer kernel may need).
+template <int EP, bool SPIN>
 __global__ void __launch_bounds__(kEpThreads)
 ep_ipc_combine_kernel(const int* __restrict__ slot, int T, int H, int capmax, ArPeers peers, int rank, EpLayout L,
                       bf16* __restrict__ out) {
   char* my = peers.base[rank];
-  const uint32_t e = __hip_atomic_load(ep_word(my, kEpCur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (threadIdx.x < EP) ep_spin(ep_word(my, kEpFlagsR) + threadIdx.x, e, ep_word(my, kEpErr), peers.herr);
-  __syncthreads();
+  if constexpr (SPIN) {
+    const uint32_t e = __hip_atomic_load(ep_word(my, kEpCur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < EP) ep_spin(ep_word(my, kEpFlagsR) + threadIdx.x, e, ep_word(my, kEpErr), peers.herr);
+    __syncthreads();
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const long t = blockIdx.x;
   if (t >= T) return;
@@ -243,6 +248,17 @@ ep_ipc_combine_kernel(const int* __restrict__ slot, int T, int H, int capmax, Ar
     for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
     reinterpret_cast<bf16x8*>(out + t * H)[c] = o;
   }
+}
+
+// one workgroup: wait until every expert rank returned this epoch's rows (flag_r)
+template <int EP>
+__global__ void __launch_bounds__(64)
+ep_ipc_wait_return_kernel(ArPeers peers, int rank) {
+  char* my = peers.base[rank];
+  const uint32_t e = __hip_atomic_load(ep_word(my, kEpCur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < EP) ep_spin(ep_word(my, kEpFlagsR) + threadIdx.x, e, ep_word(my, kEpErr), peers.herr);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
 // ---- prefill-sized dispatch (T up to capmax: thousands of tokens) ----------------------
@@ -431,8 +447,19 @@ int launch_ep_ipc_combine(const int* slot, int T, int H, int K, int ep, int capm
   if (H % 8 != 0 || capmax <= 0 || rank < 0 || rank >= ep) return -1;
   if (T < 0) return -1;
   const EpLayout L = ep_ipc_layout(ep, capmax, H, K);
-#define EP_COMBINE(N) \
-  ep_ipc_combine_kernel<N><<<T > 0 ? T : 1, kEpThreads, 0, stream>>>(slot, T, H, capmax, peers, rank, L, out)
+  // decode-sized batches wait inside the combine (one launch); larger ones wait in one
+  // workgroup first, so no spinning workgroup holds a CU a co-resident peer kernel needs
+  const bool sep = T > kEpSpinCombineMaxRows;
+#define EP_COMBINE(N)                                                                                      \
+  do {                                                                                                     \
+    if (sep) {                                                                                             \
+      ep_ipc_wait_return_kernel<N><<<1, 64, 0, stream>>>(peers, rank);                                     \
+      ep_ipc_combine_kernel<N, false><<<T, kEpThreads, 0, stream>>>(slot, T, H, capmax, peers, rank, L, out); \
+    } else {                                                                                               \
+      ep_ipc_combine_kernel<N, true><<<T > 0 ? T : 1, kEpThreads, 0, stream>>>(slot, T, H, capmax, peers,  \
+                                                                             rank, L, out);                \
+    }                                                                                                      \
+  } while (0)
   EP_SWITCH(ep, EP_COMBINE)
 #undef EP_COMBINE
   return 0;
