@@ -93,6 +93,9 @@ class TransformerLM:
         self.rowscale_rows = (flags.get("BFLY_NORM_ROWSCALE_MAX_ROWS")
                               if (self.device.type == "cuda" and cfg.norm == "rms" and self.tp == 1
                                   and not cfg.is_moe and flags.get("BFLY_NORM_ROWSCALE")) else 0)
+        # ... and with the add+RMSNorm folded into the producing O / down GEMM's split-K seam
+        # (ops.linear_rmsnorm_rows): no separate norm launch at all
+        self.norm_seam = bool(self.rowscale_rows) and flags.get("BFLY_GEMM_NORM_SEAM")
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
@@ -387,6 +390,9 @@ class TransformerLM:
         else:
             attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
         o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
+        if self.norm_seam and o_b is None and T <= self.rowscale_rows:
+            # issued by the consuming add+RMSNorm (_add_norm), fused into the GEMM's split-K seam
+            return ops.LazyLinear(attn.view(T, d.hq * D), self.p[pre + "o_w"], self.defer_reduce)
         return ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce)
 
     # ------------------------------------------------------------------------------------
@@ -471,7 +477,12 @@ class TransformerLM:
         if consumer is not None and not partial and 0 < residual.shape[0] <= self.rowscale_rows:
             cw = self.p[consumer[0]]
             if ops.rowscale_ok(residual.shape[0], cw.shape[0], cw.shape[1], consumer[1]):
-                return ops.rms_norm(t, w, self.cfg.norm_eps, residual=residual, rows=True)
+                if isinstance(t, ops.LazyLinear):
+                    rn = ops.linear_rmsnorm_rows(t.x, t.w, w, self.cfg.norm_eps, residual)
+                    if rn is not None:
+                        return rn
+                return ops.rms_norm(ops.run_lazy(t), w, self.cfg.norm_eps, residual=residual, rows=True)
+        t = ops.run_lazy(t)
         if partial:
             if self.cfg.norm == "rms":
                 return self.comm.all_reduce_rms_norm_(t, w, self.cfg.norm_eps, residual, "tp")
@@ -526,6 +537,9 @@ class TransformerLM:
             return out, self.tp > 1
         if c.act == "silu":
             hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu")
+            if self.norm_seam and hmid.shape[0] <= self.rowscale_rows:
+                # the next block's add+RMSNorm issues it with the norm in the split-K seam
+                return ops.LazyLinear(hmid, self.p[pre + "down_w"], self.defer_reduce), self.tp > 1
             out = ops.linear(hmid, self.p[pre + "down_w"], defer=self.defer_reduce)
         else:
             hmid = ops.linear(x, self.p[pre + "fc_w"], bias=self.p.get(pre + "fc_b"))

@@ -122,6 +122,7 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
                  for b in range(1, max_batch + 1))
         _arena.get(device, "attn_o", max_batch * num_kv_heads * ns * 16 * head_dim, torch.float32)
         _arena.get(device, "attn_ml", max_batch * num_kv_heads * ns * 16 * 2, torch.float32)
+    _arena.get(device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
     _arena.get(device, "sample", max(max_batch, max_tokens, 1) * 64, torch.int64)
     _arena.get(device, "tkp", max(max_batch, max_tokens, 1) * 521, torch.float32)
 
@@ -149,7 +150,36 @@ class Partial:
         return self.out
 
 
+class LazyLinear:
+    """A GEMM `x @ w.T` not issued yet (decode O / down projections): the consuming add+RMSNorm
+    can run it with the norm fused into its split-K seam (`linear_rmsnorm_rows`); anything else
+    `materialize()`s it into a deferred linear (Partial or bf16 tensor)."""
+
+    __slots__ = ("x", "w", "defer")
+
+    def __init__(self, x: torch.Tensor, w: torch.Tensor, defer: bool = True):
+        self.x, self.w, self.defer = x, w, defer
+
+    @property
+    def shape(self):
+        return (self.x.shape[0], self.w.shape[0])
+
+    def materialize(self):
+        return materialize(linear(self.x, self.w, defer=self.defer))
+
+    def run(self):
+        """The GEMM as `linear(..., defer=...)` would return it (a Partial when split-K)."""
+        return linear(self.x, self.w, defer=self.defer)
+
+
+def run_lazy(x):
+    """A LazyLinear issued as its deferred GEMM (Partial / tensor); anything else unchanged."""
+    return x.run() if isinstance(x, LazyLinear) else x
+
+
 def materialize(x):
+    if isinstance(x, LazyLinear):
+        return x.materialize()
     return x.materialize() if isinstance(x, Partial) else x
 
 
@@ -206,6 +236,41 @@ def rms_norm(x, w, eps: float, out=None, residual=None, rows: bool = False):
         out = torch.empty_like(x)
     torch.ops.bfly.rms_norm(x, w, eps, out, residual)
     return out
+
+
+_norm_seam: dict = {}
+
+
+def norm_seam_ok(M: int, N: int, K: int) -> bool:
+    """True if the split-K GEMM plan of this shape can run the fused add+RMSNorm seam."""
+    key = (M, N, K)
+    ok = _norm_seam.get(key)
+    if ok is None:
+        ok = load_library() and torch.cuda.is_available() and torch.ops.bfly.gemm_norm_check(M, N, K) > 0
+        _norm_seam[key] = ok
+    return ok
+
+
+def linear_rmsnorm_rows(x, w, gamma, eps: float, residual) -> Optional[RowNormed]:
+    """residual += x @ w.T (bf16, in place); returns the RowNormed of the updated residual
+    (y = residual * gamma, per-128-column sums of squares) for a row-scaling consumer GEMM —
+    ONE kernel: every split-K workgroup of the GEMM reduces its share of its tile's rows after
+    its siblings arrived (gemm.hip seam_norm), so no separate add+RMSNorm launch runs. None
+    when this shape's plan cannot (the caller falls back to GEMM + rms_norm(rows=True))."""
+    if not _gpu(x):
+        return None
+    M, K, N = x.shape[0], x.shape[1], w.shape[0]
+    if not norm_seam_ok(M, N, K):
+        return None
+    need = torch.ops.bfly.gemm_workspace_size(M, N, K)
+    ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
+    cnt = _arena.get(x.device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    ssp = torch.empty(M, N // 128, dtype=torch.float32, device=x.device)
+    chunks = torch.ops.bfly.gemm_norm(x, w, ws, residual, gamma, y, ssp, cnt)
+    if chunks <= 0:
+        return None
+    return RowNormed(y, ssp, eps)
 
 
 def layer_norm(x, w, b, eps: float, out=None, residual=None):

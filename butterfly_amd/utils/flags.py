@@ -47,6 +47,9 @@ define("BFLY_NORM_ROWSCALE", True, _bool, "decode add+RMSNorm split over (row, 1
        "and partial sums of squares; the consuming QKV / gate-up GEMM applies the 1/rms row scale in its epilogue "
        "(tp == 1, batches <= BFLY_NORM_ROWSCALE_MAX_ROWS; 0: one-workgroup-per-row add+RMSNorm)")
 define("BFLY_NORM_ROWSCALE_MAX_ROWS", 256, int, "largest batch that takes the row-split add+RMSNorm")
+define("BFLY_GEMM_NORM_SEAM", True, _bool, "with the row-split add+RMSNorm: fold it into the producing O / down "
+       "GEMM's split-K seam (every split reduces its share of its tile's rows after its siblings arrive), "
+       "removing the separate norm launch (0: GEMM + rmsnorm_rows kernel)")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
 define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "

@@ -417,6 +417,37 @@ void gemm_rs(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<
   TORCH_CHECK(rc == 0, "gemm_rs: unsupported plan M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
 }
 
+// Split-K GEMM with the fused add + RMSNorm seam (gemm.hip seam_norm): y = (residual + x.W^T) *
+// gamma (bf16), residual updated in place, ssp [M, chunks] row sums of squares per 128-column
+// tile. Returns chunks (> 0) or <= 0 when the shape's plan cannot run the seam (nothing ran).
+int64_t gemm_norm(const Tensor& x, const Tensor& w, Tensor& workspace, Tensor& residual, const Tensor& gamma,
+                  Tensor& y, Tensor& ssp, Tensor& counters) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(residual); CHECK_BF16(gamma); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "gemm_norm: 2-D operands");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 128 == 0, "gemm_norm: shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && x.stride(1) == 1 && w.stride(0) % 8 == 0 && w.stride(1) == 1,
+              "gemm_norm: row strides % 8");
+  TORCH_CHECK(residual.is_contiguous() && residual.size(0) == M && residual.size(1) == N, "gemm_norm: residual");
+  TORCH_CHECK(y.is_contiguous() && y.size(0) == M && y.size(1) == N, "gemm_norm: y");
+  TORCH_CHECK(gamma.is_contiguous() && gamma.numel() == N, "gemm_norm: gamma");
+  TORCH_CHECK(ssp.scalar_type() == at::kFloat && ssp.is_contiguous() && ssp.dim() == 2 && ssp.size(0) == M &&
+                  ssp.size(1) == N / 128, "gemm_norm: ssp [M, N / 128] f32");
+  CHECK_I32(counters);
+  TORCH_CHECK(counters.is_contiguous() && counters.numel() > 16384, "gemm_norm: counters [16385]");
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_contiguous(), "gemm_norm: workspace");
+  const bfly::NormSeam seam{bf(residual), bf(gamma), bf(y), ssp.data_ptr<float>(), counters.data_ptr<int>(),
+                            reinterpret_cast<uint32_t*>(counters.data_ptr<int>() + 16384)};   // error word
+  c10::DeviceGuard g(x.device());
+  return bfly::launch_gemm_norm(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, workspace.data_ptr<float>(),
+                                workspace.numel() * sizeof(float), seam, cur_stream(), false);
+}
+
+int64_t gemm_norm_check(int64_t M, int64_t N, int64_t K) {
+  const bfly::NormSeam seam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  return bfly::launch_gemm_norm(nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, nullptr, 0, seam, nullptr, true);
+}
+
 int64_t gemm_deferred_rs(const Tensor& x, const Tensor& w, Tensor& out, Tensor& workspace, const Tensor& ssp,
                          double eps) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
@@ -1000,6 +1031,9 @@ TORCH_LIBRARY(bfly, m) {
   m.def("gemm_slab_offset() -> int", []() -> int64_t { return (int64_t)bfly::gemm_slab_offset_floats(); });
   m.def("gemm_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace, "
         "Tensor ssp, float eps) -> ()");
+  m.def("gemm_norm(Tensor x, Tensor w, Tensor(a!) workspace, Tensor(b!) residual, Tensor gamma, Tensor(c!) y, "
+        "Tensor(d!) ssp, Tensor(e!) counters) -> int");
+  m.def("gemm_norm_check(int M, int N, int K) -> int", &gemm_norm_check);
   m.def("gemm_deferred_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) workspace, Tensor ssp, float eps) -> int");
   m.def("rms_norm_rows(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) ssp, Tensor(c!)? residual) -> ()");
   m.def("rms_norm_rows_chunks(int dim) -> int", [](int64_t dim) -> int64_t { return bfly::rmsnorm_rows_chunks(dim); });
@@ -1102,6 +1136,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("rms_norm_rows", &rms_norm_rows);
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
+  m.impl("gemm_norm", &gemm_norm);
   m.impl("attn_prefill_paged", &attn_prefill_paged);
   m.impl("attn_lse_merge", &attn_lse_merge);
   m.impl("probe", &probe);

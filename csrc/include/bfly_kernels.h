@@ -19,6 +19,21 @@ struct RowScale {
   float inv_dim, eps;
 };
 
+// Split-K add + RMSNorm seam (decode O / down projections, tp = 1): after its partial slab,
+// every split workgroup of a tile waits for its sibling splits and then reduces ITS share of
+// the tile's rows: sum of the sk slabs (split order) -> bf16 -> + residual (bf16, written back)
+// -> y = x * gamma (bf16) and the row's sum of squares over the tile's columns into
+// ssp[row][n-tile]. The consumer GEMM applies rsqrt(sum(ssp[row]) / N + eps) (RowScale with
+// N / BN chunks). Replaces the separate add+RMSNorm kernel and its launch.
+struct NormSeam {
+  bf16* residual;       // [M, N] in/out (nullptr: no seam)
+  const bf16* gamma;    // [N]
+  bf16* y;              // [M, N]
+  float* ssp;           // [M, N / BN]
+  int* counters;        // per-tile arrival counters: monotonic, never reset (own region)
+  uint32_t* err;        // sibling-wait timeout word (nullable)
+};
+
 struct GemmPlan {
   int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 3 = decode ring,
              // 4 = 256x256 8-phase big tile (BK 64, prefill; kind 2 was the removed ring kernel)
@@ -91,6 +106,10 @@ int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, 
 int gemm_check(int M, int N, int K, int epi);
 // 0 if the auto plan for this shape takes a RowScale (tile and decode-ring kernels)
 int gemm_rowscale_check(int M, int N, int K, int epi);
+// Split-K GEMM with the add+RMSNorm seam (NormSeam). Returns the number of ssp chunks per row
+// (N / BN, > 0), or <= 0 when this shape's plan cannot run the seam (caller falls back).
+int launch_gemm_norm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
+                     size_t ws_bytes, const NormSeam& seam, hipStream_t stream, bool dry);
 // Y = X W^T without epilogue; when the plan splits K, the f32 slabs are left in the workspace
 // (at gemm_slab_offset_floats(), layout [sk][M][N]) for the consumer kernel to reduce, and the
 // split count is returned; otherwise `out` is written and 1 is returned. < 0: error.

@@ -177,6 +177,82 @@ __device__ __forceinline__ void splitk_fixup(const float* __restrict__ part, int
   }
 }
 
+// Add + RMSNorm seam (NormSeam, bfly_kernels.h): every split of a tile publishes its slab (the
+// split-K hand-off recipe above: drained plain stores, ONE agent-scope release, relaxed
+// ticket), waits until all `sk` siblings of its generation arrived (the counter is monotonic:
+// ticket / sk is this call's generation, so nothing is ever re-armed; wrap-safe compare), and
+// then reduces its 1/sk share of the tile's rows in split order 0..sk-1 — the numerics of the
+// separate rmsnorm_rows kernel: bf16 sum, bf16 residual add, y = x * gamma, f32 sum of squares
+// over the tile's columns. Siblings are co-resident (the launcher checks the grid fits), and the
+// wait is bounded: a sibling later than ~2 s sets the error word and the share proceeds.
+constexpr long long kSeamSpinTicks = 2LL * 100000000LL;   // 2 s of the 100 MHz constant clock
+
+template <int BN>
+__device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk, int split, int tile, int M,
+                                          int N, int m0, int BM, int n0, const NormSeam& seam) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* cnt = seam.counters + tile;
+    const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int target = (ticket / sk + 1) * sk;
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target < 0) {
+      const long long t0 = wall_clock64();
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > kSeamSpinTicks) {
+          if (seam.err != nullptr) __hip_atomic_store(seam.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  constexpr int TPR = BN / 8;                       // threads per row: 8 columns each
+  const int rpp = blockDim.x / TPR;                 // rows per pass
+  const int R = (BM + sk - 1) / sk;
+  const int r0 = m0 + split * R;
+  const int r1 = min(min(m0 + BM, r0 + R), M);
+  const int tn = n0 / BN, nchunks = N / BN;
+  const long slab = (long)M * N;
+  const int c = n0 + (threadIdx.x % TPR) * 8;
+  const bf16x8 g = *reinterpret_cast<const bf16x8*>(seam.gamma + c);
+  for (int base = r0; base < r1; base += rpp) {
+    const int row = base + threadIdx.x / TPR;
+    const bool ok = row < r1;
+    float ss = 0.f;
+    if (ok) {
+      const float* pr = part + (long)row * N + c;
+      f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+      for (int k = 1; k < sk; ++k) {
+        lo += *reinterpret_cast<const f32x4*>(pr + k * slab);
+        hi += *reinterpret_cast<const f32x4*>(pr + k * slab + 4);
+      }
+      bf16x8* rp = reinterpret_cast<bf16x8*>(seam.residual + (long)row * N + c);
+      const bf16x8 r = *rp;
+      bf16x8 sm, o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = bf2f(f2bf(j < 4 ? lo[j] : hi[j - 4]));     // the bf16 GEMM result
+        sm[j] = f2bf(a + bf2f(r[j]));                               // the stored bf16 residual
+        const float v = bf2f(sm[j]);
+        ss += v * v;
+        o[j] = f2bf(v * bf2f(g[j]));
+      }
+      *rp = sm;
+      *reinterpret_cast<bf16x8*>(seam.y + (long)row * N + c) = o;
+    }
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, TPR);
+    if (ok && threadIdx.x % TPR == 0) seam.ssp[(long)row * nchunks + tn] = ss;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Skinny (decode) GEMM
 // ---------------------------------------------------------------------------------------
@@ -419,7 +495,8 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
                  bf16* __restrict__ out, long ldo, float* __restrict__ part,
                  int* __restrict__ counters, const int* __restrict__ grows = nullptr,
                  const int4* __restrict__ gtiles = nullptr, const int* __restrict__ gcount = nullptr,
-                 long w_estride = 0, RowScale rsc = RowScale{nullptr, 0, 0.f, 0.f}) {
+                 long w_estride = 0, RowScale rsc = RowScale{nullptr, 0, 0.f, 0.f},
+                 NormSeam seam = NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}) {
   constexpr int WNW = 4 / WMW;                // waves along M x waves along N
   constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
@@ -504,6 +581,12 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
                         part ? part + (long)blockIdx.y * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
+  if constexpr (!GROUPED) {
+    if (part && seam.residual != nullptr) {
+      seam_norm<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
+      return;
+    }
+  }
   if (part && counters && splitk_arrive(counters + tile, gridDim.y, reinterpret_cast<int*>(smem)))
     splitk_fixup(part, gridDim.y, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
 }
@@ -555,7 +638,8 @@ template <int BM, int BN, int NWM, int NWN, int SW>
 __global__ void __launch_bounds__(kDecThreads)
 gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                bf16* __restrict__ out, long ldo, float* __restrict__ part, RowScale rsc) {
+                bf16* __restrict__ out, long ldo, float* __restrict__ part, RowScale rsc,
+                NormSeam seam = NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}) {
   constexpr int SX = 3, NW = NWM * NWN;
   static_assert(NW * 64 <= kDecThreads && SW >= SX, "decode ring configuration");
   constexpr int WM = BM / NWM, WN = BN / NWN;   // per-wave output block
@@ -624,6 +708,7 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
                         part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0, rsc);
+  if (part && seam.residual != nullptr) seam_norm<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
 }
 
 // Prefill tiles are walked in GROUP_M super-rows inside each XCD's contiguous range, so the
@@ -880,7 +965,7 @@ static void init_nt_policy() {
 template <int BM, int BN, int WMW, int STAGES>
 static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                     hipStream_t stream, const RowScale& rsc) {
+                     hipStream_t stream, const RowScale& rsc, const NormSeam* seam) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const size_t lds = (size_t)STAGES * (BM + BN) * kBK * 2;
@@ -893,13 +978,14 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   }
   gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
-      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr, nullptr, nullptr, nullptr, 0, rsc);
+      sk > 1 && fixup_enabled() && seam == nullptr ? reinterpret_cast<int*>(ws) : nullptr, nullptr, nullptr,
+      nullptr, 0, rsc, seam ? *seam : NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr});
 }
 
 template <int BM, int BN, int NWM, int NWN, int SW>
 static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                    hipStream_t stream, const RowScale& rsc) {
+                    hipStream_t stream, const RowScale& rsc, const NormSeam* seam) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   constexpr size_t lds = (size_t)(3 * BM + SW * BN) * kBK * 2;
@@ -912,7 +998,8 @@ static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
   }
   dim3 grid(tiles, sk);
   gemm_dec_kernel<BM, BN, NWM, NWN, SW><<<grid, NWM * NWN * 64, lds, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, rsc);
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, rsc,
+      seam ? *seam : NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr});
 }
 
 static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
@@ -1069,9 +1156,12 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                     hipStream_t stream, bool dry = false, bool defer = false,
-                    const RowScale* rs = nullptr) {
+                    const RowScale* rs = nullptr, const NormSeam* seam = nullptr) {
   const RowScale rsc = rs ? *rs : RowScale{nullptr, 0, 0.f, 0.f};
   if (rs != nullptr && p.kind != 1 && p.kind != 3) return -4;   // row scale: tile / ring epilogues only
+  // norm seam: split-K tile / ring plans, 128-column tiles (16 threads per row share), no epilogue
+  if (seam != nullptr && ((p.kind != 1 && p.kind != 3) || p.sk < 2 || p.bn != 128 || epi != EPI_NONE))
+    return -5;
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
@@ -1084,7 +1174,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     bool done = false;
 #define DEC_CASE(BM_, BN_, NWM_, NWN_, SW_)                                                      \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == NWM_ && p.nt == NWM_ * NWN_ && p.mt == SW_) { \
-    if (!dry) run_dec<BM_, BN_, NWM_, NWN_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    if (!dry) run_dec<BM_, BN_, NWM_, NWN_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc, seam); \
     done = true;                                                                                 \
   }
     DEC_CASE(128, 224, 8, 1, 4) DEC_CASE(128, 224, 8, 1, 3) DEC_CASE(128, 256, 8, 1, 3)
@@ -1118,7 +1208,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     const int st = p.mt > 0 ? p.mt : 2;   // tile plans reuse `mt` as the pipeline depth
 #define TL_CASE(BM_, BN_, WMW_, ST_)                                                            \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_ && st == ST_) {                       \
-    if (!dry) run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    if (!dry) run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc, seam); \
     done = true;                                                                                \
   }
 #define TL_ST(BM_, BN_, WMW_) TL_CASE(BM_, BN_, WMW_, 2) TL_CASE(BM_, BN_, WMW_, 3) TL_CASE(BM_, BN_, WMW_, 4)
@@ -1132,7 +1222,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind == 4)) {   // big kernels: no fixup path
+  if (p.sk > 1 && !dry && !defer && seam == nullptr && (!fixup_enabled() || p.kind == 4)) {   // big kernels: no fixup path
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);
@@ -1228,6 +1318,47 @@ int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M
                           false, defer, rs);
   if (rc != 0) return rc;
   return defer ? p.sk : 1;
+}
+
+// Grid residency of the seam: every split of a tile must be running while its siblings wait.
+// Splits are the grid's y dimension, dispatched after all x of the previous split, so the whole
+// grid must be resident: tiles x sk <= CUs x workgroups per CU (occupancy query, one block of
+// margin per CU below the API's answer where it answers more than one: the API can over-report
+// by one for SGPR-heavy kernels, cdna_hip_programming.md §1).
+template <typename KFN>
+static bool seam_fits(KFN* kfn, int threads, size_t lds, long grid) {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    ncu = prop.multiProcessorCount;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kfn), threads, lds) !=
+      hipSuccess)
+    return false;
+  if (per_cu > 1) per_cu -= 1;
+  return grid <= (long)ncu * per_cu;
+}
+
+int launch_gemm_norm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
+                     size_t ws_bytes, const NormSeam& seam, hipStream_t stream, bool dry) {
+  if (M <= 0) return -1;
+  const GemmPlan p = select_plan(M, N, K, EPI_NONE);
+  if (p.sk < 2 || p.bn != 128 || (p.kind != 1 && p.kind != 3)) return -1;
+  if (!dry && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float))) return -3;
+  const long grid = (long)((M + p.bm - 1) / p.bm) * (N / p.bn) * p.sk;
+  if ((M + p.bm - 1) / p.bm * (N / p.bn) > kSplitCounters) return -1;
+  bool fits = false;
+  if (p.kind == 1 && p.bm == 64 && p.wk == 2 && p.mt == 3)
+    fits = seam_fits(&gemm_tile_kernel<64, 128, 2, 3>, kTileThreads, (size_t)3 * (64 + 128) * kBK * 2, grid);
+  else if (p.kind == 3 && p.bm == 64 && p.wk == 4 && p.nt == 8 && p.mt == 6)
+    fits = seam_fits(&gemm_dec_kernel<64, 128, 4, 2, 6>, 512, (size_t)(3 * 64 + 6 * 128) * kBK * 2, grid);
+  if (!fits) return -2;
+  const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, nullptr, 0, ws, stream, dry, true,
+                          nullptr, &seam);
+  return rc != 0 ? rc : N / p.bn;
 }
 
 size_t gemm_slab_offset_floats() { return kCounterBytes / sizeof(float); }

@@ -306,6 +306,33 @@ def test_attn_prefill_paged_vs_fp32(Hq, Hkv, kv_dtype):
     _close(o, want, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 8192, 8192), (64, 8192, 28672), (40, 8192, 8192)])
+def test_linear_rmsnorm_rows_seam(M, N, K):
+    """The add+RMSNorm folded into the split-K seam of the decode O / down GEMMs (gemm.hip
+    seam_norm): residual += x W^T (bf16), y = residual * gamma, per-tile sums of squares; the
+    row-scaling consumer GEMM then equals rms_norm(residual) @ W2^T. Three calls in a row
+    exercise the monotonic arrival counters' later generations."""
+    x = _bf(M, K, scale=1.0, seed=120)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=121)
+    g = (1.0 + 0.1 * _bf(N, seed=122).float()).to(torch.bfloat16)
+    w2 = _bf(256, N, scale=1.0 / math.sqrt(N), seed=123)
+    res0 = _bf(M, N, seed=124)
+    if not ops.norm_seam_ok(M, N, K):
+        assert M != 64, "the Llama-3-70B decode shapes must take the seam"
+        pytest.skip("this plan has no seam")
+    for it in range(3):
+        res = res0.clone()
+        rn = ops.linear_rmsnorm_rows(x, w, g, 1e-5, res)
+        assert rn is not None and rn.ssp.shape == (M, N // 128)
+        want_res = (res0.float() + (x.float() @ w.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
+        _close(res, want_res, 2e-2, 2e-2)
+        _close(rn.y, (want_res.float() * g.float()).to(torch.bfloat16), 3e-2, 3e-2)
+        _close(rn.ssp.sum(1), want_res.float().pow(2).sum(1), 1e-2, 1e-2)
+        got = ops.linear(rn, w2)
+        want = ref.rms_norm(want_res.cpu().float(), g.cpu().float(), 1e-5) @ w2.cpu().float().t()
+        _close(got, want, 3e-2, 3e-2)
+
+
 def test_attn_decode_strided_q():
     # q as a view into a fused QKV row (row stride > Hq*D), as the model passes it
     D, BS, Hq, Hkv, B = 128, 32, 8, 1, 3
