@@ -1322,9 +1322,11 @@ int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M
 
 // Grid residency of the seam: every split of a tile must be running while its siblings wait.
 // Splits are the grid's y dimension, dispatched after all x of the previous split, so the whole
-// grid must be resident: tiles x sk <= CUs x workgroups per CU (occupancy query, one block of
-// margin per CU below the API's answer where it answers more than one: the API can over-report
-// by one for SGPR-heavy kernels, cdna_hip_programming.md §1).
+// grid must be resident: tiles x sk <= CUs x workgroups per CU. The occupancy query (after the
+// kernel's dynamic-LDS opt-in, without which it answers 0) is capped by the LDS bound, which is
+// exact; the API's known over-report (one block per CU for SGPR-bound 256-thread kernels,
+// cdna_hip_programming.md §1) cannot apply to these LDS-bound kernels. The sibling wait is
+// bounded anyway (kSeamSpinTicks): a non-resident grid would end late, with the error word set.
 template <typename KFN>
 static bool seam_fits(KFN* kfn, int threads, size_t lds, long grid) {
   static int ncu = 0;
@@ -1334,12 +1336,17 @@ static bool seam_fits(KFN* kfn, int threads, size_t lds, long grid) {
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
     ncu = prop.multiProcessorCount;
   }
+  if (lds > 65536 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return false;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kfn), threads, lds) !=
       hipSuccess)
     return false;
-  if (per_cu > 1) per_cu -= 1;
-  return grid <= (long)ncu * per_cu;
+  const int by_lds = (int)((160 * 1024) / (lds > 0 ? lds : 1));
+  if (per_cu > by_lds) per_cu = by_lds;
+  return per_cu > 0 && grid <= (long)ncu * per_cu;
 }
 
 int launch_gemm_norm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
