@@ -251,6 +251,12 @@ def norm_seam_ok(M: int, N: int, K: int) -> bool:
     return ok
 
 
+def norm_seam_error(device) -> int:
+    """Non-zero once a norm-seam sibling wait timed out on this device (its results are late and
+    may be wrong): the seam's error word, after the arrival counters."""
+    return int(_arena.get(device, "gemm_seam_cnt", 16385, torch.int32, zero=True)[16384].item())
+
+
 def linear_rmsnorm_rows(x, w, gamma, eps: float, residual) -> Optional[RowNormed]:
     """residual += x @ w.T (bf16, in place); returns the RowNormed of the updated residual
     (y = residual * gamma, per-128-column sums of squares) for a row-scaling consumer GEMM —

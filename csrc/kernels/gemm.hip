@@ -186,6 +186,7 @@ __device__ __forceinline__ void splitk_fixup(const float* __restrict__ part, int
 // over the tile's columns. Siblings are co-resident (the launcher checks the grid fits), and the
 // wait is bounded: a sibling later than ~2 s sets the error word and the share proceeds.
 constexpr long long kSeamSpinTicks = 2LL * 100000000LL;   // 2 s of the 100 MHz constant clock
+constexpr int kSeamTiles = 1024;                            // counters per split-count region
 
 template <int BN>
 __device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk, int split, int tile, int M,
@@ -195,7 +196,9 @@ __device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int* cnt = seam.counters + tile;
+    // one counter region per split count: a tile's counter only ever advances by whole
+    // generations of `sk` (O at sk 8 and down at sk 4 share tile indices, not counters)
+    int* cnt = seam.counters + sk * kSeamTiles + tile;
     const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int target = (ticket / sk + 1) * sk;
     if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target < 0) {
@@ -1356,7 +1359,7 @@ int launch_gemm_norm(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   if (p.sk < 2 || p.bn != 128 || (p.kind != 1 && p.kind != 3)) return -1;
   if (!dry && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float))) return -3;
   const long grid = (long)((M + p.bm - 1) / p.bm) * (N / p.bn) * p.sk;
-  if ((M + p.bm - 1) / p.bm * (N / p.bn) > kSplitCounters) return -1;
+  if ((M + p.bm - 1) / p.bm * (N / p.bn) > kSeamTiles || p.sk >= kSplitCounters / kSeamTiles) return -1;
   bool fits = false;
   if (p.kind == 1 && p.bm == 64 && p.wk == 2 && p.mt == 3)
     fits = seam_fits(&gemm_tile_kernel<64, 128, 2, 3>, kTileThreads, (size_t)3 * (64 + 128) * kBK * 2, grid);

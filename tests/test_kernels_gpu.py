@@ -331,6 +331,32 @@ def test_linear_rmsnorm_rows_seam(M, N, K):
         got = ops.linear(rn, w2)
         want = ref.rms_norm(want_res.cpu().float(), g.cpu().float(), 1e-5) @ w2.cpu().float().t()
         _close(got, want, 3e-2, 3e-2)
+    assert ops.norm_seam_error(x.device) == 0
+
+
+def test_norm_seam_interleaved_split_counts():
+    """The decode layer alternates the O seam (split-K 8) and the down seam (split-K 4) on the
+    same tile indices: each split count has its own arrival counters, so no generation ever
+    straddles the two (a shared counter would strand half of a call's splits)."""
+    shapes = [(64, 8192, 8192), (64, 8192, 28672)]
+    if not all(ops.norm_seam_ok(*s) for s in shapes):
+        pytest.skip("no seam plans")
+    data = []
+    for i, (M, N, K) in enumerate(shapes):
+        x = _bf(M, K, seed=130 + i)
+        w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=140 + i)
+        g = _bf(N, seed=150 + i)
+        res0 = _bf(M, N, seed=160 + i)
+        want = (res0.float() + (x.float() @ w.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
+        data.append((x, w, g, res0, want))
+    for it in range(5):
+        for x, w, g, res0, want in data:
+            res = res0.clone()
+            rn = ops.linear_rmsnorm_rows(x, w, g, 1e-5, res)
+            torch.cuda.synchronize()
+            _close(res, want, 2e-2, 2e-2)
+            _close(rn.ssp.sum(1), want.float().pow(2).sum(1), 1e-2, 1e-2)
+    assert ops.norm_seam_error(data[0][0].device) == 0
 
 
 def test_attn_decode_strided_q():
