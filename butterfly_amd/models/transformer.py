@@ -96,6 +96,9 @@ class TransformerLM:
         # ... and with the add+RMSNorm folded into the producing O / down GEMM's split-K seam
         # (ops.linear_rmsnorm_rows): no separate norm launch at all
         self.norm_seam = bool(self.rowscale_rows) and flags.get("BFLY_GEMM_NORM_SEAM")
+        # RoPE + KV append folded into the decode QKV GEMM's split-K seam (ops.linear_rope_kv)
+        self.rope_seam = (self.defer_qkv and not cfg.bias and flags.get("BFLY_GEMM_ROPE_SEAM"))
+        self.rope_seam_rows = flags.get("BFLY_NORM_ROWSCALE_MAX_ROWS")
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
@@ -359,17 +362,23 @@ class TransformerLM:
         """normed x [T, h] -> QKV GEMM -> RoPE + KV append -> attention -> O GEMM (TP-partial)."""
         c, d = self.cfg, self.dims
         T, D = fb.num_tokens, c.head_dim
-        # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
-        # when no all-reduce sits in between (tp == 1)
-        qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
         kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
         slots = fb.slots if kc is not None else None
-        if c.pos_emb == "rope":
-            qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
-        elif kc is not None:
-            k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
-            v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
-            ops.kv_append(k3, v3, fb.slots, kc, vc)
+        qkv = None
+        if self.rope_seam and T <= self.rope_seam_rows and fb.cp is None:
+            # one launch: QKV GEMM with RoPE + KV append in its split-K seam
+            qkv = ops.linear_rope_kv(x, self.p[pre + "qkv_w"], fb.positions, self.cos, self.sin, d.hq, d.hkv,
+                                     slots, kc, vc)
+        if qkv is None:
+            # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
+            # when no all-reduce sits in between (tp == 1)
+            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
+            if c.pos_emb == "rope":
+                qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
+            elif kc is not None:
+                k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
+                v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
+                ops.kv_append(k3, v3, fb.slots, kc, vc)
         q = qkv[:, : d.hq * D].view(T, d.hq, D)
         if fb.is_prefill:
             k = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)

@@ -241,14 +241,42 @@ def rms_norm(x, w, eps: float, out=None, residual=None, rows: bool = False):
 _norm_seam: dict = {}
 
 
-def norm_seam_ok(M: int, N: int, K: int) -> bool:
-    """True if the split-K GEMM plan of this shape can run the fused add+RMSNorm seam."""
-    key = (M, N, K)
+SEAM_NORM, SEAM_ROPE = 1, 2
+
+
+def norm_seam_ok(M: int, N: int, K: int, mode: int = SEAM_NORM) -> bool:
+    """True if the split-K GEMM plan of this shape can run the seam (SEAM_NORM: fused
+    add+RMSNorm; SEAM_ROPE: RoPE + paged KV append)."""
+    key = (M, N, K, mode)
     ok = _norm_seam.get(key)
     if ok is None:
-        ok = load_library() and torch.cuda.is_available() and torch.ops.bfly.gemm_norm_check(M, N, K) > 0
+        ok = load_library() and torch.cuda.is_available() and torch.ops.bfly.gemm_seam_check(M, N, K, mode) > 0
         _norm_seam[key] = ok
     return ok
+
+
+def linear_rope_kv(x, w, positions, cos, sin, n_q: int, n_kv: int, slots=None, k_cache=None, v_cache=None):
+    """qkv = x @ w.T with RoPE on the Q / K heads and the paged KV append done in the GEMM's
+    split-K seam (every split rotates its share of its head tile's rows after its siblings
+    arrive, gemm.hip seam_rope): one launch instead of QKV GEMM + rope_kv. `x` may be a
+    RowNormed. Returns the bf16 [M, N] rows, or None when this shape's plan cannot (fallback:
+    linear(defer=True) + rope_kv)."""
+    rn = None
+    if isinstance(x, RowNormed):
+        rn, x = x, x.y
+    if not _gpu(x):
+        return None
+    M, K, N = x.shape[0], x.shape[1], w.shape[0]
+    if not norm_seam_ok(M, N, K, SEAM_ROPE):
+        return None
+    need = torch.ops.bfly.gemm_workspace_size(M, N, K)
+    ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
+    cnt = _arena.get(x.device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
+    qkv = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    rc = torch.ops.bfly.gemm_rope_kv(x, w, ws, qkv, positions, cos, sin, n_q, n_kv, slots if k_cache is not None else None,
+                                     k_cache, v_cache, cnt, rn.ssp if rn is not None else None,
+                                     rn.eps if rn is not None else 0.0)
+    return qkv if rc > 0 else None
 
 
 def norm_seam_error(device) -> int:
@@ -266,7 +294,7 @@ def linear_rmsnorm_rows(x, w, gamma, eps: float, residual) -> Optional[RowNormed
     if not _gpu(x):
         return None
     M, K, N = x.shape[0], x.shape[1], w.shape[0]
-    if not norm_seam_ok(M, N, K):
+    if not norm_seam_ok(M, N, K, SEAM_NORM):
         return None
     need = torch.ops.bfly.gemm_workspace_size(M, N, K)
     ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)

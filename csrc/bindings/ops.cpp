@@ -420,6 +420,15 @@ void gemm_rs(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<
 // Split-K GEMM with the fused add + RMSNorm seam (gemm.hip seam_norm): y = (residual + x.W^T) *
 // gamma (bf16), residual updated in place, ssp [M, chunks] row sums of squares per 128-column
 // tile. Returns chunks (> 0) or <= 0 when the shape's plan cannot run the seam (nothing ran).
+static bfly::Seam seam_base(Tensor& counters) {
+  CHECK_I32(counters);
+  TORCH_CHECK(counters.is_contiguous() && counters.numel() > 16384, "gemm seam: counters [16385]");
+  bfly::Seam s = bfly::no_seam();
+  s.counters = counters.data_ptr<int>();
+  s.err = reinterpret_cast<uint32_t*>(counters.data_ptr<int>() + 16384);   // error word
+  return s;
+}
+
 int64_t gemm_norm(const Tensor& x, const Tensor& w, Tensor& workspace, Tensor& residual, const Tensor& gamma,
                   Tensor& y, Tensor& ssp, Tensor& counters) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(residual); CHECK_BF16(gamma); CHECK_BF16(y);
@@ -433,19 +442,67 @@ int64_t gemm_norm(const Tensor& x, const Tensor& w, Tensor& workspace, Tensor& r
   TORCH_CHECK(gamma.is_contiguous() && gamma.numel() == N, "gemm_norm: gamma");
   TORCH_CHECK(ssp.scalar_type() == at::kFloat && ssp.is_contiguous() && ssp.dim() == 2 && ssp.size(0) == M &&
                   ssp.size(1) == N / 128, "gemm_norm: ssp [M, N / 128] f32");
-  CHECK_I32(counters);
-  TORCH_CHECK(counters.is_contiguous() && counters.numel() > 16384, "gemm_norm: counters [16385]");
   TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_contiguous(), "gemm_norm: workspace");
-  const bfly::NormSeam seam{bf(residual), bf(gamma), bf(y), ssp.data_ptr<float>(), counters.data_ptr<int>(),
-                            reinterpret_cast<uint32_t*>(counters.data_ptr<int>() + 16384)};   // error word
+  bfly::Seam seam = seam_base(counters);
+  seam.mode = bfly::kSeamNorm;
+  seam.residual = bf(residual);
+  seam.gamma = bf(gamma);
+  seam.y = bf(y);
+  seam.ssp = ssp.data_ptr<float>();
   c10::DeviceGuard g(x.device());
-  return bfly::launch_gemm_norm(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, workspace.data_ptr<float>(),
+  return bfly::launch_gemm_seam(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, workspace.data_ptr<float>(),
                                 workspace.numel() * sizeof(float), seam, cur_stream(), false);
 }
 
-int64_t gemm_norm_check(int64_t M, int64_t N, int64_t K) {
-  const bfly::NormSeam seam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  return bfly::launch_gemm_norm(nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, nullptr, 0, seam, nullptr, true);
+// Split-K QKV GEMM with RoPE + paged KV append in its seam (gemm.hip seam_rope): writes the
+// bf16 rotated row into `qkv` and K / V into the caches. `ssp` / `eps`: the input is a
+// RowNormed (RMSNorm row scale applied in the GEMM). Returns > 0, or <= 0 (nothing ran).
+int64_t gemm_rope_kv(const Tensor& x, const Tensor& w, Tensor& workspace, Tensor& qkv, const Tensor& positions,
+                     const Tensor& cos_t, const Tensor& sin_t, int64_t hq, int64_t hkv,
+                     const c10::optional<Tensor>& slots, const c10::optional<Tensor>& k_cache,
+                     const c10::optional<Tensor>& v_cache, Tensor& counters, const c10::optional<Tensor>& ssp,
+                     double eps) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(qkv); CHECK_I32(positions);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && w.dim() == 2 && w.stride(1) == 1 &&
+                  w.stride(0) % 8 == 0 && w.size(1) == K && K % 64 == 0, "gemm_rope_kv: operands");
+  TORCH_CHECK(N == (hq + 2 * hkv) * 128, "gemm_rope_kv: N = (hq + 2 hkv) * 128");
+  TORCH_CHECK(qkv.is_contiguous() && qkv.size(0) == M && qkv.size(1) == N, "gemm_rope_kv: qkv");
+  TORCH_CHECK(positions.numel() >= M, "gemm_rope_kv: positions");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.size(1) == 64 &&
+                  cos_t.is_contiguous() && sin_t.is_contiguous(), "gemm_rope_kv: cos / sin [max_pos, 64] f32");
+  bfly::Seam seam = seam_base(counters);
+  seam.mode = bfly::kSeamRope;
+  seam.qkv = bf(qkv);
+  seam.positions = positions.data_ptr<int>();
+  seam.cos_t = cos_t.data_ptr<float>();
+  seam.sin_t = sin_t.data_ptr<float>();
+  seam.hq = (int)hq;
+  seam.hkv = (int)hkv;
+  seam.block_size = 1;
+  if (slots.has_value() && k_cache.has_value() && v_cache.has_value()) {
+    CHECK_I32(*slots); CHECK_KV(*k_cache, *v_cache);
+    TORCH_CHECK(slots->numel() >= M && k_cache->is_contiguous() && v_cache->is_contiguous() &&
+                    k_cache->size(1) == hkv && k_cache->size(3) == 128, "gemm_rope_kv: caches");
+    seam.slots = slots->data_ptr<int>();
+    seam.k_cache = k_cache->data_ptr();
+    seam.v_cache = v_cache->data_ptr();
+    seam.block_size = (int)k_cache->size(2);
+    seam.kv_fp8 = k_cache->scalar_type() == at::kFloat8_e4m3fn;
+  }
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_contiguous(), "gemm_rope_kv: workspace");
+  c10::DeviceGuard g(x.device());
+  bfly::RowScale rs{nullptr, 0, 0.f, 0.f};
+  if (ssp.has_value()) rs = row_scale(*ssp, eps, M, K);
+  return bfly::launch_gemm_seam(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, workspace.data_ptr<float>(),
+                                workspace.numel() * sizeof(float), seam, cur_stream(), false,
+                                ssp.has_value() ? &rs : nullptr);
+}
+
+int64_t gemm_seam_check(int64_t M, int64_t N, int64_t K, int64_t mode) {
+  bfly::Seam seam = bfly::no_seam();
+  seam.mode = (int)mode;
+  return bfly::launch_gemm_seam(nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, nullptr, 0, seam, nullptr, true);
 }
 
 int64_t gemm_deferred_rs(const Tensor& x, const Tensor& w, Tensor& out, Tensor& workspace, const Tensor& ssp,
@@ -1033,7 +1090,10 @@ TORCH_LIBRARY(bfly, m) {
         "Tensor ssp, float eps) -> ()");
   m.def("gemm_norm(Tensor x, Tensor w, Tensor(a!) workspace, Tensor(b!) residual, Tensor gamma, Tensor(c!) y, "
         "Tensor(d!) ssp, Tensor(e!) counters) -> int");
-  m.def("gemm_norm_check(int M, int N, int K) -> int", &gemm_norm_check);
+  m.def("gemm_seam_check(int M, int N, int K, int mode) -> int", &gemm_seam_check);
+  m.def("gemm_rope_kv(Tensor x, Tensor w, Tensor(a!) workspace, Tensor(b!) qkv, Tensor positions, Tensor cos_t, "
+        "Tensor sin_t, int hq, int hkv, Tensor? slots, Tensor(c!)? k_cache, Tensor(d!)? v_cache, Tensor(e!) counters, "
+        "Tensor? ssp, float eps) -> int");
   m.def("gemm_deferred_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) workspace, Tensor ssp, float eps) -> int");
   m.def("rms_norm_rows(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) ssp, Tensor(c!)? residual) -> ()");
   m.def("rms_norm_rows_chunks(int dim) -> int", [](int64_t dim) -> int64_t { return bfly::rmsnorm_rows_chunks(dim); });
@@ -1137,6 +1197,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("gemm_norm", &gemm_norm);
+  m.impl("gemm_rope_kv", &gemm_rope_kv);
   m.impl("attn_prefill_paged", &attn_prefill_paged);
   m.impl("attn_lse_merge", &attn_lse_merge);
   m.impl("probe", &probe);

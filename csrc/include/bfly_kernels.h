@@ -19,20 +19,37 @@ struct RowScale {
   float inv_dim, eps;
 };
 
-// Split-K add + RMSNorm seam (decode O / down projections, tp = 1): after its partial slab,
-// every split workgroup of a tile waits for its sibling splits and then reduces ITS share of
-// the tile's rows: sum of the sk slabs (split order) -> bf16 -> + residual (bf16, written back)
-// -> y = x * gamma (bf16) and the row's sum of squares over the tile's columns into
-// ssp[row][n-tile]. The consumer GEMM applies rsqrt(sum(ssp[row]) / N + eps) (RowScale with
-// N / BN chunks). Replaces the separate add+RMSNorm kernel and its launch.
-struct NormSeam {
-  bf16* residual;       // [M, N] in/out (nullptr: no seam)
+// Split-K seams: after its partial slab, every split workgroup of a tile waits for its sibling
+// splits and then reduces ITS share of the tile's rows (sum of the sk slabs in split order ->
+// bf16) and finishes them, so the consumer kernel that used to do it never launches:
+//   kSeamNorm (decode O / down projections, tp = 1): + residual (bf16, written back) ->
+//     y = x * gamma (bf16) and the row's sum of squares over the tile's columns into
+//     ssp[row][n-tile]; the consumer GEMM applies rsqrt(sum(ssp[row]) / N + eps) (RowScale with
+//     N / BN chunks). Replaces the separate add+RMSNorm kernel.
+//   kSeamRope (decode QKV projection, 128-column tile = one head): RoPE on Q / K heads, bf16 row
+//     into `qkv`, K / V into the paged cache. Replaces rope_kv.
+constexpr int kSeamNone = 0, kSeamNorm = 1, kSeamRope = 2;
+struct Seam {
+  int mode;
+  // kSeamNorm
+  bf16* residual;       // [M, N] in/out
   const bf16* gamma;    // [N]
   bf16* y;              // [M, N]
   float* ssp;           // [M, N / BN]
+  // kSeamRope
+  bf16* qkv;            // [M, N] (Q heads, K heads, V heads; N = (hq + 2 hkv) * 128)
+  const int* positions; // [M]
+  const float* cos_t;   // [max_pos, 64]
+  const float* sin_t;
+  const int* slots;     // [M] cache slot (< 0: not cached)
+  void* k_cache;        // [blocks, hkv, BS, 128]
+  void* v_cache;        // [blocks, hkv, 128, BS]
+  int hq, hkv, block_size, kv_fp8;
+  // both
   int* counters;        // per-tile arrival counters: monotonic, never reset (own region)
   uint32_t* err;        // sibling-wait timeout word (nullable)
 };
+__host__ __device__ inline Seam no_seam() { Seam s{}; s.mode = kSeamNone; return s; }
 
 struct GemmPlan {
   int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 3 = decode ring,
@@ -106,10 +123,11 @@ int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, 
 int gemm_check(int M, int N, int K, int epi);
 // 0 if the auto plan for this shape takes a RowScale (tile and decode-ring kernels)
 int gemm_rowscale_check(int M, int N, int K, int epi);
-// Split-K GEMM with the add+RMSNorm seam (NormSeam). Returns the number of ssp chunks per row
-// (N / BN, > 0), or <= 0 when this shape's plan cannot run the seam (caller falls back).
-int launch_gemm_norm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
-                     size_t ws_bytes, const NormSeam& seam, hipStream_t stream, bool dry);
+// Split-K GEMM with a seam (Seam). Returns N / BN (> 0: the ssp chunks per row of kSeamNorm),
+// or <= 0 when this shape's plan cannot run the seam (nothing ran; the caller falls back).
+// `rs`: the input's RMSNorm row scale (a RowNormed X), applied before the slabs.
+int launch_gemm_seam(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
+                     size_t ws_bytes, const Seam& seam, hipStream_t stream, bool dry, const RowScale* rs = nullptr);
 // Y = X W^T without epilogue; when the plan splits K, the f32 slabs are left in the workspace
 // (at gemm_slab_offset_floats(), layout [sk][M][N]) for the consumer kernel to reduce, and the
 // split count is returned; otherwise `out` is written and 1 is returned. < 0: error.

@@ -31,6 +31,7 @@
 #include <string>
 #include <vector>
 #include "bfly_kernels.h"
+#include "bfly_kv.h"
 
 namespace bfly {
 
@@ -177,7 +178,7 @@ __device__ __forceinline__ void splitk_fixup(const float* __restrict__ part, int
   }
 }
 
-// Add + RMSNorm seam (NormSeam, bfly_kernels.h): every split of a tile publishes its slab (the
+// Split-K seams (Seam, bfly_kernels.h): every split of a tile publishes its slab (the
 // split-K hand-off recipe above: drained plain stores, ONE agent-scope release, relaxed
 // ticket), waits until all `sk` siblings of its generation arrived (the counter is monotonic:
 // ticket / sk is this call's generation, so nothing is ever re-armed; wrap-safe compare), and
@@ -188,9 +189,8 @@ __device__ __forceinline__ void splitk_fixup(const float* __restrict__ part, int
 constexpr long long kSeamSpinTicks = 2LL * 100000000LL;   // 2 s of the 100 MHz constant clock
 constexpr int kSeamTiles = 1024;                            // counters per split-count region
 
-template <int BN>
-__device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk, int split, int tile, int M,
-                                          int N, int m0, int BM, int n0, const NormSeam& seam) {
+// Publish this split's slab and wait for the tile's sibling splits of the same generation.
+__device__ __forceinline__ void seam_arrive(int sk, int tile, const Seam& seam) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -216,6 +216,26 @@ __device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// 8 consecutive columns of one row, summed over the sk slabs in split order and rounded to
+// bf16 (what the separate reduce / norm / rope kernels compute)
+__device__ __forceinline__ void seam_sum8(const float* __restrict__ pr, int sk, long slab, float (&a)[8]) {
+  f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+  for (int k = 1; k < sk; ++k) {
+    lo += *reinterpret_cast<const f32x4*>(pr + k * slab);
+    hi += *reinterpret_cast<const f32x4*>(pr + k * slab + 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a[j] = bf2f(f2bf(lo[j]));
+    a[j + 4] = bf2f(f2bf(hi[j]));
+  }
+}
+
+template <int BN>
+__device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk, int split, int M, int N, int m0,
+                                          int BM, int n0, const Seam& seam) {
   constexpr int TPR = BN / 8;                       // threads per row: 8 columns each
   const int rpp = blockDim.x / TPR;                 // rows per pass
   const int R = (BM + sk - 1) / sk;
@@ -230,19 +250,14 @@ __device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk
     const bool ok = row < r1;
     float ss = 0.f;
     if (ok) {
-      const float* pr = part + (long)row * N + c;
-      f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
-      for (int k = 1; k < sk; ++k) {
-        lo += *reinterpret_cast<const f32x4*>(pr + k * slab);
-        hi += *reinterpret_cast<const f32x4*>(pr + k * slab + 4);
-      }
+      float a[8];
+      seam_sum8(part + (long)row * N + c, sk, slab, a);
       bf16x8* rp = reinterpret_cast<bf16x8*>(seam.residual + (long)row * N + c);
       const bf16x8 r = *rp;
       bf16x8 sm, o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float a = bf2f(f2bf(j < 4 ? lo[j] : hi[j - 4]));     // the bf16 GEMM result
-        sm[j] = f2bf(a + bf2f(r[j]));                               // the stored bf16 residual
+        sm[j] = f2bf(a[j] + bf2f(r[j]));                           // the stored bf16 residual
         const float v = bf2f(sm[j]);
         ss += v * v;
         o[j] = f2bf(v * bf2f(g[j]));
@@ -253,6 +268,76 @@ __device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk
 #pragma unroll
     for (int o = TPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, TPR);
     if (ok && threadIdx.x % TPR == 0) seam.ssp[(long)row * nchunks + tn] = ss;
+  }
+}
+
+// RoPE (rotate-half, rope.hip's arithmetic) + paged KV append of one 128-column head tile:
+// thread t of a row owns columns [8t, 8t + 8) and their rotation partners [64 + 8t, +8).
+template <typename CT>
+__device__ __forceinline__ void seam_rope(const float* __restrict__ part, int sk, int split, int M, int N, int m0,
+                                          int BM, int n0, const Seam& seam) {
+  constexpr int D = 128, H2 = 64, TPR = H2 / 8;
+  const int rpp = blockDim.x / TPR;
+  const int R = (BM + sk - 1) / sk;
+  const int r0 = m0 + split * R;
+  const int r1 = min(min(m0 + BM, r0 + R), M);
+  const long slab = (long)M * N;
+  const int head = n0 / D, p0 = (threadIdx.x % TPR) * 8;
+  const bool is_v = head >= seam.hq + seam.hkv, is_k = !is_v && head >= seam.hq;
+  for (int row = r0 + threadIdx.x / TPR; row < r1; row += rpp) {
+    float a[8], b[8];
+    const float* pr = part + (long)row * N + n0 + p0;
+    seam_sum8(pr, sk, slab, a);
+    seam_sum8(pr + H2, sk, slab, b);
+    bf16x8 oa, ob;
+    if (!is_v) {
+      const int pos = seam.positions[row];
+      const float* cr = seam.cos_t + (long)pos * H2 + p0;
+      const float* sr = seam.sin_t + (long)pos * H2 + p0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        oa[j] = f2bf(a[j] * cr[j] - b[j] * sr[j]);
+        ob[j] = f2bf(b[j] * cr[j] + a[j] * sr[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        oa[j] = f2bf(a[j]);
+        ob[j] = f2bf(b[j]);
+      }
+    }
+    bf16* qrow = seam.qkv + (long)row * N + n0;
+    *reinterpret_cast<bf16x8*>(qrow + p0) = oa;
+    *reinterpret_cast<bf16x8*>(qrow + p0 + H2) = ob;
+    const int slot = seam.slots != nullptr ? seam.slots[row] : -1;
+    if (slot < 0 || (!is_k && !is_v)) continue;
+    const int BS = seam.block_size, blk = slot / BS, off = slot % BS;
+    if (is_k) {
+      const int kh = head - seam.hq;
+      CT* kp = static_cast<CT*>(seam.k_cache) + (((long)blk * seam.hkv + kh) * BS + off) * D;
+      KV<CT>::store8(kp + p0, oa);
+      KV<CT>::store8(kp + p0 + H2, ob);
+    } else {
+      const int vh = head - seam.hq - seam.hkv;
+      CT* vp = static_cast<CT*>(seam.v_cache) + ((long)blk * seam.hkv + vh) * D * BS + off;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        KV<CT>::store1(vp + (long)(p0 + j) * BS, oa[j]);
+        KV<CT>::store1(vp + (long)(p0 + H2 + j) * BS, ob[j]);
+      }
+    }
+  }
+}
+
+template <int BN>
+__device__ __forceinline__ void seam_finish(const float* __restrict__ part, int sk, int split, int tile, int M,
+                                            int N, int m0, int BM, int n0, const Seam& seam) {
+  seam_arrive(sk, tile, seam);
+  if (seam.mode == kSeamNorm) {
+    seam_norm<BN>(part, sk, split, M, N, m0, BM, n0, seam);
+  } else if constexpr (BN == 128) {
+    if (seam.kv_fp8) seam_rope<fp8_t>(part, sk, split, M, N, m0, BM, n0, seam);
+    else seam_rope<bf16>(part, sk, split, M, N, m0, BM, n0, seam);
   }
 }
 
@@ -499,7 +584,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
                  int* __restrict__ counters, const int* __restrict__ grows = nullptr,
                  const int4* __restrict__ gtiles = nullptr, const int* __restrict__ gcount = nullptr,
                  long w_estride = 0, RowScale rsc = RowScale{nullptr, 0, 0.f, 0.f},
-                 NormSeam seam = NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}) {
+                 Seam seam = no_seam()) {
   constexpr int WNW = 4 / WMW;                // waves along M x waves along N
   constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
@@ -585,8 +670,8 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
                         part ? part + (long)blockIdx.y * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
   if constexpr (!GROUPED) {
-    if (part && seam.residual != nullptr) {
-      seam_norm<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
+    if (part && seam.mode != kSeamNone) {
+      seam_finish<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
       return;
     }
   }
@@ -642,7 +727,7 @@ __global__ void __launch_bounds__(kDecThreads)
 gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
                 bf16* __restrict__ out, long ldo, float* __restrict__ part, RowScale rsc,
-                NormSeam seam = NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr}) {
+                Seam seam = no_seam()) {
   constexpr int SX = 3, NW = NWM * NWN;
   static_assert(NW * 64 <= kDecThreads && SW >= SX, "decode ring configuration");
   constexpr int WM = BM / NWM, WN = BN / NWN;   // per-wave output block
@@ -711,7 +796,7 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
                         part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0, rsc);
-  if (part && seam.residual != nullptr) seam_norm<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
+  if (part && seam.mode != kSeamNone) seam_finish<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
 }
 
 // Prefill tiles are walked in GROUP_M super-rows inside each XCD's contiguous range, so the
@@ -968,7 +1053,7 @@ static void init_nt_policy() {
 template <int BM, int BN, int WMW, int STAGES>
 static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                     hipStream_t stream, const RowScale& rsc, const NormSeam* seam) {
+                     hipStream_t stream, const RowScale& rsc, const Seam* seam) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const size_t lds = (size_t)STAGES * (BM + BN) * kBK * 2;
@@ -982,13 +1067,13 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
       sk > 1 && fixup_enabled() && seam == nullptr ? reinterpret_cast<int*>(ws) : nullptr, nullptr, nullptr,
-      nullptr, 0, rsc, seam ? *seam : NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr});
+      nullptr, 0, rsc, seam ? *seam : no_seam());
 }
 
 template <int BM, int BN, int NWM, int NWN, int SW>
 static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                    hipStream_t stream, const RowScale& rsc, const NormSeam* seam) {
+                    hipStream_t stream, const RowScale& rsc, const Seam* seam) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   constexpr size_t lds = (size_t)(3 * BM + SW * BN) * kBK * 2;
@@ -1002,7 +1087,7 @@ static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
   dim3 grid(tiles, sk);
   gemm_dec_kernel<BM, BN, NWM, NWN, SW><<<grid, NWM * NWN * 64, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, rsc,
-      seam ? *seam : NormSeam{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr});
+      seam ? *seam : no_seam());
 }
 
 static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
@@ -1159,7 +1244,7 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                     hipStream_t stream, bool dry = false, bool defer = false,
-                    const RowScale* rs = nullptr, const NormSeam* seam = nullptr) {
+                    const RowScale* rs = nullptr, const Seam* seam = nullptr) {
   const RowScale rsc = rs ? *rs : RowScale{nullptr, 0, 0.f, 0.f};
   if (rs != nullptr && p.kind != 1 && p.kind != 3) return -4;   // row scale: tile / ring epilogues only
   // norm seam: split-K tile / ring plans, 128-column tiles (16 threads per row share), no epilogue
@@ -1352,9 +1437,10 @@ static bool seam_fits(KFN* kfn, int threads, size_t lds, long grid) {
   return per_cu > 0 && grid <= (long)ncu * per_cu;
 }
 
-int launch_gemm_norm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
-                     size_t ws_bytes, const NormSeam& seam, hipStream_t stream, bool dry) {
-  if (M <= 0) return -1;
+int launch_gemm_seam(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
+                     size_t ws_bytes, const Seam& seam, hipStream_t stream, bool dry, const RowScale* rs) {
+  if (M <= 0 || seam.mode == kSeamNone) return -1;
+  if (seam.mode == kSeamRope && !dry && (N != (seam.hq + 2 * seam.hkv) * 128 || seam.block_size <= 0)) return -4;
   const GemmPlan p = select_plan(M, N, K, EPI_NONE);
   if (p.sk < 2 || p.bn != 128 || (p.kind != 1 && p.kind != 3)) return -1;
   if (!dry && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float))) return -3;
@@ -1367,7 +1453,7 @@ int launch_gemm_norm(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
     fits = seam_fits(&gemm_dec_kernel<64, 128, 4, 2, 6>, 512, (size_t)(3 * 64 + 6 * 128) * kBK * 2, grid);
   if (!fits) return -2;
   const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, nullptr, 0, ws, stream, dry, true,
-                          nullptr, &seam);
+                          rs, &seam);
   return rc != 0 ? rc : N / p.bn;
 }
 

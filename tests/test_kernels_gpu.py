@@ -334,6 +334,41 @@ def test_linear_rmsnorm_rows_seam(M, N, K):
     assert ops.norm_seam_error(x.device) == 0
 
 
+@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("rownormed", [False, True])
+def test_linear_rope_kv_seam_matches_rope_kv(kv_dtype, rownormed):
+    """RoPE + paged KV append folded into the decode QKV GEMM's split-K seam (gemm.hip
+    seam_rope) is bitwise the unfused GEMM + rope_kv: rotated Q / K rows, V rows, and the K / V
+    cache pages (a padding row with slot -1 writes no page); with a plain and a RowNormed input."""
+    M, Hq, Hkv, D, H, BS = 64, 64, 8, 128, 8192, 32
+    N = (Hq + 2 * Hkv) * D
+    if not ops.norm_seam_ok(M, N, H, ops.SEAM_ROPE):
+        pytest.fail("the Llama-3-70B decode QKV shape must take the rope seam")
+    x = _bf(M, H, seed=170)
+    w = _bf(N, H, scale=1.0 / math.sqrt(H), seed=171)
+    cos, sin = ref.rope_tables(D, 4096, 500000.0, device=DEV)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+    nblk = 3 * M
+    slots = (torch.randperm(nblk * BS, device=DEV)[:M]).to(torch.int32)
+    slots[5] = -1
+    kdt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
+    caches = [(torch.zeros(nblk, Hkv, BS, D, device=DEV).to(kdt), torch.zeros(nblk, Hkv, D, BS, device=DEV).to(kdt))
+              for _ in range(2)]
+    inp = x
+    if rownormed:
+        res = _bf(M, H, seed=172)
+        inp = ops.rms_norm(x, _bf(H, seed=173), 1e-5, residual=res, rows=True)
+    for it in range(2):          # second call: later generation of the seam counters
+        got = ops.linear_rope_kv(inp, w, pos, cos, sin, Hq, Hkv, slots, *caches[0])
+        base = ops.rope_kv(ops.linear(inp, w, defer=True), pos, cos, sin, Hq, Hkv, slots, *caches[1])
+        torch.cuda.synchronize()
+        assert got is not None
+        assert torch.equal(got, base)
+        assert torch.equal(caches[0][0].view(torch.uint8), caches[1][0].view(torch.uint8))
+        assert torch.equal(caches[0][1].view(torch.uint8), caches[1][1].view(torch.uint8))
+    assert ops.norm_seam_error(x.device) == 0
+
+
 def test_norm_seam_interleaved_split_counts():
     """The decode layer alternates the O seam (split-K 8) and the down seam (split-K 4) on the
     same tile indices: each split count has its own arrival counters, so no generation ever
