@@ -31,6 +31,7 @@ struct RowScale {
 constexpr int kSeamNone = 0, kSeamNorm = 1, kSeamRope = 2;
 struct Seam {
   int mode;
+  int sk;               // split count (set by launch_gemm_seam; the grid is 1-D, splits adjacent)
   // kSeamNorm
   bf16* residual;       // [M, N] in/out
   const bf16* gamma;    // [N]

@@ -609,15 +609,19 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     tile = 0;
   } else {
     const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-    tile = xcd_remap(blockIdx.x, mtiles * ntiles);
+    tile = xcd_remap(seam.mode != kSeamNone ? (int)blockIdx.x / seam.sk : (int)blockIdx.x, mtiles * ntiles);
     const int tn = tile / mtiles, tm = tile % mtiles;  // consecutive tiles share a W panel
     m0 = tm * BM;
     n0 = tn * BN;
   }
+  // split index / count: grid y, or (seam launches) the fastest-varying part of a 1-D grid so a
+  // tile's sibling splits are dispatched back to back (seam_arrive waits on them)
+  const int ksplit = seam.mode != kSeamNone ? (int)blockIdx.x % seam.sk : (int)blockIdx.y;
+  const int nsplit = seam.mode != kSeamNone ? seam.sk : (int)gridDim.y;
 
   const int ktiles = K / kBK;
-  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
-  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
+  const int kt0 = (int)(((long)ktiles * ksplit) / nsplit);
+  const int kt1 = (int)(((long)ktiles * (ksplit + 1)) / nsplit);
   // each W byte read by one workgroup: stream it non-temporally
   const bool w_nt = (GROUPED ? single : M <= BM) && g_tile_w_nt;
 
@@ -668,15 +672,15 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     if (++buf == STAGES) buf = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)blockIdx.y * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
+                        part ? part + (long)ksplit * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
   if constexpr (!GROUPED) {
     if (part && seam.mode != kSeamNone) {
-      seam_finish<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
+      seam_finish<BN>(part, nsplit, ksplit, tile, M, N, m0, BM, n0, seam);
       return;
     }
   }
-  if (part && counters && splitk_arrive(counters + tile, gridDim.y, reinterpret_cast<int*>(smem)))
-    splitk_fixup(part, gridDim.y, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
+  if (part && counters && splitk_arrive(counters + tile, nsplit, reinterpret_cast<int*>(smem)))
+    splitk_fixup(part, nsplit, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -742,12 +746,14 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
   const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-  const int tile = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int tile = xcd_remap(seam.mode != kSeamNone ? (int)blockIdx.x / seam.sk : (int)blockIdx.x, mtiles * ntiles);
   const int tn = tile / mtiles, tm = tile % mtiles;
   const int m0 = tm * BM, n0 = tn * BN;
+  const int ksplit = seam.mode != kSeamNone ? (int)blockIdx.x % seam.sk : (int)blockIdx.y;   // see gemm_tile_kernel
+  const int nsplit = seam.mode != kSeamNone ? seam.sk : (int)gridDim.y;
   const int ktiles = K / kBK;
-  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
-  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
+  const int kt0 = (int)(((long)ktiles * ksplit) / nsplit);
+  const int kt1 = (int)(((long)ktiles * (ksplit + 1)) / nsplit);
   const bool w_nt = mtiles == 1 && g_tile_w_nt;   // each weight byte read by one workgroup
 
   f32x4 acc[TI][TJ];
@@ -795,8 +801,8 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
     if (++wslot == SW) wslot = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0, rsc);
-  if (part && seam.mode != kSeamNone) seam_finish<BN>(part, gridDim.y, blockIdx.y, tile, M, N, m0, BM, n0, seam);
+                        part ? part + (long)ksplit * M * N + (long)m0 * N : nullptr, m0, rsc);
+  if (part && seam.mode != kSeamNone) seam_finish<BN>(part, nsplit, ksplit, tile, M, N, m0, BM, n0, seam);
 }
 
 // Prefill tiles are walked in GROUP_M super-rows inside each XCD's contiguous range, so the
@@ -1057,7 +1063,8 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const size_t lds = (size_t)STAGES * (BM + BN) * kBK * 2;
-  dim3 grid(tiles, sk);
+  // seam launches: 1-D grid with the splits of a tile adjacent (dispatched back to back)
+  const dim3 grid = seam != nullptr ? dim3(tiles * sk, 1) : dim3(tiles, sk);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
   if (!attr_set && lds > 65536) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW, STAGES>),
@@ -1084,7 +1091,7 @@ static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  dim3 grid(tiles, sk);
+  const dim3 grid = seam != nullptr ? dim3(tiles * sk, 1) : dim3(tiles, sk);   // see run_tile
   gemm_dec_kernel<BM, BN, NWM, NWN, SW><<<grid, NWM * NWN * 64, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, rsc,
       seam ? *seam : no_seam());
@@ -1409,8 +1416,10 @@ int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M
 }
 
 // Grid residency of the seam: every split of a tile must be running while its siblings wait.
-// Splits are the grid's y dimension, dispatched after all x of the previous split, so the whole
-// grid must be resident: tiles x sk <= CUs x workgroups per CU. The occupancy query (after the
+// The splits of a tile are adjacent in the 1-D seam grid, so with in-order dispatch sk resident
+// workgroups already guarantee progress (the oldest unfinished tile always gets all its splits
+// resident); the check below is stricter (the whole grid resident at once), so a kernel on a
+// side stream (an RCCL send of the pipeline) holding a few CUs cannot even slow the seam. The occupancy query (after the
 // kernel's dynamic-LDS opt-in, without which it answers 0) is capped by the LDS bound, which is
 // exact; the API's known over-report (one block per CU for SGPR-bound 256-thread kernels,
 // cdna_hip_programming.md §1) cannot apply to these LDS-bound kernels. The sibling wait is
@@ -1452,8 +1461,10 @@ int launch_gemm_seam(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   else if (p.kind == 3 && p.bm == 64 && p.wk == 4 && p.nt == 8 && p.mt == 6)
     fits = seam_fits(&gemm_dec_kernel<64, 128, 4, 2, 6>, 512, (size_t)(3 * 64 + 6 * 128) * kBK * 2, grid);
   if (!fits) return -2;
+  Seam sm = seam;
+  sm.sk = p.sk;
   const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, nullptr, 0, ws, stream, dry, true,
-                          rs, &seam);
+                          rs, &sm);
   return rc != 0 ? rc : N / p.bn;
 }
 
