@@ -336,21 +336,29 @@ def test_linear_rmsnorm_rows_seam(M, N, K):
 
 @pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
 @pytest.mark.parametrize("rownormed", [False, True])
-def test_linear_rope_kv_seam_matches_rope_kv(kv_dtype, rownormed):
+@pytest.mark.parametrize("M,Hq,Hkv", [(64, 64, 8), (8, 64, 8), (128, 64, 8), (64, 8, 1), (32, 16, 2), (1, 64, 8)])
+def test_linear_rope_kv_seam_matches_rope_kv(kv_dtype, rownormed, M, Hq, Hkv):
     """RoPE + paged KV append folded into the decode QKV GEMM's split-K seam (gemm.hip
     seam_rope) is bitwise the unfused GEMM + rope_kv: rotated Q / K rows, V rows, and the K / V
-    cache pages (a padding row with slot -1 writes no page); with a plain and a RowNormed input."""
-    M, Hq, Hkv, D, H, BS = 64, 64, 8, 128, 8192, 32
+    cache pages (a padding row with slot -1 writes no page); with a plain and a RowNormed input.
+    Shapes: Llama-3-70B tp1 at several decode buckets, and its tp8 / tp4 QKV shards (8 / 16
+    query heads); a shape without a seam plan must decline (None), never run a wrong plan."""
+    D, H, BS = 128, 8192, 32
     N = (Hq + 2 * Hkv) * D
     if not ops.norm_seam_ok(M, N, H, ops.SEAM_ROPE):
-        pytest.fail("the Llama-3-70B decode QKV shape must take the rope seam")
+        if (M, Hq) == (64, 64):
+            pytest.fail("the Llama-3-70B decode QKV shape must take the rope seam")
+        cos, sin = ref.rope_tables(D, 64, 500000.0, device=DEV)
+        assert ops.linear_rope_kv(_bf(M, H, seed=1), _bf(N, H, seed=2), torch.zeros(M, dtype=torch.int32, device=DEV),
+                                  cos, sin, Hq, Hkv, None, None, None) is None
+        pytest.skip(f"no rope seam plan for M={M} N={N}")
     x = _bf(M, H, seed=170)
     w = _bf(N, H, scale=1.0 / math.sqrt(H), seed=171)
     cos, sin = ref.rope_tables(D, 4096, 500000.0, device=DEV)
     pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
     nblk = 3 * M
     slots = (torch.randperm(nblk * BS, device=DEV)[:M]).to(torch.int32)
-    slots[5] = -1
+    slots[M // 2] = -1
     kdt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
     caches = [(torch.zeros(nblk, Hkv, BS, D, device=DEV).to(kdt), torch.zeros(nblk, Hkv, D, BS, device=DEV).to(kdt))
               for _ in range(2)]
