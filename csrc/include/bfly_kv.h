@@ -23,6 +23,14 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kFp8Max = 448.f;
 
+// Rotate-half RoPE of one pair (x0 at d, x1 at d + D/2) with explicit FMAs, shared by every
+// kernel that rotates (rope.hip, the QKV GEMM's seam in gemm.hip): a plain `x0*c - x1*s` leaves
+// the contraction choice to the compiler per call site, so two kernels could round differently.
+__device__ __forceinline__ void rope_rotate(float x0, float x1, float c, float s, float& o0, float& o1) {
+  o0 = __builtin_fmaf(x0, c, -(x1 * s));
+  o1 = __builtin_fmaf(x1, c, x0 * s);
+}
+
 __device__ __forceinline__ float fp8_clamp(float x) { return fminf(fmaxf(x, -kFp8Max), kFp8Max); }
 
 // 4 floats -> 4 e4m3 bytes (RNE), little-endian in one dword

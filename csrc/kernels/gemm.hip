@@ -296,8 +296,10 @@ __device__ __forceinline__ void seam_rope(const float* __restrict__ part, int sk
       const float* sr = seam.sin_t + (long)pos * H2 + p0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        oa[j] = f2bf(a[j] * cr[j] - b[j] * sr[j]);
-        ob[j] = f2bf(b[j] * cr[j] + a[j] * sr[j]);
+        float r0, r1;
+        rope_rotate(a[j], b[j], cr[j], sr[j], r0, r1);
+        oa[j] = f2bf(r0);
+        ob[j] = f2bf(r1);
       }
     } else {
 #pragma unroll

@@ -73,9 +73,10 @@ rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
     for (int j = 0; j < 8; ++j) {
       const float c = j < 4 ? c0[j] : c1[j - 4];
       const float s = j < 4 ? s0[j] : s1[j - 4];
-      const float x0 = bf2f(a[j]), x1 = bf2f(b[j]);
-      oa[j] = f2bf(x0 * c - x1 * s);
-      ob[j] = f2bf(x1 * c + x0 * s);
+      float r0, r1;
+      rope_rotate(bf2f(a[j]), bf2f(b[j]), c, s, r0, r1);
+      oa[j] = f2bf(r0);
+      ob[j] = f2bf(r1);
     }
     bf16* hp = row + (long)h * D;
     *reinterpret_cast<bf16x8*>(hp + p0) = oa;
