@@ -32,6 +32,7 @@ constexpr int kSeamNone = 0, kSeamNorm = 1, kSeamRope = 2;
 struct Seam {
   int mode;
   int sk;               // split count (set by launch_gemm_seam; the grid is 1-D, splits adjacent)
+  int xcd_local;        // (set by launch_gemm_seam) a tile's splits share an XCD (seam_tile_split)
   // kSeamNorm
   bf16* residual;       // [M, N] in/out
   const bf16* gamma;    // [N]

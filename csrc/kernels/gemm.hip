@@ -74,8 +74,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(float* base, long by
                                            (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
 }
 
-__device__ __forceinline__ void store_slab4(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+// Cache-policy bit of a buffer access: sc1 (write-through store / agent-coherent load).
+constexpr int kCpolSc1 = 16;
+
+// `wt`: write-through (sc1) — the slabs of a split-K seam, read by sibling workgroups of the
+// same launch (seam_arrive's hand-off without cache-wide write-back / invalidate)
+__device__ __forceinline__ void store_slab4(__amdgpu_buffer_rsrc_t r, int off, f32x4 v, bool wt = false) {
+  if (wt) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, kCpolSc1);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
 }
 
 // Reduce split-K partial slabs [SK][M][N] (f32) and apply the epilogue.
@@ -190,12 +196,16 @@ constexpr long long kSeamSpinTicks = 2LL * 100000000LL;   // 2 s of the 100 MHz 
 constexpr int kSeamTiles = 1024;                            // counters per split-count region
 
 // Publish this split's slab and wait for the tile's sibling splits of the same generation.
+// The hand-off of MI355X_MICROARCH.md's table (row 1), with no cache-wide maintenance: the slabs
+// were stored write-through (sc1, tile_epilogue), every wave drains its stores (vmcnt(0)) before
+// the workgroup barrier, then ONE lane adds to the tile's counter (agent scope) and polls it
+// (agent-coherent loads); the other waves pass the barrier that lane joins, and every slab read
+// is an sc1 load (seam_sum8). (The first version used agent release / acquire fences: each
+// wrote back and invalidated the whole L2 per workgroup — 36.9 vs 29.3 ms per 70B decode step.)
 __device__ __forceinline__ void seam_arrive(int sk, int tile, const Seam& seam) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // one counter region per split count: a tile's counter only ever advances by whole
     // generations of `sk` (O at sk 8 and down at sk 4 share tile indices, not counters)
     int* cnt = seam.counters + sk * kSeamTiles + tile;
@@ -211,20 +221,40 @@ __device__ __forceinline__ void seam_arrive(int sk, int tile, const Seam& seam) 
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// Tile and split of a seam workgroup (1-D grid). xcd_local (the tile count a multiple of 8):
+// the dispatcher deals workgroups round-robin over the 8 XCDs (b % 8 share an L2), so a tile's
+// splits get ids b = 8 (q sk + s) + x — all on XCD x, whose slabs then stay in its L2 for the
+// siblings' reduce — and XCD x owns the contiguous tiles [x T/8, (x + 1) T/8) (the row tiles of
+// one weight panel side by side). Ids 0 .. 8 sk - 1 still hold 8 complete tiles, so progress
+// needs no more resident workgroups than the adjacent layout (`else`: splits at consecutive ids).
+// Placement is a speed matter only: the hand-off is agent-scope either way.
+__device__ __forceinline__ void seam_tile_split(const Seam& seam, int ntiles, int& tile, int& split) {
+  const int b = blockIdx.x, sk = seam.sk;
+  if (seam.xcd_local && (ntiles & 7) == 0) {
+    const int x = b & 7, j = b >> 3;
+    split = j % sk;
+    tile = x * (ntiles >> 3) + j / sk;
+  } else {
+    tile = xcd_remap(b / sk, ntiles);
+    split = b % sk;
+  }
 }
 
 // 8 consecutive columns of one row, summed over the sk slabs in split order and rounded to
-// bf16 (what the separate reduce / norm / rope kernels compute)
-__device__ __forceinline__ void seam_sum8(const float* __restrict__ pr, int sk, long slab, float (&a)[8]) {
-  f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
+// bf16 (what the separate reduce / norm / rope kernels compute). Agent-coherent (sc1) loads
+// through a descriptor over all sk slabs: the siblings' write-through stores, never a stale line.
+__device__ __forceinline__ void seam_sum8(__amdgpu_buffer_rsrc_t rs, int off, int sk, int slab_bytes, float (&a)[8]) {
+  auto ld = [&](int o) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kCpolSc1));
+  };
+  f32x4 lo = ld(off), hi = ld(off + 16);
   for (int k = 1; k < sk; ++k) {
-    lo += *reinterpret_cast<const f32x4*>(pr + k * slab);
-    hi += *reinterpret_cast<const f32x4*>(pr + k * slab + 4);
+    lo += ld(off + k * slab_bytes);
+    hi += ld(off + k * slab_bytes + 16);
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -242,7 +272,8 @@ __device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk
   const int r0 = m0 + split * R;
   const int r1 = min(min(m0 + BM, r0 + R), M);
   const int tn = n0 / BN, nchunks = N / BN;
-  const long slab = (long)M * N;
+  const int slab = M * N * 4;                       // bytes (the launcher bounds sk x slab)
+  const auto rs = slab_rsrc(const_cast<float*>(part), (long)sk * slab);
   const int c = n0 + (threadIdx.x % TPR) * 8;
   const bf16x8 g = *reinterpret_cast<const bf16x8*>(seam.gamma + c);
   for (int base = r0; base < r1; base += rpp) {
@@ -251,7 +282,7 @@ __device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk
     float ss = 0.f;
     if (ok) {
       float a[8];
-      seam_sum8(part + (long)row * N + c, sk, slab, a);
+      seam_sum8(rs, (row * N + c) * 4, sk, slab, a);
       bf16x8* rp = reinterpret_cast<bf16x8*>(seam.residual + (long)row * N + c);
       const bf16x8 r = *rp;
       bf16x8 sm, o;
@@ -281,14 +312,15 @@ __device__ __forceinline__ void seam_rope(const float* __restrict__ part, int sk
   const int R = (BM + sk - 1) / sk;
   const int r0 = m0 + split * R;
   const int r1 = min(min(m0 + BM, r0 + R), M);
-  const long slab = (long)M * N;
+  const int slab = M * N * 4;                       // bytes (the launcher bounds sk x slab)
+  const auto rs = slab_rsrc(const_cast<float*>(part), (long)sk * slab);
   const int head = n0 / D, p0 = (threadIdx.x % TPR) * 8;
   const bool is_v = head >= seam.hq + seam.hkv, is_k = !is_v && head >= seam.hq;
   for (int row = r0 + threadIdx.x / TPR; row < r1; row += rpp) {
     float a[8], b[8];
-    const float* pr = part + (long)row * N + n0 + p0;
-    seam_sum8(pr, sk, slab, a);
-    seam_sum8(pr + H2, sk, slab, b);
+    const int poff = (row * N + n0 + p0) * 4;
+    seam_sum8(rs, poff, sk, slab, a);
+    seam_sum8(rs, poff + H2 * 4, sk, slab, b);
     bf16x8 oa, ob;
     if (!is_v) {
       const int pos = seam.positions[row];
@@ -524,7 +556,7 @@ template <int TI, int TJ>
 __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw, int nw, int lane,
                                               int M, int N, int epi, const bf16* __restrict__ bias,
                                               bf16* __restrict__ out, long ldo, float* __restrict__ pslab,
-                                              int m0, const RowScale& rsc) {
+                                              int m0, const RowScale& rsc, bool wt = false) {
   const int lr = lane & 15, lc = 4 * (lane >> 4);
   const auto rs = slab_rsrc(pslab, pslab ? (long)(M - m0) * N * 4 : 0);
   const bool vec = (ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
@@ -547,7 +579,7 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw
     for (int j = 0; j < TJ; ++j) {
       const int n = nw + 16 * j + lc;
       if (pslab) {
-        store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j] * sc[i]);
+        store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j] * sc[i], wt);
       } else if (epi == EPI_SILU) {
         if constexpr (TJ % 2 == 0) {   // gate/up 16-row groups pair up inside the wave
           if (j & 1) continue;
@@ -597,7 +629,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
-  int tile, m0, n0;
+  int tile, m0, n0, ksplit = 0;
   const int m_slab = M;             // split-K slab row stride (grouped: all row slots)
   bool single = false;              // grouped: this expert has one row tile (W read once)
   if constexpr (GROUPED) {
@@ -611,14 +643,15 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     tile = 0;
   } else {
     const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-    tile = xcd_remap(seam.mode != kSeamNone ? (int)blockIdx.x / seam.sk : (int)blockIdx.x, mtiles * ntiles);
+    if (seam.mode != kSeamNone) seam_tile_split(seam, mtiles * ntiles, tile, ksplit);
+    else tile = xcd_remap((int)blockIdx.x, mtiles * ntiles);
     const int tn = tile / mtiles, tm = tile % mtiles;  // consecutive tiles share a W panel
     m0 = tm * BM;
     n0 = tn * BN;
   }
-  // split index / count: grid y, or (seam launches) the fastest-varying part of a 1-D grid so a
-  // tile's sibling splits are dispatched back to back (seam_arrive waits on them)
-  const int ksplit = seam.mode != kSeamNone ? (int)blockIdx.x % seam.sk : (int)blockIdx.y;
+  // split index / count: grid y, or (seam launches) from the 1-D grid id so a tile's sibling
+  // splits are dispatched close together (seam_arrive waits on them)
+  if (seam.mode == kSeamNone) ksplit = (int)blockIdx.y;
   const int nsplit = seam.mode != kSeamNone ? seam.sk : (int)gridDim.y;
 
   const int ktiles = K / kBK;
@@ -674,7 +707,8 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     if (++buf == STAGES) buf = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)ksplit * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
+                        part ? part + (long)ksplit * m_slab * N + (long)m0 * N : nullptr, m0, rsc,
+                        seam.mode != kSeamNone);
   if constexpr (!GROUPED) {
     if (part && seam.mode != kSeamNone) {
       seam_finish<BN>(part, nsplit, ksplit, tile, M, N, m0, BM, n0, seam);
@@ -748,10 +782,15 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
   const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-  const int tile = xcd_remap(seam.mode != kSeamNone ? (int)blockIdx.x / seam.sk : (int)blockIdx.x, mtiles * ntiles);
+  int tile, ksplit;   // see gemm_tile_kernel
+  if (seam.mode != kSeamNone) {
+    seam_tile_split(seam, mtiles * ntiles, tile, ksplit);
+  } else {
+    tile = xcd_remap((int)blockIdx.x, mtiles * ntiles);
+    ksplit = (int)blockIdx.y;
+  }
   const int tn = tile / mtiles, tm = tile % mtiles;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int ksplit = seam.mode != kSeamNone ? (int)blockIdx.x % seam.sk : (int)blockIdx.y;   // see gemm_tile_kernel
   const int nsplit = seam.mode != kSeamNone ? seam.sk : (int)gridDim.y;
   const int ktiles = K / kBK;
   const int kt0 = (int)(((long)ktiles * ksplit) / nsplit);
@@ -803,7 +842,8 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
     if (++wslot == SW) wslot = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)ksplit * M * N + (long)m0 * N : nullptr, m0, rsc);
+                        part ? part + (long)ksplit * M * N + (long)m0 * N : nullptr, m0, rsc,
+                        seam.mode != kSeamNone);
   if (part && seam.mode != kSeamNone) seam_finish<BN>(part, nsplit, ksplit, tile, M, N, m0, BM, n0, seam);
 }
 
@@ -1457,14 +1497,21 @@ int launch_gemm_seam(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   if (!dry && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float))) return -3;
   const long grid = (long)((M + p.bm - 1) / p.bm) * (N / p.bn) * p.sk;
   if ((M + p.bm - 1) / p.bm * (N / p.bn) > kSeamTiles || p.sk >= kSplitCounters / kSeamTiles) return -1;
+  if ((long)p.sk * M * N * 4 > 0x7fffffffL) return -1;   // seam_sum8: 32-bit descriptor offsets
   bool fits = false;
   if (p.kind == 1 && p.bm == 64 && p.wk == 2 && p.mt == 3)
     fits = seam_fits(&gemm_tile_kernel<64, 128, 2, 3>, kTileThreads, (size_t)3 * (64 + 128) * kBK * 2, grid);
   else if (p.kind == 3 && p.bm == 64 && p.wk == 4 && p.nt == 8 && p.mt == 6)
     fits = seam_fits(&gemm_dec_kernel<64, 128, 4, 2, 6>, 512, (size_t)(3 * 64 + 6 * 128) * kBK * 2, grid);
   if (!fits) return -2;
+  // BFLY_SEAM_XCD=0: a tile's splits at consecutive ids, i.e. on different XCDs (A/B runs)
+  static const int xcd_local = [] {
+    const char* e = getenv("BFLY_SEAM_XCD");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
   Seam sm = seam;
   sm.sk = p.sk;
+  sm.xcd_local = xcd_local;
   const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, nullptr, 0, ws, stream, dry, true,
                           rs, &sm);
   return rc != 0 ? rc : N / p.bn;

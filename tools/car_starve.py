@@ -14,7 +14,10 @@ same all-reduce. Reported per rank: wall time of its queue, the device error wor
 host-mapped health word. Control: every rank queues the GEMMs first (no early spinner).
 A starved run shows ~20 s and error words set; a healthy protocol finishes in the GEMM time.
 
-usage: python -m butterfly_amd launch -n 4 -- python tools/car_starve.py [--two-shot] [--control]
+Variant --late 1: three early spinners, one late rank (the round-3 rehearsal's pattern): the
+spinners hold every CU, the late rank's GEMM cannot be placed until they give up.
+
+usage: python -m butterfly_amd launch -n 4 -- python tools/car_starve.py [--two-shot] [--control] [--late N]
 """
 import argparse
 import os
@@ -32,6 +35,8 @@ def main() -> int:
     ap.add_argument("--control", action="store_true", help="every rank queues the GEMMs first")
     ap.add_argument("--gemms", type=int, default=12)
     ap.add_argument("--rows", type=int, default=256)
+    ap.add_argument("--late", type=int, default=None,
+                    help="ranks that queue the GEMMs before the all-reduce (the LAST ones; default all but rank 0)")
     a = ap.parse_args()
 
     import torch
@@ -62,14 +67,15 @@ def main() -> int:
     torch.ops.bfly.health_clear()
     dist.barrier()
     t0 = time.perf_counter()
-    if rank > 0 or a.control:
+    late = world - 1 if a.late is None else a.late
+    if rank >= world - late or a.control:
         for _ in range(a.gemms):
             ops.linear(x, w)
     car.all_reduce_(t, two_shot=a.two_shot)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ok = bool((t.float() == sum(range(1, world + 1))).all())
-    print(f"STARVE rank={rank} world={world} two_shot={a.two_shot} control={a.control} rows={a.rows} "
+    print(f"STARVE rank={rank} world={world} late={late} two_shot={a.two_shot} control={a.control} rows={a.rows} "
           f"gemm_queue_alone={gemm_s * 1e3:.1f}ms wall={dt * 1e3:.1f}ms err_word={car.error()} "
           f"health_words={list(torch.ops.bfly.health_words())} result_ok={ok}", flush=True)
     dist.barrier()
