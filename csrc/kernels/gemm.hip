@@ -363,10 +363,15 @@ __device__ __forceinline__ void seam_rope(const float* __restrict__ part, int sk
   }
 }
 
+// BFLY_SEAM_PROBE (timing experiments only, tools/seam_bench.py; results are WRONG when set):
+// bit 0 skips the sibling wait, bit 1 skips the share's reduce
+__constant__ int g_seam_probe = 0;
+
 template <int BN>
 __device__ __forceinline__ void seam_finish(const float* __restrict__ part, int sk, int split, int tile, int M,
                                             int N, int m0, int BM, int n0, const Seam& seam) {
-  seam_arrive(sk, tile, seam);
+  if (!(g_seam_probe & 1)) seam_arrive(sk, tile, seam);
+  if (g_seam_probe & 2) return;
   if (seam.mode == kSeamNorm) {
     seam_norm<BN>(part, sk, split, M, N, m0, BM, n0, seam);
   } else if constexpr (BN == 128) {
@@ -562,12 +567,29 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw
   const bool vec = (ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
   float sc[TI];
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    const int m = mw + 16 * i + lr;
-    sc[i] = 1.f;
-    if (rsc.ss != nullptr && m < M) {
+  for (int i = 0; i < TI; ++i) sc[i] = 1.f;
+  if (rsc.ss != nullptr) {
+    // sum of the row's partial sums of squares: the 4 lanes of a row (lane >> 4) take every
+    // 4th group of 4 chunks as 16-B loads, all in flight together, then two shuffles (a norm
+    // seam leaves one chunk per 128 columns: 64 for d 8192 — a serial loop of dependent loads
+    // there cost ~20 us per consumer GEMM); chunks % 4 != 0: one chunk per lane and step
+    const int q = lane >> 4, nc = rsc.chunks;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int m = min(mw + 16 * i + lr, M - 1);
+      const float* sp = rsc.ss + (long)m * nc;
       float t = 0.f;
-      for (int c = 0; c < rsc.chunks; ++c) t += rsc.ss[(long)m * rsc.chunks + c];
+      if ((nc & 3) == 0) {
+#pragma unroll 4
+        for (int c = 4 * q; c < nc; c += 16) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(sp + c);
+          t += (v[0] + v[1]) + (v[2] + v[3]);
+        }
+      } else {
+        for (int c = q; c < nc; c += 4) t += sp[c];
+      }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
       sc[i] = rsqrtf(t * rsc.inv_dim + rsc.eps);
     }
   }
@@ -1509,6 +1531,13 @@ int launch_gemm_seam(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
     const char* e = getenv("BFLY_SEAM_XCD");
     return e && e[0] == '0' ? 0 : 1;
   }();
+  static const bool probe_set = [] {
+    const char* e = getenv("BFLY_SEAM_PROBE");
+    const int v = e ? atoi(e) : 0;
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_seam_probe), &v, sizeof(int));
+    return true;
+  }();
+  (void)probe_set;
   Seam sm = seam;
   sm.sk = p.sk;
   sm.xcd_local = xcd_local;
