@@ -724,15 +724,13 @@ class LLMEngine:
         where = {r: i for i, r in enumerate(src.rids)} if src is not None and src is self._valued else {}
         if not where or not any(r in where for r in p.rids):
             return np.asarray([self.requests[r].tokens[-1] for r in p.rids], dtype=np.int32)
-        host = [0 if r in where else self.requests[r].tokens[-1] for r in p.rids]
-        rows = [i for i, r in enumerate(p.rids) if r in where]
-        idx = [where[p.rids[i]] for i in rows]
-        dev = src.ids.device
-        ids = torch.tensor(host, dtype=torch.int32).to(dev, non_blocking=True)
-        if len(rows) == len(p.rids):
-            return src.ids.index_select(0, torch.tensor(idx, dtype=torch.long).to(dev, non_blocking=True))
-        ids[torch.tensor(rows, dtype=torch.long).to(dev, non_blocking=True)] = \
-            src.ids.index_select(0, torch.tensor(idx, dtype=torch.long).to(dev, non_blocking=True))
+        # one H2D copy of [host ids | source rows] and one row gather (ops.gather_rows: rows
+        # with source -1 keep their host id)
+        n = len(p.rids)
+        staged = torch.tensor([0 if r in where else self.requests[r].tokens[-1] for r in p.rids] +
+                              [where.get(r, -1) for r in p.rids], dtype=torch.int32).to(src.ids.device, non_blocking=True)
+        ids = staged[:n]
+        ops.gather_rows(src.ids.view(-1, 1), staged[n:], out=ids.view(-1, 1))
         return ids
 
     def _pp_stage_work(self, p: PipePlan) -> None:

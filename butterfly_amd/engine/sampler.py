@@ -65,10 +65,13 @@ class Sampler:
         ids, scores = ops.sample(lv, temps, seeds, vstart=self.vocab_start, check_finite=check_finite)
         if self.tp == 1:
             return ids
-        pair = torch.stack([scores, ids.to(torch.float32)], 1)        # ids < 2^24: exact in f32
-        allp = self.comm.all_gather(pair, "tp").view(self.tp, -1, 2)  # [tp, R, 2]
-        best = allp[:, :, 0].argmax(0)                                 # ties -> lowest rank
-        return allp.gather(0, best.view(1, -1, 1).expand(1, -1, 2))[0, :, 1].to(torch.int32)
+        return self._merge(ids, scores)
+
+    def _merge(self, ids: torch.Tensor, scores: torch.Tensor) -> torch.Tensor:
+        """Each vocab shard's winner -> the global winner: (score, id) pairs all-gathered over
+        the TP group, best score per row, lowest rank on ties (sample.hip pack / merge)."""
+        allp = self.comm.all_gather(ops.sample_pack(scores, ids), "tp").view(self.tp, -1, 2)
+        return ops.sample_merge(allp)
 
     def thresholds(self, lv: torch.Tensor, temps: torch.Tensor, params: list) -> torch.Tensor:
         """Per-row lower bound on logit / temperature implementing top-k / top-p (module doc).
@@ -97,7 +100,4 @@ class Sampler:
                                  check_finite=check_finite)
         if self.tp == 1:
             return ids
-        pair = torch.stack([scores, ids.to(torch.float32)], 1)
-        allp = self.comm.all_gather(pair, "tp").view(self.tp, -1, 2)
-        best = allp[:, :, 0].argmax(0)
-        return allp.gather(0, best.view(1, -1, 1).expand(1, -1, 2))[0, :, 1].to(torch.int32)
+        return self._merge(ids, scores)

@@ -346,10 +346,10 @@ class TransformerLM:
                 delta = self.comm.all_reduce_(delta, "tp")
             return ops.add(residual, ops.materialize(delta))
         idx = fb.logits_idx
-        r = residual if idx is None else residual.index_select(0, idx)
+        r = residual if idx is None else ops.gather_rows(residual, idx)
         if delta is not None:
             # all-reduce is linear: select the sampled rows first and reduce only those
-            dl = delta if idx is None else ops.materialize(delta).index_select(0, idx)
+            dl = delta if idx is None else ops.gather_rows(ops.materialize(delta), idx)
             if idx is None:
                 r = r.clone()
             x = self._add_norm(dl, "final", r, partial)
@@ -455,7 +455,7 @@ class TransformerLM:
         if not self.last:
             return full
         if fb.logits_idx is not None:
-            full = full.index_select(0, fb.logits_idx)
+            full = ops.gather_rows(full, fb.logits_idx)
         return ops.linear(self._norm(full, self.p["final_w"], self.p.get("final_b")), self.head_weight)
 
     def _mixed_attention(self, q, k, v, fb: ForwardBatch, kc, vc) -> torch.Tensor:

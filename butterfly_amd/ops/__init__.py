@@ -372,6 +372,39 @@ def embed(ids, table, vstart: int = 0, out=None):
     return out
 
 
+def gather_rows(src, idx, out=None):
+    """out[i] = src[idx[i]] (rows of a 2-D tensor; `idx` int32 / int64). Rows whose idx is < 0
+    keep what `out` holds (pass a pre-filled `out`). Our row-gather kernel on the GPU, not
+    torch's index_select (elementwise.hip gather_rows_kernel)."""
+    if out is None:
+        out = torch.empty(idx.numel(), *src.shape[1:], dtype=src.dtype, device=src.device)
+    if not _gpu(src):
+        return ref.gather_rows(src, idx, out)
+    s2 = src if src.dim() == 2 else src.view(src.shape[0], -1)
+    o2 = out if out.dim() == 2 else out.view(out.shape[0], -1)
+    torch.ops.bfly.gather_rows(s2, idx, o2)
+    return out
+
+
+def sample_pack(scores, ids):
+    """Per-shard sampling winners -> [rows, 2] f32 (score, id) pairs for the TP all-gather."""
+    if not _gpu(scores):
+        return ref.sample_pack(scores, ids)
+    pair = torch.empty(scores.numel(), 2, dtype=torch.float32, device=scores.device)
+    torch.ops.bfly.sample_pack(scores.contiguous(), ids.contiguous(), pair)
+    return pair
+
+
+def sample_merge(allp):
+    """All-gathered pairs [tp, rows, 2] -> int32 ids of the best score per row (lowest rank on
+    ties: torch.argmax's first maximum)."""
+    if not _gpu(allp):
+        return ref.sample_merge(allp)
+    out = torch.empty(allp.shape[1], dtype=torch.int32, device=allp.device)
+    torch.ops.bfly.sample_merge(allp.contiguous(), out)
+    return out
+
+
 def sample(logits, temps=None, seeds=None, vstart: int = 0, out_ids=None, out_scores=None, thresh=None,
            check_finite: bool = False):
     """Greedy / Gumbel-max sampling over a (vocab-shard of) logits -> (ids int32, scores f32).

@@ -79,6 +79,26 @@ def _rotate(x, cos, sin):
     return torch.cat([x0 * cos - x1 * sin, x1 * cos + x0 * sin], -1)
 
 
+def sample_pack(scores, ids):
+    return torch.stack([scores.float(), ids.to(torch.float32)], 1)
+
+
+def sample_merge(allp):
+    best = allp[:, :, 0].argmax(0)
+    return allp.gather(0, best.view(1, -1, 1).expand(1, -1, 2))[0, :, 1].to(torch.int32)
+
+
+def gather_rows(src, idx, out):
+    """out[i] = src[idx[i]] where idx[i] >= 0; other rows of `out` are left as they are."""
+    ok = idx >= 0
+    if bool(ok.all()):
+        out.copy_(src.index_select(0, idx.long()))
+    else:
+        rows = ok.nonzero().flatten()
+        out[rows] = src.index_select(0, idx[rows].long())
+    return out
+
+
 def rope_kv(qkv, positions, cos, sin, n_q, n_kv, slots=None, k_cache=None, v_cache=None):
     T = qkv.shape[0]
     D = qkv.shape[1] // (n_q + 2 * n_kv)

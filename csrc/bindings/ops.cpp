@@ -191,6 +191,39 @@ void embed(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) 
                      cur_stream());
 }
 
+void gather_rows(const Tensor& src, const Tensor& idx, Tensor& out) {
+  CHECK_GPU(src); CHECK_GPU(idx); CHECK_GPU(out);
+  TORCH_CHECK(src.dim() == 2 && out.dim() == 2 && src.stride(1) == 1 && out.stride(1) == 1, "gather_rows: 2-D rows");
+  TORCH_CHECK(src.scalar_type() == out.scalar_type() && src.size(1) == out.size(1), "gather_rows: row types");
+  TORCH_CHECK(idx.dim() == 1 && idx.is_contiguous() && idx.numel() == out.size(0) &&
+              (idx.scalar_type() == at::kInt || idx.scalar_type() == at::kLong), "gather_rows: idx");
+  const long es = src.element_size();
+  TORCH_CHECK((src.size(1) * es) % 4 == 0 && (src.stride(0) * es) % 4 == 0 && (out.stride(0) * es) % 4 == 0,
+              "gather_rows: rows must be whole 4-byte words");
+  c10::DeviceGuard g(src.device());
+  bfly::launch_gather_rows(src.data_ptr(), src.stride(0) * es / 4, idx.data_ptr(), idx.scalar_type() == at::kLong,
+                           out.data_ptr(), out.stride(0) * es / 4, (int)(src.size(1) * es / 4), out.size(0),
+                           src.size(0), cur_stream());
+}
+
+void sample_pack(const Tensor& scores, const Tensor& ids, Tensor& pair) {
+  CHECK_GPU(scores); CHECK_GPU(ids); CHECK_I32(ids);
+  TORCH_CHECK(scores.scalar_type() == at::kFloat && pair.scalar_type() == at::kFloat && scores.is_contiguous() &&
+              ids.is_contiguous() && pair.is_contiguous() && pair.numel() == 2 * scores.numel() &&
+              ids.numel() == scores.numel(), "sample_pack: shapes");
+  c10::DeviceGuard g(scores.device());
+  bfly::launch_sample_pack(scores.data_ptr<float>(), ids.data_ptr<int>(), pair.data_ptr<float>(), scores.numel(),
+                           cur_stream());
+}
+
+void sample_merge(const Tensor& allp, Tensor& out) {
+  CHECK_GPU(allp); CHECK_I32(out);
+  TORCH_CHECK(allp.scalar_type() == at::kFloat && allp.is_contiguous() && allp.dim() == 3 && allp.size(2) == 2 &&
+              out.is_contiguous() && out.numel() == allp.size(1), "sample_merge: shapes");
+  c10::DeviceGuard g(allp.device());
+  bfly::launch_sample_merge(allp.data_ptr<float>(), allp.size(0), allp.size(1), out.data_ptr<int>(), cur_stream());
+}
+
 void sample(const Tensor& logits, const c10::optional<Tensor>& temps,
             const c10::optional<Tensor>& seeds, int64_t vstart, Tensor& out_ids,
             Tensor& out_scores, Tensor& workspace, const c10::optional<Tensor>& thresh,
@@ -1105,6 +1138,9 @@ TORCH_LIBRARY(bfly, m) {
   m.def("add(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("init_hash(Tensor(a!) out, int grow0, int gcol0, int gcols, int seed, float amp) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vstart) -> ()");
+  m.def("gather_rows(Tensor src, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("sample_pack(Tensor scores, Tensor ids, Tensor(a!) pair) -> ()");
+  m.def("sample_merge(Tensor allp, Tensor(a!) out) -> ()");
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
         "Tensor(b!) out_scores, Tensor(c!) workspace, Tensor? thresh=None, bool check_finite=False) -> ()");
   m.def("tkp_begin(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor(a!) ws) -> ()");
@@ -1180,6 +1216,9 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("gelu", &gelu);
   m.impl("add", &add);
   m.impl("embed", &embed);
+  m.impl("gather_rows", &gather_rows);
+  m.impl("sample_pack", &sample_pack);
+  m.impl("sample_merge", &sample_merge);
   m.impl("init_hash", &init_hash);
   m.impl("sample", &sample);
   m.impl("tkp_begin", &tkp_begin);

@@ -99,6 +99,10 @@ void launch_init_hash(bf16* out, long rows, int cols, long ld, long grow0, long 
                       uint32_t seed, float amp, hipStream_t stream);
 void launch_embed(const int* ids, const bf16* table, bf16* out, int T, int dim, int vstart,
                   int vlocal, hipStream_t stream);
+// out[i, :] = src[idx[i], :] over rows of `words` 4-byte words (strides in words); idx < 0 or
+// out of range leaves row i untouched
+void launch_gather_rows(const void* src, long src_ld, const void* idx, bool idx64, void* out, long out_ld,
+                        int words, long rows, long nsrc, hipStream_t stream);
 
 // sample.hip
 constexpr int kSampleMaxChunks = 64;
@@ -106,6 +110,9 @@ void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vst
                    const float* temps, const long* seeds, uint64_t* workspace, int* out_ids,
                    float* out_scores, hipStream_t stream, const float* thresh = nullptr,
                    int check_finite = 0);
+// TP merge of per-shard winners: pair [rows][2] f32 (score, id); allp [tp][rows][2] -> ids
+void launch_sample_pack(const float* scores, const int* ids, float* pair, int rows, hipStream_t stream);
+void launch_sample_merge(const float* allp, int tp, int rows, int* out, hipStream_t stream);
 // exact top-k / top-p thresholds by radix select (sample.hip): state [rows, 8] f32 bits,
 // smax [rows] int32 (zeroed), hist [rows, 512] f32 (zeroed); see the kernel comment
 void launch_tkp_begin(const bf16* logits, long row_stride, int rows, int V, const float* temps,

@@ -86,6 +86,26 @@ __global__ void embed_kernel(const int* __restrict__ ids, const bf16* __restrict
   }
 }
 
+// Row gather: out[i] = src[idx[i]] for rows of `words` 4-byte words (bf16 / f32 / int32 rows);
+// rows with idx < 0 are left as they are (the caller pre-filled them). Replaces torch's
+// index_select / gather on serving paths (final-token rows, pipeline input ids): one small
+// launch of our own instead of an at::native kernel.
+template <typename IT>
+__global__ void gather_rows_kernel(const uint32_t* __restrict__ src, long src_ld, const IT* __restrict__ idx,
+                                   uint32_t* __restrict__ out, long out_ld, int words, long nsrc) {
+  const long i = blockIdx.x;
+  const long j = (long)idx[i];
+  if (j < 0 || j >= nsrc) return;
+  const uint32_t* s = src + j * src_ld;
+  uint32_t* o = out + i * out_ld;
+  if ((words & 3) == 0 && ((src_ld | out_ld) & 3) == 0) {
+    for (int c = threadIdx.x; c < words / 4; c += kEwThreads)
+      reinterpret_cast<u32x4*>(o)[c] = reinterpret_cast<const u32x4*>(s)[c];
+  } else {
+    for (int c = threadIdx.x; c < words; c += kEwThreads) o[c] = s[c];
+  }
+}
+
 // Deterministic, partition-independent random init: element (global_row, global_col) of a
 // logical weight gets a value that depends only on (seed, global index), so every rank can
 // generate exactly its own shard and any partition reproduces the same global weights.
@@ -131,6 +151,19 @@ void launch_gelu(const bf16* x, bf16* out, long n, hipStream_t stream) {
 void launch_add(const bf16* a, const bf16* b, bf16* out, long n, hipStream_t stream) {
   if (n <= 0) return;
   add_kernel<<<ew_grid(n / 8), kEwThreads, 0, stream>>>(a, b, out, n / 8);
+}
+
+void launch_gather_rows(const void* src, long src_ld, const void* idx, bool idx64, void* out, long out_ld,
+                        int words, long rows, long nsrc, hipStream_t stream) {
+  if (rows <= 0 || words <= 0) return;
+  if (idx64)
+    gather_rows_kernel<long><<<rows, kEwThreads, 0, stream>>>(static_cast<const uint32_t*>(src), src_ld,
+                                                              static_cast<const long*>(idx),
+                                                              static_cast<uint32_t*>(out), out_ld, words, nsrc);
+  else
+    gather_rows_kernel<int><<<rows, kEwThreads, 0, stream>>>(static_cast<const uint32_t*>(src), src_ld,
+                                                             static_cast<const int*>(idx),
+                                                             static_cast<uint32_t*>(out), out_ld, words, nsrc);
 }
 
 void launch_embed(const int* ids, const bf16* table, bf16* out, int T, int dim, int vstart,

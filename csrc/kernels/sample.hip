@@ -385,6 +385,43 @@ void launch_tkp_final(const float* state, int rows, float* thresh, hipStream_t s
   tkp_final_kernel<<<(rows + 63) / 64, 64, 0, stream>>>(state, rows, thresh);
 }
 
+// TP sampling merge: each vocab shard's winner as an f32 (score, id) pair
+// (ids < 2^24 are exact in f32) -> all-gathered [tp][rows][2] -> the highest score per row, the
+// lowest rank on ties (torch.argmax's first maximum). Two tiny kernels in place of torch's
+// stack / cast / argmax / gather on every TP decode step.
+__global__ void sample_pack_kernel(const float* __restrict__ scores, const int* __restrict__ ids,
+                                   float* __restrict__ pair, int rows) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  pair[2 * r] = scores[r];
+  pair[2 * r + 1] = (float)ids[r];
+}
+
+__global__ void sample_merge_kernel(const float* __restrict__ allp, int tp, int rows, int* __restrict__ out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  int best = 0;
+  float bs = allp[2 * r];
+  for (int k = 1; k < tp; ++k) {
+    const float sc = allp[((long)k * rows + r) * 2];
+    if (sc > bs || (sc != sc && bs == bs)) {   // argmax semantics: NaN counts as the maximum
+      bs = sc;
+      best = k;
+    }
+  }
+  out[r] = (int)allp[((long)best * rows + r) * 2 + 1];
+}
+
+void launch_sample_pack(const float* scores, const int* ids, float* pair, int rows, hipStream_t stream) {
+  if (rows <= 0) return;
+  sample_pack_kernel<<<(rows + 255) / 256, 256, 0, stream>>>(scores, ids, pair, rows);
+}
+
+void launch_sample_merge(const float* allp, int tp, int rows, int* out, hipStream_t stream) {
+  if (rows <= 0) return;
+  sample_merge_kernel<<<(rows + 255) / 256, 256, 0, stream>>>(allp, tp, rows, out);
+}
+
 void launch_sample(const bf16* logits, long row_stride, int rows, int V, int vstart,
                    const float* temps, const long* seeds, uint64_t* workspace, int* out_ids,
                    float* out_scores, hipStream_t stream, const float* thresh, int check_finite) {

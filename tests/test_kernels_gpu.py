@@ -892,3 +892,37 @@ def test_sample_check_finite():
     assert torch.equal(rid.cpu(), ids)
 
 
+
+
+def test_gather_rows_matches_index_select():
+    """ops.gather_rows (elementwise.hip): bf16 hidden rows by int64 indices (final-token rows),
+    int32 single-column rows with -1 holes keeping their pre-filled values (pipeline input ids),
+    and odd-width f32 rows from a strided view (4-byte fallback path)."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    src = torch.randn(50, 8192, device=DEV, generator=g).to(torch.bfloat16)
+    idx = torch.tensor([49, 0, 7, 7, 31], dtype=torch.int64, device=DEV)
+    assert torch.equal(ops.gather_rows(src, idx), src.index_select(0, idx))
+    ids = torch.arange(100, 140, dtype=torch.int32, device=DEV).view(-1, 1)
+    sel = torch.tensor([3, -1, 0, 39, -1, 5], dtype=torch.int32, device=DEV)
+    out = torch.full((6, 1), -7, dtype=torch.int32, device=DEV)
+    ops.gather_rows(ids, sel, out=out)
+    assert out.flatten().tolist() == [103, -7, 100, 139, -7, 105]
+    big = torch.randn(20, 8, device=DEV, generator=g)
+    view = big[:, 1:4]                                   # 3 words per row, row stride 8
+    want = view.index_select(0, idx.clamp(max=19))
+    assert torch.equal(ops.gather_rows(view, idx.clamp(max=19)), want)
+
+
+@pytest.mark.parametrize("tp", [2, 4, 8])
+def test_sample_pack_merge_matches_torch(tp):
+    """TP sampling merge kernels (sample.hip) against the torch stack / argmax / gather they
+    replace: best score per row, lowest rank on ties, ids exact through f32."""
+    rows = 37
+    g = torch.Generator(device=DEV).manual_seed(tp)
+    scores = [torch.randn(rows, device=DEV, generator=g) for _ in range(tp)]
+    scores[1][:5] = scores[0][:5]                        # ties go to the lower rank
+    scores[tp - 1][7] = float("inf")                     # a non-finite row's +inf wins
+    ids = [torch.randint(0, 128256, (rows,), dtype=torch.int32, device=DEV, generator=g) for _ in range(tp)]
+    allp = torch.stack([ops.sample_pack(s, i) for s, i in zip(scores, ids)])
+    assert torch.equal(allp, torch.stack([ref.sample_pack(s, i) for s, i in zip(scores, ids)]))
+    assert torch.equal(ops.sample_merge(allp), ref.sample_merge(allp))

@@ -18,6 +18,9 @@ import os
 import sys
 import time
 
+# every EP rank shares cuda:0 here: opt in to shared-GPU IPC groups (refused in production)
+os.environ.setdefault("BFLY_IPC_SHARED_DEVICE", "1")
+
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
