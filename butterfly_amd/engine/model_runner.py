@@ -25,6 +25,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from .. import ops
 from .batch import ForwardBatch
 
 
@@ -43,8 +44,6 @@ def _recover_from_capture(device) -> None:
         torch.cuda.synchronize(device)
     except Exception:  # noqa: BLE001 — the error being cleared may surface here first
         pass
-    from .. import ops
-
     if ops.load_library():
         torch.ops.bfly.hip_clear_error()
 
@@ -59,20 +58,23 @@ class _DecodeGraph:
         b = bucket
         self.bucket = bucket
         self.max_blocks = max_blocks
-        self.inbuf = torch.zeros(b * (4 + max_blocks), dtype=torch.int32, device=device)
+        # initial state built on the host and copied once: padding rows have no cache slot (-1)
+        # and context 1 (no torch fill kernels on the device)
+        init = torch.zeros(b * (4 + max_blocks), dtype=torch.int32)
+        init[2 * b:3 * b] = -1
+        init[3 * b:4 * b] = 1
+        self.inbuf = init.to(device)
         self.input_ids = self.inbuf[0:b]
         self.positions = self.inbuf[b:2 * b]
         self.slots = self.inbuf[2 * b:3 * b]
         self.ctx_lens = self.inbuf[3 * b:4 * b]
         self.block_tables = self.inbuf[4 * b:].view(b, max_blocks)
-        self.slots.fill_(-1)
-        self.ctx_lens.fill_(1)
         pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
         self.host = [torch.zeros(self.inbuf.numel(), dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self.host_np = [h.numpy() for h in self.host]
         self.host_events = [None, None]
         self.host_flip = 0
-        self.hidden_in = None if first else torch.zeros(bucket, hidden, dtype=torch.bfloat16, device=device)
+        self.hidden_in = None if first else torch.zeros(bucket, hidden, dtype=torch.bfloat16).to(device)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.output: Optional[torch.Tensor] = None
         self.send_done = None        # event: the send of `output` has completed (pipeline stages)
@@ -317,7 +319,7 @@ class ModelRunner:
         if ids_dev:
             g.input_ids[:B].copy_(ids)
             if B < b:
-                g.input_ids[B:].zero_()
+                ops.zero_(g.input_ids[B:])
         if g.hidden_in is not None and hidden_in is not None:
             g.hidden_in[:B].copy_(hidden_in)
 

@@ -464,17 +464,17 @@ class TransformerLM:
         With a cached prefix that is ONE pass over the paged cache (ops.attn_prefill_paged: the
         chunk's K/V were appended by rope_kv just before), else flash attention over the chunk."""
         nd = fb.num_decode
-        parts = []
+        out = torch.empty(q.shape, dtype=q.dtype, device=q.device)   # both kernels write their rows
         if nd:
-            parts.append(ops.attn_decode(q[:nd], kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx))
+            ops.attn_decode(q[:nd], kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx, out=out[:nd])
         if q.shape[0] > nd:
             qp = q[nd:]
             if fb.prefix_lens is not None and any(fb.prefix_lens):
-                parts.append(ops.attn_prefill_paged(qp, kc, vc, fb.prefix_tables, fb.cu_seqlens,
-                                                    fb.positions[nd:], fb.max_seqlen, self.scale))
+                ops.attn_prefill_paged(qp, kc, vc, fb.prefix_tables, fb.cu_seqlens, fb.positions[nd:], fb.max_seqlen,
+                                       self.scale, out=out[nd:])
             else:
-                parts.append(ops.attn_prefill(qp, k[nd:], v[nd:], fb.cu_seqlens, fb.max_seqlen, self.scale, True))
-        return parts[0] if len(parts) == 1 else torch.cat(parts)
+                ops.attn_prefill(qp, k[nd:], v[nd:], fb.cu_seqlens, fb.max_seqlen, self.scale, True, out=out[nd:])
+        return out
 
     def _add_norm(self, t: torch.Tensor, prefix: str, residual: torch.Tensor, partial: bool,
                   consumer: Optional[tuple] = None) -> torch.Tensor:

@@ -92,9 +92,20 @@ class _Arena:
                 raise RuntimeError(
                     f"workspace '{name}' needs {numel} elements but is frozen/capturing; "
                     "call ops.reserve_workspace() before capture")
-            buf = (torch.zeros if zero else torch.empty)(max(numel, 1), dtype=dtype, device=device)
+            buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
+            if zero:
+                zero_(buf)
             self.bufs[key] = buf
         return buf
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """t.zero_() through the runtime's memset on the GPU (keeps torch kernels out of traces)."""
+    if t.is_cuda and load_library():
+        torch.ops.bfly.zero_(t)
+    else:
+        t.zero_()
+    return t
 
 
 _scope = threading.local()
@@ -434,10 +445,10 @@ def topkp_threshold(logits, temps, top_k, top_p, reduce_sum=None, reduce_max=Non
     R = logits.shape[0]
     L = torch.ops.bfly
     ws = _arena.get(logits.device, "tkp", R * 521, torch.float32)[: R * 521]
-    ws.zero_()
+    zero_(ws)
     # the row-max slot starts at the smallest ordered key (INT_MIN = below signed_ordered(-inf)):
     # a zero would read as +0.0 and clamp the max of an all-negative row
-    ws[R * 8:R * 9].view(torch.int32).fill_(-2 ** 31)
+    L.fill32_(ws[R * 8:R * 9], -2 ** 31)
     L.tkp_begin(logits, temps, top_k, top_p, ws)
     if reduce_max is not None:
         reduce_max(ws[R * 8:R * 9].view(torch.int32))
@@ -605,7 +616,7 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
     k = topk_ids.shape[1]
     TK = T * k
     if TK == 0:
-        return torch.zeros(T, H, dtype=x.dtype, device=x.device)
+        return zero_(torch.empty(T, H, dtype=x.dtype, device=x.device))
     L = torch.ops.bfly
     dev = x.device
     bcnt, bcap = block_counts if block_counts is not None else (None, 0)

@@ -191,6 +191,26 @@ void embed(const Tensor& ids, const Tensor& table, Tensor& out, int64_t vstart) 
                      cur_stream());
 }
 
+// zero a device buffer with the runtime's fill (no torch elementwise kernel in a trace)
+void zero_(Tensor& t) {
+  CHECK_GPU(t);
+  TORCH_CHECK(t.is_contiguous(), "zero_: contiguous tensors only");
+  c10::DeviceGuard g(t.device());
+  if (t.numel() > 0)
+    TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()) == hipSuccess,
+                "zero_: hipMemsetAsync failed");
+}
+
+// fill a 4-byte-element device buffer with one 32-bit pattern (runtime memset, no torch kernel)
+void fill32_(Tensor& t, int64_t value) {
+  CHECK_GPU(t);
+  TORCH_CHECK(t.is_contiguous() && t.element_size() == 4, "fill32_: contiguous 4-byte elements");
+  c10::DeviceGuard g(t.device());
+  if (t.numel() > 0)
+    TORCH_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(t.data_ptr()), (int)value, t.numel(),
+                                  cur_stream()) == hipSuccess, "fill32_: hipMemsetD32Async failed");
+}
+
 void gather_rows(const Tensor& src, const Tensor& idx, Tensor& out) {
   CHECK_GPU(src); CHECK_GPU(idx); CHECK_GPU(out);
   TORCH_CHECK(src.dim() == 2 && out.dim() == 2 && src.stride(1) == 1 && out.stride(1) == 1, "gather_rows: 2-D rows");
@@ -1139,6 +1159,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("init_hash(Tensor(a!) out, int grow0, int gcol0, int gcols, int seed, float amp) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vstart) -> ()");
   m.def("gather_rows(Tensor src, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("zero_(Tensor(a!) t) -> ()");
+  m.def("fill32_(Tensor(a!) t, int value) -> ()");
   m.def("sample_pack(Tensor scores, Tensor ids, Tensor(a!) pair) -> ()");
   m.def("sample_merge(Tensor allp, Tensor(a!) out) -> ()");
   m.def("sample(Tensor logits, Tensor? temps, Tensor? seeds, int vstart, Tensor(a!) out_ids, "
@@ -1217,6 +1239,8 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("add", &add);
   m.impl("embed", &embed);
   m.impl("gather_rows", &gather_rows);
+  m.impl("zero_", &zero_);
+  m.impl("fill32_", &fill32_);
   m.impl("sample_pack", &sample_pack);
   m.impl("sample_merge", &sample_merge);
   m.impl("init_hash", &init_hash);

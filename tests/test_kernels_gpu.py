@@ -926,3 +926,13 @@ def test_sample_pack_merge_matches_torch(tp):
     allp = torch.stack([ops.sample_pack(s, i) for s, i in zip(scores, ids)])
     assert torch.equal(allp, torch.stack([ref.sample_pack(s, i) for s, i in zip(scores, ids)]))
     assert torch.equal(ops.sample_merge(allp), ref.sample_merge(allp))
+
+
+def test_runtime_fills():
+    """ops.zero_ / fill32_ (runtime memsets that replace torch fill kernels on serving paths)."""
+    t = torch.randn(1000, device=DEV)
+    ops.zero_(t)
+    assert int((t != 0).sum()) == 0
+    u = torch.zeros(77, dtype=torch.int32, device=DEV)
+    torch.ops.bfly.fill32_(u[10:20], -2 ** 31)
+    assert u[10:20].tolist() == [-2 ** 31] * 10 and int(u[:10].abs().sum() + u[20:].abs().sum()) == 0
