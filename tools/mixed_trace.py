@@ -27,7 +27,7 @@ def summary(path: str) -> None:
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     cnt, dur = collections.Counter(), collections.Counter()
     for r in rows:
-        name = r["Kernel_Name"].replace("void ", "").split("(")[0][:90]
+        name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:90]
         cnt[name] += 1
         dur[name] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     print("| kernel | calls | total us | torch (at::native) |")
