@@ -266,12 +266,10 @@ def test_attn_decode_paged(part_tokens, Hq, Hkv):
     _close(o, want, 2e-2, 2e-2)
 
 
-def _paged_chunk_case(Hq, Hkv, kv_dtype, seed=40):
+def _paged_chunk_case(Hq, Hkv, kv_dtype, seed=40, pre=(0, 40, 95, 700, 31), chunk=(37, 1, 50, 16, 129)):
     """Sequences with (cached prefix, chunk) lengths, their pages scattered over a pool with
     holes (random permutation, unused blocks in between), queries as a fused-QKV row view."""
     D, BS = 128, 32
-    pre = [0, 40, 95, 700, 31]
-    chunk = [37, 1, 50, 16, 129]
     S = len(pre)
     maxb = max((p + c + BS - 1) // BS for p, c in zip(pre, chunk))
     nblk = S * maxb + 7
@@ -293,13 +291,24 @@ def _paged_chunk_case(Hq, Hkv, kv_dtype, seed=40):
     return q, kc, vc, tables, i32(cu), i32(pos), max(chunk)
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(64, 8), (32, 8), (8, 2), (8, 8)])
+@pytest.mark.parametrize("Hq,Hkv", [(64, 8), (32, 8), (8, 2), (8, 8), (12, 4), (16, 16)])
 @pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
 def test_attn_prefill_paged_vs_fp32(Hq, Hkv, kv_dtype):
     """Chunked prefill over the paged cache (attention_paged.hip): prefixes of 0 .. 700 cached
     tokens, chunks of 1 .. 129 tokens (ragged 16-token blocks), pages with holes, bf16 and FP8
     pages, GQA groups of 8 / 4 / 4 / 1 — against the fp32 reference over the same pages."""
     q, kc, vc, tables, cu, pos, mq = _paged_chunk_case(Hq, Hkv, kv_dtype)
+    scale = 1.0 / math.sqrt(128)
+    o = ops.attn_prefill_paged(q, kc, vc, tables, cu, pos, mq, scale)
+    want = ref.attn_prefill_paged(q.cpu(), kc.cpu(), vc.cpu(), tables.cpu(), cu.cpu(), pos.cpu(), mq, scale)
+    _close(o, want, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(64, 8), (32, 8)])
+@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
+def test_attn_prefill_paged_single_sequence(Hq, Hkv, kv_dtype):
+    """One sequence's chunk (the launcher's register-kernel path) over a 700-token prefix."""
+    q, kc, vc, tables, cu, pos, mq = _paged_chunk_case(Hq, Hkv, kv_dtype, seed=60, pre=(700,), chunk=(129,))
     scale = 1.0 / math.sqrt(128)
     o = ops.attn_prefill_paged(q, kc, vc, tables, cu, pos, mq, scale)
     want = ref.attn_prefill_paged(q.cpu(), kc.cpu(), vc.cpu(), tables.cpu(), cu.cpu(), pos.cpu(), mq, scale)
