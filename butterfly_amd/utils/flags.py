@@ -42,6 +42,20 @@ define("BFLY_CUSTOM_AR_2SHOT_BYTES", 512 << 10, int, "IPC all-reduces of at leas
 define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0: heuristic plans only; read by the kernel library)")
 define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
+define("BFLY_GEMM_PLAN", "", str, "force GEMM plans for whole-model A/B runs: \"N,K,Mbucket:kind,mt,nt,wk,bm,bn,sk;...\" "
+       "(read by the kernel library)")
+define("BFLY_ATTN_XCD", 1, int, "prefill attention: XCD-aware item walk (0: plain order; read by the kernel library)")
+define("BFLY_ATTN_TRACE", "", str, "set: the prefill attention kernel stamps its item phases into the LSE buffer "
+       "instead of writing results (tools/attn_trace.py; read by the kernel library)")
+define("BFLY_KERNEL_LIB", "", str, "path of another build of the kernel library (same-box A/B runs of kernel changes)")
+define("BFLY_LOG_JSON", False, _bool, "emit log records as one JSON object per line")
+define("BFLY_RESTART", 0, int, "restart attempt of this job (set by `launch --max-restarts`; 0 = first run)")
+define("BFLY_SEAM_XCD", True, _bool, "GEMM seams (BFLY_GEMM_*_SEAM): place a tile's split-K workgroups on one XCD "
+       "(read by the kernel library)")
+define("BFLY_SEAM_PROBE", 0, int, "timing experiments only (tools/seam_bench.py): 1 skips the seam's sibling wait, "
+       "2 its reduce, 3 both — results are WRONG when set (read by the kernel library)")
+define("BFLY_ATTN_PAGED_LDS", True, _bool, "paged-prefix prefill attention: the LDS-staged kernel for chunks of "
+       "several sequences (0: the register kernel everywhere; read by the kernel library)")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
 define("BFLY_NORM_ROWSCALE", True, _bool, "decode add+RMSNorm split over (row, 1024-column) workgroups that write x * g "
        "and partial sums of squares; the consuming QKV / gate-up GEMM applies the 1/rms row scale in its epilogue "
