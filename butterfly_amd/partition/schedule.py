@@ -12,10 +12,10 @@ routed rows) — written down ahead of time so that it can be
 
   * checked for cross-rank consistency without running anything (`check_programs`: every
     group collective is issued by all members in the same order with the same payload, every
-    send has its recv at the same position of the pair's stream). This catches mismatched
-    collectives and send/recv pairs; it does not simulate blocking semantics, so a wait cycle
-    ACROSS groups (e.g. a blocking send interleaved with another group's collective) is not
-    detected;
+    send has its recv at the same position of the pair's stream), then executed against each
+    other under blocking semantics by the native simulator (`simulate`,
+    csrc/runtime/program_sim.h), which finds wait cycles ACROSS groups (a collective of one
+    group waiting on a rank stuck in another group's) and names every blocked rank;
   * priced per xGMI link (`link_bytes`: bytes each directed GPU pair carries per step, ring
     all-reduce/all-gather/reduce-scatter, chain broadcast and point-to-point hops). The
     partitioner reports it per plan (`search.link_traffic`) and uses the busiest link's bytes
@@ -221,6 +221,26 @@ def check_programs(progs: dict) -> None:
         for r, s in seqs.items():
             if s != ref:
                 raise ValueError(f"group {g}: rank {r} issues {s[:4]}... vs {ref[:4]}...")
+    # consistent per group and per pair; now run them against each other (cross-group cycles)
+    sim = simulate(progs)
+    if not sim["ok"]:
+        raise ValueError(f"programs deadlock: {sim['error'] or ''} blocked {sim['blocked'][:8]}")
+
+
+def simulate(progs: dict, rendezvous: bool = False) -> dict:
+    """Run every rank's communication program against the others under blocking semantics
+    (native runtime, csrc/runtime/program_sim.h): collectives meet all members, recvs wait for
+    their message, sends are buffered (`rendezvous`: block until the receiver is at the
+    matching recv, except side-stream sends). Finds wait cycles ACROSS groups, which the
+    per-group sequence comparison of `check_programs` cannot see. Returns {ok, error,
+    blocked: [(rank, index, instruction)], completed}."""
+    from .. import _native_loader
+
+    native = _native_loader.native()
+    n = max(progs) + 1
+    flat = [[(i.op, list(i.group), int(i.nbytes), i.stream) for i in progs[r].comm()] if r in progs else []
+            for r in range(n)]
+    return native.simulate_programs(flat, rendezvous)
 
 
 def link_bytes(plan: PartitionPlan, progs: dict) -> dict:

@@ -17,6 +17,7 @@
 #include <vector>
 
 #define BFLY_RT_NO_PYTHON
+#include "../program_sim.h"
 #include "../scheduler.h"
 
 using namespace bfly_rt;
@@ -149,7 +150,39 @@ static void run_stream(bool mixed, unsigned seed, bool prefix_cache = false) {
               (int)mixed, (int)prefix_cache, seed, reqs.size(), steps, (long long)sch.prefix_hit_tokens());
 }
 
+// rank-program simulator: a random pipeline of S stages x M microbatches (recv -> TP
+// all-reduce -> send) runs to the end under rendezvous semantics; the same programs with two
+// ranks' collective order swapped across groups deadlock
+static void test_program_sim() {
+  std::mt19937 rng(7);
+  for (int trial = 0; trial < 50; ++trial) {
+    const int S = 2 + (int)(rng() % 4), T = 1 + (int)(rng() % 2), M = 1 + (int)(rng() % 4);
+    std::vector<std::vector<SimOp>> progs(S * T);
+    for (int m = 0; m < M; ++m)
+      for (int s = 0; s < S; ++s)
+        for (int t = 0; t < T; ++t) {
+          const int r = s * T + t;
+          if (s > 0) progs[r].push_back({kSimRecv, "recv", {(s - 1) * T + t, r}, 1000 + m, false});
+          if (T > 1) {
+            std::vector<int> g;
+            for (int u = 0; u < T; ++u) g.push_back(s * T + u);
+            progs[r].push_back({kSimCollective, "all_reduce", g, 64, false});
+          }
+          if (s + 1 < S) progs[r].push_back({kSimSend, "send", {r, (s + 1) * T + t}, 1000 + m, (m & 1) != 0});
+        }
+    const SimResult ok = simulate_programs(progs, true);
+    CHECK(ok.ok && ok.error.empty() && ok.blocked.empty());
+  }
+  std::vector<std::vector<SimOp>> cyc = {
+      {{kSimCollective, "all_reduce", {0, 1}, 8, false}, {kSimCollective, "all_reduce", {0, 2}, 8, false}},
+      {{kSimCollective, "all_reduce", {1, 2}, 8, false}, {kSimCollective, "all_reduce", {0, 1}, 8, false}},
+      {{kSimCollective, "all_reduce", {0, 2}, 8, false}, {kSimCollective, "all_reduce", {1, 2}, 8, false}}};
+  const SimResult dl = simulate_programs(cyc, false);
+  CHECK(!dl.ok && dl.error.empty() && dl.blocked.size() == 3);
+}
+
 int main() {
+  test_program_sim();
   test_kv_manager();
   test_prefix_cache_pages();
   for (unsigned seed = 1; seed <= 20; ++seed) {
