@@ -105,6 +105,14 @@ class LLMEngine:
                                   ep=mesh.ep, stages=[tuple(x) for x in stage_layers],
                                   placement=list(range(mesh.world_size)))
         self._exec_ops: dict = {}
+        if mesh.world_size > 1:
+            # every rank's program of a step, run against the others before anything is issued
+            # (csrc/runtime/program_sim.h): a cross-group wait cycle or a mismatched collective
+            # fails here, naming the ranks, instead of hanging the first step
+            from ..partition.schedule import check_programs, programs
+
+            for mb in sorted({1, mesh.pp}):
+                check_programs(programs(self.plan, max(1, engine_cfg.max_batch), microbatches=mb))
         a, b = stage_layers[coord.pp]
         shard = Shard(tp_rank=coord.tp, tp_size=mesh.tp, layer_start=a, layer_end=b,
                       ep_rank=coord.dp if mesh.ep > 1 else 0, ep_size=mesh.ep)
