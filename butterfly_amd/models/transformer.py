@@ -99,6 +99,8 @@ class TransformerLM:
         # RoPE + KV append folded into the decode QKV GEMM's split-K seam (ops.linear_rope_kv)
         self.rope_seam = (self.defer_qkv and not cfg.bias and flags.get("BFLY_GEMM_ROPE_SEAM"))
         self.rope_seam_rows = flags.get("BFLY_NORM_ROWSCALE_MAX_ROWS")
+        # decode: RoPE + KV append inside the paged attention kernel (ops.attn_decode_rope)
+        self.decode_rope = flags.get("BFLY_DECODE_FUSED_ROPE") and not self.rope_seam
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
@@ -373,6 +375,12 @@ class TransformerLM:
             # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
             # when no all-reduce sits in between (tp == 1)
             qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
+            if (self.decode_rope and not fb.is_prefill and kc is not None and c.pos_emb == "rope"
+                    and self.device.type == "cuda"):
+                # decode: RoPE + KV append inside the attention kernel (one launch fewer)
+                attn = ops.attn_decode_rope(qkv, fb.positions, self.cos, self.sin, d.hq, fb.slots, kc, vc,
+                                            fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
+                return self._o_proj(pre, attn, T)
             if c.pos_emb == "rope":
                 qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
             elif kc is not None:
@@ -398,6 +406,10 @@ class TransformerLM:
                 attn = ops.attn_prefill(q, k, v, fb.cu_seqlens, fb.max_seqlen, self.scale, True)
         else:
             attn = ops.attn_decode(q, kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
+        return self._o_proj(pre, attn, T)
+
+    def _o_proj(self, pre: str, attn: torch.Tensor, T: int):
+        d, D = self.dims, self.cfg.head_dim
         o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
         if self.norm_seam and o_b is None and T <= self.rowscale_rows:
             # issued by the consuming add+RMSNorm (_add_norm), fused into the GEMM's split-K seam

@@ -551,6 +551,33 @@ def attn_lse_merge_(acc_o, acc_lse, o, lse):
     return acc_o, acc_lse
 
 
+def attn_decode_rope(qkv, positions, cos, sin, n_q: int, slots, k_cache, v_cache, block_tables, ctx_lens,
+                     scale: float, max_ctx: int, part_tokens: int = DECODE_PART_TOKENS, out=None):
+    """Decode attention with rope_kv's work inside the kernel (attention.hip, ROPE): `qkv` is
+    the QKV projection's un-rotated output — bf16 rows, or a `Partial` whose split-K slabs the
+    kernel reduces itself; Q is rotated in registers and the new token's K / V row stored into
+    the paged cache at `slots` (the same values as rope_kv + attn_decode, one launch fewer)."""
+    rows, part = (qkv.out, qkv.slabs) if isinstance(qkv, Partial) else (qkv, None)
+    if not _gpu(rows):
+        full = qkv.materialize() if part is not None else rows
+        full = rope_kv(full, positions, cos, sin, n_q, k_cache.shape[1], slots, k_cache, v_cache)
+        q = full[:, : n_q * 128].view(full.shape[0], n_q, 128)
+        return attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx, part_tokens, out)
+    B, Hkv = rows.shape[0], k_cache.shape[1]
+    if out is None:
+        out = torch.empty(B, n_q, 128, dtype=rows.dtype, device=rows.device)
+    if part_tokens <= 0:
+        part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
+    ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
+    po = pml = None
+    if ns > 1:
+        po = _arena.get(rows.device, "attn_o", B * Hkv * ns * 16 * 128, torch.float32)
+        pml = _arena.get(rows.device, "attn_ml", B * Hkv * ns * 16 * 2, torch.float32)
+    torch.ops.bfly.attn_decode_rope(rows, part, positions, cos, sin, slots, n_q, k_cache, v_cache, block_tables,
+                                    ctx_lens, scale, max_ctx, part_tokens, out, po, pml)
+    return out
+
+
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_ctx: int,
                 part_tokens: int = DECODE_PART_TOKENS, out=None):
     """One query token per sequence against the paged cache. `max_ctx` bounds ctx_lens (it

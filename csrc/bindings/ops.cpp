@@ -683,6 +683,70 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   TORCH_CHECK(rc == 0, "attn_decode: unsupported configuration (rc=", rc, ")");
 }
 
+// Decode attention with rope_kv folded in: `qkv` [B, (Hq + 2 Hkv) D] is the QKV projection's
+// un-rotated output (bf16 rows, or with `partial` its f32 split-K slabs [sk, B, N]); Q is rotated
+// in-kernel and the new token's K / V row written into the caches at `slots` (-1: none).
+void attn_decode_rope(const Tensor& qkv, const c10::optional<Tensor>& partial, const Tensor& positions,
+                      const Tensor& cos_t, const Tensor& sin_t, const c10::optional<Tensor>& slots,
+                      int64_t num_q_heads, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
+                      const Tensor& ctx_lens, double scale, int64_t max_ctx, int64_t part_tokens, Tensor& out,
+                      const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml) {
+  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_KV(k_cache, v_cache); CHECK_BF16(out);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous(), "attn_decode_rope: qkv [B, N]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "attn_decode_rope: caches");
+  const int B = qkv.size(0), Hq = num_q_heads, Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
+  const int N = (Hq + 2 * Hkv) * D;
+  TORCH_CHECK(D == 128 && qkv.size(1) == N, "attn_decode_rope: qkv row must be (Hq + 2 Hkv) x 128");
+  TORCH_CHECK(v_cache.size(2) == D && v_cache.size(3) == BS, "attn_decode_rope: cache dims");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)B * Hq * D, "attn_decode_rope: out");
+  CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_I32(positions);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1,
+              "attn_decode_rope: block_tables");
+  TORCH_CHECK(ctx_lens.numel() >= B && positions.numel() >= B, "attn_decode_rope: ctx_lens / positions");
+  TORCH_CHECK((long)block_tables.size(1) * BS >= max_ctx, "attn_decode_rope: block table too narrow for max_ctx");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.size(-1) == D / 2 && sin_t.sizes() == cos_t.sizes(),
+              "attn_decode_rope: f32 tables [max_pos, D/2]");
+  bfly::DecodeRope rp;
+  rp.qkv = bf(qkv);
+  rp.N = N;
+  if (partial.has_value()) {
+    TORCH_CHECK(partial->scalar_type() == at::kFloat && partial->is_contiguous() && partial->dim() == 3 &&
+                    partial->size(1) == B && partial->size(2) == N,
+                "attn_decode_rope: partial must be [sk, B, N] f32");
+    rp.part = partial->data_ptr<float>();
+    rp.sk = partial->size(0);
+    rp.slab = (long)B * N;
+  }
+  rp.positions = positions.data_ptr<int>();
+  rp.cos_t = cos_t.data_ptr<float>();
+  rp.sin_t = sin_t.data_ptr<float>();
+  if (slots.has_value()) {
+    CHECK_I32(*slots);
+    TORCH_CHECK(slots->numel() >= B, "attn_decode_rope: slots");
+    rp.slots = slots->data_ptr<int>();
+  }
+  rp.k_out = k_cache.data_ptr();
+  rp.v_out = v_cache.data_ptr();
+  if (part_tokens <= 0) part_tokens = bfly::attn_decode_part_tokens(B, Hkv, max_ctx);
+  const int nsplit = bfly::attn_decode_splits(max_ctx, part_tokens);
+  float *po = nullptr, *pml = nullptr;
+  if (nsplit > 1) {
+    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "attn_decode_rope: partial buffers required");
+    TORCH_CHECK(part_o->numel() >= (long)B * Hkv * nsplit * 16 * D, "attn_decode_rope: part_o too small");
+    TORCH_CHECK(part_ml->numel() >= (long)B * Hkv * nsplit * 16 * 2, "attn_decode_rope: part_ml too small");
+    po = part_o->data_ptr<float>();
+    pml = part_ml->data_ptr<float>();
+  }
+  c10::DeviceGuard g(qkv.device());
+  const int rc = bfly::launch_attn_decode(nullptr, 0, k_cache.data_ptr(), v_cache.data_ptr(),
+                                          block_tables.data_ptr<int>(), block_tables.stride(0),
+                                          ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale, max_ctx,
+                                          part_tokens, bf(out), po, pml, cur_stream(),
+                                          k_cache.scalar_type() == at::kFloat8_e4m3fn, &rp);
+  TORCH_CHECK(rc == 0, "attn_decode_rope: unsupported configuration (rc=", rc, ")");
+}
+
 // Chunked prefill over the paged cache (attention_paged.hip): q [T, Hq, D] rows grouped per
 // sequence by cu_q, positions [T] their absolute positions, tables [nseq, max_blocks].
 void attn_prefill_paged(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& tables,
@@ -1182,6 +1246,9 @@ TORCH_LIBRARY(bfly, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
         "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
         "Tensor(c!)? part_ml) -> ()");
+  m.def("attn_decode_rope(Tensor qkv, Tensor? partial, Tensor positions, Tensor cos_t, Tensor sin_t, Tensor? slots, "
+        "int num_q_heads, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor ctx_lens, float scale, "
+        "int max_ctx, int part_tokens, Tensor(c!) out, Tensor(d!)? part_o, Tensor(e!)? part_ml) -> ()");
   m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
   m.def("moe_max_tiles(int tk, int num_local, int bm=64) -> int", &moe_max_tiles);
@@ -1258,6 +1325,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("gemm_deferred_rs", &gemm_deferred_rs);
   m.impl("rms_norm_rows", &rms_norm_rows);
   m.impl("attn_decode", &attn_decode);
+  m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("gemm_norm", &gemm_norm);
   m.impl("gemm_rope_kv", &gemm_rope_kv);

@@ -154,11 +154,26 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 // attention.hip
 int attn_decode_splits(int max_ctx, int part_tokens);
 int attn_decode_part_tokens(int B, int Hkv, int max_ctx);
+// Decode attention with rope_kv's work folded in (attention.hip): the QKV projection's
+// un-rotated output (f32 split-K slabs `part` [sk][B][N], or bf16 rows `qkv` [B][N]) supplies Q,
+// and the new token's K / V row goes into the cache (`k_out` / `v_out`) at slots[b].
+struct DecodeRope {
+  const float* part = nullptr;
+  const bf16* qkv = nullptr;
+  long slab = 0;                       // elements between split slabs (B * N)
+  int sk = 1, N = 0;                   // N = (Hq + 2 Hkv) * D
+  const int* positions = nullptr;
+  const float* cos_t = nullptr;        // [max_pos, D / 2]
+  const float* sin_t = nullptr;
+  const int* slots = nullptr;          // [B], -1 = no cache write
+  void* k_out = nullptr;
+  void* v_out = nullptr;
+};
 int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
                        bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                       int kv_fp8 = 0);            // caches hold FP8 e4m3 (bfly_kv.h)
+                       int kv_fp8 = 0, const DecodeRope* rope = nullptr);            // caches hold FP8 e4m3 (bfly_kv.h)
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,

@@ -945,3 +945,43 @@ def test_runtime_fills():
     u = torch.zeros(77, dtype=torch.int32, device=DEV)
     torch.ops.bfly.fill32_(u[10:20], -2 ** 31)
     assert u[10:20].tolist() == [-2 ** 31] * 10 and int(u[:10].abs().sum() + u[20:].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("deferred", [True, False])
+@pytest.mark.parametrize("part_tokens", [0, 128])
+@pytest.mark.parametrize("Hq,Hkv", [(64, 8), (32, 8), (16, 2)])
+def test_attn_decode_rope_matches_rope_kv_then_attention(kv_dtype, deferred, part_tokens, Hq, Hkv):
+    """Decode attention with rope_kv folded in (attention.hip ROPE: Q rotated in registers from
+    the QKV GEMM's split-K slabs or bf16 rows, the new token's K / V row stored by the split that
+    reads its page) is bitwise the two-launch path: same output, same cache bytes (a padding row
+    with slot -1 writes nothing; lengths 1 .. 700, one and several context splits)."""
+    D, BS, H = 128, 32, 1024
+    lens = ([1, 31, 32, 100, 700, 5] * 11)[:64]     # 64 rows: the decode batch's split-K plan
+    B = len(lens)
+    N = (Hq + 2 * Hkv) * D
+    max_blocks = (max(lens) + BS - 1) // BS
+    nblk = B * max_blocks + 3
+    kdt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
+    k0, v0 = _bf(nblk, Hkv, BS, D, seed=80).to(kdt), _bf(nblk, Hkv, D, BS, seed=81).to(kdt)
+    tables = torch.randperm(nblk)[: B * max_blocks].view(B, max_blocks).to(torch.int32).to(DEV)
+    ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    pos = ctx - 1
+    slots = torch.stack([tables[b, (lens[b] - 1) // BS] * BS + (lens[b] - 1) % BS for b in range(B)]).to(torch.int32)
+    slots[2] = -1                                    # a graph-padding row
+    cos, sin = ref.rope_tables(D, 4096, 500000.0, device=DEV)
+    x = _bf(B, H, seed=82)
+    w = _bf(N, H, scale=1.0 / math.sqrt(H), seed=83)
+    scale = 1.0 / math.sqrt(D)
+    caches = [(k0.clone(), v0.clone()) for _ in range(2)]
+    qkv = ops.linear(x, w, defer=deferred)
+    if deferred and not isinstance(qkv, ops.Partial):
+        pytest.skip("this plan writes the projection directly")
+    got = ops.attn_decode_rope(qkv, pos, cos, sin, Hq, slots, *caches[0], tables, ctx, scale, max(lens), part_tokens)
+    qkv = ops.linear(x, w, defer=deferred)
+    rows = ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, slots, *caches[1])
+    want = ops.attn_decode(rows[:, : Hq * D].view(B, Hq, D), *caches[1], tables, ctx, scale, max(lens), part_tokens)
+    torch.cuda.synchronize()
+    assert torch.equal(caches[0][0].view(torch.uint8), caches[1][0].view(torch.uint8))
+    assert torch.equal(caches[0][1].view(torch.uint8), caches[1][1].view(torch.uint8))
+    assert torch.equal(got, want)
