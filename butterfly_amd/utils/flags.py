@@ -69,6 +69,8 @@ define("BFLY_GEMM_ROPE_SEAM", False, _bool, "decode-sized QKV projections: RoPE 
        "split-K seam instead of the rope_kv kernel. Off for the same reason (QKV 39.7 vs 37.2 us)")
 define("BFLY_DECODE_FUSED_ROPE", False, _bool, "decode: RoPE on Q and the new token's K plus the paged KV append "
        "done by the attention kernel from the QKV GEMM's deferred output (0: rope_kv + attention)")
+define("BFLY_DECODE_ROPE_OVERLAP", True, _bool, "with BFLY_DECODE_FUSED_ROPE: the attention kernel's page loads "
+       "start before the new K / V row is stored (only the wave loading its page waits; read by the kernel library)")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
 define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "

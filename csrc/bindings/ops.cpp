@@ -728,6 +728,11 @@ void attn_decode_rope(const Tensor& qkv, const c10::optional<Tensor>& partial, c
   }
   rp.k_out = k_cache.data_ptr();
   rp.v_out = v_cache.data_ptr();
+  static const int overlap = [] {   // BFLY_DECODE_ROPE_OVERLAP=0: barrier before the page loop
+    const char* e = getenv("BFLY_DECODE_ROPE_OVERLAP");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  rp.overlap = overlap;
   if (part_tokens <= 0) part_tokens = bfly::attn_decode_part_tokens(B, Hkv, max_ctx);
   const int nsplit = bfly::attn_decode_splits(max_ctx, part_tokens);
   float *po = nullptr, *pml = nullptr;

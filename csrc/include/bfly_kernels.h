@@ -168,6 +168,8 @@ struct DecodeRope {
   const int* slots = nullptr;          // [B], -1 = no cache write
   void* k_out = nullptr;
   void* v_out = nullptr;
+  int overlap = 1;                     // page loads start before the new row is stored (only the
+                                       // last page's load waits); 0: a workgroup barrier first
 };
 int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,

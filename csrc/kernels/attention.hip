@@ -65,6 +65,7 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   const long part_base = ((long)(b * Hkv + h) * nsplit + s);
 
   __shared__ float s_o[4][8][4][64];
+  __shared__ int s_kv_ready;   // ROPE overlap: wave 0 stored the new K / V row
   __shared__ float s_m[4][16], s_l[4][16];
 
   if (tok0 >= tok1) {  // empty split: mark it so the combine skips it
@@ -130,7 +131,12 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
     // the new token's K / V row (position ctx - 1) goes into the cache from the split that
     // reads its page; wave 0, lane l: columns l and l + 64 of the kv head
     const int slot = rp.slots != nullptr ? rp.slots[b] : -1;
-    if (wid == 0 && slot >= 0 && ctx - 1 >= tok0 && ctx - 1 < tok1) {
+    const bool appends = slot >= 0 && ctx - 1 >= tok0 && ctx - 1 < tok1;
+    if (rp.overlap) {
+      if (threadIdx.x == 0) s_kv_ready = appends ? 0 : 1;
+      __syncthreads();
+    }
+    if (wid == 0 && appends) {
       auto col2 = [&](int base, float& x0, float& x1) {
         float v[2];
 #pragma unroll
@@ -159,8 +165,11 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
       KV<CT>::store1(vp + (long)lane * BS, f2bf(v0));
       KV<CT>::store1(vp + (long)(lane + 64) * BS, f2bf(v1));
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stored before any wave loads the page
+      if (rp.overlap && lane == 0) __hip_atomic_store(&s_kv_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __syncthreads();
+    // overlap: only the wave that loads the split's last page (the new token's) waits for the
+    // store, right before that load (load_page); otherwise every wave waits here
+    if (!rp.overlap) __syncthreads();
   } else {
     const int qr = r < G ? r : 0;
     const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D;
@@ -184,6 +193,13 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   // their MFMA, so the prefetched page costs half the VGPRs with an FP8 cache
   typedef typename KV<CT>::raw_t raw_t;
   auto load_page = [&](int p, raw_t (&kf)[2][4], raw_t (&vf)[8]) {
+    if constexpr (ROPE) {
+      if (rp.overlap && p == p1 - 1) {
+        while (__hip_atomic_load(&s_kv_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+          __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+      }
+    }
     const long blk = bt[p];
     const CT* kb = k_cache + ((blk * Hkv + h) * BS) * D;
     const CT* vb = v_cache + (blk * Hkv + h) * (long)D * BS;
