@@ -956,8 +956,8 @@ def test_attn_decode_rope_matches_rope_kv_then_attention(kv_dtype, deferred, par
     the QKV GEMM's split-K slabs or bf16 rows, the new token's K / V row stored by the split that
     reads its page) is bitwise the two-launch path: same output, same cache bytes (a padding row
     with slot -1 writes nothing; lengths 1 .. 700, one and several context splits)."""
-    D, BS, H = 128, 32, 1024
-    lens = ([1, 31, 32, 100, 700, 5] * 11)[:64]     # 64 rows: the decode batch's split-K plan
+    D, BS, H = 128, 32, 8192
+    lens = ([1, 31, 32, 100, 700, 5] * 11)[:64]     # 64 rows x 8192: the 70B decode split-K plan
     B = len(lens)
     N = (Hq + 2 * Hkv) * D
     max_blocks = (max(lens) + BS - 1) // BS
@@ -976,6 +976,7 @@ def test_attn_decode_rope_matches_rope_kv_then_attention(kv_dtype, deferred, par
     caches = [(k0.clone(), v0.clone()) for _ in range(2)]
     qkv = ops.linear(x, w, defer=deferred)
     if deferred and not isinstance(qkv, ops.Partial):
+        assert Hq != 64, "the 70B decode QKV projection must be split-K (deferred slabs)"
         pytest.skip("this plan writes the projection directly")
     got = ops.attn_decode_rope(qkv, pos, cos, sin, Hq, slots, *caches[0], tables, ctx, scale, max(lens), part_tokens)
     qkv = ops.linear(x, w, defer=deferred)
