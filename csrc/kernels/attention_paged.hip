@@ -164,14 +164,33 @@ attn_prefill_paged_kernel(const bf16* __restrict__ q, long q_stride, const CT* _
 
   raw_t kA[2][4], vA[8], kB[2][4], vB[8];
   int p = 0;
-  if (p < npages) load_page(p, kA, vA);
-  while (p < npages) {
+  if constexpr (HPW == 1) {
+    // one head per wave leaves the VGPRs for a third page set: two pages in flight per wave
+    // (the per-wave page stream is latency-bound: one workgroup per CU for a single sequence)
+    raw_t kC[2][4], vC[8];
+    if (p < npages) load_page(p, kA, vA);
     if (p + 1 < npages) load_page(p + 1, kB, vB);
-    compute_page(p, kA, vA);
-    if (++p >= npages) break;
-    if (p + 1 < npages) load_page(p + 1, kA, vA);
-    compute_page(p, kB, vB);
-    ++p;
+    while (p < npages) {
+      if (p + 2 < npages) load_page(p + 2, kC, vC);
+      compute_page(p, kA, vA);
+      if (++p >= npages) break;
+      if (p + 2 < npages) load_page(p + 2, kA, vA);
+      compute_page(p, kB, vB);
+      if (++p >= npages) break;
+      if (p + 2 < npages) load_page(p + 2, kB, vB);
+      compute_page(p, kC, vC);
+      ++p;
+    }
+  } else {
+    if (p < npages) load_page(p, kA, vA);
+    while (p < npages) {
+      if (p + 1 < npages) load_page(p + 1, kB, vB);
+      compute_page(p, kA, vA);
+      if (++p >= npages) break;
+      if (p + 1 < npages) load_page(p + 1, kA, vA);
+      compute_page(p, kB, vB);
+      ++p;
+    }
   }
 #pragma unroll
   for (int c = 0; c < HPW; ++c) {
