@@ -243,7 +243,7 @@ __device__ __forceinline__ int pg_swz_k(int key) {
 }
 template <typename CT>
 __device__ __forceinline__ int pg_swz_v(int d) {
-  if constexpr (sizeof(CT) == 2) return (d >> 2) & 3;                              // 4 chunks per 64-B row
+  if constexpr (sizeof(CT) == 2) return (d >> 1) & 3;                              // 4 chunks per 64-B row
   else return (d >> 3) & 1;                                                        // 2 chunks per 32-B row
 }
 

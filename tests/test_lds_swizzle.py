@@ -65,3 +65,48 @@ def test_tile_gemm_fragment_reads_conflict_free(base, ks):
 def test_prefill_attention_k_reads_conflict_free(kt, ks):
     # S^T = K Q^T on 32x32x16: lane reads K row 32kt + (lane & 31), chunk 2ks + (lane >> 5)
     assert _extra_cycles([pf_off(32 * kt + (lane & 31), 2 * ks + (lane >> 5)) for lane in range(64)]) == 0
+
+
+# paged-prefix prefill attention, LDS-staged kernel (attention_paged.hip): K page image of
+# 256-B (bf16) / 128-B (fp8) rows, V^T page image of 64-B / 32-B rows
+def pg_swz_k(key, fp8):
+    return (((key >> 1) & 1) | (((key >> 3) & 3) << 1)) if fp8 else ((key & 3) | (((key >> 3) & 3) << 2))
+
+
+def pg_k(lane, kt, ds, fp8):
+    g, r = lane >> 4, lane & 15
+    key = 8 * (r >> 2) + 4 * kt + (r & 3)
+    c = (4 * (ds >> 1) + g) if fp8 else (4 * ds + g)
+    return key * (128 if fp8 else 256) + 16 * (c ^ pg_swz_k(key, fp8))
+
+
+def pg_v(lane, dt):                 # bf16: 16 B per lane
+    g, r = lane >> 4, lane & 15
+    d = 16 * dt + r
+    return d * 64 + 16 * (g ^ ((d >> 1) & 3))
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("kt", [0, 1])
+@pytest.mark.parametrize("ds", [0, 1, 2, 3])
+def test_paged_prefill_k_reads_conflict_free(fp8, kt, ds):
+    if fp8 and ds & 1:
+        pytest.skip("an FP8 lane reads sub-steps ds and ds + 1 in one 16-B load")
+    assert _extra_cycles([pg_k(lane, kt, ds, fp8) for lane in range(64)]) == 0
+
+
+@pytest.mark.parametrize("dt", range(8))
+def test_paged_prefill_v_reads_conflict_free(dt):
+    assert _extra_cycles([pg_v(lane, dt) for lane in range(64)]) == 0
+    # the first choice, (d >> 2) & 3, was conflict-free for 16 consecutive lanes but 2-way
+    # under the hardware's lane groups
+    old = [(16 * dt + (lane & 15)) * 64 + 16 * ((lane >> 4) ^ (((16 * dt + (lane & 15)) >> 2) & 3)) for lane in range(64)]
+    assert _extra_cycles(old) == 4
+
+
+def test_paged_prefill_swizzles_are_permutations():
+    for row in range(32):
+        assert sorted(c ^ pg_swz_k(row, False) for c in range(16)) == list(range(16))
+        assert sorted(c ^ pg_swz_k(row, True) for c in range(8)) == list(range(8))
+    for d in range(128):
+        assert sorted(g ^ ((d >> 1) & 3) for g in range(4)) == [0, 1, 2, 3]
