@@ -185,14 +185,32 @@ class Communicator:
         g = self.groups["tp"]
         if g.size not in (2, 4, 8) or not torch.cuda.is_available():
             return False
+        import logging
+
+        from ..utils import flags
         from .custom_allreduce import CustomAllReduce
 
+        log = logging.getLogger("butterfly_amd.comm")
         car = CustomAllReduce(g.ranks, g.rank_in_group, g.pg, max_bytes=max_bytes)
         self.custom_ar = car if car.ok else None
         if not car.ok:
             car.close()
-        else:
-            self._start_poller()
+            return False
+        self._start_poller()
+        if flags.get("BFLY_CUSTOM_AR_AUTOTUNE") and (g.native is not None or dist.get_backend(g.pg) == "nccl"):
+            # route by measurement on this node (IPC kernel vs RCCL per message size)
+            def rccl(t, g=g):
+                if g.native is not None:
+                    return g.native.all_reduce_(t)
+                dist.all_reduce(t, group=g.pg)
+                return t
+
+            tuning = car.autotune(g.pg, rccl)
+            log.info("custom all-reduce routing: %s", tuning)
+            if car.route_bytes <= 0:
+                log.info("custom all-reduce: RCCL is faster at every decode size here; keeping RCCL")
+                car.close()
+                self.custom_ar = None
         return self.custom_ar is not None
 
     def enable_ep_ipc(self, capmax: int, hidden: int, top_k: int) -> bool:

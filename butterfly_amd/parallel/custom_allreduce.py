@@ -51,6 +51,30 @@ def shared_device_refusal(idents: list, what: str) -> str | None:
             "(BFLY_IPC_SHARED_DEVICE=1 allows it for tests)")
 
 
+def choose_routing(sizes: list, times: list) -> tuple:
+    """(route_bytes, two_shot_bytes) from measured times per size (ascending) of [one-shot,
+    two-shot, RCCL] (inf = not available): messages go to the IPC kernel up to the largest size
+    of the prefix of sizes where its faster variant beats RCCL (0: never), and the two-shot
+    variant from the smallest size on which it beats the one-shot one at that and every larger
+    routed size (0: never)."""
+    route = 0
+    for sz, (one, two, rccl) in zip(sizes, times):
+        if min(one, two) <= rccl:
+            route = sz
+        else:
+            break
+    two_from = 0
+    for i in range(len(sizes) - 1, -1, -1):
+        if sizes[i] > route:
+            continue
+        one, two, _ = times[i]
+        if two < one:
+            two_from = sizes[i]
+        else:
+            break
+    return route, two_from
+
+
 class CustomAllReduce:
     def __init__(self, ranks: list, rank_in_group: int, pg, max_bytes: int = 8 << 20,
                  device: torch.device | None = None, two_shot_bytes: int | None = None):
@@ -58,6 +82,8 @@ class CustomAllReduce:
         self.world = len(ranks)
         self.rank = rank_in_group
         self.cap = int(max_bytes)
+        self.route_bytes = self.cap        # largest message routed here (autotune may lower it)
+        self.tuning: dict | None = None
         if two_shot_bytes is None:
             from ..utils import flags
 
@@ -120,7 +146,7 @@ class CustomAllReduce:
             t = t.out
         return (self.ok and t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2
                 and t.is_contiguous() and t.shape[1] % 8 == 0 and t.shape[1] <= 16384
-                and t.numel() * 2 <= self.cap and t.data_ptr() % 16 == 0)
+                and t.numel() * 2 <= self.route_bytes and t.data_ptr() % 16 == 0)
 
     def use_two_shot(self, t: torch.Tensor) -> bool:
         return (self.world >= 4 and 0 < self.two_shot_bytes <= t.numel() * 2
@@ -150,6 +176,50 @@ class CustomAllReduce:
         torch.ops.bfly.custom_all_reduce(t, out, residual, w, float(eps), self.bases, self.rank, self.cap, slabs,
                                          self.use_two_shot(t))
         return out
+
+    def autotune(self, pg, rccl_all_reduce, sizes=(32 << 10, 128 << 10, 512 << 10, 2 << 20, 8 << 20),
+                 iters: int = 20) -> dict:
+        """Route by measurement instead of by fixed thresholds: time this kernel (one-shot and,
+        for groups of 4 / 8, two-shot) against `rccl_all_reduce` at decode-sized messages, take
+        the slowest rank's time per (size, variant) — a MAX all-reduce over the group, so every
+        rank decides the same — and set `route_bytes` / `two_shot_bytes` from it
+        (`choose_routing`). Collective: every rank of the group calls it, in the same order."""
+        dev = self.device
+        inf = float("inf")
+        rows_of = [max(1, sz // (8192 * 2)) for sz in sizes]
+        times = []
+        for rows in rows_of:
+            t = torch.randn(rows, 8192, device=dev).to(torch.bfloat16)
+            fits = rows * 8192 * 2 <= self.cap
+            row = []
+            for fn in ((lambda: self.all_reduce_(t, two_shot=False)) if fits else None,
+                       (lambda: self.all_reduce_(t, two_shot=True)) if fits and self.world >= 4 else None,
+                       lambda: rccl_all_reduce(t)):
+                if fn is None:
+                    row.append(inf)
+                    continue
+                for _ in range(3):
+                    fn()
+                torch.cuda.synchronize(dev)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(iters):
+                    fn()
+                b.record()
+                torch.cuda.synchronize(dev)
+                row.append(a.elapsed_time(b) * 1e3 / iters)
+            times.append(row)
+        T = torch.tensor([[min(v, 1e30) for v in r] for r in times], dtype=torch.float64)
+        T = T.to(dev) if dist.get_backend(pg) == "nccl" else T
+        dist.all_reduce(T, op=dist.ReduceOp.MAX, group=pg)
+        T = T.cpu().tolist()
+        route, two = choose_routing([r * 8192 * 2 for r in rows_of], T)
+        self.route_bytes, self.two_shot_bytes = min(route, self.cap), two
+        self.tuning = {"sizes": [r * 8192 * 2 for r in rows_of], "us": [[round(v, 1) for v in r] for r in T],
+                       "route_bytes": self.route_bytes, "two_shot_bytes": self.two_shot_bytes}
+        if not self._vote(self.error() == 0, pg):      # a flag wait timed out somewhere: RCCL
+            self.route_bytes = 0
+        return self.tuning
 
     def error(self) -> int:
         """Sticky device error word (non-zero after a flag-wait timeout)."""

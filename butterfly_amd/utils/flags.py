@@ -37,6 +37,8 @@ define("BFLY_DISABLE_GRAPHS", False, _bool, "run decode steps eagerly instead of
 define("BFLY_CUSTOM_AR", True, _bool, "use the one-shot IPC all-reduce kernel (self-tested at start-up, "
        "RCCL otherwise) for small TP all-reduces")
 define("BFLY_CUSTOM_AR_MAX_BYTES", 8 << 20, int, "largest all-reduce (bytes) routed to the IPC kernel")
+define("BFLY_CUSTOM_AR_AUTOTUNE", True, _bool, "time the IPC all-reduce (one- / two-shot) against RCCL at start-up "
+       "and route each message size to the faster one (0: the fixed BFLY_CUSTOM_AR_* thresholds)")
 define("BFLY_CUSTOM_AR_2SHOT_BYTES", 512 << 10, int, "IPC all-reduces of at least this many bytes over 4 or 8 "
        "ranks run as reduce-scatter + all-gather (2S/W bytes per link instead of S; 0 = always one-shot)")
 define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0: heuristic plans only; read by the kernel library)")

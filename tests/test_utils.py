@@ -100,3 +100,20 @@ def test_default_failure_runs_abort_hooks_before_exit(monkeypatch):
     monkeypatch.setattr(health.os, "_exit", lambda code: order.append(("exit", code)))
     health._default_failure("test")
     assert order == ["abort", ("exit", 75)]
+
+
+def test_custom_all_reduce_routing_choice():
+    """parallel/custom_allreduce.choose_routing: IPC up to the largest size of the winning
+    prefix, two-shot from the smallest size where it wins through the routed range."""
+    from butterfly_amd.parallel.custom_allreduce import choose_routing
+
+    inf = float("inf")
+    sizes = [32 << 10, 128 << 10, 512 << 10, 2 << 20, 8 << 20]
+    # IPC wins everywhere; two-shot wins from 512 KiB on
+    t = [[5, 7, 20], [8, 9, 24], [20, 15, 35], [60, 40, 70], [200, 120, 150]]
+    assert choose_routing(sizes, t) == (8 << 20, 512 << 10)
+    # RCCL wins from 2 MiB on: route only up to 512 KiB; two-shot never (groups of 2)
+    t = [[5, inf, 20], [8, inf, 24], [20, inf, 35], [80, inf, 70], [300, inf, 150]]
+    assert choose_routing(sizes, t) == (512 << 10, 0)
+    # RCCL faster at the smallest size: never route to IPC
+    assert choose_routing(sizes, [[30, inf, 20]] + t[1:]) == (0, 0)
