@@ -169,6 +169,27 @@ if "--bench" in sys.argv:
                 print(f"custom all-reduce {'two' if two else 'one'}-shot world={world} rows={rows} dim=8192 "
                       f"({rows * 16} KiB): {us:.1f} us/call", flush=True)
 
+# routing by measurement (CustomAllReduce.autotune): collective, group-agreed decision. The
+# reference collective here is gloo over host copies (no RCCL with ranks sharing one GPU), so
+# only the mechanics are checked: every rank ends with the same routing, within the range.
+def _gloo_ar(t):
+    h = t.float().cpu()
+    dist.all_reduce(h)
+    t.copy_(h.to(torch.bfloat16))
+    return t
+
+
+if not fails:
+    tun = car.autotune(dist.group.WORLD, _gloo_ar, iters=3)
+    everyone = [None] * world
+    dist.all_gather_object(everyone, (car.route_bytes, car.two_shot_bytes))
+    if len(set(everyone)) != 1:
+        fails.append(f"autotune decisions differ across ranks: {everyone}")
+    if not (0 <= car.route_bytes <= car.cap and 0 <= car.two_shot_bytes <= max(car.route_bytes, 0) + 1):
+        fails.append(f"autotune out of range: {tun}")
+    if rank == 0:
+        print(f"autotune (shared GPU, gloo reference): {tun}", flush=True)
+
 car.close()
 print(f"rank {rank}: custom all-reduce world={world} -> {'PASS' if not fails else 'FAIL ' + '; '.join(fails)}", flush=True)
 dist.destroy_process_group()
