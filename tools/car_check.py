@@ -179,7 +179,7 @@ def _gloo_ar(t):
     return t
 
 
-if not fails:
+if not fails and world <= 4:      # 8 ranks' grids are not all co-resident on one GPU
     tun = car.autotune(dist.group.WORLD, _gloo_ar, iters=3)
     everyone = [None] * world
     dist.all_gather_object(everyone, (car.route_bytes, car.two_shot_bytes))
