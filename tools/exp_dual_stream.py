@@ -137,6 +137,32 @@ def main():
         res["graph_dual_lag_ms"] = graphed(lambda: dual(True))
     except Exception as e:  # noqa: BLE001
         res["graph_dual_error"] = repr(e)[:200]
+    # two graphs (one per half) replayed on two streams: concurrency that does not depend on
+    # the runtime running one graph's parallel branches together
+    try:
+        single(ha)
+        single(hb)
+        torch.cuda.synchronize()
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga):
+            single(ha)
+        with torch.cuda.graph(gb):
+            single(hb)
+        torch.cuda.synchronize()
+
+        def two_graphs():
+            cur = torch.cuda.current_stream()
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            s_side.wait_event(ev)
+            ga.replay()
+            with torch.cuda.stream(s_side):
+                gb.replay()
+            cur.wait_stream(s_side)
+
+        res["two_graphs_ms"] = timed(two_graphs)
+    except Exception as e:  # noqa: BLE001
+        res["two_graphs_error"] = repr(e)[:200]
     # HBM floor of one layer's weights at 6.3 TB/s
     res["floor_ms_at_6.3TBps"] = round(res["layer_weight_GB"] / 6.3, 4)
     print(json.dumps(res), flush=True)
