@@ -43,13 +43,6 @@ class ForwardBatch:
             return int(self.cu_seqlens.shape[0]) - 1
         return int(self.ctx_lens.shape[0])
 
-    def decode_rows(self, a: int, b: int) -> "ForwardBatch":
-        """Rows [a, b) of a decode batch (views: same tensors, no copies)."""
-        assert not self.is_prefill and self.logits_idx is None
-        return ForwardBatch(self.input_ids[a:b], self.positions[a:b], self.slots[a:b], False,
-                            block_tables=self.block_tables[a:b], ctx_lens=self.ctx_lens[a:b],
-                            max_ctx=self.max_ctx, ep_tokens=min(self.ep_tokens, b - a))
-
     def to(self, device) -> "ForwardBatch":
         mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
         return ForwardBatch(mv(self.input_ids), mv(self.positions), mv(self.slots), self.is_prefill,

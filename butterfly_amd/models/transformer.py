@@ -111,10 +111,6 @@ class TransformerLM:
                                                  cfg.rope_scaling, device=self.device)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.seq_parallel = self.tp > 1 and self.ep == 1 and flags.get("BFLY_SEQ_PARALLEL")
-        # decode batches of >= dual_rows rows run as two half-batches on two streams
-        # (_forward_dual; one rank per model only: no collective inside the halves)
-        self.dual_rows = flags.get("BFLY_DECODE_DUAL_ROWS") if (self.tp == 1 and self.ep == 1) else 0
-        self._side = None
         self.sp_min_tokens = flags.get("BFLY_SEQ_PARALLEL_MIN_TOKENS")
 
     # ------------------------------------------------------------------------------------
@@ -328,9 +324,6 @@ class TransformerLM:
         if (self.seq_parallel and fb.is_prefill and fb.cp is None
                 and fb.num_tokens >= max(self.sp_min_tokens, self.tp)):
             return self._forward_sp(fb, kv_caches, hidden_in)
-        if (self.dual_rows and not fb.is_prefill and self.first and self.last and fb.cp is None
-                and fb.num_tokens >= self.dual_rows and fb.num_tokens % 2 == 0):
-            return self._forward_dual(fb, kv_caches)
         residual = self.embed(fb) if self.first else hidden_in
         if residual is None:
             raise ValueError("non-first pipeline stage needs hidden_in")
@@ -372,49 +365,6 @@ class TransformerLM:
                                consumer=(pre + "gu_w", "silu") if self.cfg.act == "silu" else None)
             delta, partial = self._ffn(pre, x, fb)
         return delta, partial
-
-    def _forward_dual(self, fb: ForwardBatch, kv_caches: Optional[list]) -> torch.Tensor:
-        """Decode as two half-batches on two streams (BFLY_DECODE_DUAL_ROWS; single-stage,
-        tp == 1). The decode step is a chain of ~8 HBM-streaming launches per layer, each with
-        a ramp and a tail in which HBM idles; with the halves' chains on two streams one
-        half's ramp / tail overlaps the other half's steady streaming, and the second reader
-        of a weight panel finds it in L2 / the Infinity Cache (tools/exp_dual_stream.py). Each
-        half has its own kernel workspaces (split-K slabs, attention partials: an arena scope)
-        and writes its own rows of the final normed activations; the LM head runs once over
-        the whole batch after the join. Same math per row as `forward` (the GEMM plans of
-        B/2 rows may split K differently, so logits agree to rounding, not bitwise)."""
-        import contextlib
-
-        B = fb.num_tokens
-        h = B // 2
-        cuda = self.device.type == "cuda"
-        xs = torch.empty(B, self.cfg.hidden_size, dtype=self.dtype, device=self.device)
-        main = torch.cuda.current_stream(self.device) if cuda else None
-        if cuda:
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
-            self._side.wait_stream(main)
-        scope = ops.current_arena_scope()
-        try:
-            for j in range(2):
-                f = fb.decode_rows(j * h, (j + 1) * h)
-                ops.arena_scope(scope if j == 0 else ("dual-half", scope))
-                with (torch.cuda.stream(self._side) if cuda and j == 1 else contextlib.nullcontext()):
-                    residual = self.embed(f)
-                    delta, partial = self._layers(f, kv_caches, residual)
-                    out = xs[j * h:(j + 1) * h]
-                    if delta is None:
-                        out.copy_(self._norm(residual, self.p["final_w"], self.p.get("final_b")))
-                    elif self.cfg.norm == "rms":
-                        ops.rms_norm(ops.run_lazy(delta), self.p["final_w"], self.cfg.norm_eps, out=out,
-                                     residual=residual)
-                    else:
-                        out.copy_(self._add_norm(delta, "final", residual, partial))
-        finally:
-            ops.arena_scope(scope)
-        if cuda:
-            main.wait_stream(self._side)
-        return ops.linear(xs, self.head_weight)
 
     def _attention_block(self, li: int, pre: str, x: torch.Tensor, fb: ForwardBatch,
                          kv_caches: Optional[list]):

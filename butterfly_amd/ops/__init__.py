@@ -117,11 +117,6 @@ def arena_scope(name) -> None:
     _scope.name = name
 
 
-def current_arena_scope():
-    """The workspace scope of this host thread (`arena_scope`)."""
-    return getattr(_scope, "name", None)
-
-
 def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch: int = 0,
                       max_ctx: int = 0, num_kv_heads: int = 0, head_dim: int = 128) -> None:
     """Pre-size every workspace for problems up to the given bounds (call before capture)."""

@@ -73,9 +73,6 @@ define("BFLY_DECODE_FUSED_ROPE", False, _bool, "decode: RoPE on Q and the new to
        "done by the attention kernel from the QKV GEMM's deferred output (0: rope_kv + attention)")
 define("BFLY_DECODE_ROPE_OVERLAP", True, _bool, "with BFLY_DECODE_FUSED_ROPE: the attention kernel's page loads "
        "start before the new K / V row is stored (only the wave loading its page waits; read by the kernel library)")
-define("BFLY_DECODE_DUAL_ROWS", 0, int, "decode batches of at least this many rows (even) run as two half-batches on "
-       "two streams so each half's kernel ramps and tails overlap the other's streaming (single-stage, tp == 1; "
-       "0 = off; tools/exp_dual_stream.py)")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
 define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "

@@ -122,17 +122,3 @@ def test_nan_fault_fails_the_step(monkeypatch):
     eng.step()
     with pytest.raises(RuntimeError, match="non-finite"):
         eng.step()
-
-
-def test_engine_dual_half_batch_decode_matches(monkeypatch):
-    """BFLY_DECODE_DUAL_ROWS: the engine's decode steps of >= 2 rows run as two half-batches
-    (odd batches and prefill as one); greedy tokens equal full recompute."""
-    monkeypatch.setenv("BFLY_DECODE_DUAL_ROWS", "2")
-    cfg = ModelConfig.from_preset("llama-tiny")
-    ecfg = EngineConfig(max_batch=4, max_seq_len=128, kv_cache_tokens=1024, use_graphs=False)
-    eng = LLMEngine(cfg, engine_cfg=ecfg, device="cpu")
-    assert eng.model.dual_rows == 2
-    prompts = [[1, 2, 3], [7, 8, 9, 10, 11, 12], [42], [5, 5, 5, 5], [100, 200]]
-    outs = eng.generate(prompts, SamplingParams(max_tokens=6))
-    for p, o in zip(prompts, outs):
-        assert o == _greedy_reference(eng.model, p, 6)

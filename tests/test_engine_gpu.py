@@ -151,48 +151,3 @@ def test_fp8_kv_decode_logits_close_to_bf16():
         db = make_decode_batch(toks, pos, sl, tables, mb, mb * bs)
         logits[dt] = g.forward(db.to("cuda"), kv)[:, :cfg.vocab_size]
     assert _rel(logits[torch.float8_e4m3fn], logits[torch.bfloat16]) < 0.1
-
-
-def test_dual_half_batch_decode_graph(monkeypatch):
-    """BFLY_DECODE_DUAL_ROWS: decode batches as two half-batches on two streams inside the
-    captured graph; the decode logits stay within rounding of the fp32 reference and greedy
-    generation through graph replay matches the eager one-stream engine's on most tokens
-    (the half-batch GEMMs may split K differently, so exact token equality is not required)."""
-    monkeypatch.setenv("BFLY_DECODE_DUAL_ROWS", "2")
-    cfg, g, c = _pair("llama-small")
-    assert g.dual_rows == 2
-    bs = 32
-    prompts = [[3, 1, 4, 1, 5, 9, 2, 6] * 5, list(range(1, 30)), [7, 7], [2, 4, 6, 8]]
-    tables, slots, nxt = [], [], 0
-    for p in prompts:
-        nb = (len(p) + 8 + bs - 1) // bs
-        tables.append(list(range(nxt, nxt + nb)))
-        nxt += nb
-        slots.append([tables[-1][j // bs] * bs + j % bs for j in range(len(p))])
-    kg = g.allocate_kv_cache(nxt + 1, bs)
-    kc = c.allocate_kv_cache(nxt + 1, bs)
-    fb = make_prefill_batch(prompts, slots)
-    g.forward(fb.to("cuda"), kg)
-    lc = c.forward(fb, kc)
-    V = cfg.vocab_size
-    toks = [int(t) for t in lc[:, :V].argmax(-1)]
-    pos = [len(p) for p in prompts]
-    sl = [tables[i][pos[i] // bs] * bs + pos[i] % bs for i in range(len(prompts))]
-    mb = max(len(t) for t in tables)
-    db = make_decode_batch(toks, pos, sl, tables, mb, mb * bs)
-    dg = g.forward(db.to("cuda"), kg)
-    torch.cuda.synchronize()
-    dc = c.forward(db, kc)
-    assert _rel(dg[:, :V], dc[:, :V]) < 3e-2
-    ecfg = EngineConfig(max_batch=8, max_seq_len=256, kv_cache_tokens=4096, use_graphs=True,
-                        graph_batch_sizes=[4, 8], seed=11)
-    eng = LLMEngine(cfg, engine_cfg=ecfg, device="cuda")
-    gen = [[i + 1, 2 * i + 3, 5] * 7 for i in range(6)]
-    dual = eng.generate(gen, SamplingParams(max_tokens=12, ignore_eos=True))
-    assert 8 in eng.runner.captured_buckets or 4 in eng.runner.captured_buckets
-    monkeypatch.setenv("BFLY_DECODE_DUAL_ROWS", "0")
-    eng1 = LLMEngine(cfg, engine_cfg=EngineConfig(max_batch=8, max_seq_len=256, kv_cache_tokens=4096,
-                                                  use_graphs=False, seed=11), device="cuda")
-    one = eng1.generate(gen, SamplingParams(max_tokens=12, ignore_eos=True))
-    same = sum(a == b for x, y in zip(dual, one) for a, b in zip(x, y))
-    assert same >= 0.8 * sum(len(x) for x in one), (dual, one)

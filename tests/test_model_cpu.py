@@ -104,26 +104,3 @@ def test_paged_prefill_reference_equals_flash_over_the_whole_prompt():
                                  i32(list(range(st, L))), L - st, scale)
     want = ref.attn_prefill(q, k, v, i32([0, L]), L, scale, True)[st:]
     torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-5)
-
-
-def test_dual_half_batch_decode_matches_single(monkeypatch):
-    """BFLY_DECODE_DUAL_ROWS: a decode batch run as two half-batches (two streams on the GPU,
-    in sequence here) gives the logits of the one-batch forward, and writes the same cache."""
-
-    torch.manual_seed(0)
-    for preset in ("llama-tiny", "gpt2-tiny"):
-        cfg = ModelConfig.from_preset(preset)
-        prompts = [[5, 17, 99, 3, 8], [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11], [4, 4, 4], [9, 8, 7, 6]]
-        outs = []
-        for rows in (0, 2):
-            monkeypatch.setenv("BFLY_DECODE_DUAL_ROWS", str(rows))
-            m = build_model(cfg, dtype=torch.float32)
-            m.init_random(seed=1)
-            assert m.dual_rows == rows
-            logits, caches, tables = _prefill_logits(m, prompts)
-            nxt = [int(t) for t in logits.argmax(-1)]
-            dec = _decode(m, caches, tables, nxt, [len(p) for p in prompts])
-            outs.append((dec, [c[0].clone() for c in caches]))
-        torch.testing.assert_close(outs[1][0], outs[0][0], atol=1e-5, rtol=1e-5)
-        for a, b in zip(outs[1][1], outs[0][1]):
-            assert torch.equal(a, b), preset
