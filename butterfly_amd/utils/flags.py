@@ -70,7 +70,9 @@ define("BFLY_GEMM_NORM_SEAM", False, _bool, "with the row-split add+RMSNorm: fol
 define("BFLY_GEMM_ROPE_SEAM", False, _bool, "decode-sized QKV projections: RoPE + paged KV append in the GEMM's "
        "split-K seam instead of the rope_kv kernel. Off for the same reason (QKV 39.7 vs 37.2 us)")
 define("BFLY_DECODE_FUSED_ROPE", False, _bool, "decode: RoPE on Q and the new token's K plus the paged KV append "
-       "done by the attention kernel from the QKV GEMM's deferred output (0: rope_kv + attention)")
+       "done by the attention kernel from the QKV GEMM's deferred output (0: rope_kv + attention). Off: bitwise equal "
+       "but the step is 1.1 % slower (70B: 29.74 vs 29.38-29.53 ms; every attention workgroup rebuilds its Q from "
+       "the slabs, which costs more than the rope_kv launch it removes; profiles/r4_fused_decode_rope_ab.log)")
 define("BFLY_DECODE_ROPE_OVERLAP", True, _bool, "with BFLY_DECODE_FUSED_ROPE: the attention kernel's page loads "
        "start before the new K / V row is stored (only the wave loading its page waits; read by the kernel library)")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "

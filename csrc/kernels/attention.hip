@@ -46,6 +46,9 @@ constexpr float kNegInf = -INFINITY;
 // context split holds the new token rotates its K row and stores K and V into the paged cache,
 // then a barrier, before any wave loads a page. Same sums, roundings and rotation as
 // rope.hip, so the caches are bitwise those of rope_kv + attention; one launch fewer per layer.
+// Measured 1.1 % slower per 70B decode step than rope_kv + attention (29.74 vs 29.38-29.53 ms,
+// profiles/r4_fused_decode_rope_ab.log): 512 workgroups each rebuilding Q from the split-K slabs
+// cost more than the 5.8 us launch removed. Opt-in (BFLY_DECODE_FUSED_ROPE).
 template <int D, int BS, typename CT, bool ROPE = false>
 __global__ void __launch_bounds__(kAttnThreads)
 attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restrict__ k_cache,
