@@ -940,7 +940,56 @@ __device__ __forceinline__ void b8_stage(const bf16* __restrict__ X, long ldx, c
   }
 }
 
-template <bool EARLY>
+// Buffer-descriptor staging (BUF): the tile's A / B rows start at an SGPR base (the descriptor),
+// the K offset and the hi-half row shift (A-hi = A-lo + 64 rows, B-hi = B-lo + 32 rows: the same
+// XOR pattern, since it depends on row bits 1-3 only) ride in the scalar soffset, and each lane
+// keeps 4 constant byte offsets (A / B x its 2 instructions) — no per-lane 64-bit address math
+// per stage, and A rows past M read as zeros (never stored) instead of a clamped re-read.
+struct B8Dma {
+  int a[2], b[2];
+};
+
+__device__ __forceinline__ B8Dma b8_dma_offsets(long ldx, long ldw, int wid, int lane) {
+  B8Dma d;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ra = b8_block(0, 2 * wid + i) * 8 + (lane >> 3);
+    const int rb = b8_block(1, 2 * wid + i) * 8 + (lane >> 3);
+    d.a[i] = (int)((ra * ldx + (((lane & 7) ^ ((ra >> 1) & 7)) * 8)) * 2);
+    d.b[i] = (int)((rb * ldw + (((lane & 7) ^ ((rb >> 1) & 7)) * 8)) * 2);
+  }
+  return d;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t b8_rsrc(const bf16* base, long rows, long ld) {
+  const long bytes = rows * ld * 2;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                           0x00020000);
+}
+
+__device__ __forceinline__ void b8_stage_buf(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, long ldx,
+                                             long ldw, int k0, char* buf, int half, int wid, const B8Dma& d) {
+  const bool isA = half == 0 || half == 3;
+  char* lds = buf + (isA ? 0 : 256 * 128);
+  const int shift = half == 3 ? (int)(64 * ldx * 2) : half == 2 ? (int)(32 * ldw * 2) : 0;
+  const int soff = k0 * 2 + shift;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = b8_block(half, 2 * wid + i);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? ra : rb, (lds_ptr_t)(lds + blk * 1024), 16, isA ? d.a[i] : d.b[i],
+                                             soff, 0, 0);
+  }
+}
+
+// LA (plan mt 2, with EARLY and BUF): the A-lo fragments of K-tile k+1 are read in phase q3 of K-tile k,
+// whose read segment is otherwise empty, instead of in q0 of k+1 beside the B-lo reads. Per
+// K-tile the read segments then hold 4 / 4 / 8 / 8 ds_read_b128 instead of 12 / 4 / 8 / 0, so
+// no window between two barriers carries more than 8 reads of one wave group next to the other
+// group's 16-MFMA segment (12 x 4 waves x 4 LDS cycles + the phase's DMA exceed that segment's
+// 256 cycles). Safety: a counted wait in q2 retires this wave's A-lo / B-lo(k+1) DMA, and the
+// barrier ending q2 of group 0 (= the one starting q2's MFMAs of group 1) is passed by both
+// groups after their q2 waits, before either reads in q3.
+template <bool EARLY, bool LA = false, bool BUF = false>
 __global__ void __launch_bounds__(kB8Threads)
 gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -968,8 +1017,16 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto bufp = [&](int k) -> char* { return smem + (k & 1) * (2 * 256 * 128); };
+  // BUF: descriptors at the tile's first A / B row (SGPRs), 4 per-lane offsets
+  const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);
+  const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
+  B8Dma dma{};
+  if constexpr (BUF) dma = b8_dma_offsets(ldx, ldw, wid, lane);
   auto stage = [&](int k, int half) {
-    b8_stage(X, ldx, W, ldw, m0, M, n0, N, (kt0 + k) * 64, bufp(k), half, wid, lane);
+    if constexpr (BUF)
+      b8_stage_buf(rsa, rsb, ldx, ldw, (kt0 + k) * 64, bufp(k), half, wid, dma);
+    else
+      b8_stage(X, ldx, W, ldw, m0, M, n0, N, (kt0 + k) * 64, bufp(k), half, wid, lane);
   };
   // prologue: all of K-tile 0, then A-lo, B-lo, B-hi of K-tile 1 (the load stream's order)
   stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
@@ -981,6 +1038,13 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   const int ar = wr * 128 + (lane & 15);  // A fragment row of block i: ar + 16 i
   const int bc = wc * 64 + (lane & 15);   // B fragment row (output column) of block j
   bf16x8 a_lo[4][2], a_hi[4][2], b_lo[2][2], b_hi[2][2];
+  auto read_a_lo = [&](const char* As) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
+  };
+  if constexpr (LA) read_a_lo(bufp(0));
   for (int k = 0; k < nk; ++k) {
     const char* As = bufp(k);
     const char* Bs = As + 256 * 128;
@@ -992,10 +1056,7 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     // releases the barrier earlier (guide §5 template: "lgkmcnt(8) retires the reads issued
     // first"). Without EARLY every load segment drains its reads before the barrier.
     if constexpr (EARLY) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
+      if constexpr (!LA) read_a_lo(As);    // LA: read in q3 of the previous K-tile
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1047,6 +1108,12 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) a_hi[i][ks] = lds_frag(As, ar + 64 + 16 * i, ks * 4 + (lane >> 4));
     if (more2) stage(k + 2, 1);
+    if constexpr (LA) {
+      // this wave's A-lo / B-lo(k+1) DMA retired (left in flight: B-hi, A-hi(k+1) and, while
+      // K-tile k+2 exists, A-lo / B-lo(k+2))
+      if (more2) vm_wait<8>();
+      else if (more) vm_wait<4>();
+    }
     if constexpr (!EARLY) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
@@ -1058,7 +1125,14 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
         for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b_hi[j][ks], a_hi[i][ks], acc[4 + i][2 + j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
-    // ---- q3: no reads; DMA B-hi(k+2) (B-hi(k) was read in q1); retire K-tile k+1
+    // ---- q3: no reads (LA: A-lo(k+1)); DMA B-hi(k+2) (B-hi(k) was read in q1); retire K-tile k+1
+    if constexpr (LA) {
+      // a_lo(k) is dead since q1; q3's MFMAs use a_hi / b_lo. Unconditional (past the last
+      // K-tile it reads the other buffer's stale image, never used), and pinned here: under a
+      // branch the scheduler sank the reads behind q3's MFMAs and barrier, i.e. back into q0
+      read_a_lo(bufp(k + 1));
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (more2) stage(k + 2, 2);
     if (more2) vm_wait<6>();   // A-hi(k+1) and older landed; A-lo/B-lo/B-hi(k+2) fly
     else vm_wait<0>();
@@ -1170,12 +1244,20 @@ static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
                         hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true, true, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true, false, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
     attr = true;
   }
   const int tiles = ((M + 255) / 256) * (N / 256);
   dim3 grid(tiles, sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  if (early)
+  if (early == 2)
+    gemm_big8_kernel<true, true, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  else if (early == 3)
+    gemm_big8_kernel<true, false, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  else if (early)
     gemm_big8_kernel<true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
   else
     gemm_big8_kernel<false><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
@@ -1324,7 +1406,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
-    if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, p.mt, stream);   // mt: EARLY
+    if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, p.mt, stream);   // mt: 0 plain, 1 EARLY, 2 EARLY + LA + BUF, 3 EARLY + BUF
   } else if (p.kind == 3) {
     // decode ring GEMM: plan {3, SW (weight ring depth), waves, waves along M, BM, BN, sk}
     if (N % p.bn != 0 || K % kBK != 0 || K / kBK < p.sk * 2) return -1;

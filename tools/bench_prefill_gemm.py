@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Prefill GEMM A/B on the Llama-3-70B projections: gemm_big8_kernel (plan kind 4, 8-phase
-BK 64; big8e = its early-release variant, plan mt = 1, the default) vs torch.matmul (hipBLASLt,
+BK 64; big8e = its early-release variant, plan mt = 1, the default; big8buf = big8e with
+buffer-descriptor staging, mt = 3; big8la = big8buf with the A-lo fragments read one phase ahead,
+mt = 2) vs torch.matmul (hipBLASLt,
 yardstick only; not used by the framework). The round-3 variants that lost (the BK-32 ring
 kernel, three one-wave-per-SIMD kernels) are recorded in profiles/r3_gemm_prefill_pmc.md.
 
@@ -33,20 +35,21 @@ def uni(*shape):
 def check(ws):
     """kind 4 vs the fp32 reference: M tails, split-K, bias and SiLU epilogues."""
     bad = []
-    for kind, M, N, K, epi, sk in [(k,) + c for k in (4,) for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
+    for mt, M, N, K, epi, sk in [(m,) + c for m in (1, 2, 3) for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
                              (1024, 1024, 2048, "silu", 1), (512, 1280, 4096, "none", 4), (777, 512, 1024, "bias", 1),
                              (2048, 2560, 8192, "none", 2)]]:
+        kind = 4
         x = uni(M, K) * 0.5
         w = uni(N, K) * 0.05
         b = uni(N) if epi == "bias" else None
         nout = N // 2 if epi == "silu" else N
         out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
-        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 1, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, mt, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
         want = ref.linear(x.float(), w.float(), b.float() if b is not None else None,
                           "silu" if epi == "silu" else "none")
         err = ((out.float() - want).abs() / (want.abs() + 2e-2)).max().item()
         rel = ((out.float() - want).norm() / want.norm()).item()
-        row = {"kind": kind, "M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
+        row = {"kind": kind, "mt": mt, "M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
         print(json.dumps({"check": row}), flush=True)
         if rel > 1e-2:
             bad.append(row)
@@ -82,6 +85,8 @@ def main():
                 variants["big8e" + sfx] = lambda sk=sk: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 1, 0, 0, 256, 256, sk], e, ws)
             variants.update({
                 "big8": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, 1], e, ws),
+                "big8la": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 2, 0, 0, 256, 256, 1], e, ws),
+                "big8buf": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 3, 0, 0, 256, 256, 1], e, ws),
             })
             if a.variants:
                 keep = a.variants.split(",")
