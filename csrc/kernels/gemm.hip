@@ -1330,7 +1330,9 @@ GemmPlan plan_gemm(int M, int N, int K) {
   if (bucket == 0) return plan_gemm_heuristic(M, N, K);
   for (const TunedPlan& t : kTuned)
     if (t.N == N && t.K == K && t.M == bucket)
-      return GemmPlan{t.kind, t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
+      // the sweep's 8-phase plans (mt 1) run as the lookahead variant (mt 2), +2.4-3.8 % on
+      // every 70B projection at M = 8192 (profiles/r4_gemm_prefill_la.log)
+      return GemmPlan{t.kind, t.kind == 4 && t.mt == 1 ? 2 : t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
   return plan_gemm_heuristic(M, N, K);
 }
 
@@ -1354,12 +1356,13 @@ static GemmPlan plan_gemm_heuristic(int M, int N, int K) {
     return p;
   }
   if (M > 256 && N % 256 == 0 && K % 64 == 0) {
-    // prefill / large batch: 256x256 8-phase tile with early LDS release (gemm_big8_kernel
-    // <EARLY>: 1.36-1.39 PF at M = 8192 on the 70B projections, +2-7 % over the 5-slot ring
-    // kernel; profiles/r3_gemm_prefill_pmc.md); split K only when the tile grid cannot fill
-    // the 256 CUs
+    // prefill / large batch: 256x256 8-phase tile with early LDS release, A-lo fragments read
+    // one phase ahead and buffer-descriptor staging (gemm_big8_kernel<true, true, true>: 1.35-
+    // 1.36 PF at M = 8192 on the 70B projections against 1.30-1.33 for <true> alone on the same
+    // box, profiles/r4_gemm_prefill_la.log); split K only when the tile grid cannot fill the
+    // 256 CUs
     p.kind = 4;
-    p.mt = 1;
+    p.mt = 2;   // EARLY + A-lo lookahead + buffer-descriptor staging
     p.bm = p.bn = 256;
     const int tiles = ((M + 255) / 256) * (N / 256);
     int sk = 1;
