@@ -989,6 +989,9 @@ __device__ __forceinline__ void b8_stage_buf(__amdgpu_buffer_rsrc_t ra, __amdgpu
 // 256 cycles). Safety: a counted wait in q2 retires this wave's A-lo / B-lo(k+1) DMA, and the
 // barrier ending q2 of group 0 (= the one starting q2's MFMAs of group 1) is passed by both
 // groups after their q2 waits, before either reads in q3.
+// Measured and dropped: spreading the 24 reads 6 / 6 / 6 / 6 over the four read segments (A-hi
+// and the next A-lo split across phases, A-lo DMA retired in q1): 0.7-1.5 % slower than LA's
+// 4 / 4 / 8 / 8 (profiles/r4_gemm_prefill_bal.log).
 template <bool EARLY, bool LA = false, bool BUF = false>
 __global__ void __launch_bounds__(kB8Threads)
 gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
@@ -1044,6 +1047,7 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
   };
+
   if constexpr (LA) read_a_lo(bufp(0));
   for (int k = 0; k < nk; ++k) {
     const char* As = bufp(k);

@@ -2,7 +2,7 @@
 """Prefill GEMM A/B on the Llama-3-70B projections: gemm_big8_kernel (plan kind 4, 8-phase
 BK 64; big8e = its early-release variant, plan mt = 1, the default; big8buf = big8e with
 buffer-descriptor staging, mt = 3; big8la = big8buf with the A-lo fragments read one phase ahead,
-mt = 2) vs torch.matmul (hipBLASLt,
+mt = 2, the default) vs torch.matmul (hipBLASLt,
 yardstick only; not used by the framework). The round-3 variants that lost (the BK-32 ring
 kernel, three one-wave-per-SIMD kernels) are recorded in profiles/r3_gemm_prefill_pmc.md.
 
