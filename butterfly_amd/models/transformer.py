@@ -559,7 +559,8 @@ class TransformerLM:
             else:
                 hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
                 ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
-                out = ops.linear(hmid, self.p[pre + "moe_down_w"])
+                # one rank: the split-K reduce goes into the next add+RMSNorm, as for dense FFNs
+                out = ops.linear(hmid, self.p[pre + "moe_down_w"], defer=self.defer_reduce and self.ep == 1)
             if self.ep > 1:
                 return self.comm.reduce_scatter(out, "ep")[:T], False
             return out, self.tp > 1
