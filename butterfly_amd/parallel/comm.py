@@ -147,10 +147,29 @@ class Communicator:
         if group == "tp" and self.custom_ar is not None and self.custom_ar.should_use(t):
             return self.custom_ar.all_reduce_(t)
         t = ops.materialize(t)
+        if self._butterfly_fits(g, t):
+            from .butterfly import butterfly_all_reduce_
+
+            return butterfly_all_reduce_(t, g.ranks, g.pg)
         if g.native is not None:
             return g.native.all_reduce_(t)
         dist.all_reduce(t, group=g.pg)
         return t
+
+    @staticmethod
+    def _butterfly_fits(g: GroupHandle, t: torch.Tensor) -> bool:
+        """The probe routed this message size to the butterfly all-reduce (BFLY_AR_BUTTERFLY),
+        the group is a power of two and no graph is being captured (its point-to-point steps
+        run eagerly)."""
+        from ..utils import flags
+
+        rng = flags.get("BFLY_AR_BUTTERFLY")
+        if not rng or g.size & (g.size - 1) or g.pg is None:
+            return False
+        if t.is_cuda and torch.cuda.is_current_stream_capturing():
+            return False
+        lo, hi = (int(v) for v in rng.split(":"))
+        return lo <= t.numel() * t.element_size() <= hi
 
     def all_reduce_max_(self, t: torch.Tensor, group: str = "tp") -> torch.Tensor:
         """In-place element-wise max over the group (stream-ordered, capturable on RCCL)."""

@@ -7,6 +7,10 @@ all groups of a size running at once — exactly the contention a dp x tp layout
   * RCCL all-reduce over groups of 2, 4, ... world ranks (message sizes 16 KiB .. 32 MiB);
   * the IPC all-reduce kernel (parallel/custom_allreduce.py), one-shot and two-shot, over
     the same group sizes (up to its 8 MiB buffer);
+  * the butterfly all-reduce (parallel/butterfly.py: recursive halving + doubling over
+    point-to-point transfers) over the same power-of-two groups (BFLY_PROBE_BUTTERFLY: its
+    pairwise steps open a point-to-point communicator per rank pair on first use, so it is
+    timed on request, not on every job start);
   * RCCL send/recv between rank pairs (pipeline boundary hops);
   * RCCL all-to-all over the world (EP dispatch).
 Each timing is the median of several back-to-back calls, then the MAX over ranks, so every
@@ -50,7 +54,7 @@ def _groups_of(world: int, n: int) -> list:
 
 
 def probe_comm(world: int, device: Optional[torch.device] = None, iters: int = 8,
-               custom_ar: bool = True) -> dict:
+               custom_ar: bool = True, butterfly: Optional[bool] = None) -> dict:
     """Run the probe (collective); returns {"all_reduce": {impl: {n: [[bytes, s], ...]}},
     "p2p": [[bytes, s], ...], "all_to_all": {n: [[bytes, s], ...]}, "seconds": wall}."""
     if world <= 1 or not dist.is_initialized():
@@ -60,10 +64,14 @@ def probe_comm(world: int, device: Optional[torch.device] = None, iters: int = 8
             return {}
         device = torch.device("cuda", torch.cuda.current_device())
     custom_ar = custom_ar and device.type == "cuda"
+    if butterfly is None:
+        from ..utils import flags
+
+        butterfly = flags.get("BFLY_PROBE_BUTTERFLY")
     t_start = time.perf_counter()
     rank = dist.get_rank()
     sizes_n = [n for n in (2, 4, 8, 16) if n <= world and world % n == 0]
-    ar: dict = {"rccl": {}, "oneshot": {}, "twoshot": {}}
+    ar: dict = {"rccl": {}, "oneshot": {}, "twoshot": {}, "butterfly": {}}
     keys = []          # (kind, impl, n, bytes) in a fixed order on every rank
     vals = []
     for n in sizes_n:
@@ -88,6 +96,14 @@ def probe_comm(world: int, device: Optional[torch.device] = None, iters: int = 8
                     t = torch.ones(rows, 8192, dtype=torch.bfloat16, device=device)
                     vals.append(_time(lambda: car.all_reduce_(t, two_shot=two), iters, device))
             car.close()
+        if butterfly and n & (n - 1) == 0:
+            from .butterfly import butterfly_all_reduce_
+
+            grp = _groups_of(world, n)[rank // n]
+            for nb in AR_SIZES:
+                t = torch.ones(nb // 2, dtype=torch.bfloat16, device=device)
+                keys.append(("ar", "butterfly", n, nb))
+                vals.append(_time(lambda: butterfly_all_reduce_(t, grp, mine), iters, device))
     # pipeline hops: even ranks send to odd ranks (all pairs at once)
     peer = rank ^ 1
     for nb in P2P_SIZES:
@@ -128,7 +144,9 @@ def probe_comm(world: int, device: Optional[torch.device] = None, iters: int = 8
 def ar_policy(table: dict) -> dict:
     """Per group size n: which all-reduce implementation to run by message size, read off the
     measurements: {"twoshot_min": bytes from which two-shot beats one-shot (inf: never),
-    "ipc_max": largest message for which the IPC kernel beats RCCL (0: never)}."""
+    "ipc_max": largest message for which the IPC kernel beats RCCL (0: never),
+    "butterfly": [lo, hi] message sizes on which the butterfly beats whatever else would run
+    (the longest such run of measured sizes; None: never)}."""
     out = {}
     ar = (table or {}).get("all_reduce") or {}
     get = lambda impl, n: {int(b): t for b, t in ((ar.get(impl) or {}).get(n) or (ar.get(impl) or {}).get(str(n)) or [])}  # noqa: E731
@@ -147,7 +165,17 @@ def ar_policy(table: dict) -> dict:
             if ipc is None or (s in rc and rc[s] < ipc):
                 break
             ipc_max = s
-        out[n] = {"twoshot_min": two_min, "ipc_max": ipc_max}
+        bf = get("butterfly", n)
+        run, best = [], []
+        for s in sorted(set(rc) | set(bf)):
+            other = [v for v in (rc.get(s), (two.get(s) if s >= two_min else one.get(s)) if s <= ipc_max else None)
+                     if v is not None]
+            if s in bf and other and bf[s] < min(other):
+                run.append(s)
+                best = run if len(run) > len(best) else best
+            else:
+                run = []
+        out[n] = {"twoshot_min": two_min, "ipc_max": ipc_max, "butterfly": [best[0], best[-1]] if best else None}
     return out
 
 
@@ -165,6 +193,9 @@ def apply_policy(policy: dict, tp: int) -> dict:
     else:
         env["BFLY_CUSTOM_AR_MAX_BYTES"] = str(int(pol["ipc_max"]))
         env["BFLY_CUSTOM_AR_2SHOT_BYTES"] = "0" if pol["twoshot_min"] == float("inf") else str(int(pol["twoshot_min"]))
+    if pol.get("butterfly"):
+        lo, hi = pol["butterfly"]
+        env["BFLY_AR_BUTTERFLY"] = f"{int(lo)}:{int(hi)}"
     os.environ.update(env)
     return env
 

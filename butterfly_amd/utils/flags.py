@@ -39,6 +39,11 @@ define("BFLY_CUSTOM_AR", True, _bool, "use the one-shot IPC all-reduce kernel (s
 define("BFLY_CUSTOM_AR_MAX_BYTES", 8 << 20, int, "largest all-reduce (bytes) routed to the IPC kernel")
 define("BFLY_CUSTOM_AR_AUTOTUNE", True, _bool, "time the IPC all-reduce (one- / two-shot) against RCCL at start-up "
        "and route each message size to the faster one (0: the fixed BFLY_CUSTOM_AR_* thresholds)")
+define("BFLY_AR_BUTTERFLY", "", str, "\"lo:hi\": all-reduces of lo..hi bytes over a power-of-two group run as the butterfly "
+       "(recursive halving + doubling over point-to-point transfers, parallel/butterfly.py), outside graph capture; set by "
+       "the start-up probe only where it measured faster than RCCL and the IPC kernel (empty = never)")
+define("BFLY_PROBE_BUTTERFLY", False, _bool, "the start-up comm probe also times the butterfly all-reduce (and may "
+       "route sizes to it through BFLY_AR_BUTTERFLY)")
 define("BFLY_CUSTOM_AR_2SHOT_BYTES", 512 << 10, int, "IPC all-reduces of at least this many bytes over 4 or 8 "
        "ranks run as reduce-scatter + all-gather (2S/W bytes per link instead of S; 0 = always one-shot)")
 define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0: heuristic plans only; read by the kernel library)")

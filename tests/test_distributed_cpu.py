@@ -138,7 +138,7 @@ def _probe_worker(rank, world):
 
     from butterfly_amd.parallel.probe import ar_policy, probe_comm, summarize
 
-    tab = probe_comm(world, device=torch.device("cpu"), iters=2)
+    tab = probe_comm(world, device=torch.device("cpu"), iters=2, butterfly=True)
     return tab, ar_policy(tab), summarize(tab)
 
 
@@ -157,6 +157,11 @@ def test_comm_probe_plumbing_gloo():
     assert sorted(ar) == [2, 4] and all(len(v) == 6 for v in ar.values())
     assert len(tabs[0]["p2p"]) == 3 and 4 in tabs[0]["all_to_all"]
     assert res[0][1][4]["ipc_max"] == 0            # no IPC kernel on CPU: RCCL-only policy
+    bf = tabs[0]["all_reduce"]["butterfly"]         # the butterfly is timed on every pow2 group
+    assert sorted(bf) == [2, 4] and all(len(v) == 6 for v in bf.values())
+    for n in (2, 4):
+        rng = res[0][1][n]["butterfly"]
+        assert rng is None or (rng[0] <= rng[1] and all(r[1][n]["butterfly"] == rng for r in res))
     cm = CostModel(ModelConfig.from_preset("llama3-8b"), MI355X.with_comm_table(dict(tabs[0], policy=res[0][1])))
     assert cm.allreduce(1 << 20, 4) > 0 and cm.p2p(1 << 20) > 0
 
