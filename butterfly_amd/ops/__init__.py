@@ -108,6 +108,32 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+# Output poisoning (`set_poison`): every op output is allocated filled with NaN
+# (floating point) or a negative sentinel (integers) instead of left uninitialised, so an
+# element a kernel forgot to write shows up in the comparison against the unpoisoned run.
+_POISON = os.environ.get("BFLY_POISON_OUTPUTS", "0").strip().lower() in ("1", "true", "yes", "on")
+
+
+def set_poison(on: bool) -> None:
+    """Allocate op outputs poisoned (debug / tests; costs one fill per output)."""
+    global _POISON
+    _POISON = bool(on)
+
+
+def _poisoned(t: torch.Tensor) -> torch.Tensor:
+    return t.fill_(float("nan") if t.is_floating_point() else -7777777)
+
+
+def _empty(*shape, **kw) -> torch.Tensor:
+    t = torch.empty(*shape, **kw)
+    return _poisoned(t) if _POISON else t
+
+
+def _empty_like(x: torch.Tensor, **kw) -> torch.Tensor:
+    t = torch.empty_like(x, **kw)
+    return _poisoned(t) if _POISON else t
+
+
 _scope = threading.local()
 _arena = _Arena()
 
@@ -232,19 +258,19 @@ def rms_norm(x, w, eps: float, out=None, residual=None, rows: bool = False):
         src = x.slabs if isinstance(x, Partial) else x
         M, dim = src.shape[-2], src.shape[-1]
         if out is None:
-            out = torch.empty(M, dim, dtype=w.dtype, device=w.device)
-        ssp = torch.empty(M, torch.ops.bfly.rms_norm_rows_chunks(dim), dtype=torch.float32, device=w.device)
+            out = _empty(M, dim, dtype=w.dtype, device=w.device)
+        ssp = _empty(M, torch.ops.bfly.rms_norm_rows_chunks(dim), dtype=torch.float32, device=w.device)
         torch.ops.bfly.rms_norm_rows(src, w, out, ssp, residual)
         return RowNormed(out, ssp, eps)
     if isinstance(x, Partial):
         if out is None:
-            out = torch.empty_like(x.out)
+            out = _empty_like(x.out)
         torch.ops.bfly.rms_norm_partial(x.slabs, w, eps, out, residual)
         return out
     if not _gpu(x):
         return ref.rms_norm(x, w, eps, out, residual)
     if out is None:
-        out = torch.empty_like(x)
+        out = _empty_like(x)
     torch.ops.bfly.rms_norm(x, w, eps, out, residual)
     return out
 
@@ -283,7 +309,7 @@ def linear_rope_kv(x, w, positions, cos, sin, n_q: int, n_kv: int, slots=None, k
     need = torch.ops.bfly.gemm_workspace_size(M, N, K)
     ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
     cnt = _arena.get(x.device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
-    qkv = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    qkv = _empty(M, N, dtype=x.dtype, device=x.device)
     rc = torch.ops.bfly.gemm_rope_kv(x, w, ws, qkv, positions, cos, sin, n_q, n_kv, slots if k_cache is not None else None,
                                      k_cache, v_cache, cnt, rn.ssp if rn is not None else None,
                                      rn.eps if rn is not None else 0.0)
@@ -310,8 +336,8 @@ def linear_rmsnorm_rows(x, w, gamma, eps: float, residual) -> Optional[RowNormed
     need = torch.ops.bfly.gemm_workspace_size(M, N, K)
     ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
     cnt = _arena.get(x.device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
-    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
-    ssp = torch.empty(M, N // 128, dtype=torch.float32, device=x.device)
+    y = _empty(M, N, dtype=x.dtype, device=x.device)
+    ssp = _empty(M, N // 128, dtype=torch.float32, device=x.device)
     chunks = torch.ops.bfly.gemm_norm(x, w, ws, residual, gamma, y, ssp, cnt)
     if chunks <= 0:
         return None
@@ -322,7 +348,7 @@ def layer_norm(x, w, b, eps: float, out=None, residual=None):
     if not _gpu(x):
         return ref.layer_norm(x, w, b, eps, out, residual)
     if out is None:
-        out = torch.empty_like(x)
+        out = _empty_like(x)
     torch.ops.bfly.layer_norm(x, w, b, eps, out, residual)
     return out
 
@@ -350,7 +376,7 @@ def silu_mul(gu, out=None, interleave: int = 0):
     if not _gpu(gu):
         return ref.silu_mul(gu, out, interleave)
     if out is None:
-        out = torch.empty(*gu.shape[:-1], gu.shape[-1] // 2, dtype=gu.dtype, device=gu.device)
+        out = _empty(*gu.shape[:-1], gu.shape[-1] // 2, dtype=gu.dtype, device=gu.device)
     torch.ops.bfly.silu_mul(gu, out, interleave)
     return out
 
@@ -359,7 +385,7 @@ def gelu(x, out=None):
     if not _gpu(x):
         return ref.gelu(x, out)
     if out is None:
-        out = torch.empty_like(x)
+        out = _empty_like(x)
     torch.ops.bfly.gelu(x, out)
     return out
 
@@ -369,7 +395,7 @@ def add(a, b, out=None):
     if not _gpu(a):
         return ref.add(a, b, out)
     if out is None:
-        out = torch.empty_like(a)
+        out = _empty_like(a)
     torch.ops.bfly.add(a, b, out)
     return out
 
@@ -378,7 +404,7 @@ def embed(ids, table, vstart: int = 0, out=None):
     if not _gpu(ids):
         return ref.embed(ids, table, vstart, out)
     if out is None:
-        out = torch.empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
+        out = _empty(ids.numel(), table.shape[1], dtype=table.dtype, device=table.device)
     torch.ops.bfly.embed(ids, table, out, vstart)
     return out
 
@@ -388,7 +414,7 @@ def gather_rows(src, idx, out=None):
     keep what `out` holds (pass a pre-filled `out`). Our row-gather kernel on the GPU, not
     torch's index_select (elementwise.hip gather_rows_kernel)."""
     if out is None:
-        out = torch.empty(idx.numel(), *src.shape[1:], dtype=src.dtype, device=src.device)
+        out = _empty(idx.numel(), *src.shape[1:], dtype=src.dtype, device=src.device)
     if not _gpu(src):
         return ref.gather_rows(src, idx, out)
     s2 = src if src.dim() == 2 else src.view(src.shape[0], -1)
@@ -401,7 +427,7 @@ def sample_pack(scores, ids):
     """Per-shard sampling winners -> [rows, 2] f32 (score, id) pairs for the TP all-gather."""
     if not _gpu(scores):
         return ref.sample_pack(scores, ids)
-    pair = torch.empty(scores.numel(), 2, dtype=torch.float32, device=scores.device)
+    pair = _empty(scores.numel(), 2, dtype=torch.float32, device=scores.device)
     torch.ops.bfly.sample_pack(scores.contiguous(), ids.contiguous(), pair)
     return pair
 
@@ -411,7 +437,7 @@ def sample_merge(allp):
     ties: torch.argmax's first maximum)."""
     if not _gpu(allp):
         return ref.sample_merge(allp)
-    out = torch.empty(allp.shape[1], dtype=torch.int32, device=allp.device)
+    out = _empty(allp.shape[1], dtype=torch.int32, device=allp.device)
     torch.ops.bfly.sample_merge(allp.contiguous(), out)
     return out
 
@@ -425,9 +451,9 @@ def sample(logits, temps=None, seeds=None, vstart: int = 0, out_ids=None, out_sc
         return ref.sample(logits, temps, seeds, vstart, thresh, check_finite)
     rows = logits.shape[0]
     if out_ids is None:
-        out_ids = torch.empty(rows, dtype=torch.int32, device=logits.device)
+        out_ids = _empty(rows, dtype=torch.int32, device=logits.device)
     if out_scores is None:
-        out_scores = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        out_scores = _empty(rows, dtype=torch.float32, device=logits.device)
     ws = _arena.get(logits.device, "sample", rows * 64, torch.int64)
     torch.ops.bfly.sample(logits, temps, seeds, vstart, out_ids, out_scores, ws, thresh, check_finite)
     return out_ids, out_scores
@@ -461,7 +487,7 @@ def topkp_threshold(logits, temps, top_k, top_p, reduce_sum=None, reduce_max=Non
             if reduce_sum is not None:
                 reduce_sum(hist)
             L.tkp_select(top_p, ws, R, p, phase)
-    thr = torch.empty(R, dtype=torch.float32, device=logits.device)
+    thr = _empty(R, dtype=torch.float32, device=logits.device)
     L.tkp_final(ws, R, thr)
     return thr
 
@@ -478,7 +504,7 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     if defer and bias is None and epilogue == "none":
         M, N = x.shape[0], w.shape[0]
         if out is None:
-            out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+            out = _empty(M, N, dtype=x.dtype, device=x.device)
         need = torch.ops.bfly.gemm_workspace_size(M, N, x.shape[1])
         ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
         if rn is not None:
@@ -495,7 +521,7 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     M, N = x.shape[0], w.shape[0]
     nout = N // 2 if epilogue == "silu" else N
     if out is None:
-        out = torch.empty(M, nout, dtype=x.dtype, device=x.device)
+        out = _empty(M, nout, dtype=x.dtype, device=x.device)
     need = torch.ops.bfly.gemm_workspace_size(M, N, x.shape[1])
     # zero-initialised once: its head holds the split-K arrival counters, which every GEMM
     # leaves re-armed at zero
@@ -523,8 +549,8 @@ def attn_prefill(q, k, v, cu_seqlens, max_seqlen: int, scale: float, causal: boo
     if not _gpu(q):
         return ref.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out, cu_seqlens_k, return_lse)
     if out is None:
-        out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
-    lse = torch.empty(q.shape[0], q.shape[1], dtype=torch.float32, device=q.device) if return_lse else None
+        out = _empty(q.shape, dtype=q.dtype, device=q.device)
+    lse = _empty(q.shape[0], q.shape[1], dtype=torch.float32, device=q.device) if return_lse else None
     torch.ops.bfly.attn_prefill(q, k, v, cu_seqlens, max_seqlen, scale, causal, out, cu_seqlens_k, lse)
     return (out, lse) if return_lse else out
 
@@ -537,7 +563,7 @@ def attn_prefill_paged(q, k_cache, v_cache, tables, cu_q, positions, max_q: int,
     if not _gpu(q):
         return ref.attn_prefill_paged(q, k_cache, v_cache, tables, cu_q, positions, max_q, scale, out)
     if out is None:
-        out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        out = _empty(q.shape, dtype=q.dtype, device=q.device)
     torch.ops.bfly.attn_prefill_paged(q, k_cache, v_cache, tables, cu_q, positions, int(max_q), float(scale), out)
     return out
 
@@ -565,7 +591,7 @@ def attn_decode_rope(qkv, positions, cos, sin, n_q: int, slots, k_cache, v_cache
         return attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx, part_tokens, out)
     B, Hkv = rows.shape[0], k_cache.shape[1]
     if out is None:
-        out = torch.empty(B, n_q, 128, dtype=rows.dtype, device=rows.device)
+        out = _empty(B, n_q, 128, dtype=rows.dtype, device=rows.device)
     if part_tokens <= 0:
         part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
     ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
@@ -588,7 +614,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_c
     B, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     if out is None:
-        out = torch.empty(B, Hq, D, dtype=q.dtype, device=q.device)
+        out = _empty(B, Hq, D, dtype=q.dtype, device=q.device)
     if part_tokens <= 0:
         part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
     ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
@@ -614,11 +640,11 @@ def moe_route(x, wr, top_k: int, gates=None, topk_ids=None, topk_w=None):
         return ref.moe_route(x, wr, top_k)
     T, E = x.shape[0], wr.shape[0]
     if gates is None:
-        gates = torch.empty(T, E, dtype=torch.float32, device=x.device)
+        gates = _empty(T, E, dtype=torch.float32, device=x.device)
     if topk_ids is None:
-        topk_ids = torch.empty(T, top_k, dtype=torch.int32, device=x.device)
+        topk_ids = _empty(T, top_k, dtype=torch.int32, device=x.device)
     if topk_w is None:
-        topk_w = torch.empty(T, top_k, dtype=torch.float32, device=x.device)
+        topk_w = _empty(T, top_k, dtype=torch.float32, device=x.device)
     torch.ops.bfly.moe_route(x, wr, top_k, gates, topk_ids, topk_w)
     return gates, topk_ids, topk_w
 
@@ -659,9 +685,9 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
     tiles = _arena.get(dev, "moe_tiles", nt * 4, torch.int32)[:nt * 4].view(nt, 4)
     count = _arena.get(dev, "moe_count", 1, torch.int32)[:1]
     L.moe_align(topk_ids, e0, num_local, rows, slot_of, tiles, count, bm, bcnt, bcap)
-    hmid = torch.empty(TK, ffn, dtype=x.dtype, device=dev)
+    hmid = _empty(TK, ffn, dtype=x.dtype, device=dev)
     L.moe_grouped_gemm(x, gu_w, hmid, rows, tiles, count, 2 * ffn * H, 2 * ffn, H, num_local, EPILOGUES["silu"], bm)
-    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    out = _empty(T, H, dtype=x.dtype, device=dev)
     sk = moe_down_splits(exp, num_local, H, ffn, bm)
     if sk > 1:
         # decode-sized expert batches: split K of the down projection over sk workgroups so the
@@ -671,7 +697,7 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
                            EPILOGUES["none"], bm, part)
         L.moe_combine_slabs(part, slot_of, topk_w, out, bcnt, bcap)
         return out
-    y = torch.empty(TK, H, dtype=x.dtype, device=dev)
+    y = _empty(TK, H, dtype=x.dtype, device=dev)
     L.moe_grouped_gemm(hmid, down_w, y, None, tiles, count, ffn, H, ffn, num_local, EPILOGUES["none"], bm)
     L.moe_combine(y, slot_of, topk_w, out, bcnt, bcap)
     return out
@@ -683,9 +709,9 @@ def ep_pack(x, ids, w, slots, experts_per_rank: int, ep: int, cap: int):
         return ref.ep_pack(x, ids, w, slots, experts_per_rank, ep, cap)
     T, H = x.shape
     k = ids.shape[1]
-    send = torch.empty(ep * cap, H, dtype=x.dtype, device=x.device)
-    meta = torch.empty(ep * cap, 2 * k, dtype=torch.float32, device=x.device)
-    slot = torch.empty(T, ep, dtype=torch.int32, device=x.device)
+    send = _empty(ep * cap, H, dtype=x.dtype, device=x.device)
+    meta = _empty(ep * cap, 2 * k, dtype=torch.float32, device=x.device)
+    slot = _empty(T, ep, dtype=torch.int32, device=x.device)
     torch.ops.bfly.ep_pack(x.contiguous(), ids.contiguous(), w.contiguous(), slots, experts_per_rank, ep, cap,
                            send, meta, slot)
     return send, meta, slot
@@ -695,7 +721,7 @@ def ep_combine(back, slot):
     """Sum each token's returned partial outputs (one per rank it was sent to)."""
     if not _gpu(back):
         return ref.ep_combine(back, slot)
-    out = torch.empty(slot.shape[0], back.shape[1], dtype=back.dtype, device=back.device)
+    out = _empty(slot.shape[0], back.shape[1], dtype=back.dtype, device=back.device)
     torch.ops.bfly.ep_combine(back, slot, out)
     return out
 

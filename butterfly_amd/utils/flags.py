@@ -33,6 +33,8 @@ def define(name: str, default, parse, help: str) -> Flag:
     return f
 
 
+define("BFLY_POISON_OUTPUTS", False, _bool, "allocate every op output filled with NaN / a negative sentinel so elements "
+       "a kernel leaves unwritten show up (debug; read at import, ops.set_poison at run time)")
 define("BFLY_DISABLE_GRAPHS", False, _bool, "run decode steps eagerly instead of replaying hipGraphs")
 define("BFLY_CUSTOM_AR", True, _bool, "use the one-shot IPC all-reduce kernel (self-tested at start-up, "
        "RCCL otherwise) for small TP all-reduces")

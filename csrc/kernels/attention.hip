@@ -439,6 +439,14 @@ __device__ __forceinline__ void pf_qk(const char* kb, const bf16x8 (&qf)[8], int
 // index math or scalar mask merging.
 template <bool MASK>
 __device__ __forceinline__ float pf_tile_max(f32x16 (&s)[2], int lim, float scale_log2) {
+  // The v_max3 below are inline asm, and hipcc pads no hazard whose consumer is inside an asm
+  // string: read straight off the accumulators they raced the MFMAs' write-back (8-pass XDL D
+  // -> VALU read needs 12 wait states; cdna_hip_programming.md §5.7 item 2). The row max then
+  // came from stale values on some waves of some launches — finite, rounding-level different
+  // outputs from launch to launch on every unmasked tile. This statement redefines both
+  // accumulators after their last MFMA, with the wait states inside it, so every reader
+  // (the masking select or the asm) comes later.
+  asm volatile("s_nop 15\n\ts_nop 3" : "+v"(s[0]), "+v"(s[1]));
   if (MASK) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)

@@ -151,3 +151,42 @@ def test_fp8_kv_decode_logits_close_to_bf16():
         db = make_decode_batch(toks, pos, sl, tables, mb, mb * bs)
         logits[dt] = g.forward(db.to("cuda"), kv)[:, :cfg.vocab_size]
     assert _rel(logits[torch.float8_e4m3fn], logits[torch.bfloat16]) < 0.1
+
+
+@pytest.mark.parametrize("preset", ["llama-small", "mixtral-tiny"])
+def test_poisoned_outputs_change_nothing(preset):
+    """Output poisoning (ops.set_poison): with every op output allocated as NaN
+    / a negative sentinel, prefill and decode logits are bitwise those of the normal run — no
+    kernel leaves an element of its output unwritten."""
+    from butterfly_amd import ops
+
+    cfg = ModelConfig.from_preset(preset)
+    g = build_model(cfg, device="cuda", dtype=torch.bfloat16)
+    g.init_random(seed=7)
+    bs = 32
+    prompts = [[3, 1, 4, 1, 5, 9, 2, 6] * 9, list(range(1, 40)), [7]]
+    outs = []
+    for poison in (False, True):
+        ops.set_poison(poison)
+        try:
+            tables, slots, nxt = [], [], 0
+            for p in prompts:
+                nb = (len(p) + 8 + bs - 1) // bs
+                tables.append(list(range(nxt, nxt + nb)))
+                nxt += nb
+                slots.append([tables[-1][j // bs] * bs + j % bs for j in range(len(p))])
+            kg = g.allocate_kv_cache(nxt + 1, bs)
+            lg = g.forward(make_prefill_batch(prompts, slots).to("cuda"), kg)
+            toks = [int(t) for t in lg[:, :cfg.vocab_size].argmax(-1)]
+            pos = [len(p) for p in prompts]
+            sl = [tables[i][pos[i] // bs] * bs + pos[i] % bs for i in range(len(prompts))]
+            mb = max(len(t) for t in tables)
+            dg = g.forward(make_decode_batch(toks, pos, sl, tables, mb, mb * bs).to("cuda"), kg)
+            torch.cuda.synchronize()
+            outs.append((lg.clone(), dg.clone()))
+        finally:
+            ops.set_poison(False)
+    V = cfg.vocab_size
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.isfinite(b[:, :V].float()).all()
+        assert torch.equal(a[:, :V], b[:, :V])

@@ -986,3 +986,22 @@ def test_attn_decode_rope_matches_rope_kv_then_attention(kv_dtype, deferred, par
     assert torch.equal(caches[0][0].view(torch.uint8), caches[1][0].view(torch.uint8))
     assert torch.equal(caches[0][1].view(torch.uint8), caches[1][1].view(torch.uint8))
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_attn_prefill_is_deterministic(causal):
+    """Launch-to-launch bit equality of the persistent flash prefill on ragged multi-tile
+    sequences. Regression test for an MFMA -> inline-asm read hazard (the row max read the
+    S accumulators before their write-back on some waves of some launches: finite outputs
+    that differed by rounding from launch to launch on every unmasked tile)."""
+    torch.manual_seed(0)
+    lens = [72, 39, 1, 300, 1030]
+    T, Hq, Hkv = sum(lens), 16, 4
+    q = torch.randn(T, Hq, 128, device="cuda").to(torch.bfloat16)
+    kv = torch.randn(T, 2 * Hkv, 128, device="cuda").to(torch.bfloat16)
+    cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+    outs = [ops.attn_prefill(q, kv[:, :Hkv], kv[:, Hkv:], cu, max(lens), 128 ** -0.5, causal).clone()
+            for _ in range(12)]
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
