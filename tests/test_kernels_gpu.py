@@ -1005,3 +1005,40 @@ def test_attn_prefill_is_deterministic(causal):
     torch.cuda.synchronize()
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
+
+
+def _same_every_launch(fn, n=8):
+    outs = []
+    for _ in range(n):
+        r = fn()
+        outs.append(tuple(t.clone() for t in (r if isinstance(r, tuple) else (r,))))
+    torch.cuda.synchronize()
+    return all(all(torch.equal(a, b) for a, b in zip(o, outs[0])) for o in outs[1:])
+
+
+@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
+def test_hot_kernels_are_deterministic(kv_dtype):
+    """Launch-to-launch bit equality of the other hot kernels (the class of bug the flash
+    prefill hazard was): paged-prefix prefill (register kernel for one sequence, LDS kernel for
+    several), decode attention with and without context splits, split-K decode / prefill GEMMs
+    with the SiLU epilogue, the row-split add+RMSNorm."""
+    scale = 1.0 / math.sqrt(128)
+    q, kc, vc, tables, cu, pos, mq = _paged_chunk_case(8, 2, kv_dtype)
+    assert _same_every_launch(lambda: ops.attn_prefill_paged(q, kc, vc, tables, cu, pos, mq, scale))
+    q1, kc1, vc1, t1, cu1, pos1, mq1 = _paged_chunk_case(64, 8, kv_dtype, seed=60, pre=(700,), chunk=(129,))
+    assert _same_every_launch(lambda: ops.attn_prefill_paged(q1, kc1, vc1, t1, cu1, pos1, mq1, scale))
+    # decode over the same pages: one split and several
+    B = tables.shape[0]
+    ctx = torch.tensor([p + c for p, c in zip((0, 40, 95, 700, 31), (37, 1, 50, 16, 129))], dtype=torch.int32,
+                       device=DEV)
+    qd = _bf(B, 8, 128, seed=71)
+    for part in (0, 64):
+        assert _same_every_launch(lambda: ops.attn_decode(qd, kc, vc, tables, ctx, scale, int(ctx.max()), part))
+    if kv_dtype == "fp8":
+        return
+    for M, N, K, epi in ((64, 2048, 4096, "silu"), (64, 1024, 8192, "none"), (300, 512, 4096, "none"),
+                         (1024, 1024, 2048, "silu")):
+        x, w = _bf(M, K, seed=M + K), _bf(N, K, seed=N) * 0.05
+        assert _same_every_launch(lambda: ops.linear(x, w, epilogue=epi)), (M, N, K, epi)
+    h, g, res = _bf(64, 8192, seed=3), _bf(8192, seed=4), _bf(64, 8192, seed=5)
+    assert _same_every_launch(lambda: ops.rms_norm(h, g, 1e-5, residual=res.clone(), rows=True).y)
