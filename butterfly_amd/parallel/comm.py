@@ -75,6 +75,7 @@ class Communicator:
         self.pp_native_send = None
         self.pp_native_recv = None
         self._send_stream = None
+        self._bf_range = None            # BFLY_AR_BUTTERFLY, parsed on first use
 
     # -- construction ---------------------------------------------------------------------
     @classmethod
@@ -156,19 +157,20 @@ class Communicator:
         dist.all_reduce(t, group=g.pg)
         return t
 
-    @staticmethod
-    def _butterfly_fits(g: GroupHandle, t: torch.Tensor) -> bool:
-        """The probe routed this message size to the butterfly all-reduce (BFLY_AR_BUTTERFLY),
-        the group is a power of two and no graph is being captured (its point-to-point steps
-        run eagerly)."""
-        from ..utils import flags
+    def _butterfly_fits(self, g: GroupHandle, t: torch.Tensor) -> bool:
+        """The probe routed this message size to the butterfly all-reduce (BFLY_AR_BUTTERFLY,
+        read at the first all-reduce: the probe sets it before any), the group is a power of
+        two and no graph is being captured (its point-to-point steps run eagerly)."""
+        if getattr(self, "_bf_range", None) is None:
+            from ..utils import flags
 
-        rng = flags.get("BFLY_AR_BUTTERFLY")
-        if not rng or g.size & (g.size - 1) or g.pg is None:
+            rng = flags.get("BFLY_AR_BUTTERFLY")
+            self._bf_range = tuple(int(v) for v in rng.split(":")) if rng else ()
+        if not self._bf_range or g.size & (g.size - 1) or g.pg is None:
             return False
         if t.is_cuda and torch.cuda.is_current_stream_capturing():
             return False
-        lo, hi = (int(v) for v in rng.split(":"))
+        lo, hi = self._bf_range
         return lo <= t.numel() * t.element_size() <= hi
 
     def all_reduce_max_(self, t: torch.Tensor, group: str = "tp") -> torch.Tensor:
