@@ -393,9 +393,16 @@ constexpr int kPfLPW = 2 * kPfIters;      // LDS-DMA instructions per wave per s
 __device__ __forceinline__ int pf_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 __device__ __forceinline__ int pf_off(int row, int ch) { return row * 256 + 16 * (ch ^ pf_swz(row)); }
 
+// PAD: the first read of an MFMA accumulator — 12 wait states inside the string (8-pass XDL D
+// -> VALU read; hipcc pads no hazard whose consumer is inside an asm string). volatile keeps
+// the later reads of the same accumulator behind it.
+template <bool PAD = false>
 __device__ __forceinline__ float pf_max3(float a, float b, float c) {
   float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  if constexpr (PAD)
+    asm volatile("s_nop 11\n\tv_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  else
+    asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 
@@ -443,10 +450,9 @@ __device__ __forceinline__ float pf_tile_max(f32x16 (&s)[2], int lim, float scal
   // string: read straight off the accumulators they raced the MFMAs' write-back (8-pass XDL D
   // -> VALU read needs 12 wait states; cdna_hip_programming.md §5.7 item 2). The row max then
   // came from stale values on some waves of some launches — finite, rounding-level different
-  // outputs from launch to launch on every unmasked tile. This statement redefines both
-  // accumulators after their last MFMA, with the wait states inside it, so every reader
-  // (the masking select or the asm) comes later.
-  asm volatile("s_nop 15\n\ts_nop 3" : "+v"(s[0]), "+v"(s[1]));
+  // outputs from launch to launch on every unmasked tile. The first read of each accumulator
+  // carries the wait states in its own string (pf_max3<true>); every later read is ordered
+  // behind it (volatile) — no register copies, 2 x 12 states per tile.
   if (MASK) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -458,7 +464,10 @@ __device__ __forceinline__ float pf_tile_max(f32x16 (&s)[2], int lim, float scal
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int kt = c >> 1, r0 = 8 * (c & 1);
-    tc[c] = pf_max3(s[kt][r0], s[kt][r0 + 1], s[kt][r0 + 2]);
+    // c = 0 / 2: the first reads of s[0] / s[1] (padded; the masked path reads the select's
+    // outputs instead, which the compiler padded)
+    tc[c] = (c & 1) ? pf_max3(s[kt][r0], s[kt][r0 + 1], s[kt][r0 + 2])
+                    : pf_max3<!MASK>(s[kt][r0], s[kt][r0 + 1], s[kt][r0 + 2]);
     tc[c] = pf_max3(tc[c], s[kt][r0 + 3], s[kt][r0 + 4]);
     tc[c] = pf_max3(tc[c], s[kt][r0 + 5], s[kt][r0 + 6]);
     tc[c] = pf_max3(tc[c], s[kt][r0 + 7], tc[c]);
