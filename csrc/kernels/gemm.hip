@@ -989,10 +989,13 @@ __device__ __forceinline__ void b8_stage_buf(__amdgpu_buffer_rsrc_t ra, __amdgpu
 // 256 cycles). Safety: a counted wait in q2 retires this wave's A-lo / B-lo(k+1) DMA, and the
 // barrier ending q2 of group 0 (= the one starting q2's MFMAs of group 1) is passed by both
 // groups after their q2 waits, before either reads in q3.
+// LB (plan mt 5, the default, with LA): B-lo(k+1) is read too, right behind q3's MFMAs (b_lo(k)'s
+// last use), so its latency is spent in the closing barrier and q0's read segment instead of
+// after q0's barrier; q0 then reads nothing. +2.2-3.3 % over LA (profiles/r4_gemm_prefill_lb.log).
 // Measured and dropped: spreading the 24 reads 6 / 6 / 6 / 6 over the four read segments (A-hi
 // and the next A-lo split across phases, A-lo DMA retired in q1): 0.7-1.5 % slower than LA's
 // 4 / 4 / 8 / 8 (profiles/r4_gemm_prefill_bal.log).
-template <bool EARLY, bool LA = false, bool BUF = false>
+template <bool EARLY, bool LA = false, bool BUF = false, bool LB = false>
 __global__ void __launch_bounds__(kB8Threads)
 gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -1048,7 +1051,14 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
       for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
   };
 
+  auto read_b_lo = [&](const char* Bs) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b_lo[j][ks] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
+  };
   if constexpr (LA) read_a_lo(bufp(0));
+  if constexpr (LB) read_b_lo(bufp(0) + 256 * 128);
   for (int k = 0; k < nk; ++k) {
     const char* As = bufp(k);
     const char* Bs = As + 256 * 128;
@@ -1061,10 +1071,7 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     // first"). Without EARLY every load segment drains its reads before the barrier.
     if constexpr (EARLY) {
       if constexpr (!LA) read_a_lo(As);    // LA: read in q3 of the previous K-tile
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b_lo[j][ks] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
+      if constexpr (!LB) read_b_lo(Bs);    // LB: read at the end of q3 of the previous K-tile
       if (more) stage(k + 1, 3);
       asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
     } else {
@@ -1149,6 +1156,12 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b_lo[j][ks], a_hi[i][ks], acc[4 + i][j]);
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (LB) {
+      // B-lo(k+1) behind q3's MFMAs, so its latency is spent in the barrier and q0's read
+      // segment instead of after q0's barrier (its DMA retired with LA's q2 wait)
+      read_b_lo(bufp(k + 1) + 256 * 128);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     __builtin_amdgcn_s_barrier();
     (void)more;
   }
@@ -1252,6 +1265,8 @@ static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
                         hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true, false, true>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true, true, true, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
     attr = true;
   }
   const int tiles = ((M + 255) / 256) * (N / 256);
@@ -1259,6 +1274,8 @@ static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
   if (early == 2)
     gemm_big8_kernel<true, true, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  else if (early == 5)
+    gemm_big8_kernel<true, true, true, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
   else if (early == 3)
     gemm_big8_kernel<true, false, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
   else if (early)
@@ -1334,9 +1351,10 @@ GemmPlan plan_gemm(int M, int N, int K) {
   if (bucket == 0) return plan_gemm_heuristic(M, N, K);
   for (const TunedPlan& t : kTuned)
     if (t.N == N && t.K == K && t.M == bucket)
-      // the sweep's 8-phase plans (mt 1) run as the lookahead variant (mt 2), +2.4-3.8 % on
-      // every 70B projection at M = 8192 (profiles/r4_gemm_prefill_la.log)
-      return GemmPlan{t.kind, t.kind == 4 && t.mt == 1 ? 2 : t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
+      // the sweep's 8-phase plans (mt 1) run as the lookahead variant (mt 5: A-lo and B-lo of
+      // the next K-tile read one phase early), +4.6-5.2 % on every 70B projection at M = 8192
+      // (profiles/r4_gemm_prefill_la.log, r4_gemm_prefill_lb.log)
+      return GemmPlan{t.kind, t.kind == 4 && t.mt == 1 ? 5 : t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
   return plan_gemm_heuristic(M, N, K);
 }
 
@@ -1360,13 +1378,13 @@ static GemmPlan plan_gemm_heuristic(int M, int N, int K) {
     return p;
   }
   if (M > 256 && N % 256 == 0 && K % 64 == 0) {
-    // prefill / large batch: 256x256 8-phase tile with early LDS release, A-lo fragments read
-    // one phase ahead and buffer-descriptor staging (gemm_big8_kernel<true, true, true>: 1.35-
-    // 1.36 PF at M = 8192 on the 70B projections against 1.30-1.33 for <true> alone on the same
-    // box, profiles/r4_gemm_prefill_la.log); split K only when the tile grid cannot fill the
-    // 256 CUs
+    // prefill / large batch: 256x256 8-phase tile with early LDS release, A-lo and B-lo
+    // fragments of the next K-tile read one phase early, buffer-descriptor staging
+    // (gemm_big8_kernel<true, true, true, true>: 1.39-1.40 PF at M = 8192 on the 70B
+    // projections against 1.33-1.35 for <true> alone on the same box,
+    // profiles/r4_gemm_prefill_lb.log); split K only when the tile grid cannot fill the 256 CUs
     p.kind = 4;
-    p.mt = 2;   // EARLY + A-lo lookahead + buffer-descriptor staging
+    p.mt = 5;   // EARLY + A-lo / B-lo lookahead + buffer-descriptor staging
     p.bm = p.bn = 256;
     const int tiles = ((M + 255) / 256) * (N / 256);
     int sk = 1;
@@ -1413,7 +1431,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
-    if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, p.mt, stream);   // mt: 0 plain, 1 EARLY, 2 EARLY + LA + BUF, 3 EARLY + BUF
+    if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, p.mt, stream);   // mt: 0 plain, 1 EARLY, 2 EARLY + LA + BUF, 3 EARLY + BUF, 5 EARLY + LA + BUF + LB
   } else if (p.kind == 3) {
     // decode ring GEMM: plan {3, SW (weight ring depth), waves, waves along M, BM, BN, sk}
     if (N % p.bn != 0 || K % kBK != 0 || K / kBK < p.sk * 2) return -1;

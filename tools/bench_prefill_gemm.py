@@ -2,7 +2,7 @@
 """Prefill GEMM A/B on the Llama-3-70B projections: gemm_big8_kernel (plan kind 4, 8-phase
 BK 64; big8e = its early-release variant, plan mt = 1, the default; big8buf = big8e with
 buffer-descriptor staging, mt = 3; big8la = big8buf with the A-lo fragments read one phase ahead,
-mt = 2, the default) vs torch.matmul (hipBLASLt,
+mt = 2; big8lb = big8la with the B-lo fragments read early too, mt = 5, the default) vs torch.matmul (hipBLASLt,
 yardstick only; not used by the framework). The round-3 variants that lost (the BK-32 ring
 kernel, three one-wave-per-SIMD kernels) are recorded in profiles/r3_gemm_prefill_pmc.md.
 
@@ -35,7 +35,7 @@ def uni(*shape):
 def check(ws):
     """kind 4 vs the fp32 reference: M tails, split-K, bias and SiLU epilogues."""
     bad = []
-    for mt, M, N, K, epi, sk in [(m,) + c for m in (1, 2, 3) for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
+    for mt, M, N, K, epi, sk in [(m,) + c for m in (1, 2, 3, 5) for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
                              (1024, 1024, 2048, "silu", 1), (512, 1280, 4096, "none", 4), (777, 512, 1024, "bias", 1),
                              (2048, 2560, 8192, "none", 2)]]:
         kind = 4
@@ -87,6 +87,7 @@ def main():
                 "big8": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, 1], e, ws),
                 "big8la": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 2, 0, 0, 256, 256, 1], e, ws),
                 "big8buf": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 3, 0, 0, 256, 256, 1], e, ws),
+                "big8lb": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 5, 0, 0, 256, 256, 1], e, ws),
             })
             if a.variants:
                 keep = a.variants.split(",")
