@@ -992,6 +992,8 @@ __device__ __forceinline__ void b8_stage_buf(__amdgpu_buffer_rsrc_t ra, __amdgpu
 // LB (plan mt 5, the default, with LA): B-lo(k+1) is read too, right behind q3's MFMAs (b_lo(k)'s
 // last use), so its latency is spent in the closing barrier and q0's read segment instead of
 // after q0's barrier; q0 then reads nothing. +2.2-3.3 % over LA (profiles/r4_gemm_prefill_lb.log).
+// Measured and dropped: A-hi read in q0's then empty read segment instead of q2 (a_hi is free
+// since q3): 1.5-2.8 % below LB (profiles/r4_gemm_prefill_lh.log).
 // Measured and dropped: spreading the 24 reads 6 / 6 / 6 / 6 over the four read segments (A-hi
 // and the next A-lo split across phases, A-lo DMA retired in q1): 0.7-1.5 % slower than LA's
 // 4 / 4 / 8 / 8 (profiles/r4_gemm_prefill_bal.log).
