@@ -93,14 +93,6 @@ class TransformerLM:
         self.rowscale_rows = (flags.get("BFLY_NORM_ROWSCALE_MAX_ROWS")
                               if (self.device.type == "cuda" and cfg.norm == "rms" and self.tp == 1
                                   and not cfg.is_moe and flags.get("BFLY_NORM_ROWSCALE")) else 0)
-        # ... and with the add+RMSNorm folded into the producing O / down GEMM's split-K seam
-        # (ops.linear_rmsnorm_rows): no separate norm launch at all
-        self.norm_seam = bool(self.rowscale_rows) and flags.get("BFLY_GEMM_NORM_SEAM")
-        # RoPE + KV append folded into the decode QKV GEMM's split-K seam (ops.linear_rope_kv)
-        self.rope_seam = (self.defer_qkv and not cfg.bias and flags.get("BFLY_GEMM_ROPE_SEAM"))
-        self.rope_seam_rows = flags.get("BFLY_NORM_ROWSCALE_MAX_ROWS")
-        # decode: RoPE + KV append inside the paged attention kernel (ops.attn_decode_rope)
-        self.decode_rope = flags.get("BFLY_DECODE_FUSED_ROPE") and not self.rope_seam
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
@@ -373,27 +365,15 @@ class TransformerLM:
         T, D = fb.num_tokens, c.head_dim
         kc, vc = kv_caches[li] if kv_caches is not None else (None, None)
         slots = fb.slots if kc is not None else None
-        qkv = None
-        if self.rope_seam and T <= self.rope_seam_rows and fb.cp is None:
-            # one launch: QKV GEMM with RoPE + KV append in its split-K seam
-            qkv = ops.linear_rope_kv(x, self.p[pre + "qkv_w"], fb.positions, self.cos, self.sin, d.hq, d.hkv,
-                                     slots, kc, vc)
-        if qkv is None:
-            # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
-            # when no all-reduce sits in between (tp == 1)
-            qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
-            if (self.decode_rope and not fb.is_prefill and kc is not None and c.pos_emb == "rope"
-                    and self.device.type == "cuda"):
-                # decode: RoPE + KV append inside the attention kernel (one launch fewer)
-                attn = ops.attn_decode_rope(qkv, fb.positions, self.cos, self.sin, d.hq, fb.slots, kc, vc,
-                                            fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx)
-                return self._o_proj(pre, attn, T)
-            if c.pos_emb == "rope":
-                qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
-            elif kc is not None:
-                k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
-                v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
-                ops.kv_append(k3, v3, fb.slots, kc, vc)
+        # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
+        # when no all-reduce sits in between (tp == 1)
+        qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
+        if c.pos_emb == "rope":
+            qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
+        elif kc is not None:
+            k3 = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
+            v3 = qkv[:, (d.hq + d.hkv) * D:].view(T, d.hkv, D)
+            ops.kv_append(k3, v3, fb.slots, kc, vc)
         q = qkv[:, : d.hq * D].view(T, d.hq, D)
         if fb.is_prefill:
             k = qkv[:, d.hq * D:(d.hq + d.hkv) * D].view(T, d.hkv, D)
@@ -418,9 +398,6 @@ class TransformerLM:
     def _o_proj(self, pre: str, attn: torch.Tensor, T: int):
         d, D = self.dims, self.cfg.head_dim
         o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
-        if self.norm_seam and o_b is None and T <= self.rowscale_rows:
-            # issued by the consuming add+RMSNorm (_add_norm), fused into the GEMM's split-K seam
-            return ops.LazyLinear(attn.view(T, d.hq * D), self.p[pre + "o_w"], self.defer_reduce)
         return ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce)
 
     # ------------------------------------------------------------------------------------
@@ -505,12 +482,7 @@ class TransformerLM:
         if consumer is not None and not partial and 0 < residual.shape[0] <= self.rowscale_rows:
             cw = self.p[consumer[0]]
             if ops.rowscale_ok(residual.shape[0], cw.shape[0], cw.shape[1], consumer[1]):
-                if isinstance(t, ops.LazyLinear):
-                    rn = ops.linear_rmsnorm_rows(t.x, t.w, w, self.cfg.norm_eps, residual)
-                    if rn is not None:
-                        return rn
-                return ops.rms_norm(ops.run_lazy(t), w, self.cfg.norm_eps, residual=residual, rows=True)
-        t = ops.run_lazy(t)
+                return ops.rms_norm(t, w, self.cfg.norm_eps, residual=residual, rows=True)
         if partial:
             if self.cfg.norm == "rms":
                 return self.comm.all_reduce_rms_norm_(t, w, self.cfg.norm_eps, residual, "tp")
@@ -566,9 +538,6 @@ class TransformerLM:
             return out, self.tp > 1
         if c.act == "silu":
             hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu")
-            if self.norm_seam and hmid.shape[0] <= self.rowscale_rows:
-                # the next block's add+RMSNorm issues it with the norm in the split-K seam
-                return ops.LazyLinear(hmid, self.p[pre + "down_w"], self.defer_reduce), self.tp > 1
             out = ops.linear(hmid, self.p[pre + "down_w"], defer=self.defer_reduce)
         else:
             hmid = ops.linear(x, self.p[pre + "fc_w"], bias=self.p.get(pre + "fc_b"))

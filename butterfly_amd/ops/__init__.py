@@ -112,6 +112,8 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
 # (floating point) or a negative sentinel (integers) instead of left uninitialised, so an
 # element a kernel forgot to write shows up in the comparison against the unpoisoned run.
 _POISON = os.environ.get("BFLY_POISON_OUTPUTS", "0").strip().lower() in ("1", "true", "yes", "on")
+# Host-side index checks of ops whose kernels cannot raise (BFLY_DEBUG_CHECKS; each costs a sync)
+_DEBUG_CHECKS = os.environ.get("BFLY_DEBUG_CHECKS", "0").strip().lower() in ("1", "true", "yes", "on")
 
 
 def set_poison(on: bool) -> None:
@@ -159,7 +161,6 @@ def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch
                  for b in range(1, max_batch + 1))
         _arena.get(device, "attn_o", max_batch * num_kv_heads * ns * 16 * head_dim, torch.float32)
         _arena.get(device, "attn_ml", max_batch * num_kv_heads * ns * 16 * 2, torch.float32)
-    _arena.get(device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
     _arena.get(device, "sample", max(max_batch, max_tokens, 1) * 64, torch.int64)
     _arena.get(device, "tkp", max(max_batch, max_tokens, 1) * 521, torch.float32)
 
@@ -187,36 +188,7 @@ class Partial:
         return self.out
 
 
-class LazyLinear:
-    """A GEMM `x @ w.T` not issued yet (decode O / down projections): the consuming add+RMSNorm
-    can run it with the norm fused into its split-K seam (`linear_rmsnorm_rows`); anything else
-    `materialize()`s it into a deferred linear (Partial or bf16 tensor)."""
-
-    __slots__ = ("x", "w", "defer")
-
-    def __init__(self, x: torch.Tensor, w: torch.Tensor, defer: bool = True):
-        self.x, self.w, self.defer = x, w, defer
-
-    @property
-    def shape(self):
-        return (self.x.shape[0], self.w.shape[0])
-
-    def materialize(self):
-        return materialize(linear(self.x, self.w, defer=self.defer))
-
-    def run(self):
-        """The GEMM as `linear(..., defer=...)` would return it (a Partial when split-K)."""
-        return linear(self.x, self.w, defer=self.defer)
-
-
-def run_lazy(x):
-    """A LazyLinear issued as its deferred GEMM (Partial / tensor); anything else unchanged."""
-    return x.run() if isinstance(x, LazyLinear) else x
-
-
 def materialize(x):
-    if isinstance(x, LazyLinear):
-        return x.materialize()
     return x.materialize() if isinstance(x, Partial) else x
 
 
@@ -273,75 +245,6 @@ def rms_norm(x, w, eps: float, out=None, residual=None, rows: bool = False):
         out = _empty_like(x)
     torch.ops.bfly.rms_norm(x, w, eps, out, residual)
     return out
-
-
-_norm_seam: dict = {}
-
-
-SEAM_NORM, SEAM_ROPE = 1, 2
-
-
-def norm_seam_ok(M: int, N: int, K: int, mode: int = SEAM_NORM) -> bool:
-    """True if the split-K GEMM plan of this shape can run the seam (SEAM_NORM: fused
-    add+RMSNorm; SEAM_ROPE: RoPE + paged KV append)."""
-    key = (M, N, K, mode)
-    ok = _norm_seam.get(key)
-    if ok is None:
-        ok = load_library() and torch.cuda.is_available() and torch.ops.bfly.gemm_seam_check(M, N, K, mode) > 0
-        _norm_seam[key] = ok
-    return ok
-
-
-def linear_rope_kv(x, w, positions, cos, sin, n_q: int, n_kv: int, slots=None, k_cache=None, v_cache=None):
-    """qkv = x @ w.T with RoPE on the Q / K heads and the paged KV append done in the GEMM's
-    split-K seam (every split rotates its share of its head tile's rows after its siblings
-    arrive, gemm.hip seam_rope): one launch instead of QKV GEMM + rope_kv. `x` may be a
-    RowNormed. Returns the bf16 [M, N] rows, or None when this shape's plan cannot (fallback:
-    linear(defer=True) + rope_kv)."""
-    rn = None
-    if isinstance(x, RowNormed):
-        rn, x = x, x.y
-    if not _gpu(x):
-        return None
-    M, K, N = x.shape[0], x.shape[1], w.shape[0]
-    if not norm_seam_ok(M, N, K, SEAM_ROPE):
-        return None
-    need = torch.ops.bfly.gemm_workspace_size(M, N, K)
-    ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
-    cnt = _arena.get(x.device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
-    qkv = _empty(M, N, dtype=x.dtype, device=x.device)
-    rc = torch.ops.bfly.gemm_rope_kv(x, w, ws, qkv, positions, cos, sin, n_q, n_kv, slots if k_cache is not None else None,
-                                     k_cache, v_cache, cnt, rn.ssp if rn is not None else None,
-                                     rn.eps if rn is not None else 0.0)
-    return qkv if rc > 0 else None
-
-
-def norm_seam_error(device) -> int:
-    """Non-zero once a norm-seam sibling wait timed out on this device (its results are late and
-    may be wrong): the seam's error word, after the arrival counters."""
-    return int(_arena.get(device, "gemm_seam_cnt", 16385, torch.int32, zero=True)[16384].item())
-
-
-def linear_rmsnorm_rows(x, w, gamma, eps: float, residual) -> Optional[RowNormed]:
-    """residual += x @ w.T (bf16, in place); returns the RowNormed of the updated residual
-    (y = residual * gamma, per-128-column sums of squares) for a row-scaling consumer GEMM —
-    ONE kernel: every split-K workgroup of the GEMM reduces its share of its tile's rows after
-    its siblings arrived (gemm.hip seam_norm), so no separate add+RMSNorm launch runs. None
-    when this shape's plan cannot (the caller falls back to GEMM + rms_norm(rows=True))."""
-    if not _gpu(x):
-        return None
-    M, K, N = x.shape[0], x.shape[1], w.shape[0]
-    if not norm_seam_ok(M, N, K, SEAM_NORM):
-        return None
-    need = torch.ops.bfly.gemm_workspace_size(M, N, K)
-    ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True)
-    cnt = _arena.get(x.device, "gemm_seam_cnt", 16385, torch.int32, zero=True)
-    y = _empty(M, N, dtype=x.dtype, device=x.device)
-    ssp = _empty(M, N // 128, dtype=torch.float32, device=x.device)
-    chunks = torch.ops.bfly.gemm_norm(x, w, ws, residual, gamma, y, ssp, cnt)
-    if chunks <= 0:
-        return None
-    return RowNormed(y, ssp, eps)
 
 
 def layer_norm(x, w, b, eps: float, out=None, residual=None):
@@ -419,6 +322,10 @@ def gather_rows(src, idx, out=None):
         return ref.gather_rows(src, idx, out)
     s2 = src if src.dim() == 2 else src.view(src.shape[0], -1)
     o2 = out if out.dim() == 2 else out.view(out.shape[0], -1)
+    if _DEBUG_CHECKS and not torch.cuda.is_current_stream_capturing() and idx.numel():
+        hi = int(idx.max())
+        if hi >= src.shape[0]:
+            raise IndexError(f"gather_rows: index {hi} out of range for {src.shape[0]} source rows")
     torch.ops.bfly.gather_rows(s2, idx, o2)
     return out
 
@@ -536,7 +443,7 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
 def gemm_plan(M: int, N: int, K: int) -> dict:
     load_library()
     k, mt, nt, bm, bn, sk, wk = torch.ops.bfly.gemm_plan(M, N, K)
-    return {"kind": ("skinny", "tile", "big", "dec", "big8")[k], "mt": mt, "nt": nt, "wk": wk, "bm": bm, "bn": bn,
+    return {"kind": ("skinny", "tile", "big", "dec", "big8", "mid8")[k], "mt": mt, "nt": nt, "wk": wk, "bm": bm, "bn": bn,
             "splitk": sk}
 
 
@@ -575,33 +482,6 @@ def attn_lse_merge_(acc_o, acc_lse, o, lse):
         return ref.attn_lse_merge_(acc_o, acc_lse, o, lse)
     torch.ops.bfly.attn_lse_merge(acc_o, acc_lse, o, lse)
     return acc_o, acc_lse
-
-
-def attn_decode_rope(qkv, positions, cos, sin, n_q: int, slots, k_cache, v_cache, block_tables, ctx_lens,
-                     scale: float, max_ctx: int, part_tokens: int = DECODE_PART_TOKENS, out=None):
-    """Decode attention with rope_kv's work inside the kernel (attention.hip, ROPE): `qkv` is
-    the QKV projection's un-rotated output — bf16 rows, or a `Partial` whose split-K slabs the
-    kernel reduces itself; Q is rotated in registers and the new token's K / V row stored into
-    the paged cache at `slots` (the same values as rope_kv + attn_decode, one launch fewer)."""
-    rows, part = (qkv.out, qkv.slabs) if isinstance(qkv, Partial) else (qkv, None)
-    if not _gpu(rows):
-        full = qkv.materialize() if part is not None else rows
-        full = rope_kv(full, positions, cos, sin, n_q, k_cache.shape[1], slots, k_cache, v_cache)
-        q = full[:, : n_q * 128].view(full.shape[0], n_q, 128)
-        return attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale, max_ctx, part_tokens, out)
-    B, Hkv = rows.shape[0], k_cache.shape[1]
-    if out is None:
-        out = _empty(B, n_q, 128, dtype=rows.dtype, device=rows.device)
-    if part_tokens <= 0:
-        part_tokens = torch.ops.bfly.attn_decode_part_tokens(B, Hkv, max_ctx)
-    ns = torch.ops.bfly.attn_decode_splits(max_ctx, part_tokens)
-    po = pml = None
-    if ns > 1:
-        po = _arena.get(rows.device, "attn_o", B * Hkv * ns * 16 * 128, torch.float32)
-        pml = _arena.get(rows.device, "attn_ml", B * Hkv * ns * 16 * 2, torch.float32)
-    torch.ops.bfly.attn_decode_rope(rows, part, positions, cos, sin, slots, n_q, k_cache, v_cache, block_tables,
-                                    ctx_lens, scale, max_ctx, part_tokens, out, po, pml)
-    return out
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale: float, max_ctx: int,

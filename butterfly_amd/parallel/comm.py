@@ -75,7 +75,6 @@ class Communicator:
         self.pp_native_send = None
         self.pp_native_recv = None
         self._send_stream = None
-        self._bf_range = None            # BFLY_AR_BUTTERFLY, parsed on first use
 
     # -- construction ---------------------------------------------------------------------
     @classmethod
@@ -158,19 +157,19 @@ class Communicator:
         return t
 
     def _butterfly_fits(self, g: GroupHandle, t: torch.Tensor) -> bool:
-        """The probe routed this message size to the butterfly all-reduce (BFLY_AR_BUTTERFLY,
-        read at the first all-reduce: the probe sets it before any), the group is a power of
-        two and no graph is being captured (its point-to-point steps run eagerly)."""
-        if getattr(self, "_bf_range", None) is None:
-            from ..utils import flags
-
-            rng = flags.get("BFLY_AR_BUTTERFLY")
-            self._bf_range = tuple(int(v) for v in rng.split(":")) if rng else ()
-        if not self._bf_range or g.size & (g.size - 1) or g.pg is None:
+        """The probe routed this message size, for groups of this size, to the butterfly
+        all-reduce (BFLY_AR_BUTTERFLY), the group is a power of two and no graph is being
+        captured (its point-to-point steps run eagerly). The flag is re-parsed whenever its value
+        changes, so an all-reduce issued before the probe sets it does not switch it off."""
+        ranges = butterfly_ranges()
+        if not ranges or g.size & (g.size - 1) or g.pg is None:
+            return False
+        rng = ranges.get(g.size)
+        if rng is None:
             return False
         if t.is_cuda and torch.cuda.is_current_stream_capturing():
             return False
-        lo, hi = self._bf_range
+        lo, hi = rng
         return lo <= t.numel() * t.element_size() <= hi
 
     def all_reduce_max_(self, t: torch.Tensor, group: str = "tp") -> torch.Tensor:
@@ -601,3 +600,29 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] =
     dist.init_process_group(backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=t), **kwargs)
     return rank, world, local
+
+
+_bf_cache: tuple = ("", {})
+
+
+def butterfly_ranges() -> dict:
+    """BFLY_AR_BUTTERFLY as {group size: (lo, hi) bytes}. Entries "W@lo:hi" separated by ','
+    (what the probe writes: the range it measured for groups of W ranks); a bare "lo:hi"
+    applies to every power-of-two group (manual runs)."""
+    global _bf_cache
+    import os
+
+    raw = os.environ.get("BFLY_AR_BUTTERFLY", "")
+    if raw == _bf_cache[0]:
+        return _bf_cache[1]
+    out: dict = {}
+    for ent in filter(None, (e.strip() for e in raw.split(","))):
+        size, _, rng = ent.rpartition("@")
+        lo, hi = (int(v) for v in rng.split(":"))
+        if size:
+            out[int(size)] = (lo, hi)
+        else:
+            for w in (2, 4, 8, 16, 32, 64):
+                out.setdefault(w, (lo, hi))
+    _bf_cache = (raw, out)
+    return out

@@ -137,8 +137,16 @@ class CustomAllReduce:
             except Exception as e:  # noqa: BLE001
                 log.warning("custom all-reduce: opening a peer buffer failed (%r)", e)
                 local_ok = False
+        self._armed = False
         if self._vote(local_ok, pg):
-            self.ok = self._self_test(pg)
+            from .rccl import health_arm, health_quiet
+
+            with health_quiet() as q:       # a timeout here is a fallback vote, not a failure
+                self.ok = self._self_test(pg)
+                q.failed(not self.ok)
+            if self.ok:
+                health_arm("car")
+                self._armed = True
 
     # ---------------------------------------------------------------------------------------
     def should_use(self, t) -> bool:
@@ -184,12 +192,23 @@ class CustomAllReduce:
         the slowest rank's time per (size, variant) — a MAX all-reduce over the group, so every
         rank decides the same — and set `route_bytes` / `two_shot_bytes` from it
         (`choose_routing`). Collective: every rank of the group calls it, in the same order."""
+        from .rccl import health_quiet
+
+        with health_quiet() as q:
+            tuning = self._autotune(pg, rccl_all_reduce, sizes, iters)
+            q.failed(self.route_bytes == 0)
+        return tuning
+
+    def _autotune(self, pg, rccl_all_reduce, sizes, iters: int) -> dict:
         dev = self.device
         inf = float("inf")
         rows_of = [max(1, sz // (8192 * 2)) for sz in sizes]
         times = []
         for rows in rows_of:
-            t = torch.randn(rows, 8192, device=dev).to(torch.bfloat16)
+            # every call sums W copies in place: small values, restored before each variant, so
+            # the timed data stays finite (W = 8 x 23 calls would overflow bf16 otherwise)
+            src = (torch.randn(rows, 8192, device=dev) * 1e-3).to(torch.bfloat16)
+            t = src.clone()
             fits = rows * 8192 * 2 <= self.cap
             row = []
             for fn in ((lambda: self.all_reduce_(t, two_shot=False)) if fits else None,
@@ -198,6 +217,7 @@ class CustomAllReduce:
                 if fn is None:
                     row.append(inf)
                     continue
+                t.copy_(src)
                 for _ in range(3):
                     fn()
                 torch.cuda.synchronize(dev)
@@ -272,6 +292,11 @@ class CustomAllReduce:
 
     def close(self) -> None:
         L = torch.ops.bfly
+        if getattr(self, "_armed", False):
+            from .rccl import health_arm
+
+            health_arm("car", False)
+            self._armed = False
         for p in self._opened:
             L.car_ipc_close(p)
         self._opened = []

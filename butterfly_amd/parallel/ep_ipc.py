@@ -70,6 +70,7 @@ class EpIpc:
         self._opened: list = []
         self.bases: list = []
         self.ok = False
+        self._armed = False
         handle = None
         try:
             self._ptr = L.car_alloc(self._off["total"])
@@ -111,7 +112,14 @@ class EpIpc:
             self.idv = L.ep_ipc_view(self._ptr, self._off["ids"], rows, self.K, 1, dev)
             self.wv = L.ep_ipc_view(self._ptr, self._off["w"], rows, self.K, 2, dev)
             self.countsv = L.ep_ipc_view(self._ptr, L.ep_ipc_counts_offset(), 1, self.ep, 1, dev).view(self.ep)
-            self.ok = self._self_test(pg)
+            from .rccl import health_arm, health_quiet
+
+            with health_quiet() as q:       # a timeout here is a fallback vote, not a failure
+                self.ok = self._self_test(pg)
+                q.failed(not self.ok)
+            if self.ok:
+                health_arm("ep")
+                self._armed = True
 
     def fits(self, x: torch.Tensor, ids: torch.Tensor, cap: int) -> bool:
         return (self.ok and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] == self.H
@@ -197,6 +205,11 @@ class EpIpc:
 
     def close(self) -> None:
         L = torch.ops.bfly
+        if self._armed:
+            from .rccl import health_arm
+
+            health_arm("ep", False)
+            self._armed = False
         for p in self._opened:
             L.car_ipc_close(p)
         self._opened = []

@@ -195,7 +195,7 @@ def apply_policy(policy: dict, tp: int) -> dict:
         env["BFLY_CUSTOM_AR_2SHOT_BYTES"] = "0" if pol["twoshot_min"] == float("inf") else str(int(pol["twoshot_min"]))
     if pol.get("butterfly"):
         lo, hi = pol["butterfly"]
-        env["BFLY_AR_BUTTERFLY"] = f"{int(lo)}:{int(hi)}"
+        env["BFLY_AR_BUTTERFLY"] = f"{int(tp)}@{int(lo)}:{int(hi)}"   # measured for groups of tp ranks
     os.environ.update(env)
     return env
 

@@ -21,6 +21,7 @@ must be dropped before it is closed (LLMEngine.close orders this).
 """
 from __future__ import annotations
 
+import threading
 from typing import Optional
 
 import torch
@@ -174,22 +175,75 @@ def abort_all() -> int:
     return int(_lib().rccl_abort_all())
 
 
-def async_errors() -> Optional[str]:
-    """None when every live communicator is healthy and no IPC flag wait timed out, else a
-    description of the first failure (the ErrorPoller check). The IPC kernels' timeouts are
-    read from host-mapped health words (plain loads: safe while the stream is stuck)."""
-    lib = _lib()
-    car, ep = (int(v) for v in lib.health_words())
-    if car:
-        return "custom all-reduce peer wait timed out (health word)"
-    if ep:
-        return "EP IPC dispatch peer wait timed out (health word)"
+# ncclResult_t values that mean "no failure": ncclSuccess, and ncclInProgress, which a
+# NON-BLOCKING communicator reports while an operation (a collective's lazy connection setup,
+# a split, a group end) is still being set up in RCCL's background thread
+NCCL_SUCCESS, NCCL_IN_PROGRESS = 0, 7
+HEALTHY_STATES = (NCCL_SUCCESS, NCCL_IN_PROGRESS)
+
+
+# Host-mapped IPC health words (custom all-reduce, EP IPC) are acted on only for IPC paths
+# that went LIVE (passed their self-test and route traffic): a flag-wait timeout inside a
+# self-test, autotune or preflight check is a vote to fall back, not a failure of the job.
+_health_lock = threading.Lock()
+_health_live = {"car": 0, "ep": 0}     # live IPC objects per word
+_health_quiet = 0                      # self-tests / autotunes in progress: words not read
+
+
+def health_arm(word: str, on: bool = True) -> None:
+    """An IPC object of `word` ("car" / "ep") went live (on) or was closed (off)."""
+    with _health_lock:
+        _health_live[word] = max(0, _health_live[word] + (1 if on else -1))
+
+
+class health_quiet:
+    """Context of a collective self-test / autotune: the poller ignores the health words while
+    it runs, and a test that ends in a fallback (`failed(True)` or an exception) clears them."""
+
+    def __init__(self, lib=None):
+        self.lib, self.fallback = lib, False
+
+    def failed(self, fallback: bool = True) -> None:
+        self.fallback = fallback
+
+    def __enter__(self):
+        global _health_quiet
+        with _health_lock:
+            _health_quiet += 1
+        return self
+
+    def __exit__(self, et, ev, tb):
+        global _health_quiet
+        try:
+            if self.fallback or et is not None:
+                (self.lib or _lib()).health_clear()
+        finally:
+            with _health_lock:
+                _health_quiet -= 1
+        return False
+
+
+def async_errors(lib=None) -> Optional[str]:
+    """None when every live communicator is healthy and no live IPC path's flag wait timed out,
+    else a description of the first failure (the ErrorPoller check). The IPC kernels' timeouts
+    are read from host-mapped health words (plain loads: safe while the stream is stuck).
+    `lib`: the op namespace to query (tests pass a stub)."""
+    lib = _lib() if lib is None else lib
+    with _health_lock:
+        watch = _health_quiet == 0
+        live = dict(_health_live)
+    if watch:
+        car, ep = (int(v) for v in lib.health_words())
+        if car and live["car"]:
+            return "custom all-reduce peer wait timed out (health word)"
+        if ep and live["ep"]:
+            return "EP IPC dispatch peer wait timed out (health word)"
     for h in lib.rccl_live():
         try:
             err = int(lib.rccl_async_error(h))
         except RuntimeError:   # released between the listing and the query
             continue
-        if err:
+        if err not in HEALTHY_STATES:
             return f"RCCL communicator {int(h)} async error {err}"
     return None
 

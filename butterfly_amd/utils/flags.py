@@ -35,13 +35,16 @@ def define(name: str, default, parse, help: str) -> Flag:
 
 define("BFLY_POISON_OUTPUTS", False, _bool, "allocate every op output filled with NaN / a negative sentinel so elements "
        "a kernel leaves unwritten show up (debug; read at import, ops.set_poison at run time)")
+define("BFLY_DEBUG_CHECKS", False, _bool, "host-side index checks (one sync each) in ops whose kernels cannot raise, "
+       "e.g. gather_rows (read at import)")
 define("BFLY_DISABLE_GRAPHS", False, _bool, "run decode steps eagerly instead of replaying hipGraphs")
 define("BFLY_CUSTOM_AR", True, _bool, "use the one-shot IPC all-reduce kernel (self-tested at start-up, "
        "RCCL otherwise) for small TP all-reduces")
 define("BFLY_CUSTOM_AR_MAX_BYTES", 8 << 20, int, "largest all-reduce (bytes) routed to the IPC kernel")
 define("BFLY_CUSTOM_AR_AUTOTUNE", True, _bool, "time the IPC all-reduce (one- / two-shot) against RCCL at start-up "
        "and route each message size to the faster one (0: the fixed BFLY_CUSTOM_AR_* thresholds)")
-define("BFLY_AR_BUTTERFLY", "", str, "\"lo:hi\": all-reduces of lo..hi bytes over a power-of-two group run as the butterfly "
+define("BFLY_AR_BUTTERFLY", "", str, "\"W@lo:hi[,...]\": all-reduces of lo..hi bytes over a group of W ranks (bare "
+       "\"lo:hi\": any power-of-two group) run as the butterfly "
        "(recursive halving + doubling over point-to-point transfers, parallel/butterfly.py), outside graph capture; set by "
        "the start-up probe only where it measured faster than RCCL and the IPC kernel (empty = never)")
 define("BFLY_PROBE_BUTTERFLY", False, _bool, "the start-up comm probe also times the butterfly all-reduce (and may "
@@ -59,10 +62,6 @@ define("BFLY_ATTN_TRACE", "", str, "set: the prefill attention kernel stamps its
 define("BFLY_KERNEL_LIB", "", str, "path of another build of the kernel library (same-box A/B runs of kernel changes)")
 define("BFLY_LOG_JSON", False, _bool, "emit log records as one JSON object per line")
 define("BFLY_RESTART", 0, int, "restart attempt of this job (set by `launch --max-restarts`; 0 = first run)")
-define("BFLY_SEAM_XCD", True, _bool, "GEMM seams (BFLY_GEMM_*_SEAM): place a tile's split-K workgroups on one XCD "
-       "(read by the kernel library)")
-define("BFLY_SEAM_PROBE", 0, int, "timing experiments only (tools/seam_bench.py): 1 skips the seam's sibling wait, "
-       "2 its reduce, 3 both — results are WRONG when set (read by the kernel library)")
 define("BFLY_ATTN_PAGED_LDS", True, _bool, "paged-prefix prefill attention: the LDS-staged kernel for chunks of "
        "several sequences (0: the register kernel everywhere; read by the kernel library)")
 define("BFLY_DEFER_REDUCE", True, _bool, "fuse split-K GEMM reduces into the consuming rope / add+rmsnorm kernels")
@@ -70,18 +69,6 @@ define("BFLY_NORM_ROWSCALE", True, _bool, "decode add+RMSNorm split over (row, 1
        "and partial sums of squares; the consuming QKV / gate-up GEMM applies the 1/rms row scale in its epilogue "
        "(tp == 1, batches <= BFLY_NORM_ROWSCALE_MAX_ROWS; 0: one-workgroup-per-row add+RMSNorm)")
 define("BFLY_NORM_ROWSCALE_MAX_ROWS", 256, int, "largest batch that takes the row-split add+RMSNorm")
-define("BFLY_GEMM_NORM_SEAM", False, _bool, "with the row-split add+RMSNorm: fold it into the producing O / down "
-       "GEMM's split-K seam (every split reduces its share of its tile's rows after its siblings arrive). Off: "
-       "at decode sizes the in-launch hand-off (drain, counter, poll) costs more than the launch it removes "
-       "(70B: 30.98 vs 29.41 ms per step, profiles/r4_seams/README.md)")
-define("BFLY_GEMM_ROPE_SEAM", False, _bool, "decode-sized QKV projections: RoPE + paged KV append in the GEMM's "
-       "split-K seam instead of the rope_kv kernel. Off for the same reason (QKV 39.7 vs 37.2 us)")
-define("BFLY_DECODE_FUSED_ROPE", False, _bool, "decode: RoPE on Q and the new token's K plus the paged KV append "
-       "done by the attention kernel from the QKV GEMM's deferred output (0: rope_kv + attention). Off: bitwise equal "
-       "but the step is 1.1 % slower (70B: 29.74 vs 29.38-29.53 ms; every attention workgroup rebuilds its Q from "
-       "the slabs, which costs more than the rope_kv launch it removes; profiles/r4_fused_decode_rope_ab.log)")
-define("BFLY_DECODE_ROPE_OVERLAP", True, _bool, "with BFLY_DECODE_FUSED_ROPE: the attention kernel's page loads "
-       "start before the new K / V row is stored (only the wave loading its page waits; read by the kernel library)")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
 define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "

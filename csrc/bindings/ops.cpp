@@ -470,94 +470,6 @@ void gemm_rs(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<
   TORCH_CHECK(rc == 0, "gemm_rs: unsupported plan M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
 }
 
-// Split-K GEMM with the fused add + RMSNorm seam (gemm.hip seam_norm): y = (residual + x.W^T) *
-// gamma (bf16), residual updated in place, ssp [M, chunks] row sums of squares per 128-column
-// tile. Returns chunks (> 0) or <= 0 when the shape's plan cannot run the seam (nothing ran).
-static bfly::Seam seam_base(Tensor& counters) {
-  CHECK_I32(counters);
-  TORCH_CHECK(counters.is_contiguous() && counters.numel() > 16384, "gemm seam: counters [16385]");
-  bfly::Seam s = bfly::no_seam();
-  s.counters = counters.data_ptr<int>();
-  s.err = reinterpret_cast<uint32_t*>(counters.data_ptr<int>() + 16384);   // error word
-  return s;
-}
-
-int64_t gemm_norm(const Tensor& x, const Tensor& w, Tensor& workspace, Tensor& residual, const Tensor& gamma,
-                  Tensor& y, Tensor& ssp, Tensor& counters) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(residual); CHECK_BF16(gamma); CHECK_BF16(y);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "gemm_norm: 2-D operands");
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 128 == 0, "gemm_norm: shape");
-  TORCH_CHECK(x.stride(0) % 8 == 0 && x.stride(1) == 1 && w.stride(0) % 8 == 0 && w.stride(1) == 1,
-              "gemm_norm: row strides % 8");
-  TORCH_CHECK(residual.is_contiguous() && residual.size(0) == M && residual.size(1) == N, "gemm_norm: residual");
-  TORCH_CHECK(y.is_contiguous() && y.size(0) == M && y.size(1) == N, "gemm_norm: y");
-  TORCH_CHECK(gamma.is_contiguous() && gamma.numel() == N, "gemm_norm: gamma");
-  TORCH_CHECK(ssp.scalar_type() == at::kFloat && ssp.is_contiguous() && ssp.dim() == 2 && ssp.size(0) == M &&
-                  ssp.size(1) == N / 128, "gemm_norm: ssp [M, N / 128] f32");
-  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_contiguous(), "gemm_norm: workspace");
-  bfly::Seam seam = seam_base(counters);
-  seam.mode = bfly::kSeamNorm;
-  seam.residual = bf(residual);
-  seam.gamma = bf(gamma);
-  seam.y = bf(y);
-  seam.ssp = ssp.data_ptr<float>();
-  c10::DeviceGuard g(x.device());
-  return bfly::launch_gemm_seam(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, workspace.data_ptr<float>(),
-                                workspace.numel() * sizeof(float), seam, cur_stream(), false);
-}
-
-// Split-K QKV GEMM with RoPE + paged KV append in its seam (gemm.hip seam_rope): writes the
-// bf16 rotated row into `qkv` and K / V into the caches. `ssp` / `eps`: the input is a
-// RowNormed (RMSNorm row scale applied in the GEMM). Returns > 0, or <= 0 (nothing ran).
-int64_t gemm_rope_kv(const Tensor& x, const Tensor& w, Tensor& workspace, Tensor& qkv, const Tensor& positions,
-                     const Tensor& cos_t, const Tensor& sin_t, int64_t hq, int64_t hkv,
-                     const c10::optional<Tensor>& slots, const c10::optional<Tensor>& k_cache,
-                     const c10::optional<Tensor>& v_cache, Tensor& counters, const c10::optional<Tensor>& ssp,
-                     double eps) {
-  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(qkv); CHECK_I32(positions);
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && w.dim() == 2 && w.stride(1) == 1 &&
-                  w.stride(0) % 8 == 0 && w.size(1) == K && K % 64 == 0, "gemm_rope_kv: operands");
-  TORCH_CHECK(N == (hq + 2 * hkv) * 128, "gemm_rope_kv: N = (hq + 2 hkv) * 128");
-  TORCH_CHECK(qkv.is_contiguous() && qkv.size(0) == M && qkv.size(1) == N, "gemm_rope_kv: qkv");
-  TORCH_CHECK(positions.numel() >= M, "gemm_rope_kv: positions");
-  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.size(1) == 64 &&
-                  cos_t.is_contiguous() && sin_t.is_contiguous(), "gemm_rope_kv: cos / sin [max_pos, 64] f32");
-  bfly::Seam seam = seam_base(counters);
-  seam.mode = bfly::kSeamRope;
-  seam.qkv = bf(qkv);
-  seam.positions = positions.data_ptr<int>();
-  seam.cos_t = cos_t.data_ptr<float>();
-  seam.sin_t = sin_t.data_ptr<float>();
-  seam.hq = (int)hq;
-  seam.hkv = (int)hkv;
-  seam.block_size = 1;
-  if (slots.has_value() && k_cache.has_value() && v_cache.has_value()) {
-    CHECK_I32(*slots); CHECK_KV(*k_cache, *v_cache);
-    TORCH_CHECK(slots->numel() >= M && k_cache->is_contiguous() && v_cache->is_contiguous() &&
-                    k_cache->size(1) == hkv && k_cache->size(3) == 128, "gemm_rope_kv: caches");
-    seam.slots = slots->data_ptr<int>();
-    seam.k_cache = k_cache->data_ptr();
-    seam.v_cache = v_cache->data_ptr();
-    seam.block_size = (int)k_cache->size(2);
-    seam.kv_fp8 = k_cache->scalar_type() == at::kFloat8_e4m3fn;
-  }
-  TORCH_CHECK(workspace.scalar_type() == at::kFloat && workspace.is_contiguous(), "gemm_rope_kv: workspace");
-  c10::DeviceGuard g(x.device());
-  bfly::RowScale rs{nullptr, 0, 0.f, 0.f};
-  if (ssp.has_value()) rs = row_scale(*ssp, eps, M, K);
-  return bfly::launch_gemm_seam(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, workspace.data_ptr<float>(),
-                                workspace.numel() * sizeof(float), seam, cur_stream(), false,
-                                ssp.has_value() ? &rs : nullptr);
-}
-
-int64_t gemm_seam_check(int64_t M, int64_t N, int64_t K, int64_t mode) {
-  bfly::Seam seam = bfly::no_seam();
-  seam.mode = (int)mode;
-  return bfly::launch_gemm_seam(nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, nullptr, 0, seam, nullptr, true);
-}
-
 int64_t gemm_deferred_rs(const Tensor& x, const Tensor& w, Tensor& out, Tensor& workspace, const Tensor& ssp,
                          double eps) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
@@ -681,75 +593,6 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                                           max_ctx, part_tokens, bf(out), po, pml, cur_stream(),
                                           k_cache.scalar_type() == at::kFloat8_e4m3fn);
   TORCH_CHECK(rc == 0, "attn_decode: unsupported configuration (rc=", rc, ")");
-}
-
-// Decode attention with rope_kv folded in: `qkv` [B, (Hq + 2 Hkv) D] is the QKV projection's
-// un-rotated output (bf16 rows, or with `partial` its f32 split-K slabs [sk, B, N]); Q is rotated
-// in-kernel and the new token's K / V row written into the caches at `slots` (-1: none).
-void attn_decode_rope(const Tensor& qkv, const c10::optional<Tensor>& partial, const Tensor& positions,
-                      const Tensor& cos_t, const Tensor& sin_t, const c10::optional<Tensor>& slots,
-                      int64_t num_q_heads, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
-                      const Tensor& ctx_lens, double scale, int64_t max_ctx, int64_t part_tokens, Tensor& out,
-                      const c10::optional<Tensor>& part_o, const c10::optional<Tensor>& part_ml) {
-  CHECK_GPU(qkv); CHECK_BF16(qkv); CHECK_KV(k_cache, v_cache); CHECK_BF16(out);
-  TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous(), "attn_decode_rope: qkv [B, N]");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous(), "attn_decode_rope: caches");
-  const int B = qkv.size(0), Hq = num_q_heads, Hkv = k_cache.size(1), BS = k_cache.size(2), D = k_cache.size(3);
-  const int N = (Hq + 2 * Hkv) * D;
-  TORCH_CHECK(D == 128 && qkv.size(1) == N, "attn_decode_rope: qkv row must be (Hq + 2 Hkv) x 128");
-  TORCH_CHECK(v_cache.size(2) == D && v_cache.size(3) == BS, "attn_decode_rope: cache dims");
-  TORCH_CHECK(out.is_contiguous() && out.numel() == (long)B * Hq * D, "attn_decode_rope: out");
-  CHECK_I32(block_tables); CHECK_I32(ctx_lens); CHECK_I32(positions);
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.stride(1) == 1,
-              "attn_decode_rope: block_tables");
-  TORCH_CHECK(ctx_lens.numel() >= B && positions.numel() >= B, "attn_decode_rope: ctx_lens / positions");
-  TORCH_CHECK((long)block_tables.size(1) * BS >= max_ctx, "attn_decode_rope: block table too narrow for max_ctx");
-  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
-                  sin_t.is_contiguous() && cos_t.size(-1) == D / 2 && sin_t.sizes() == cos_t.sizes(),
-              "attn_decode_rope: f32 tables [max_pos, D/2]");
-  bfly::DecodeRope rp;
-  rp.qkv = bf(qkv);
-  rp.N = N;
-  if (partial.has_value()) {
-    TORCH_CHECK(partial->scalar_type() == at::kFloat && partial->is_contiguous() && partial->dim() == 3 &&
-                    partial->size(1) == B && partial->size(2) == N,
-                "attn_decode_rope: partial must be [sk, B, N] f32");
-    rp.part = partial->data_ptr<float>();
-    rp.sk = partial->size(0);
-    rp.slab = (long)B * N;
-  }
-  rp.positions = positions.data_ptr<int>();
-  rp.cos_t = cos_t.data_ptr<float>();
-  rp.sin_t = sin_t.data_ptr<float>();
-  if (slots.has_value()) {
-    CHECK_I32(*slots);
-    TORCH_CHECK(slots->numel() >= B, "attn_decode_rope: slots");
-    rp.slots = slots->data_ptr<int>();
-  }
-  rp.k_out = k_cache.data_ptr();
-  rp.v_out = v_cache.data_ptr();
-  static const int overlap = [] {   // BFLY_DECODE_ROPE_OVERLAP=0: barrier before the page loop
-    const char* e = getenv("BFLY_DECODE_ROPE_OVERLAP");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  rp.overlap = overlap;
-  if (part_tokens <= 0) part_tokens = bfly::attn_decode_part_tokens(B, Hkv, max_ctx);
-  const int nsplit = bfly::attn_decode_splits(max_ctx, part_tokens);
-  float *po = nullptr, *pml = nullptr;
-  if (nsplit > 1) {
-    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "attn_decode_rope: partial buffers required");
-    TORCH_CHECK(part_o->numel() >= (long)B * Hkv * nsplit * 16 * D, "attn_decode_rope: part_o too small");
-    TORCH_CHECK(part_ml->numel() >= (long)B * Hkv * nsplit * 16 * 2, "attn_decode_rope: part_ml too small");
-    po = part_o->data_ptr<float>();
-    pml = part_ml->data_ptr<float>();
-  }
-  c10::DeviceGuard g(qkv.device());
-  const int rc = bfly::launch_attn_decode(nullptr, 0, k_cache.data_ptr(), v_cache.data_ptr(),
-                                          block_tables.data_ptr<int>(), block_tables.stride(0),
-                                          ctx_lens.data_ptr<int>(), B, Hq, Hkv, D, BS, (float)scale, max_ctx,
-                                          part_tokens, bf(out), po, pml, cur_stream(),
-                                          k_cache.scalar_type() == at::kFloat8_e4m3fn, &rp);
-  TORCH_CHECK(rc == 0, "attn_decode_rope: unsupported configuration (rc=", rc, ")");
 }
 
 // Chunked prefill over the paged cache (attention_paged.hip): q [T, Hq, D] rows grouped per
@@ -1210,12 +1053,6 @@ TORCH_LIBRARY(bfly, m) {
   m.def("gemm_slab_offset() -> int", []() -> int64_t { return (int64_t)bfly::gemm_slab_offset_floats(); });
   m.def("gemm_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace, "
         "Tensor ssp, float eps) -> ()");
-  m.def("gemm_norm(Tensor x, Tensor w, Tensor(a!) workspace, Tensor(b!) residual, Tensor gamma, Tensor(c!) y, "
-        "Tensor(d!) ssp, Tensor(e!) counters) -> int");
-  m.def("gemm_seam_check(int M, int N, int K, int mode) -> int", &gemm_seam_check);
-  m.def("gemm_rope_kv(Tensor x, Tensor w, Tensor(a!) workspace, Tensor(b!) qkv, Tensor positions, Tensor cos_t, "
-        "Tensor sin_t, int hq, int hkv, Tensor? slots, Tensor(c!)? k_cache, Tensor(d!)? v_cache, Tensor(e!) counters, "
-        "Tensor? ssp, float eps) -> int");
   m.def("gemm_deferred_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) workspace, Tensor ssp, float eps) -> int");
   m.def("rms_norm_rows(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) ssp, Tensor(c!)? residual) -> ()");
   m.def("rms_norm_rows_chunks(int dim) -> int", [](int64_t dim) -> int64_t { return bfly::rmsnorm_rows_chunks(dim); });
@@ -1251,9 +1088,6 @@ TORCH_LIBRARY(bfly, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens, "
         "float scale, int max_ctx, int part_tokens, Tensor(a!) out, Tensor(b!)? part_o, "
         "Tensor(c!)? part_ml) -> ()");
-  m.def("attn_decode_rope(Tensor qkv, Tensor? partial, Tensor positions, Tensor cos_t, Tensor sin_t, Tensor? slots, "
-        "int num_q_heads, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor ctx_lens, float scale, "
-        "int max_ctx, int part_tokens, Tensor(c!) out, Tensor(d!)? part_o, Tensor(e!)? part_ml) -> ()");
   m.def("moe_route(Tensor x, Tensor wr, int top_k, Tensor(a!) gates, Tensor(b!) topk_ids, Tensor(c!) topk_w) -> ()");
   m.def("moe_gate_scale(Tensor(a!) h, Tensor gates, int e0, int num_local) -> ()");
   m.def("moe_max_tiles(int tk, int num_local, int bm=64) -> int", &moe_max_tiles);
@@ -1330,10 +1164,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("gemm_deferred_rs", &gemm_deferred_rs);
   m.impl("rms_norm_rows", &rms_norm_rows);
   m.impl("attn_decode", &attn_decode);
-  m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("attn_prefill", &attn_prefill);
-  m.impl("gemm_norm", &gemm_norm);
-  m.impl("gemm_rope_kv", &gemm_rope_kv);
   m.impl("attn_prefill_paged", &attn_prefill_paged);
   m.impl("attn_lse_merge", &attn_lse_merge);
   m.impl("probe", &probe);

@@ -19,42 +19,8 @@ struct RowScale {
   float inv_dim, eps;
 };
 
-// Split-K seams: after its partial slab, every split workgroup of a tile waits for its sibling
-// splits and then reduces ITS share of the tile's rows (sum of the sk slabs in split order ->
-// bf16) and finishes them, so the consumer kernel that used to do it never launches:
-//   kSeamNorm (decode O / down projections, tp = 1): + residual (bf16, written back) ->
-//     y = x * gamma (bf16) and the row's sum of squares over the tile's columns into
-//     ssp[row][n-tile]; the consumer GEMM applies rsqrt(sum(ssp[row]) / N + eps) (RowScale with
-//     N / BN chunks). Replaces the separate add+RMSNorm kernel.
-//   kSeamRope (decode QKV projection, 128-column tile = one head): RoPE on Q / K heads, bf16 row
-//     into `qkv`, K / V into the paged cache. Replaces rope_kv.
-constexpr int kSeamNone = 0, kSeamNorm = 1, kSeamRope = 2;
-struct Seam {
-  int mode;
-  int sk;               // split count (set by launch_gemm_seam; the grid is 1-D, splits adjacent)
-  int xcd_local;        // (set by launch_gemm_seam) a tile's splits share an XCD (seam_tile_split)
-  // kSeamNorm
-  bf16* residual;       // [M, N] in/out
-  const bf16* gamma;    // [N]
-  bf16* y;              // [M, N]
-  float* ssp;           // [M, N / BN]
-  // kSeamRope
-  bf16* qkv;            // [M, N] (Q heads, K heads, V heads; N = (hq + 2 hkv) * 128)
-  const int* positions; // [M]
-  const float* cos_t;   // [max_pos, 64]
-  const float* sin_t;
-  const int* slots;     // [M] cache slot (< 0: not cached)
-  void* k_cache;        // [blocks, hkv, BS, 128]
-  void* v_cache;        // [blocks, hkv, 128, BS]
-  int hq, hkv, block_size, kv_fp8;
-  // both
-  int* counters;        // per-tile arrival counters: monotonic, never reset (own region)
-  uint32_t* err;        // sibling-wait timeout word (nullable)
-};
-__host__ __device__ inline Seam no_seam() { Seam s{}; s.mode = kSeamNone; return s; }
-
 struct GemmPlan {
-  int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 3 = decode ring,
+  int kind;  // 0 = skinny (decode), 1 = LDS-tiled, 3 = decode ring, 5 = mid-M 8-wave,
              // 4 = 256x256 8-phase big tile (BK 64, prefill; kind 2 was the removed ring kernel)
   int mt, nt;
   int wk;    // skinny: waves splitting K inside a workgroup (1, 2, 4)
@@ -132,11 +98,6 @@ int launch_gemm_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, 
 int gemm_check(int M, int N, int K, int epi);
 // 0 if the auto plan for this shape takes a RowScale (tile and decode-ring kernels)
 int gemm_rowscale_check(int M, int N, int K, int epi);
-// Split-K GEMM with a seam (Seam). Returns N / BN (> 0: the ssp chunks per row of kSeamNorm),
-// or <= 0 when this shape's plan cannot run the seam (nothing ran; the caller falls back).
-// `rs`: the input's RMSNorm row scale (a RowNormed X), applied before the slabs.
-int launch_gemm_seam(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
-                     size_t ws_bytes, const Seam& seam, hipStream_t stream, bool dry, const RowScale* rs = nullptr);
 // Y = X W^T without epilogue; when the plan splits K, the f32 slabs are left in the workspace
 // (at gemm_slab_offset_floats(), layout [sk][M][N]) for the consumer kernel to reduce, and the
 // split count is returned; otherwise `out` is written and 1 is returned. < 0: error.
@@ -154,28 +115,11 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 // attention.hip
 int attn_decode_splits(int max_ctx, int part_tokens);
 int attn_decode_part_tokens(int B, int Hkv, int max_ctx);
-// Decode attention with rope_kv's work folded in (attention.hip): the QKV projection's
-// un-rotated output (f32 split-K slabs `part` [sk][B][N], or bf16 rows `qkv` [B][N]) supplies Q,
-// and the new token's K / V row goes into the cache (`k_out` / `v_out`) at slots[b].
-struct DecodeRope {
-  const float* part = nullptr;
-  const bf16* qkv = nullptr;
-  long slab = 0;                       // elements between split slabs (B * N)
-  int sk = 1, N = 0;                   // N = (Hq + 2 Hkv) * D
-  const int* positions = nullptr;
-  const float* cos_t = nullptr;        // [max_pos, D / 2]
-  const float* sin_t = nullptr;
-  const int* slots = nullptr;          // [B], -1 = no cache write
-  void* k_out = nullptr;
-  void* v_out = nullptr;
-  int overlap = 1;                     // page loads start before the new row is stored (only the
-                                       // last page's load waits); 0: a workgroup barrier first
-};
 int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
                        bf16* out, float* part_o, float* part_ml, hipStream_t stream,
-                       int kv_fp8 = 0, const DecodeRope* rope = nullptr);            // caches hold FP8 e4m3 (bfly_kv.h)
+                       int kv_fp8 = 0);            // caches hold FP8 e4m3 (bfly_kv.h)
 int launch_attn_prefill(const bf16* q, long q_stride, const bf16* k, long k_stride, const bf16* v,
                         long v_stride, const int* cu_seqlens, int nseq, int max_seqlen, int Hq,
                         int Hkv, int D, float scale, bool causal, bf16* out, long o_stride,

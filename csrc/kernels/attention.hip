@@ -39,24 +39,13 @@ constexpr float kNegInf = -INFINITY;
 // ---------------------------------------------------------------------------------------
 // Decode
 // ---------------------------------------------------------------------------------------
-// ROPE (DecodeRope, bfly_kernels.h): the QKV projection's output arrives un-rotated — as the
-// f32 split-K slabs of the deferred GEMM, or bf16 rows — and this kernel does rope_kv's decode
-// work itself: every workgroup builds its rotated Q fragments from the slabs (the rotation
-// pairs d, d + 64 sit in the same lane: sub-steps ds and ds + 2), and the workgroup whose
-// context split holds the new token rotates its K row and stores K and V into the paged cache,
-// then a barrier, before any wave loads a page. Same sums, roundings and rotation as
-// rope.hip, so the caches are bitwise those of rope_kv + attention; one launch fewer per layer.
-// Measured 1.1 % slower per 70B decode step than rope_kv + attention (29.74 vs 29.38-29.53 ms,
-// profiles/r4_fused_decode_rope_ab.log): 512 workgroups each rebuilding Q from the split-K slabs
-// cost more than the 5.8 us launch removed. Opt-in (BFLY_DECODE_FUSED_ROPE).
-template <int D, int BS, typename CT, bool ROPE = false>
+template <int D, int BS, typename CT>
 __global__ void __launch_bounds__(kAttnThreads)
 attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restrict__ k_cache,
                    const CT* __restrict__ v_cache, const int* __restrict__ block_tables,
                    int bt_stride, const int* __restrict__ ctx_lens, int Hq, int Hkv,
                    float scale_log2, int part_tokens, bf16* __restrict__ out,
-                   float* __restrict__ part_o, float* __restrict__ part_ml,
-                   DecodeRope rp = DecodeRope{}) {
+                   float* __restrict__ part_o, float* __restrict__ part_ml) {
   static_assert(D == 128 && BS == 32, "decode kernel is specialised for D=128, BS=32");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -68,7 +57,6 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   const long part_base = ((long)(b * Hkv + h) * nsplit + s);
 
   __shared__ float s_o[4][8][4][64];
-  __shared__ int s_kv_ready;   // ROPE overlap: wave 0 stored the new K / V row
   __shared__ float s_m[4][16], s_l[4][16];
 
   if (tok0 >= tok1) {  // empty split: mark it so the combine skips it
@@ -89,98 +77,12 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   auto d_off = [&](int ds) { return kF8 ? 64 * (ds >> 1) + 16 * g + 8 * (ds & 1) : 32 * ds + 8 * g; };
   // Q^T fragment (B operand): lane holds Q[row r][d]; rows >= G are zero.
   bf16x8 qf[4];
-  if constexpr (ROPE) {
-    // 8 consecutive columns of row b of the QKV projection, reduced over the split-K slabs
-    // in split order and rounded to bf16 (rope.hip rope_load)
-    auto row8 = [&](int col, float (&x)[8]) {
-      if (rp.part != nullptr) {
-        const float* pr = rp.part + (long)b * rp.N + col;
-        f32x4 lo = *reinterpret_cast<const f32x4*>(pr), hi = *reinterpret_cast<const f32x4*>(pr + 4);
-        for (int k = 1; k < rp.sk; ++k) {
-          lo += *reinterpret_cast<const f32x4*>(pr + k * rp.slab);
-          hi += *reinterpret_cast<const f32x4*>(pr + k * rp.slab + 4);
-        }
+  const int qr = r < G ? r : 0;
+  const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x[j] = bf2f(f2bf(lo[j]));
-          x[j + 4] = bf2f(f2bf(hi[j]));
-        }
-      } else {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(rp.qkv + (long)b * rp.N + col);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = bf2f(v[j]);
-      }
-    };
-    const int pos = rp.positions[b];
-    const float* cr = rp.cos_t + (long)pos * (D / 2);
-    const float* sr = rp.sin_t + (long)pos * (D / 2);
-    const int qr = r < G ? r : 0;
-    float a[4][8];
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds) row8((h * G + qr) * D + d_off(ds), a[ds]);
-#pragma unroll
-    for (int ds = 0; ds < 2; ++ds)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int dd = d_off(ds) + j;                   // < 64; its partner dd + 64 is at ds + 2
-        float o0, o1;
-        rope_rotate(a[ds][j], a[ds + 2][j], cr[dd], sr[dd], o0, o1);
-        qf[ds][j] = f2bf(o0);
-        qf[ds + 2][j] = f2bf(o1);
-      }
-    if (r >= G)
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) qf[ds] = bf16x8{};
-    // the new token's K / V row (position ctx - 1) goes into the cache from the split that
-    // reads its page; wave 0, lane l: columns l and l + 64 of the kv head
-    const int slot = rp.slots != nullptr ? rp.slots[b] : -1;
-    const bool appends = slot >= 0 && ctx - 1 >= tok0 && ctx - 1 < tok1;
-    if (rp.overlap) {
-      if (threadIdx.x == 0) s_kv_ready = appends ? 0 : 1;
-      __syncthreads();
-    }
-    if (wid == 0 && appends) {
-      auto col2 = [&](int base, float& x0, float& x1) {
-        float v[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int c = base + lane + 64 * i;
-          if (rp.part != nullptr) {
-            float acc = rp.part[(long)b * rp.N + c];
-            for (int k = 1; k < rp.sk; ++k) acc += rp.part[k * rp.slab + (long)b * rp.N + c];
-            v[i] = bf2f(f2bf(acc));
-          } else {
-            v[i] = bf2f(rp.qkv[(long)b * rp.N + c]);
-          }
-        }
-        x0 = v[0];
-        x1 = v[1];
-      };
-      float k0, k1, v0, v1, rk0, rk1;
-      col2((Hq + h) * D, k0, k1);
-      col2((Hq + Hkv + h) * D, v0, v1);
-      rope_rotate(k0, k1, cr[lane], sr[lane], rk0, rk1);
-      const int blk = slot / BS, off = slot % BS;
-      CT* kp = static_cast<CT*>(rp.k_out) + (((long)blk * Hkv + h) * BS + off) * D;
-      CT* vp = static_cast<CT*>(rp.v_out) + ((long)blk * Hkv + h) * (long)D * BS + off;
-      KV<CT>::store1(kp + lane, f2bf(rk0));
-      KV<CT>::store1(kp + lane + 64, f2bf(rk1));
-      KV<CT>::store1(vp + (long)lane * BS, f2bf(v0));
-      KV<CT>::store1(vp + (long)(lane + 64) * BS, f2bf(v1));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stored before any wave loads the page
-      if (rp.overlap && lane == 0) __hip_atomic_store(&s_kv_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // overlap: only the wave that loads the split's last page (the new token's) waits for the
-    // store, right before that load (load_page); otherwise every wave waits here
-    if (!rp.overlap) __syncthreads();
-  } else {
-    const int qr = r < G ? r : 0;
-    const bf16* qp = q + (long)b * q_stride + (long)(h * G + qr) * D;
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds) {
-      qf[ds] = *reinterpret_cast<const bf16x8*>(qp + d_off(ds));
-      if (r >= G) qf[ds] = bf16x8{};
-    }
+  for (int ds = 0; ds < 4; ++ds) {
+    qf[ds] = *reinterpret_cast<const bf16x8*>(qp + d_off(ds));
+    if (r >= G) qf[ds] = bf16x8{};
   }
 
   f32x4 o[8];
@@ -196,13 +98,6 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
   // their MFMA, so the prefetched page costs half the VGPRs with an FP8 cache
   typedef typename KV<CT>::raw_t raw_t;
   auto load_page = [&](int p, raw_t (&kf)[2][4], raw_t (&vf)[8]) {
-    if constexpr (ROPE) {
-      if (rp.overlap && p == p1 - 1) {
-        while (__hip_atomic_load(&s_kv_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-          __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");
-      }
-    }
     const long blk = bt[p];
     const CT* kb = k_cache + ((blk * Hkv + h) * BS) * D;
     const CT* vb = v_cache + (blk * Hkv + h) * (long)D * BS;
@@ -808,8 +703,7 @@ int attn_decode_part_tokens(int B, int Hkv, int max_ctx) {
 int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const void* v_cache,
                        const int* block_tables, int bt_stride, const int* ctx_lens, int B, int Hq,
                        int Hkv, int D, int block_size, float scale, int max_ctx, int part_tokens,
-                       bf16* out, float* part_o, float* part_ml, hipStream_t stream, int kv_fp8,
-                       const DecodeRope* rope) {
+                       bf16* out, float* part_o, float* part_ml, hipStream_t stream, int kv_fp8) {
   if (B <= 0) return 0;
   if (D != 128 || block_size != 32 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
   if (part_tokens <= 0) part_tokens = attn_decode_part_tokens(B, Hkv, max_ctx);
@@ -819,21 +713,19 @@ int launch_attn_decode(const bf16* q, long q_stride, const void* k_cache, const 
   if (nsplit > 1 && (part_o == nullptr || part_ml == nullptr)) return -3;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(nsplit, Hkv, B);
-#define DEC_LAUNCH(CT, R)                                                                                   \
-  attn_decode_kernel<128, 32, CT, R><<<grid, kAttnThreads, 0, stream>>>(                                     \
+#define DEC_LAUNCH(CT)                                                                                      \
+  attn_decode_kernel<128, 32, CT><<<grid, kAttnThreads, 0, stream>>>(                                        \
       q, q_stride, static_cast<const CT*>(k_cache), static_cast<const CT*>(v_cache), block_tables, bt_stride, \
-      ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml, rope ? *rope : DecodeRope{})
-  if (kv_fp8) {
-    if (rope) DEC_LAUNCH(fp8_t, true); else DEC_LAUNCH(fp8_t, false);
-  } else {
-    if (rope) DEC_LAUNCH(bf16, true); else DEC_LAUNCH(bf16, false);
-  }
+      ctx_lens, Hq, Hkv, scale_log2, part_tokens, out, part_o, part_ml)
+  if (kv_fp8) DEC_LAUNCH(fp8_t);
+  else DEC_LAUNCH(bf16);
 #undef DEC_LAUNCH
   if (nsplit > 1) {
     // Measured and dropped: merging the splits inside the decode kernel (last arriver, agent-
     // scope release/acquire per workgroup) ran 2x slower than this parallel combine launch
-    // (B=64 ctx 1024: 104 vs 53 us); RoPE + KV append fused into the decode kernel ran 1 %
-    // slower per 70B step than rope_kv + attention (profiles/r2_fused_decode_rope_ab.log).
+    // (B=64 ctx 1024: 104 vs 53 us); RoPE + KV append fused into the decode kernel ran 1.1 %
+    // slower per 70B step than rope_kv + attention and was removed
+    // (profiles/r2_fused_decode_rope_ab.log, profiles/r4_fused_decode_rope_ab.log).
     dim3 g2(Hq / Hkv, Hkv, B);
     attn_decode_combine_kernel<128><<<g2, 128, 0, stream>>>(part_o, part_ml, nsplit, Hq, Hkv, out);
   }

@@ -89,15 +89,22 @@ __global__ void embed_kernel(const int* __restrict__ ids, const bf16* __restrict
 // Row gather: out[i] = src[idx[i]] for rows of `words` 4-byte words (bf16 / f32 / int32 rows);
 // rows with idx < 0 are left as they are (the caller pre-filled them). Replaces torch's
 // index_select / gather on serving paths (final-token rows, pipeline input ids): one small
-// launch of our own instead of an at::native kernel.
+// launch of our own instead of an at::native kernel. An index past the source (idx >= nsrc,
+// which index_select rejects with an error) is loud instead of silent: the row is filled with
+// all-ones words (NaN as f32 or bf16, -1 as int32 ids) so the fault shows downstream, and the
+// host wrapper checks indices eagerly under BFLY_DEBUG_CHECKS.
 template <typename IT>
 __global__ void gather_rows_kernel(const uint32_t* __restrict__ src, long src_ld, const IT* __restrict__ idx,
                                    uint32_t* __restrict__ out, long out_ld, int words, long nsrc) {
   const long i = blockIdx.x;
   const long j = (long)idx[i];
-  if (j < 0 || j >= nsrc) return;
-  const uint32_t* s = src + j * src_ld;
+  if (j < 0) return;
   uint32_t* o = out + i * out_ld;
+  if (j >= nsrc) {
+    for (int c = threadIdx.x; c < words; c += kEwThreads) o[c] = 0xffffffffu;
+    return;
+  }
+  const uint32_t* s = src + j * src_ld;
   if ((words & 3) == 0 && ((src_ld | out_ld) & 3) == 0) {
     for (int c = threadIdx.x; c < words / 4; c += kEwThreads)
       reinterpret_cast<u32x4*>(o)[c] = reinterpret_cast<const u32x4*>(s)[c];

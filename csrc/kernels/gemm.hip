@@ -74,14 +74,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(float* base, long by
                                            (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
 }
 
-// Cache-policy bit of a buffer access: sc1 (write-through store / agent-coherent load).
-constexpr int kCpolSc1 = 16;
-
-// `wt`: write-through (sc1) — the slabs of a split-K seam, read by sibling workgroups of the
-// same launch (seam_arrive's hand-off without cache-wide write-back / invalidate)
-__device__ __forceinline__ void store_slab4(__amdgpu_buffer_rsrc_t r, int off, f32x4 v, bool wt = false) {
-  if (wt) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, kCpolSc1);
-  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+__device__ __forceinline__ void store_slab4(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
 }
 
 // Reduce split-K partial slabs [SK][M][N] (f32) and apply the epilogue.
@@ -181,202 +175,6 @@ __device__ __forceinline__ void splitk_fixup(const float* __restrict__ part, int
       for (int j = 0; j < 4; ++j) o[j] = f2bf(epi == EPI_BIAS ? a[j] + bf2f(bias[n + j]) : a[j]);
       *reinterpret_cast<bf16x4*>(out + (long)m * ldo + n) = o;
     }
-  }
-}
-
-// Split-K seams (Seam, bfly_kernels.h): every split of a tile publishes its slab (the
-// split-K hand-off recipe above: drained plain stores, ONE agent-scope release, relaxed
-// ticket), waits until all `sk` siblings of its generation arrived (the counter is monotonic:
-// ticket / sk is this call's generation, so nothing is ever re-armed; wrap-safe compare), and
-// then reduces its 1/sk share of the tile's rows in split order 0..sk-1 — the numerics of the
-// separate rmsnorm_rows kernel: bf16 sum, bf16 residual add, y = x * gamma, f32 sum of squares
-// over the tile's columns. Siblings are co-resident (the launcher checks the grid fits), and the
-// wait is bounded: a sibling later than ~2 s sets the error word and the share proceeds.
-constexpr long long kSeamSpinTicks = 2LL * 100000000LL;   // 2 s of the 100 MHz constant clock
-constexpr int kSeamTiles = 1024;                            // counters per split-count region
-
-// Publish this split's slab and wait for the tile's sibling splits of the same generation.
-// The hand-off of MI355X_MICROARCH.md's table (row 1), with no cache-wide maintenance: the slabs
-// were stored write-through (sc1, tile_epilogue), every wave drains its stores (vmcnt(0)) before
-// the workgroup barrier, then ONE lane adds to the tile's counter (agent scope) and polls it
-// (agent-coherent loads); the other waves pass the barrier that lane joins, and every slab read
-// is an sc1 load (seam_sum8). (The first version used agent release / acquire fences: each
-// wrote back and invalidated the whole L2 per workgroup — 36.9 vs 29.3 ms per 70B decode step.)
-__device__ __forceinline__ void seam_arrive(int sk, int tile, const Seam& seam) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // one counter region per split count: a tile's counter only ever advances by whole
-    // generations of `sk` (O at sk 8 and down at sk 4 share tile indices, not counters)
-    int* cnt = seam.counters + sk * kSeamTiles + tile;
-    const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int target = (ticket / sk + 1) * sk;
-    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target < 0) {
-      const long long t0 = wall_clock64();
-      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target < 0) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > kSeamSpinTicks) {
-          if (seam.err != nullptr) __hip_atomic_store(seam.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// Tile and split of a seam workgroup (1-D grid). xcd_local (the tile count a multiple of 8):
-// the dispatcher deals workgroups round-robin over the 8 XCDs (b % 8 share an L2), so a tile's
-// splits get ids b = 8 (q sk + s) + x — all on XCD x, whose slabs then stay in its L2 for the
-// siblings' reduce — and XCD x owns the contiguous tiles [x T/8, (x + 1) T/8) (the row tiles of
-// one weight panel side by side). Ids 0 .. 8 sk - 1 still hold 8 complete tiles, so progress
-// needs no more resident workgroups than the adjacent layout (`else`: splits at consecutive ids).
-// Placement is a speed matter only: the hand-off is agent-scope either way.
-__device__ __forceinline__ void seam_tile_split(const Seam& seam, int ntiles, int& tile, int& split) {
-  const int b = blockIdx.x, sk = seam.sk;
-  if (seam.xcd_local && (ntiles & 7) == 0) {
-    const int x = b & 7, j = b >> 3;
-    split = j % sk;
-    tile = x * (ntiles >> 3) + j / sk;
-  } else {
-    tile = xcd_remap(b / sk, ntiles);
-    split = b % sk;
-  }
-}
-
-// 8 consecutive columns of one row, summed over the sk slabs in split order and rounded to
-// bf16 (what the separate reduce / norm / rope kernels compute). Agent-coherent (sc1) loads
-// through a descriptor over all sk slabs: the siblings' write-through stores, never a stale line.
-__device__ __forceinline__ void seam_sum8(__amdgpu_buffer_rsrc_t rs, int off, int sk, int slab_bytes, float (&a)[8]) {
-  auto ld = [&](int o) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kCpolSc1));
-  };
-  f32x4 lo = ld(off), hi = ld(off + 16);
-  for (int k = 1; k < sk; ++k) {
-    lo += ld(off + k * slab_bytes);
-    hi += ld(off + k * slab_bytes + 16);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    a[j] = bf2f(f2bf(lo[j]));
-    a[j + 4] = bf2f(f2bf(hi[j]));
-  }
-}
-
-template <int BN>
-__device__ __forceinline__ void seam_norm(const float* __restrict__ part, int sk, int split, int M, int N, int m0,
-                                          int BM, int n0, const Seam& seam) {
-  constexpr int TPR = BN / 8;                       // threads per row: 8 columns each
-  const int rpp = blockDim.x / TPR;                 // rows per pass
-  const int R = (BM + sk - 1) / sk;
-  const int r0 = m0 + split * R;
-  const int r1 = min(min(m0 + BM, r0 + R), M);
-  const int tn = n0 / BN, nchunks = N / BN;
-  const int slab = M * N * 4;                       // bytes (the launcher bounds sk x slab)
-  const auto rs = slab_rsrc(const_cast<float*>(part), (long)sk * slab);
-  const int c = n0 + (threadIdx.x % TPR) * 8;
-  const bf16x8 g = *reinterpret_cast<const bf16x8*>(seam.gamma + c);
-  for (int base = r0; base < r1; base += rpp) {
-    const int row = base + threadIdx.x / TPR;
-    const bool ok = row < r1;
-    float ss = 0.f;
-    if (ok) {
-      float a[8];
-      seam_sum8(rs, (row * N + c) * 4, sk, slab, a);
-      bf16x8* rp = reinterpret_cast<bf16x8*>(seam.residual + (long)row * N + c);
-      const bf16x8 r = *rp;
-      bf16x8 sm, o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sm[j] = f2bf(a[j] + bf2f(r[j]));                           // the stored bf16 residual
-        const float v = bf2f(sm[j]);
-        ss += v * v;
-        o[j] = f2bf(v * bf2f(g[j]));
-      }
-      *rp = sm;
-      *reinterpret_cast<bf16x8*>(seam.y + (long)row * N + c) = o;
-    }
-#pragma unroll
-    for (int o = TPR / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, TPR);
-    if (ok && threadIdx.x % TPR == 0) seam.ssp[(long)row * nchunks + tn] = ss;
-  }
-}
-
-// RoPE (rotate-half, rope.hip's arithmetic) + paged KV append of one 128-column head tile:
-// thread t of a row owns columns [8t, 8t + 8) and their rotation partners [64 + 8t, +8).
-template <typename CT>
-__device__ __forceinline__ void seam_rope(const float* __restrict__ part, int sk, int split, int M, int N, int m0,
-                                          int BM, int n0, const Seam& seam) {
-  constexpr int D = 128, H2 = 64, TPR = H2 / 8;
-  const int rpp = blockDim.x / TPR;
-  const int R = (BM + sk - 1) / sk;
-  const int r0 = m0 + split * R;
-  const int r1 = min(min(m0 + BM, r0 + R), M);
-  const int slab = M * N * 4;                       // bytes (the launcher bounds sk x slab)
-  const auto rs = slab_rsrc(const_cast<float*>(part), (long)sk * slab);
-  const int head = n0 / D, p0 = (threadIdx.x % TPR) * 8;
-  const bool is_v = head >= seam.hq + seam.hkv, is_k = !is_v && head >= seam.hq;
-  for (int row = r0 + threadIdx.x / TPR; row < r1; row += rpp) {
-    float a[8], b[8];
-    const int poff = (row * N + n0 + p0) * 4;
-    seam_sum8(rs, poff, sk, slab, a);
-    seam_sum8(rs, poff + H2 * 4, sk, slab, b);
-    bf16x8 oa, ob;
-    if (!is_v) {
-      const int pos = seam.positions[row];
-      const float* cr = seam.cos_t + (long)pos * H2 + p0;
-      const float* sr = seam.sin_t + (long)pos * H2 + p0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float r0, r1;
-        rope_rotate(a[j], b[j], cr[j], sr[j], r0, r1);
-        oa[j] = f2bf(r0);
-        ob[j] = f2bf(r1);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        oa[j] = f2bf(a[j]);
-        ob[j] = f2bf(b[j]);
-      }
-    }
-    bf16* qrow = seam.qkv + (long)row * N + n0;
-    *reinterpret_cast<bf16x8*>(qrow + p0) = oa;
-    *reinterpret_cast<bf16x8*>(qrow + p0 + H2) = ob;
-    const int slot = seam.slots != nullptr ? seam.slots[row] : -1;
-    if (slot < 0 || (!is_k && !is_v)) continue;
-    const int BS = seam.block_size, blk = slot / BS, off = slot % BS;
-    if (is_k) {
-      const int kh = head - seam.hq;
-      CT* kp = static_cast<CT*>(seam.k_cache) + (((long)blk * seam.hkv + kh) * BS + off) * D;
-      KV<CT>::store8(kp + p0, oa);
-      KV<CT>::store8(kp + p0 + H2, ob);
-    } else {
-      const int vh = head - seam.hq - seam.hkv;
-      CT* vp = static_cast<CT*>(seam.v_cache) + ((long)blk * seam.hkv + vh) * D * BS + off;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        KV<CT>::store1(vp + (long)(p0 + j) * BS, oa[j]);
-        KV<CT>::store1(vp + (long)(p0 + H2 + j) * BS, ob[j]);
-      }
-    }
-  }
-}
-
-// BFLY_SEAM_PROBE (timing experiments only, tools/seam_bench.py; results are WRONG when set):
-// bit 0 skips the sibling wait, bit 1 skips the share's reduce
-__constant__ int g_seam_probe = 0;
-
-template <int BN>
-__device__ __forceinline__ void seam_finish(const float* __restrict__ part, int sk, int split, int tile, int M,
-                                            int N, int m0, int BM, int n0, const Seam& seam) {
-  if (!(g_seam_probe & 1)) seam_arrive(sk, tile, seam);
-  if (g_seam_probe & 2) return;
-  if (seam.mode == kSeamNorm) {
-    seam_norm<BN>(part, sk, split, M, N, m0, BM, n0, seam);
-  } else if constexpr (BN == 128) {
-    if (seam.kv_fp8) seam_rope<fp8_t>(part, sk, split, M, N, m0, BM, n0, seam);
-    else seam_rope<bf16>(part, sk, split, M, N, m0, BM, n0, seam);
   }
 }
 
@@ -561,7 +359,7 @@ template <int TI, int TJ>
 __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw, int nw, int lane,
                                               int M, int N, int epi, const bf16* __restrict__ bias,
                                               bf16* __restrict__ out, long ldo, float* __restrict__ pslab,
-                                              int m0, const RowScale& rsc, bool wt = false) {
+                                              int m0, const RowScale& rsc) {
   const int lr = lane & 15, lc = 4 * (lane >> 4);
   const auto rs = slab_rsrc(pslab, pslab ? (long)(M - m0) * N * 4 : 0);
   const bool vec = (ldo & 3) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
@@ -571,8 +369,8 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw
   if (rsc.ss != nullptr) {
     // sum of the row's partial sums of squares: the 4 lanes of a row (lane >> 4) take every
     // 4th group of 4 chunks as 16-B loads, all in flight together, then two shuffles (a norm
-    // seam leaves one chunk per 128 columns: 64 for d 8192 — a serial loop of dependent loads
-    // there cost ~20 us per consumer GEMM); chunks % 4 != 0: one chunk per lane and step
+    // norm leaves a chunk per 1024 columns, but a serial loop of dependent loads over many
+    // chunks cost ~20 us per consumer GEMM); chunks % 4 != 0: one chunk per lane and step
     const int q = lane >> 4, nc = rsc.chunks;
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -601,7 +399,7 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw
     for (int j = 0; j < TJ; ++j) {
       const int n = nw + 16 * j + lc;
       if (pslab) {
-        store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j] * sc[i], wt);
+        store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j] * sc[i]);
       } else if (epi == EPI_SILU) {
         if constexpr (TJ % 2 == 0) {   // gate/up 16-row groups pair up inside the wave
           if (j & 1) continue;
@@ -639,8 +437,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
                  bf16* __restrict__ out, long ldo, float* __restrict__ part,
                  int* __restrict__ counters, const int* __restrict__ grows = nullptr,
                  const int4* __restrict__ gtiles = nullptr, const int* __restrict__ gcount = nullptr,
-                 long w_estride = 0, RowScale rsc = RowScale{nullptr, 0, 0.f, 0.f},
-                 Seam seam = no_seam()) {
+                 long w_estride = 0, RowScale rsc = RowScale{nullptr, 0, 0.f, 0.f}) {
   constexpr int WNW = 4 / WMW;                // waves along M x waves along N
   constexpr int WM = BM / WMW, WN = BN / WNW; // per-wave output tile
   constexpr int TI = WM / 16, TJ = WN / 16;  // MFMA tiles per wave
@@ -665,16 +462,13 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     tile = 0;
   } else {
     const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-    if (seam.mode != kSeamNone) seam_tile_split(seam, mtiles * ntiles, tile, ksplit);
-    else tile = xcd_remap((int)blockIdx.x, mtiles * ntiles);
+    tile = xcd_remap((int)blockIdx.x, mtiles * ntiles);
     const int tn = tile / mtiles, tm = tile % mtiles;  // consecutive tiles share a W panel
     m0 = tm * BM;
     n0 = tn * BN;
   }
-  // split index / count: grid y, or (seam launches) from the 1-D grid id so a tile's sibling
-  // splits are dispatched close together (seam_arrive waits on them)
-  if (seam.mode == kSeamNone) ksplit = (int)blockIdx.y;
-  const int nsplit = seam.mode != kSeamNone ? seam.sk : (int)gridDim.y;
+  ksplit = (int)blockIdx.y;
+  const int nsplit = (int)gridDim.y;
 
   const int ktiles = K / kBK;
   const int kt0 = (int)(((long)ktiles * ksplit) / nsplit);
@@ -729,14 +523,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     if (++buf == STAGES) buf = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)ksplit * m_slab * N + (long)m0 * N : nullptr, m0, rsc,
-                        seam.mode != kSeamNone);
-  if constexpr (!GROUPED) {
-    if (part && seam.mode != kSeamNone) {
-      seam_finish<BN>(part, nsplit, ksplit, tile, M, N, m0, BM, n0, seam);
-      return;
-    }
-  }
+                        part ? part + (long)ksplit * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
   if (part && counters && splitk_arrive(counters + tile, nsplit, reinterpret_cast<int*>(smem)))
     splitk_fixup(part, nsplit, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
 }
@@ -788,8 +575,7 @@ template <int BM, int BN, int NWM, int NWN, int SW>
 __global__ void __launch_bounds__(kDecThreads)
 gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                bf16* __restrict__ out, long ldo, float* __restrict__ part, RowScale rsc,
-                Seam seam = no_seam()) {
+                bf16* __restrict__ out, long ldo, float* __restrict__ part, RowScale rsc) {
   constexpr int SX = 3, NW = NWM * NWN;
   static_assert(NW * 64 <= kDecThreads && SW >= SX, "decode ring configuration");
   constexpr int WM = BM / NWM, WN = BN / NWN;   // per-wave output block
@@ -804,16 +590,11 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / NWN, wn = wid % NWN;
   const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-  int tile, ksplit;   // see gemm_tile_kernel
-  if (seam.mode != kSeamNone) {
-    seam_tile_split(seam, mtiles * ntiles, tile, ksplit);
-  } else {
-    tile = xcd_remap((int)blockIdx.x, mtiles * ntiles);
-    ksplit = (int)blockIdx.y;
-  }
+  const int tile = xcd_remap((int)blockIdx.x, mtiles * ntiles);
+  const int ksplit = (int)blockIdx.y;
   const int tn = tile / mtiles, tm = tile % mtiles;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nsplit = seam.mode != kSeamNone ? seam.sk : (int)gridDim.y;
+  const int nsplit = (int)gridDim.y;
   const int ktiles = K / kBK;
   const int kt0 = (int)(((long)ktiles * ksplit) / nsplit);
   const int kt1 = (int)(((long)ktiles * (ksplit + 1)) / nsplit);
@@ -864,9 +645,7 @@ gemm_dec_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W
     if (++wslot == SW) wslot = 0;
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
-                        part ? part + (long)ksplit * M * N + (long)m0 * N : nullptr, m0, rsc,
-                        seam.mode != kSeamNone);
-  if (part && seam.mode != kSeamNone) seam_finish<BN>(part, nsplit, ksplit, tile, M, N, m0, BM, n0, seam);
+                        part ? part + (long)ksplit * M * N + (long)m0 * N : nullptr, m0, rsc);
 }
 
 // Prefill tiles are walked in GROUP_M super-rows inside each XCD's contiguous range, so the
@@ -895,15 +674,33 @@ constexpr int kBigGroupM = 8;
 // in flight and retires all of K-tile k, which is read from phase 4k+1 on (one phase after the
 // wait, behind a barrier both groups pass: the template's RAW rule). Raw s_barrier only: a
 // __syncthreads() would drain the DMA in flight (§5 "Pipelining across barriers").
-// The prefill kernel for every M > 256 (plan kind 4; EARLY = plan mt 1).
-// Measured and dropped (profiles/r3_gemm_prefill_pmc.md, M = 8192, 70B projections):
+// The fragment schedule on top of that (the prefill kernel for every M > 256, plan kind 4):
+//  * early LDS release: A-lo is the one half restaged one phase after its read, so only its
+//    reads must retire before a phase's barrier (lgkmcnt(4) after A first, B last); every
+//    other read completes inside the wave's own MFMA segment;
+//  * lookahead: the A-lo fragments of K-tile k+1 are read in phase q3 of K-tile k (whose read
+//    segment is otherwise empty), and its B-lo fragments right behind q3's MFMAs (b_lo(k)'s
+//    last use), so q0 reads nothing and no read latency sits behind a barrier. A counted wait
+//    in q2 retires this wave's A-lo / B-lo(k+1) DMA, and the barrier ending q2 of group 0 (=
+//    the one starting q2's MFMAs of group 1) is passed by both groups before either reads;
+//  * buffer-descriptor staging: the tile's A / B rows start at an SGPR base (the descriptor),
+//    the K offset and the hi-half row shift ride in the scalar soffset (A-hi = A-lo + 64 rows,
+//    B-hi = B-lo + 32 rows: the same XOR pattern, which depends on row bits 1-3 only), each lane
+//    keeps 4 constant byte offsets, and A rows past M read as zeros instead of a clamped
+//    re-read (VALU per K-tile 49 -> 24).
+// 1.39-1.40 PF at M = 8192 on the 70B projections, +4.6-5.2 % over the schedule without the
+// lookahead and descriptors (profiles/r4_gemm_prefill_la.log, r4_gemm_prefill_lb.log).
+// Measured and dropped (profiles/r3_gemm_prefill_pmc.md, r4_gemm_prefill_{bal,lh}.log):
 //  - the round-2 5-slot BK-32 ring kernel (8 waves, one 16x16x32 K-step per barrier):
 //    2-7 % slower at M = 8192, within -3..+32 % at M = 256/512;
 //  - one wave per SIMD, 4 waves x 128x128 per wave (hipBLASLt's shape: MT256x256x64, 256
 //    threads): 32x32x16 with a 4/5-slot BK-32 glds ring 1.07-1.10 PF; 16x16x32 with buffer
 //    loads to LDS and the second MFMA half deferred behind the next K-tile's reads 1.13-1.23
 //    PF; the same with BK 64 in a 2-slot ring 1.00-1.12 PF (WAIT_ANY x3: one K-tile of lead
-//    does not cover HBM latency). All at 49-52 % MFMA-busy cycles against hipBLASLt's 87 %.
+//    does not cover HBM latency). All at 49-52 % MFMA-busy cycles against hipBLASLt's 87 %;
+//  - the 24 reads spread 6 / 6 / 6 / 6 over the four read segments (0.7-1.5 % slower), A-hi
+//    read in q0's empty segment (1.5-2.8 % slower), and the plain / early-release-only
+//    schedules (plan mt 0-3 of round 4).
 // ---------------------------------------------------------------------------------------
 constexpr int kB8Threads = 512;
 constexpr int kB8LdsBytes = 2 * 2 * 256 * 128;   // 2 buffers x (A, B) x 256 rows x 128 B
@@ -920,31 +717,6 @@ __device__ __forceinline__ int b8_block(int half, int h) {
   return g * 8 + (half == 2 ? 4 : 0) + b;
 }
 
-__device__ __forceinline__ void b8_stage(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W,
-                                         long ldw, int m0, int M, int n0, int N, int k0, char* buf,
-                                         int half, int wid, int lane) {
-  const bool isA = half == 0 || half == 3;
-  const bf16* src = isA ? X : W;
-  const long ld = isA ? ldx : ldw;
-  const int r0 = isA ? m0 : n0, rmax = isA ? M : N;
-  char* lds = buf + (isA ? 0 : 256 * 128);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int blk = b8_block(half, 2 * wid + i);
-    const int row = blk * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);   // lds_frag's swizzle, on the source
-    int gr = r0 + row;
-    gr = gr < rmax ? gr : rmax - 1;
-    const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 0);
-  }
-}
-
-// Buffer-descriptor staging (BUF): the tile's A / B rows start at an SGPR base (the descriptor),
-// the K offset and the hi-half row shift (A-hi = A-lo + 64 rows, B-hi = B-lo + 32 rows: the same
-// XOR pattern, since it depends on row bits 1-3 only) ride in the scalar soffset, and each lane
-// keeps 4 constant byte offsets (A / B x its 2 instructions) — no per-lane 64-bit address math
-// per stage, and A rows past M read as zeros (never stored) instead of a clamped re-read.
 struct B8Dma {
   int a[2], b[2];
 };
@@ -981,23 +753,6 @@ __device__ __forceinline__ void b8_stage_buf(__amdgpu_buffer_rsrc_t ra, __amdgpu
   }
 }
 
-// LA (plan mt 2, with EARLY and BUF): the A-lo fragments of K-tile k+1 are read in phase q3 of K-tile k,
-// whose read segment is otherwise empty, instead of in q0 of k+1 beside the B-lo reads. Per
-// K-tile the read segments then hold 4 / 4 / 8 / 8 ds_read_b128 instead of 12 / 4 / 8 / 0, so
-// no window between two barriers carries more than 8 reads of one wave group next to the other
-// group's 16-MFMA segment (12 x 4 waves x 4 LDS cycles + the phase's DMA exceed that segment's
-// 256 cycles). Safety: a counted wait in q2 retires this wave's A-lo / B-lo(k+1) DMA, and the
-// barrier ending q2 of group 0 (= the one starting q2's MFMAs of group 1) is passed by both
-// groups after their q2 waits, before either reads in q3.
-// LB (plan mt 5, the default, with LA): B-lo(k+1) is read too, right behind q3's MFMAs (b_lo(k)'s
-// last use), so its latency is spent in the closing barrier and q0's read segment instead of
-// after q0's barrier; q0 then reads nothing. +2.2-3.3 % over LA (profiles/r4_gemm_prefill_lb.log).
-// Measured and dropped: A-hi read in q0's then empty read segment instead of q2 (a_hi is free
-// since q3): 1.5-2.8 % below LB (profiles/r4_gemm_prefill_lh.log).
-// Measured and dropped: spreading the 24 reads 6 / 6 / 6 / 6 over the four read segments (A-hi
-// and the next A-lo split across phases, A-lo DMA retired in q1): 0.7-1.5 % slower than LA's
-// 4 / 4 / 8 / 8 (profiles/r4_gemm_prefill_bal.log).
-template <bool EARLY, bool LA = false, bool BUF = false, bool LB = false>
 __global__ void __launch_bounds__(kB8Threads)
 gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -1025,17 +780,11 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto bufp = [&](int k) -> char* { return smem + (k & 1) * (2 * 256 * 128); };
-  // BUF: descriptors at the tile's first A / B row (SGPRs), 4 per-lane offsets
+  // descriptors at the tile's first A / B row (SGPRs), 4 per-lane offsets
   const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);
   const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
-  B8Dma dma{};
-  if constexpr (BUF) dma = b8_dma_offsets(ldx, ldw, wid, lane);
-  auto stage = [&](int k, int half) {
-    if constexpr (BUF)
-      b8_stage_buf(rsa, rsb, ldx, ldw, (kt0 + k) * 64, bufp(k), half, wid, dma);
-    else
-      b8_stage(X, ldx, W, ldw, m0, M, n0, N, (kt0 + k) * 64, bufp(k), half, wid, lane);
-  };
+  const B8Dma dma = b8_dma_offsets(ldx, ldw, wid, lane);
+  auto stage = [&](int k, int half) { b8_stage_buf(rsa, rsb, ldx, ldw, (kt0 + k) * 64, bufp(k), half, wid, dma); };
   // prologue: all of K-tile 0, then A-lo, B-lo, B-hi of K-tile 1 (the load stream's order)
   stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
   stage(1, 0); stage(1, 1); stage(1, 2);
@@ -1052,42 +801,21 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
   };
-
   auto read_b_lo = [&](const char* Bs) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) b_lo[j][ks] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
   };
-  if constexpr (LA) read_a_lo(bufp(0));
-  if constexpr (LB) read_b_lo(bufp(0) + 256 * 128);
+  read_a_lo(bufp(0));
+  read_b_lo(bufp(0) + 256 * 128);
   for (int k = 0; k < nk; ++k) {
     const char* As = bufp(k);
     const char* Bs = As + 256 * 128;
     const bool more = k + 1 < nk, more2 = k + 2 < nk;
-    // ---- q0: read A-lo, B-lo; DMA A-hi(k+1)
-    // EARLY: A-lo is the one half restaged one phase after its read (q1 below), so only its
-    // reads must retire before this phase's barrier (lgkmcnt(4) after A first, B last); every
-    // other read completes inside the wave's own MFMA segment (compiler-placed waits), which
-    // releases the barrier earlier (guide §5 template: "lgkmcnt(8) retires the reads issued
-    // first"). Without EARLY every load segment drains its reads before the barrier.
-    if constexpr (EARLY) {
-      if constexpr (!LA) read_a_lo(As);    // LA: read in q3 of the previous K-tile
-      if constexpr (!LB) read_b_lo(Bs);    // LB: read at the end of q3 of the previous K-tile
-      if (more) stage(k + 1, 3);
-      asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b_lo[j][ks] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a_lo[i][ks] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
-      if (more) stage(k + 1, 3);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
+    // ---- q0: (A-lo, B-lo read ahead); DMA A-hi(k+1)
+    if (more) stage(k + 1, 3);
+    asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1098,13 +826,12 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b_lo[j][ks], a_lo[i][ks], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
-    // ---- q1: read B-hi; DMA A-lo(k+2) (A-lo(k) was read in q0)
+    // ---- q1: read B-hi; DMA A-lo(k+2) (A-lo(k) was read in q3 of k-1)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) b_hi[j][ks] = lds_frag(Bs, bc + 32 + 16 * j, ks * 4 + (lane >> 4));
     if (more2) stage(k + 2, 0);
-    if constexpr (!EARLY) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1115,19 +842,16 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
         for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b_hi[j][ks], a_lo[i][ks], acc[i][2 + j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
-    // ---- q2: read A-hi; DMA B-lo(k+2) (B-lo(k) was read in q0)
+    // ---- q2: read A-hi; DMA B-lo(k+2)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) a_hi[i][ks] = lds_frag(As, ar + 64 + 16 * i, ks * 4 + (lane >> 4));
     if (more2) stage(k + 2, 1);
-    if constexpr (LA) {
-      // this wave's A-lo / B-lo(k+1) DMA retired (left in flight: B-hi, A-hi(k+1) and, while
-      // K-tile k+2 exists, A-lo / B-lo(k+2))
-      if (more2) vm_wait<8>();
-      else if (more) vm_wait<4>();
-    }
-    if constexpr (!EARLY) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // this wave's A-lo / B-lo(k+1) DMA retired (left in flight: B-hi, A-hi(k+1) and, while
+    // K-tile k+2 exists, A-lo / B-lo(k+2))
+    if (more2) vm_wait<8>();
+    else if (more) vm_wait<4>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1138,14 +862,12 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
         for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b_hi[j][ks], a_hi[i][ks], acc[4 + i][2 + j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
-    // ---- q3: no reads (LA: A-lo(k+1)); DMA B-hi(k+2) (B-hi(k) was read in q1); retire K-tile k+1
-    if constexpr (LA) {
-      // a_lo(k) is dead since q1; q3's MFMAs use a_hi / b_lo. Unconditional (past the last
-      // K-tile it reads the other buffer's stale image, never used), and pinned here: under a
-      // branch the scheduler sank the reads behind q3's MFMAs and barrier, i.e. back into q0
-      read_a_lo(bufp(k + 1));
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    // ---- q3: read A-lo(k+1); DMA B-hi(k+2); retire K-tile k+1
+    // a_lo(k) is dead since q1; q3's MFMAs use a_hi / b_lo. Unconditional (past the last K-tile
+    // it reads the other buffer's stale image, never used), and pinned here: under a branch the
+    // scheduler sank the reads behind q3's MFMAs and barrier, i.e. back into q0
+    read_a_lo(bufp(k + 1));
+    __builtin_amdgcn_sched_barrier(0);
     if (more2) stage(k + 2, 2);
     if (more2) vm_wait<6>();   // A-hi(k+1) and older landed; A-lo/B-lo/B-hi(k+2) fly
     else vm_wait<0>();
@@ -1158,19 +880,162 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b_lo[j][ks], a_hi[i][ks], acc[4 + i][j]);
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (LB) {
-      // B-lo(k+1) behind q3's MFMAs, so its latency is spent in the barrier and q0's read
-      // segment instead of after q0's barrier (its DMA retired with LA's q2 wait)
-      read_b_lo(bufp(k + 1) + 256 * 128);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    // B-lo(k+1) behind q3's MFMAs, so its latency is spent in the barrier and q0's read segment
+    // instead of after q0's barrier (its DMA retired with q2's wait)
+    read_b_lo(bufp(k + 1) + 256 * 128);
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    (void)more;
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
   tile_epilogue<8, 4>(acc, m0 + wr * 128, n0 + wc * 64, lane, M, N, epi, bias, out, ldo,
                       part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0,
                       RowScale{nullptr, 0, 0.f, 0.f});
+}
+
+// ---------------------------------------------------------------------------------------
+// Mid-M GEMM (plan kind 5): the tensor-parallel shard projections at M = 128-512 rows (tp2-tp8
+// decode at 64 sequences per GPU, large single-GPU batches), where a 256x256 tile grid leaves
+// most of the 256 CUs idle (tp8 QKV at M = 512: 10 tiles) and the 4-wave tile kernel keeps the
+// matrix pipe ~25 % busy (one wave per SIMD, every K-tile behind one barrier).
+//
+// 8 waves in two groups of 4 staggered by one s_barrier (big8's scheme): each wave owns a
+// 64 x WN output block (WN = 64 for 256x128 / 128x256 tiles, 32 for 128x128), and every
+// K-tile (BK = 64) is two k-steps of 32. Per k-step a wave has a READ segment (its A and B
+// fragments of that k-step, TI + TJ ds_read_b128, and half of its share of the LDS-DMA) and an
+// MFMA segment (TI x TJ mfma_16x16x32). Group 1 runs one barrier behind group 0, so on every
+// SIMD one wave's MFMA segment overlaps its partner's read segment:
+//     global segment:  4k     4k+1   4k+2   4k+3   (k = K-tile)
+//     group 0:         R0(k)  M0(k)  R1(k)  M1(k)
+//     group 1:         M1(k-1) R0(k) M0(k)  R1(k)
+// LDS: an ST-stage ring of whole K-tiles (A | B images, 128-B rows, XOR-swizzled like
+// lds_frag). The DMA of K-tile k + ST - 1 is issued during K-tile k into the slot of K-tile
+// k - 1, whose last reader (group 1's R1(k-1), global segment 4k-1) retired its reads
+// (lgkmcnt(0)) before the barrier opening segment 4k. RAW: K-tile k+1 is first read in global
+// segment 4k+4 (group 0's R0(k+1)), so every wave retires its own DMA of K-tile k+1 before the
+// barrier that closes segment 4k+3: group 0 at the end of M1(k), group 1 at the end of R1(k).
+// DMA through buffer descriptors based at the tile's first row (A rows past M read zeros);
+// weights streamed non-temporally when one row tile covers M (each byte read by one workgroup).
+// Grid: 1-D, split-major then N-tile then M-tile, XCD-remapped, so an XCD's consecutive
+// workgroups share a weight panel (and K range) across the M tiles in its L2.
+// ---------------------------------------------------------------------------------------
+constexpr int kMidThreads = 512;
+
+template <int BM, int BN, int ST>
+struct MidCfg {
+  static constexpr int WM = 64;                          // wave rows
+  static constexpr int WN = (BM * BN) / (8 * WM);        // wave columns: 8 waves cover the tile
+  static constexpr int WGN = BN / WN, WGM = BM / WM;     // wave grid
+  static constexpr int TI = WM / 16, TJ = WN / 16;
+  static constexpr int ROWS = BM + BN;                   // LDS image rows per K-tile
+  static constexpr int SLOT = ROWS * 128;                // bytes per K-tile slot
+  static constexpr int L = ROWS / 64;                    // DMA instructions per wave per K-tile
+  static_assert(WGM * WGN == 8 && WN % 16 == 0 && L % 2 == 0, "mid tile shape");
+  static_assert(ST * SLOT <= 160 * 1024, "mid ring exceeds the LDS");
+};
+
+template <int BM, int BN, int ST>
+__global__ void __launch_bounds__(kMidThreads)
+gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
+                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
+                 bf16* __restrict__ out, long ldo, float* __restrict__ part, int nsplit,
+                 RowScale rsc) {
+  using C = MidCfg<BM, BN, ST>;
+  constexpr int TI = C::TI, TJ = C::TJ, L = C::L, H = L / 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int grp = wid >> 2;
+  const int wm = wid / C::WGN, wn = wid % C::WGN;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int t = xcd_remap((int)blockIdx.x, mtiles * ntiles * nsplit);
+  const int tm = t % mtiles, tn = (t / mtiles) % ntiles, ksplit = t / (mtiles * ntiles);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ktiles = K / kBK;
+  const int kt0 = (int)(((long)ktiles * ksplit) / nsplit);
+  const int nk = (int)(((long)ktiles * (ksplit + 1)) / nsplit) - kt0;
+
+  // DMA: wave w moves 1-KiB blocks w, w + 8, ... of the slot (blocks < BM / 8 are A rows)
+  const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);
+  const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
+  const int wpol = (mtiles == 1 && g_tile_w_nt) ? 2 : 0;   // runtime: the aux operand is an immediate
+  // (BM / 8 is a multiple of 8: instruction i of every wave is an A block iff i < BM / 64)
+  int voff[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int blk = wid + 8 * i;
+    const bool isA = i < BM / 64;
+    const int row = (isA ? blk : blk - BM / 8) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    voff[i] = (int)((row * (isA ? ldx : ldw) + chunk * 8) * 2);
+  }
+  auto slot_of = [&](int k) -> char* { return smem + (k % ST) * C::SLOT; };
+  auto dma = [&](int k, int half) {   // half 0 / 1: instructions [0, H) / [H, L) of K-tile k
+    char* s = slot_of(k);
+    const int soff = (kt0 + k) * kBK * 2;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const int i = half * H + j;
+      const int blk = wid + 8 * i;
+      if (i < BM / 64)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr_t)(s + blk * 1024), 16, voff[i], soff, 0, 0);
+      else if (wpol)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr_t)(s + blk * 1024), 16, voff[i], soff, 0, 2);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr_t)(s + blk * 1024), 16, voff[i], soff, 0, 0);
+    }
+  };
+  // retire this wave's DMA of the K-tiles before `k + 1` (k + 1 .. k + ST - 1 may fly)
+  auto wait_through = [&](int k) {
+    const int after = min(ST - 2, nk - 2 - k);   // K-tiles issued after k + 1
+    if (ST >= 4 && after >= 2) vm_wait<(ST >= 4 ? 2 : 0) * L>();
+    else if (after >= 1) vm_wait<L>();
+    else vm_wait<0>();
+  };
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-tiles 0 .. ST-2 in flight, K-tile 0 landed everywhere
+#pragma unroll
+  for (int s = 0; s < ST - 1; ++s)
+    if (s < nk) { dma(s, 0); dma(s, 1); }
+  wait_through(-1);
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();
+
+  const int ar = wm * C::WM + (lane & 15), bc = wn * C::WN + (lane & 15);
+  bf16x8 af[TI], bfr[TJ];
+  for (int k = 0; k < nk; ++k) {
+    const char* As = slot_of(k);
+    const char* Bs = As + BM * 128;
+    const bool pre = k + ST - 1 < nk;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // ---- read segment: this k-step's fragments, half of the DMA of K-tile k + ST - 1
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
+      if (pre) dma(k + ST - 1, ks);
+      if (ks == 1 && grp == 1) wait_through(k);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // ---- MFMA segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);   // C^T tile
+      __builtin_amdgcn_s_setprio(0);
+      if (ks == 1 && grp == 0) wait_through(k);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // re-align the groups' barrier counts
+  tile_epilogue<TI, TJ>(acc, m0 + wm * C::WM, n0 + wn * C::WN, lane, M, N, epi, bias, out, ldo,
+                        part ? part + (long)ksplit * M * N + (long)m0 * N : nullptr, m0, rsc);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1216,12 +1081,11 @@ static void init_nt_policy() {
 template <int BM, int BN, int WMW, int STAGES>
 static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                     hipStream_t stream, const RowScale& rsc, const Seam* seam) {
+                     hipStream_t stream, const RowScale& rsc) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const size_t lds = (size_t)STAGES * (BM + BN) * kBK * 2;
-  // seam launches: 1-D grid with the splits of a tile adjacent (dispatched back to back)
-  const dim3 grid = seam != nullptr ? dim3(tiles * sk, 1) : dim3(tiles, sk);
+  const dim3 grid(tiles, sk);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
   if (!attr_set && lds > 65536) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW, STAGES>),
@@ -1230,14 +1094,14 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   }
   gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
-      sk > 1 && fixup_enabled() && seam == nullptr ? reinterpret_cast<int*>(ws) : nullptr, nullptr, nullptr,
-      nullptr, 0, rsc, seam ? *seam : no_seam());
+      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr, nullptr, nullptr,
+      nullptr, 0, rsc);
 }
 
 template <int BM, int BN, int NWM, int NWN, int SW>
 static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
-                    hipStream_t stream, const RowScale& rsc, const Seam* seam) {
+                    hipStream_t stream, const RowScale& rsc) {
   init_nt_policy();
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   constexpr size_t lds = (size_t)(3 * BM + SW * BN) * kBK * 2;
@@ -1248,42 +1112,40 @@ static void run_dec(const bf16* X, long ldx, const bf16* W, long ldw, int M, int
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  const dim3 grid = seam != nullptr ? dim3(tiles * sk, 1) : dim3(tiles, sk);   // see run_tile
+  const dim3 grid(tiles, sk);
   gemm_dec_kernel<BM, BN, NWM, NWN, SW><<<grid, NWM * NWN * 64, lds, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, rsc,
-      seam ? *seam : no_seam());
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, rsc);
 }
 
 static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
-                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, int early,
-                     hipStream_t stream) {
+                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<false>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true, true, true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true, false, true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true, true, true, true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        kB8LdsBytes);
     attr = true;
   }
   const int tiles = ((M + 255) / 256) * (N / 256);
   dim3 grid(tiles, sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  if (early == 2)
-    gemm_big8_kernel<true, true, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
-  else if (early == 5)
-    gemm_big8_kernel<true, true, true, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
-  else if (early == 3)
-    gemm_big8_kernel<true, false, true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
-  else if (early)
-    gemm_big8_kernel<true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
-  else
-    gemm_big8_kernel<false><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  gemm_big8_kernel<<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+}
+
+template <int BM, int BN, int ST>
+static void run_mid8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
+                     const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream,
+                     const RowScale& rsc) {
+  init_nt_policy();
+  constexpr size_t lds = (size_t)ST * MidCfg<BM, BN, ST>::SLOT;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid8_kernel<BM, BN, ST>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  gemm_mid8_kernel<BM, BN, ST><<<tiles * sk, kMidThreads, lds, stream>>>(
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, sk, rsc);
 }
 
 // Plan selection, from the tools/bench_gemm.py sweep on MI355X (Llama-3-70B TP1/TP8 shapes,
@@ -1353,10 +1215,7 @@ GemmPlan plan_gemm(int M, int N, int K) {
   if (bucket == 0) return plan_gemm_heuristic(M, N, K);
   for (const TunedPlan& t : kTuned)
     if (t.N == N && t.K == K && t.M == bucket)
-      // the sweep's 8-phase plans (mt 1) run as the lookahead variant (mt 5: A-lo and B-lo of
-      // the next K-tile read one phase early), +4.6-5.2 % on every 70B projection at M = 8192
-      // (profiles/r4_gemm_prefill_la.log, r4_gemm_prefill_lb.log)
-      return GemmPlan{t.kind, t.kind == 4 && t.mt == 1 ? 5 : t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
+      return GemmPlan{t.kind, t.kind == 4 ? 0 : t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
   return plan_gemm_heuristic(M, N, K);
 }
 
@@ -1380,13 +1239,11 @@ static GemmPlan plan_gemm_heuristic(int M, int N, int K) {
     return p;
   }
   if (M > 256 && N % 256 == 0 && K % 64 == 0) {
-    // prefill / large batch: 256x256 8-phase tile with early LDS release, A-lo and B-lo
-    // fragments of the next K-tile read one phase early, buffer-descriptor staging
-    // (gemm_big8_kernel<true, true, true, true>: 1.39-1.40 PF at M = 8192 on the 70B
-    // projections against 1.33-1.35 for <true> alone on the same box,
-    // profiles/r4_gemm_prefill_lb.log); split K only when the tile grid cannot fill the 256 CUs
+    // prefill / large batch: the 256x256 8-phase tile (gemm_big8_kernel: 1.39-1.40 PF at
+    // M = 8192 on the 70B projections, profiles/r4_gemm_prefill_lb.log); split K only when the
+    // tile grid cannot fill the 256 CUs
     p.kind = 4;
-    p.mt = 5;   // EARLY + A-lo / B-lo lookahead + buffer-descriptor staging
+    p.mt = 0;
     p.bm = p.bn = 256;
     const int tiles = ((M + 255) / 256) * (N / 256);
     int sk = 1;
@@ -1424,16 +1281,26 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                     hipStream_t stream, bool dry = false, bool defer = false,
-                    const RowScale* rs = nullptr, const Seam* seam = nullptr) {
+                    const RowScale* rs = nullptr) {
   const RowScale rsc = rs ? *rs : RowScale{nullptr, 0, 0.f, 0.f};
-  if (rs != nullptr && p.kind != 1 && p.kind != 3) return -4;   // row scale: tile / ring epilogues only
-  // norm seam: split-K tile / ring plans, 128-column tiles (16 threads per row share), no epilogue
-  if (seam != nullptr && ((p.kind != 1 && p.kind != 3) || p.sk < 2 || p.bn != 128 || epi != EPI_NONE))
-    return -5;
+  if (rs != nullptr && p.kind != 1 && p.kind != 3 && p.kind != 5) return -4;   // row scale: tile / ring / mid epilogues
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
-    if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, p.mt, stream);   // mt: 0 plain, 1 EARLY, 2 EARLY + LA + BUF, 3 EARLY + BUF, 5 EARLY + LA + BUF + LB
+    if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+  } else if (p.kind == 5) {
+    // mid-M 8-wave staggered GEMM: plan {5, ST (ring depth), 0, 0, BM, BN, sk}
+    if (N % p.bn != 0 || K % kBK != 0 || K / kBK < p.sk) return -1;
+    if (epi == EPI_SILU && p.bn * p.bm / 512 % 32 != 0) return -1;
+    bool done = false;
+#define MID_CASE(BM_, BN_, ST_)                                                                   \
+  if (!done && p.bm == BM_ && p.bn == BN_ && p.mt == ST_) {                                        \
+    if (!dry) run_mid8<BM_, BN_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    done = true;                                                                                   \
+  }
+    MID_CASE(256, 128, 3) MID_CASE(128, 256, 3) MID_CASE(128, 128, 4) MID_CASE(128, 128, 3)
+#undef MID_CASE
+    if (!done) return -2;
   } else if (p.kind == 3) {
     // decode ring GEMM: plan {3, SW (weight ring depth), waves, waves along M, BM, BN, sk}
     if (N % p.bn != 0 || K % kBK != 0 || K / kBK < p.sk * 2) return -1;
@@ -1442,7 +1309,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     bool done = false;
 #define DEC_CASE(BM_, BN_, NWM_, NWN_, SW_)                                                      \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == NWM_ && p.nt == NWM_ * NWN_ && p.mt == SW_) { \
-    if (!dry) run_dec<BM_, BN_, NWM_, NWN_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc, seam); \
+    if (!dry) run_dec<BM_, BN_, NWM_, NWN_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                 \
   }
     DEC_CASE(128, 224, 8, 1, 4) DEC_CASE(128, 224, 8, 1, 3) DEC_CASE(128, 256, 8, 1, 3)
@@ -1476,7 +1343,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     const int st = p.mt > 0 ? p.mt : 2;   // tile plans reuse `mt` as the pipeline depth
 #define TL_CASE(BM_, BN_, WMW_, ST_)                                                            \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_ && st == ST_) {                       \
-    if (!dry) run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc, seam); \
+    if (!dry) run_tile<BM_, BN_, WMW_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                \
   }
 #define TL_ST(BM_, BN_, WMW_) TL_CASE(BM_, BN_, WMW_, 2) TL_CASE(BM_, BN_, WMW_, 3) TL_CASE(BM_, BN_, WMW_, 4)
@@ -1490,7 +1357,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry && !defer && seam == nullptr && (!fixup_enabled() || p.kind == 4)) {   // big kernels: no fixup path
+  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind >= 4)) {   // big / mid kernels: no fixup path
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);
@@ -1586,73 +1453,6 @@ int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M
                           false, defer, rs);
   if (rc != 0) return rc;
   return defer ? p.sk : 1;
-}
-
-// Grid residency of the seam: every split of a tile must be running while its siblings wait.
-// The splits of a tile are adjacent in the 1-D seam grid, so with in-order dispatch sk resident
-// workgroups already guarantee progress (the oldest unfinished tile always gets all its splits
-// resident); the check below is stricter (the whole grid resident at once), so a kernel on a
-// side stream (an RCCL send of the pipeline) holding a few CUs cannot even slow the seam. The occupancy query (after the
-// kernel's dynamic-LDS opt-in, without which it answers 0) is capped by the LDS bound, which is
-// exact; the API's known over-report (one block per CU for SGPR-bound 256-thread kernels,
-// cdna_hip_programming.md §1) cannot apply to these LDS-bound kernels. The sibling wait is
-// bounded anyway (kSeamSpinTicks): a non-resident grid would end late, with the error word set.
-template <typename KFN>
-static bool seam_fits(KFN* kfn, int threads, size_t lds, long grid) {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
-    ncu = prop.multiProcessorCount;
-  }
-  if (lds > 65536 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-          hipSuccess)
-    return false;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kfn), threads, lds) !=
-      hipSuccess)
-    return false;
-  const int by_lds = (int)((160 * 1024) / (lds > 0 ? lds : 1));
-  if (per_cu > by_lds) per_cu = by_lds;
-  return per_cu > 0 && grid <= (long)ncu * per_cu;
-}
-
-int launch_gemm_seam(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, float* ws,
-                     size_t ws_bytes, const Seam& seam, hipStream_t stream, bool dry, const RowScale* rs) {
-  if (M <= 0 || seam.mode == kSeamNone) return -1;
-  if (seam.mode == kSeamRope && !dry && (N != (seam.hq + 2 * seam.hkv) * 128 || seam.block_size <= 0)) return -4;
-  const GemmPlan p = select_plan(M, N, K, EPI_NONE);
-  if (p.sk < 2 || p.bn != 128 || (p.kind != 1 && p.kind != 3)) return -1;
-  if (!dry && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float))) return -3;
-  const long grid = (long)((M + p.bm - 1) / p.bm) * (N / p.bn) * p.sk;
-  if ((M + p.bm - 1) / p.bm * (N / p.bn) > kSeamTiles || p.sk >= kSplitCounters / kSeamTiles) return -1;
-  if ((long)p.sk * M * N * 4 > 0x7fffffffL) return -1;   // seam_sum8: 32-bit descriptor offsets
-  bool fits = false;
-  if (p.kind == 1 && p.bm == 64 && p.wk == 2 && p.mt == 3)
-    fits = seam_fits(&gemm_tile_kernel<64, 128, 2, 3>, kTileThreads, (size_t)3 * (64 + 128) * kBK * 2, grid);
-  else if (p.kind == 3 && p.bm == 64 && p.wk == 4 && p.nt == 8 && p.mt == 6)
-    fits = seam_fits(&gemm_dec_kernel<64, 128, 4, 2, 6>, 512, (size_t)(3 * 64 + 6 * 128) * kBK * 2, grid);
-  if (!fits) return -2;
-  // BFLY_SEAM_XCD=0: a tile's splits at consecutive ids, i.e. on different XCDs (A/B runs)
-  static const int xcd_local = [] {
-    const char* e = getenv("BFLY_SEAM_XCD");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  static const bool probe_set = [] {
-    const char* e = getenv("BFLY_SEAM_PROBE");
-    const int v = e ? atoi(e) : 0;
-    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_seam_probe), &v, sizeof(int));
-    return true;
-  }();
-  (void)probe_set;
-  Seam sm = seam;
-  sm.sk = p.sk;
-  sm.xcd_local = xcd_local;
-  const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, nullptr, 0, ws, stream, dry, true,
-                          rs, &sm);
-  return rc != 0 ? rc : N / p.bn;
 }
 
 size_t gemm_slab_offset_floats() { return kCounterBytes / sizeof(float); }

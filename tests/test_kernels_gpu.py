@@ -315,106 +315,6 @@ def test_attn_prefill_paged_single_sequence(Hq, Hkv, kv_dtype):
     _close(o, want, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(64, 8192, 8192), (64, 8192, 28672), (40, 8192, 8192)])
-def test_linear_rmsnorm_rows_seam(M, N, K):
-    """The add+RMSNorm folded into the split-K seam of the decode O / down GEMMs (gemm.hip
-    seam_norm): residual += x W^T (bf16), y = residual * gamma, per-tile sums of squares; the
-    row-scaling consumer GEMM then equals rms_norm(residual) @ W2^T. Three calls in a row
-    exercise the monotonic arrival counters' later generations."""
-    x = _bf(M, K, scale=1.0, seed=120)
-    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=121)
-    g = (1.0 + 0.1 * _bf(N, seed=122).float()).to(torch.bfloat16)
-    w2 = _bf(256, N, scale=1.0 / math.sqrt(N), seed=123)
-    res0 = _bf(M, N, seed=124)
-    if not ops.norm_seam_ok(M, N, K):
-        assert M != 64, "the Llama-3-70B decode shapes must take the seam"
-        pytest.skip("this plan has no seam")
-    for it in range(3):
-        res = res0.clone()
-        rn = ops.linear_rmsnorm_rows(x, w, g, 1e-5, res)
-        assert rn is not None and rn.ssp.shape == (M, N // 128)
-        want_res = (res0.float() + (x.float() @ w.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
-        _close(res, want_res, 2e-2, 2e-2)
-        _close(rn.y, (want_res.float() * g.float()).to(torch.bfloat16), 3e-2, 3e-2)
-        _close(rn.ssp.sum(1), want_res.float().pow(2).sum(1), 1e-2, 1e-2)
-        got = ops.linear(rn, w2)
-        want = ref.rms_norm(want_res.cpu().float(), g.cpu().float(), 1e-5) @ w2.cpu().float().t()
-        _close(got, want, 3e-2, 3e-2)
-    assert ops.norm_seam_error(x.device) == 0
-
-
-@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
-@pytest.mark.parametrize("rownormed", [False, True])
-@pytest.mark.parametrize("M,Hq,Hkv", [(64, 64, 8), (8, 64, 8), (128, 64, 8), (256, 64, 8), (64, 8, 1), (32, 16, 2),
-                                      (128, 32, 4), (256, 16, 2), (1, 64, 8)])
-def test_linear_rope_kv_seam_matches_rope_kv(kv_dtype, rownormed, M, Hq, Hkv):
-    """RoPE + paged KV append folded into the decode QKV GEMM's split-K seam (gemm.hip
-    seam_rope) is bitwise the unfused GEMM + rope_kv: rotated Q / K rows, V rows, and the K / V
-    cache pages (a padding row with slot -1 writes no page); with a plain and a RowNormed input.
-    Shapes: Llama-3-70B tp1 at several decode buckets, and its tp8 / tp4 QKV shards (8 / 16
-    query heads); a shape without a seam plan must decline (None), never run a wrong plan."""
-    D, H, BS = 128, 8192, 32
-    N = (Hq + 2 * Hkv) * D
-    if not ops.norm_seam_ok(M, N, H, ops.SEAM_ROPE):
-        if (M, Hq) == (64, 64):
-            pytest.fail("the Llama-3-70B decode QKV shape must take the rope seam")
-        cos, sin = ref.rope_tables(D, 64, 500000.0, device=DEV)
-        assert ops.linear_rope_kv(_bf(M, H, seed=1), _bf(N, H, seed=2), torch.zeros(M, dtype=torch.int32, device=DEV),
-                                  cos, sin, Hq, Hkv, None, None, None) is None
-        pytest.skip(f"no rope seam plan for M={M} N={N}")
-    x = _bf(M, H, seed=170)
-    w = _bf(N, H, scale=1.0 / math.sqrt(H), seed=171)
-    cos, sin = ref.rope_tables(D, 4096, 500000.0, device=DEV)
-    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
-    nblk = 3 * M
-    slots = (torch.randperm(nblk * BS, device=DEV)[:M]).to(torch.int32)
-    slots[M // 2] = -1
-    kdt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
-    caches = [(torch.zeros(nblk, Hkv, BS, D, device=DEV).to(kdt), torch.zeros(nblk, Hkv, D, BS, device=DEV).to(kdt))
-              for _ in range(2)]
-    inp = x
-    if rownormed:
-        res = _bf(M, H, seed=172)
-        inp = ops.rms_norm(x, _bf(H, seed=173), 1e-5, residual=res, rows=True)
-    for it in range(2):          # second call: later generation of the seam counters
-        got = ops.linear_rope_kv(inp, w, pos, cos, sin, Hq, Hkv, slots, *caches[0])
-        base = ops.rope_kv(ops.linear(inp, w, defer=True), pos, cos, sin, Hq, Hkv, slots, *caches[1])
-        torch.cuda.synchronize()
-        assert got is not None
-        diff = (got.float() - base.float()).abs()
-        assert torch.equal(got, base), (f"call {it}: {int((diff > 0).sum())} of {diff.numel()} elements differ "
-                                        f"(max {diff.max().item():.3e}; rows {sorted(set((diff > 0).nonzero()[:, 0].tolist()))[:8]}, "
-                                        f"cols {sorted(set((diff > 0).nonzero()[:, 1].tolist()))[:8]})")
-        assert torch.equal(caches[0][0].view(torch.uint8), caches[1][0].view(torch.uint8))
-        assert torch.equal(caches[0][1].view(torch.uint8), caches[1][1].view(torch.uint8))
-    assert ops.norm_seam_error(x.device) == 0
-
-
-def test_norm_seam_interleaved_split_counts():
-    """The decode layer alternates the O seam (split-K 8) and the down seam (split-K 4) on the
-    same tile indices: each split count has its own arrival counters, so no generation ever
-    straddles the two (a shared counter would strand half of a call's splits)."""
-    shapes = [(64, 8192, 8192), (64, 8192, 28672)]
-    if not all(ops.norm_seam_ok(*s) for s in shapes):
-        pytest.skip("no seam plans")
-    data = []
-    for i, (M, N, K) in enumerate(shapes):
-        x = _bf(M, K, seed=130 + i)
-        w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=140 + i)
-        g = _bf(N, seed=150 + i)
-        res0 = _bf(M, N, seed=160 + i)
-        want = (res0.float() + (x.float() @ w.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
-        data.append((x, w, g, res0, want))
-    for it in range(5):
-        for x, w, g, res0, want in data:
-            res = res0.clone()
-            rn = ops.linear_rmsnorm_rows(x, w, g, 1e-5, res)
-            torch.cuda.synchronize()
-            _close(res, want, 2e-2, 2e-2)
-            _close(rn.ssp.sum(1), want.float().pow(2).sum(1), 1e-2, 1e-2)
-    assert ops.norm_seam_error(data[0][0].device) == 0
-
-
 def test_attn_decode_strided_q():
     # q as a view into a fused QKV row (row stride > Hq*D), as the model passes it
     D, BS, Hq, Hkv, B = 128, 32, 8, 1, 3
@@ -455,21 +355,38 @@ def test_moe_route_and_gate_scale():
                                    (300, 512, 256), (520, 512, 128)])
 @pytest.mark.parametrize("epi", ["none", "bias", "silu"])
 def test_gemm_big_tile(M, N, K, epi):
-    """256x256 8-phase prefill kernel (plan kind 4, EARLY = plan mt in {0, 1}): ragged M,
-    the minimum of two 64-deep K-tiles per split, split-K, all epilogues, asymmetric operands."""
+    """256x256 8-phase prefill kernel (plan kind 4): ragged M, the minimum of two 64-deep
+    K-tiles per split, uneven split-K, all epilogues, asymmetric operands."""
     x = _bf(M, K, seed=60)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=61)
     b = _bf(N, seed=62) if epi == "bias" else None
     nout = N // 2 if epi == "silu" else N
     want = ref.linear(x, w, b, "silu" if epi == "silu" else "none")
-    for early in (0, 1):
-        for sk in (1, 2, 3):
-            if K // 64 < 2 * sk:
-                continue
-            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-            ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
-            torch.ops.bfly.gemm_with_plan(x, w, out, [4, early, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
-            _close(out, want, 2e-2, 2e-2)
+    for sk in (1, 2, 3):
+        if K // 64 < 2 * sk:
+            continue
+        out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+        ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+        _close(out, want, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,epi,sk", [(4096, 4096, 8192, "none", 1),      # 256-tile grid, K 8192
+                                          (8192, 2560, 8192, "silu", 1),      # 70B prefill shapes
+                                          (520, 7168, 8192, "silu", 4),       # tp8 gate_up at M 512+
+                                          (512, 1280, 8192, "none", 8)])      # tp8 QKV, deep split
+def test_gemm_big_tile_production(M, N, K, epi, sk):
+    """The prefill kernel at production scale: K = 8192 (128 K-tiles per split down to 16),
+    grids of >= 256 tiles (every CU busy, XCD remap and GROUP_M walk over many super-rows),
+    the SwiGLU epilogue, against the fp32 reference."""
+    x = _bf(M, K, seed=63)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=64)
+    nout = N // 2 if epi == "silu" else N
+    want = ref.linear(x, w, None, epi)
+    out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+    ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
+    torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws)
+    _close(out, want, 2e-2, 2e-2)
 
 
 TILE_CFGS = [(16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1), (64, 128, 1), (64, 128, 2),
@@ -497,6 +414,47 @@ def test_gemm_tile_plans(bm, bn, wmw, epi):
                 finally:
                     torch.ops.bfly.gemm_set_splitk_fixup(False)
                 _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+
+
+MID_CFGS = [(256, 128, 3), (128, 256, 3), (128, 128, 4), (128, 128, 3)]
+
+
+@pytest.mark.parametrize("bm,bn,st", MID_CFGS)
+def test_gemm_mid8_plans(bm, bn, st):
+    """Mid-M 8-wave staggered GEMM (plan kind 5): ragged M below and above one row tile (rows
+    past M read as zeros through the descriptor), K-tile counts of 1 .. 2 x the ring depth per
+    split (prologue / tail waits), uneven split-K, all epilogues, asymmetric operands."""
+    N = 3 * bn
+    for M, K in ((bm - 5, 1024), (bm + 9, 192), (3 * bm + 1, 4096), (7, 64 * st)):
+        x = _bf(M, K, seed=47)
+        w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=48)
+        b = _bf(N, seed=49)
+        for epi in ("none", "bias", "silu"):
+            nout = N // 2 if epi == "silu" else N
+            want = ref.linear(x, w, b if epi == "bias" else None, "silu" if epi == "silu" else "none")
+            for sk in (1, 2, 3, 7):
+                if K // 64 < sk:
+                    continue
+                out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+                ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
+                torch.ops.bfly.gemm_with_plan(x, w, out, [5, st, 0, 0, bm, bn, sk], ops.EPILOGUES[epi], ws,
+                                              b if epi == "bias" else None)
+                _close(out, want, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,plan", [(512, 1280, 8192, [5, 3, 0, 0, 128, 256, 12]),    # tp8 QKV
+                                        (512, 8192, 3584, [5, 3, 0, 0, 128, 256, 2]),     # tp8 down
+                                        (256, 14336, 8192, [5, 3, 0, 0, 256, 128, 2]),    # tp4 gate_up
+                                        (256, 2560, 8192, [5, 4, 0, 0, 128, 128, 6])])    # tp4 QKV
+def test_gemm_mid8_production(M, N, K, plan):
+    """The mid-M kernel at the TP shard shapes it is tuned for (K up to 8192, >= 240
+    workgroups), against the fp32 reference."""
+    x = _bf(M, K, seed=57)
+    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=58)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ws = torch.zeros(plan[6] * M * N + 16384, dtype=torch.float32, device=DEV)
+    torch.ops.bfly.gemm_with_plan(x, w, out, plan, 0, ws)
+    _close(out, ref.linear(x, w), 2e-2, 2e-2)
 
 
 DEC_CFGS = [(128, 224, 8, 1, 4), (128, 224, 8, 1, 3), (128, 256, 8, 1, 3), (128, 256, 4, 2, 3), (128, 128, 8, 1, 5),
@@ -945,47 +903,6 @@ def test_runtime_fills():
     u = torch.zeros(77, dtype=torch.int32, device=DEV)
     torch.ops.bfly.fill32_(u[10:20], -2 ** 31)
     assert u[10:20].tolist() == [-2 ** 31] * 10 and int(u[:10].abs().sum() + u[20:].abs().sum()) == 0
-
-
-@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
-@pytest.mark.parametrize("deferred", [True, False])
-@pytest.mark.parametrize("part_tokens", [0, 128])
-@pytest.mark.parametrize("Hq,Hkv", [(64, 8), (32, 8), (16, 2)])
-def test_attn_decode_rope_matches_rope_kv_then_attention(kv_dtype, deferred, part_tokens, Hq, Hkv):
-    """Decode attention with rope_kv folded in (attention.hip ROPE: Q rotated in registers from
-    the QKV GEMM's split-K slabs or bf16 rows, the new token's K / V row stored by the split that
-    reads its page) is bitwise the two-launch path: same output, same cache bytes (a padding row
-    with slot -1 writes nothing; lengths 1 .. 700, one and several context splits)."""
-    D, BS, H = 128, 32, 8192
-    lens = ([1, 31, 32, 100, 700, 5] * 11)[:64]     # 64 rows x 8192: the 70B decode split-K plan
-    B = len(lens)
-    N = (Hq + 2 * Hkv) * D
-    max_blocks = (max(lens) + BS - 1) // BS
-    nblk = B * max_blocks + 3
-    kdt = torch.float8_e4m3fn if kv_dtype == "fp8" else torch.bfloat16
-    k0, v0 = _bf(nblk, Hkv, BS, D, seed=80).to(kdt), _bf(nblk, Hkv, D, BS, seed=81).to(kdt)
-    tables = torch.randperm(nblk)[: B * max_blocks].view(B, max_blocks).to(torch.int32).to(DEV)
-    ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
-    pos = ctx - 1
-    slots = torch.stack([tables[b, (lens[b] - 1) // BS] * BS + (lens[b] - 1) % BS for b in range(B)]).to(torch.int32)
-    slots[2] = -1                                    # a graph-padding row
-    cos, sin = ref.rope_tables(D, 4096, 500000.0, device=DEV)
-    x = _bf(B, H, seed=82)
-    w = _bf(N, H, scale=1.0 / math.sqrt(H), seed=83)
-    scale = 1.0 / math.sqrt(D)
-    caches = [(k0.clone(), v0.clone()) for _ in range(2)]
-    qkv = ops.linear(x, w, defer=deferred)
-    if deferred and not isinstance(qkv, ops.Partial):
-        assert Hq != 64, "the 70B decode QKV projection must be split-K (deferred slabs)"
-        pytest.skip("this plan writes the projection directly")
-    got = ops.attn_decode_rope(qkv, pos, cos, sin, Hq, slots, *caches[0], tables, ctx, scale, max(lens), part_tokens)
-    qkv = ops.linear(x, w, defer=deferred)
-    rows = ops.rope_kv(qkv, pos, cos, sin, Hq, Hkv, slots, *caches[1])
-    want = ops.attn_decode(rows[:, : Hq * D].view(B, Hq, D), *caches[1], tables, ctx, scale, max(lens), part_tokens)
-    torch.cuda.synchronize()
-    assert torch.equal(caches[0][0].view(torch.uint8), caches[1][0].view(torch.uint8))
-    assert torch.equal(caches[0][1].view(torch.uint8), caches[1][1].view(torch.uint8))
-    assert torch.equal(got, want)
 
 
 @pytest.mark.parametrize("causal", [True, False])

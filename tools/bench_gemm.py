@@ -93,7 +93,7 @@ def main():
                 nout = N // 2 if epi == "silu" else N
                 out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
                 plan = ops.gemm_plan(M, N, K)
-                auto = [("skinny", "tile", "big", "dec", "big8").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
+                auto = [("skinny", "tile", "big", "dec", "big8", "mid8").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
                         plan["bn"], plan["splitk"]]
                 t = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, Ws[i % copies], out, auto, ops.EPILOGUES[epi], ws),
                            tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": auto, "auto": True})
@@ -117,7 +117,7 @@ def main():
                                 continue
                             if N % bn:
                                 continue
-                            for sk in ((1, 2, 4, 8, 16) if M <= 256 else (1,)):
+                            for sk in (1, 2, 4, 8, 16):
                                 if K // 64 < sk * 4:
                                     continue
                                 for st in (2, 3, 4):
@@ -131,10 +131,18 @@ def main():
                         for sk in (1, 2, 4, 8):
                             if K // 64 >= sk * 8:
                                 cands.append([3, sw, nwm * nwn, nwm, bm, bn, sk])
+                    # mid-M 8-wave kernel (kind 5): {5, ST, 0, 0, BM, BN, sk}
+                    if M >= 64:
+                        for bm, bn, st in ((256, 128, 3), (128, 256, 3), (128, 128, 4)):
+                            if N % bn or (bm == 256 and M <= 128):
+                                continue
+                            for sk in (1, 2, 3, 4, 6, 8, 12, 16):
+                                if K // 64 >= sk * 2:
+                                    cands.append([5, st, 0, 0, bm, bn, sk])
                     if M >= 128 and N % 256 == 0:
-                        for sk in (1, 2, 4):
+                        for sk in (1, 2, 4, 8, 16):
                             if K // 64 >= sk * 4:
-                                cands.append([4, 1, 0, 0, 256, 256, sk])
+                                cands.append([4, 5, 0, 0, 256, 256, sk])
                     for pl in cands:
                         try:
                             tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(

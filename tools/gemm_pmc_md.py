@@ -12,9 +12,8 @@ MFMA_CYCLES_PER_SIMD = 1.31e6
 
 
 def short(n):
-    m = re.search(r"gemm_big8_kernel<([^>]*)>", n) or re.search(r"gemm_big8_kernelI(\w+?)EEv", n)
-    if m:
-        return "gemm_big8_kernel<" + m.group(1) + ">"
+    if "gemm_big8_kernel" in n:
+        return "gemm_big8_kernel"
     m = re.search(r"(Cijk_\w+?MT\w+?_MI\w+?)_", n)
     return ("hipBLASLt " + m.group(1)[:60]) if m else None
 
