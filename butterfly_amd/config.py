@@ -222,11 +222,13 @@ class EngineConfig:
     # attention, parallel/context_parallel.py), its K/V collected in the cache of the replica
     # that then decodes it. 0 = off. Replicas step in lockstep while it is on.
     cp_prefill_min_tokens: int = 0
-    # overlapped decode for single-stage layouts (pp == 1, no EP): the asynchronous pipeline of
-    # engine/pipeline.py with one group, so the host schedules step k+1 (inputs gathered on the
-    # device from step k's sampled ids) while step k still runs, and token values reach the
-    # host one step late. Replaces mixed chunked prefill (prefill steps run on their own).
-    async_decode: bool = False
+    # overlapped decode for single-stage layouts (pp == 1, no EP; the serving default): the
+    # asynchronous pipeline of engine/pipeline.py with one group, so the host schedules step
+    # k+1 (inputs gathered on the device from step k's sampled ids) while step k still runs, and
+    # token values reach the host one step late. Mixed chunked prefill and prefix caching run
+    # inside it (a plan's decode rows and prompt chunks travel together). Off (synchronous
+    # steps) with context-parallel prefill, whose replicas step in lockstep.
+    async_decode: bool = True
     cp_attention: str = "ring"        # "ring" | "ulysses"
     # request-state snapshots (engine/state.py): every `snapshot_every` steps one rank per DP
     # replica writes <snapshot_dir>/replica-<dp>.json; LLM(..., resume=dir) replays it

@@ -142,16 +142,15 @@ class LLMEngine:
         # (pp == 1 with EngineConfig.async_decode: the same machinery with one group overlaps
         # the host's scheduling of step k+1 with the device's step k)
         self.async_pp = mesh.ep == 1 and flags.get("BFLY_PP_ASYNC") and (
-            mesh.pp > 1 or bool(engine_cfg.async_decode))
-        self.mixed = self.prefix_cache = False
+            mesh.pp > 1 or (bool(engine_cfg.async_decode) and not (engine_cfg.cp_prefill_min_tokens and mesh.dp > 1)))
+        # mixed steps (chunked prefill riding along decode rows, prefix caching): every
+        # non-EP layout; in the asynchronous pipeline each group's plans are mixed
+        self.mixed = bool(engine_cfg.mixed_prefill) and mesh.ep == 1 and (mesh.pp == 1 or self.async_pp)
+        self.prefix_cache = self.mixed and bool(engine_cfg.prefix_caching)
         if self.async_pp:
             self.scheduler = GroupedScheduler(native, self.kv.manager, mesh.pp, engine_cfg.max_batch,
-                                              engine_cfg.max_prefill_tokens)
+                                              engine_cfg.max_prefill_tokens, self.mixed, self.prefix_cache)
         else:
-            # mixed steps (chunked prefill riding along decode) need one forward per step over
-            # every row: single-stage, non-EP layouts
-            self.mixed = bool(engine_cfg.mixed_prefill) and mesh.pp == 1 and mesh.ep == 1
-            self.prefix_cache = self.mixed and bool(engine_cfg.prefix_caching)
             self.scheduler = native.Scheduler(self.kv.manager, engine_cfg.max_batch, engine_cfg.max_prefill_tokens,
                                               self.mixed, self.prefix_cache)
         self._tick = 0
@@ -606,7 +605,7 @@ class LLMEngine:
         if self._valued is not None:          # left at tick k - 2: values are on the host
             v, self._valued = self._valued, None
             out = self._apply_values(v, t0)
-            out.prefill_tokens = v.tokens if v.plan.kind == 1 else 0
+            out.prefill_tokens = int(sum(v.plan.prefill_lens)) if v.plan.kind in (1, 3) else 0
         if self._pending is not None:         # left at tick k - 1: advance, values next tick
             p, self._pending = self._pending, None
             self._advance(p)
@@ -616,9 +615,17 @@ class LLMEngine:
         g = k % pp
         plan = self.scheduler.groups[g].schedule()
         if plan.kind != 0:
-            rids = list(plan.seq_ids)
-            T = sum(plan.prefill_lens) if plan.kind == 1 else len(rids)
-            self._inflight.append(PipePlan(k, g, plan, rids, T, list(plan.cow)))
+            seqs = list(plan.seq_ids)
+            nd = plan.num_decode if plan.kind != 1 else 0
+            if plan.kind == 2:
+                rids, T = seqs, len(seqs)
+            else:   # prefill / mixed: decode rows, then chunks; a prompt's final chunk is sampled
+                fin = list(plan.prefill_final)
+                rids = seqs[:nd] + [r for r, f in zip(seqs[nd:], fin) if f]
+                T = nd + int(sum(plan.prefill_lens))
+            if plan.preempted:
+                self.metrics.inc("preempted_sequences", len(plan.preempted))
+            self._inflight.append(PipePlan(k, g, plan, rids, T, list(plan.cow), seqs=seqs))
             if s == 0:
                 with trace.range("pp.stage_work", tick=k, stage=0):
                     self._pp_stage_work(self._inflight[-1])
@@ -628,7 +635,8 @@ class LLMEngine:
             self._inflight.remove(leaving)
             if leaving.ids is None:
                 leaving.ids = torch.empty(len(leaving.rids), dtype=torch.int32, device=self.device)
-            self.comm.broadcast_(leaving.ids, src_in_group=pp - 1, group="pp")
+            if leaving.rids:   # (a plan of non-final prompt chunks samples nothing: every rank knows)
+                self.comm.broadcast_(leaving.ids, src_in_group=pp - 1, group="pp")
             # stream-ordered copy to pinned host memory; read one tick later
             if leaving.ids.is_cuda:
                 leaving.host = torch.empty(len(leaving.rids), dtype=torch.int32, pin_memory=True)
@@ -670,7 +678,8 @@ class LLMEngine:
         """Value-free part of applying a plan that left the pipeline: one more token per
         sequence (KV length, scheduler state), length-limit completion, and the deferred
         release of sequences whose stop token was seen while this plan was in flight."""
-        for r in p.rids:
+        sampled = set(p.rids)
+        for r in p.seqs:
             req = self.requests[r]
             if req.sched_done:
                 continue
@@ -678,6 +687,8 @@ class LLMEngine:
                 req.stopping = False
                 req.sched_done = True
                 self.scheduler.finish(r)
+                continue
+            if r not in sampled:              # a prompt chunk that does not complete the prompt
                 continue
             self.scheduler.on_token(r)
             req.n_gen += 1
@@ -696,9 +707,9 @@ class LLMEngine:
             raise RuntimeError(f"rank {self.rank}: non-finite logits at engine step {self.steps_done}")
         now = time.perf_counter()
         rids, toks, finished = [], [], []
-        inflight = {r for q in self._inflight for r in q.rids}
+        inflight = {r for q in self._inflight for r in q.seqs}
         if self._pending is not None:
-            inflight.update(self._pending.rids)
+            inflight.update(self._pending.seqs)
         for r, t in zip(p.rids, new):
             req = self.requests[r]
             if req.finished:
@@ -724,22 +735,45 @@ class LLMEngine:
         self.metrics.observe_step(p.kind, len(rids), dt)
         return StepOutput(p.kind, rids, toks, finished, dt)
 
-    def _first_stage_ids(self, p: PipePlan):
-        """Input ids of a decode plan entering stage 0: the sequences' last tokens. Those
-        sampled by the group's previous plan (values not on the host yet) are gathered on the
-        device from its broadcast ids; older ones come from the host."""
+    def _first_stage_ids(self, p: PipePlan, rids: Optional[list] = None):
+        """Input ids of the decode rows (`rids`, default the plan's) of a plan entering stage
+        0: the sequences' last tokens. Those sampled by the group's previous plan (values not on
+        the host yet) are gathered on the device from its broadcast ids; older ones come from
+        the host."""
+        rids = p.rids if rids is None else rids
         src = self._last_left.get(p.group)
         where = {r: i for i, r in enumerate(src.rids)} if src is not None and src is self._valued else {}
-        if not where or not any(r in where for r in p.rids):
-            return np.asarray([self.requests[r].tokens[-1] for r in p.rids], dtype=np.int32)
+        if not where or not any(r in where for r in rids):
+            return np.asarray([self.requests[r].tokens[-1] for r in rids], dtype=np.int32)
         # one H2D copy of [host ids | source rows] and one row gather (ops.gather_rows: rows
         # with source -1 keep their host id)
-        n = len(p.rids)
-        staged = torch.tensor([0 if r in where else self.requests[r].tokens[-1] for r in p.rids] +
-                              [where.get(r, -1) for r in p.rids], dtype=torch.int32).to(src.ids.device, non_blocking=True)
+        n = len(rids)
+        staged = torch.tensor([0 if r in where else self.requests[r].tokens[-1] for r in rids] +
+                              [where.get(r, -1) for r in rids], dtype=torch.int32).to(src.ids.device, non_blocking=True)
         ids = staged[:n]
         ops.gather_rows(src.ids.view(-1, 1), staged[n:], out=ids.view(-1, 1))
         return ids
+
+    def _chunk_tokens(self, p: PipePlan):
+        """tokens_of(sid) for the prompt chunks of a plan: the request's host tokens. A
+        sequence preempted for recompute may need the token its group's previous plan sampled,
+        whose value is not applied yet (it is applied next tick): that plan's pinned copy is
+        read now (one event wait, only in this case)."""
+        need = {}
+        nd = p.plan.num_decode if p.plan.kind != 1 else 0
+        for j, sid in enumerate(list(p.plan.seq_ids)[nd:]):
+            need[sid] = int(p.plan.prefill_starts[j]) + int(p.plan.prefill_lens[j]) if self.mixed \
+                else len(p.plan.prefill_slots[j])
+        v = self._valued
+        extra = {}
+        if v is not None and v.rids and any(len(self.requests[r].tokens) < n for r, n in need.items()):
+            if v.event is not None:
+                v.event.synchronize()
+            extra = {r: int(t) for r, t in zip(v.rids, v.host.tolist())}
+            self.metrics.inc("pp_value_peeks")
+        if not extra:
+            return lambda r: self.requests[r].tokens
+        return lambda r: self.requests[r].tokens + ([extra[r]] if r in extra else [])
 
     def _pp_stage_work(self, p: PipePlan) -> None:
         """recv the residual stream (stage > 0) -> run this stage -> isend (not last) or sample
@@ -765,8 +799,16 @@ class LLMEngine:
         def run(mb, h):
             if p.cow:
                 self.kv.copy_blocks(p.cow)
-            if p.plan.kind == 1:
-                out = self.runner.run(self.runner.prefill_batch(p.plan, lambda r: self.requests[r].tokens), h)
+            if self.mixed and p.plan.kind in (1, 3):
+                fb, _ = self.runner.mixed_batch(p.plan, self._chunk_tokens(p))
+                nd = p.plan.num_decode
+                if self.pp_first and nd:
+                    ids = self._first_stage_ids(p, list(p.plan.seq_ids)[:nd])
+                    if isinstance(ids, torch.Tensor):
+                        fb.input_ids[:nd].copy_(ids)
+                out = self.runner.run(fb, h)
+            elif p.plan.kind == 1:
+                out = self.runner.run(self.runner.prefill_batch(p.plan, self._chunk_tokens(p)), h)
             else:
                 ids = self._first_stage_ids(p) if self.pp_first else np.zeros(len(p.rids), dtype=np.int32)
                 out = self.runner.run_decode(self.runner.decode_inputs(p.plan, ids), h)
@@ -792,7 +834,7 @@ class LLMEngine:
                     self._sends.append(w)
 
         def sample(mb, out):
-            p.ids = self._sample(out, p.rids)
+            p.ids = self._sample(out, p.rids) if p.rids else torch.empty(0, dtype=torch.int32, device=self.device)
 
         self._execute(self._ops(1, native_dec), recv, run, send, sample)
 

@@ -29,19 +29,31 @@ from typing import Optional
 
 class GroupedScheduler:
     """`groups` replicated C++ schedulers (runtime/scheduler.cpp) sharing one KV block manager;
-    new requests go to the least-loaded group (deterministic: ties -> lowest index)."""
+    new requests go to the least-loaded group (deterministic: ties -> lowest index). `mixed`:
+    every group runs the scheduler's mixed mode (its decode rows and prompt chunks in one plan,
+    long prompts prefilled over several ticks), with automatic prefix caching over the shared
+    block manager when `prefix_cache`."""
 
-    def __init__(self, native, kv_manager, groups: int, max_batch: int, max_prefill_tokens: int):
+    def __init__(self, native, kv_manager, groups: int, max_batch: int, max_prefill_tokens: int,
+                 mixed: bool = False, prefix_cache: bool = False):
         self.group_batch = max(1, -(-max_batch // groups))
-        self.groups = [native.Scheduler(kv_manager, self.group_batch, max_prefill_tokens)
+        self.mixed, self.prefix_cache = mixed, mixed and prefix_cache
+        self.groups = [native.Scheduler(kv_manager, self.group_batch, max_prefill_tokens, mixed, self.prefix_cache)
                        for _ in range(groups)]
         self.owner: dict[int, int] = {}
 
-    def add(self, rid: int, prompt_len: int, max_new: int) -> None:
+    def add(self, rid: int, prompt_len: int, max_new: int, tokens: Optional[list] = None) -> None:
         g = min(range(len(self.groups)),
                 key=lambda i: (self.groups[i].num_running + self.groups[i].num_waiting, i))
-        self.groups[g].add(rid, prompt_len, max_new)
+        if self.prefix_cache and tokens is not None:
+            self.groups[g].add(rid, prompt_len, max_new, tokens)
+        else:
+            self.groups[g].add(rid, prompt_len, max_new)
         self.owner[rid] = g
+
+    @property
+    def prefix_hit_tokens(self) -> int:
+        return sum(g.prefix_hit_tokens for g in self.groups)
 
     def on_token(self, rid: int) -> None:
         self.groups[self.owner[rid]].on_token(rid)
@@ -69,14 +81,16 @@ class PipePlan:
     """One group's step plan travelling through the stages."""
     tick: int                 # tick at which it entered stage 0
     group: int
-    plan: object              # native StepPlan (kind 1 prefill / 2 decode)
-    rids: list
+    plan: object              # native StepPlan (kind 1 prefill / 2 decode / 3 mixed)
+    rids: list                # sequences whose row is sampled (mixed: decode rows and prompts
+                              # whose final chunk this plan runs), in logits-row order
     tokens: int               # rows of the residual stream between stages
     cow: list = field(default_factory=list)
+    seqs: list = field(default_factory=list)   # every sequence with a row in the plan
     ids: Optional[object] = None   # sampled ids tensor (last stage / after broadcast)
     host: Optional[object] = None  # pinned host copy of `ids` (async D2H at broadcast time)
     event: Optional[object] = None # marks that copy complete
 
     @property
     def kind(self) -> str:
-        return "prefill" if self.plan.kind == 1 else "decode"
+        return {1: "prefill", 3: "mixed"}.get(self.plan.kind, "decode")

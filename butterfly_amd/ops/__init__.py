@@ -61,8 +61,27 @@ def library_path() -> str:
     return str(_LIB_PATH)
 
 
+_FORCE_REF = False
+
+
+class reference_mode:
+    """Route every op to its fp32 PyTorch reference (ops/reference.py) even for GPU tensors:
+    tests build an fp32 reference model on the same GPU as the kernel model (full-size layers
+    whose CPU reference would take minutes). Not thread-scoped; tests only."""
+
+    def __enter__(self):
+        global _FORCE_REF
+        self._prev, _FORCE_REF = _FORCE_REF, True
+        return self
+
+    def __exit__(self, *exc):
+        global _FORCE_REF
+        _FORCE_REF = self._prev
+        return False
+
+
 def _gpu(t: torch.Tensor) -> bool:
-    if not t.is_cuda:
+    if not t.is_cuda or _FORCE_REF:
         return False
     if not load_library():
         raise RuntimeError(f"butterfly_amd HIP kernels unavailable: {_load_error}")

@@ -117,6 +117,81 @@ def test_async_pipeline_matches_single(preset, mesh_kw, world):
         assert run_world(_mixed_generate, world, preset, mesh_kw, 4, False)[0] == ref
 
 
+LONG = [[(7 * i + 3) % 97 + 1 for i in range(40)], [(5 * i + 1) % 89 + 1 for i in range(23)]]
+
+
+def _chunked_generate(rank, world, preset, mesh_kw, async_pp, shared_prefix=False, kv_tokens=2048, prompts=None,
+                      max_new=4):
+    """Prompts longer than the step's token budget (prefilled in chunks over several steps /
+    ticks, decode rows riding along), more requests than the batch holds, a request added
+    mid-run; with `shared_prefix` every prompt starts with the same 64 tokens (prefix cache);
+    with a small `kv_tokens` the cache forces preemption and recompute."""
+    import os
+
+    from butterfly_amd.parallel.comm import Communicator
+
+    saved = os.environ.get("BFLY_PP_ASYNC")
+    os.environ["BFLY_PP_ASYNC"] = "1" if async_pp else "0"
+    mesh = Mesh(**mesh_kw)
+    comm = Communicator.from_mesh(mesh) if world > 1 else None
+    cfg = ModelConfig.from_preset(preset)
+    ecfg = EngineConfig(max_batch=4, max_seq_len=160, kv_cache_tokens=kv_tokens, max_prefill_tokens=24,
+                        use_graphs=False, seed=5, async_decode=async_pp, mixed_prefill=True, prefix_caching=True)
+    try:
+        eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")
+        assert eng.mixed and eng.async_pp == async_pp
+    finally:
+        if saved is None:
+            os.environ.pop("BFLY_PP_ASYNC", None)
+        else:
+            os.environ["BFLY_PP_ASYNC"] = saved
+    head = [(11 * i) % 83 + 2 for i in range(64)] if shared_prefix else []
+    prompts = [head + p for p in (prompts or LONG + PROMPTS)]
+    rids = [eng.add_request(p, SamplingParams(max_tokens=max_new + i, ignore_eos=True)) for i, p in enumerate(prompts)]
+    kinds = set()
+    for _ in range(4):
+        kinds.add(eng.step().kind)
+    rids.append(eng.add_request(head + LONG[0][:30], SamplingParams(max_tokens=5, ignore_eos=True)))
+    while eng.has_unfinished():
+        kinds.add(eng.step().kind)
+    hits = eng.scheduler.prefix_hit_tokens
+    pre = eng.metrics.counters.get("preempted_sequences", 0) if hasattr(eng.metrics, "counters") else 0
+    return [eng.requests[r].output for r in rids], sorted(kinds), hits, pre
+
+
+@pytest.mark.parametrize("preset,mesh_kw,world", [
+    ("llama-tiny", {}, 1),
+    ("llama-tiny", dict(pp=2), 2),
+    ("llama-tiny", dict(tp=2), 2),
+    ("llama-tiny", dict(tp=2, pp=2), 4),
+])
+@pytest.mark.parametrize("shared_prefix", [False, True])
+def test_async_mixed_chunked_prefill_matches_sync(preset, mesh_kw, world, shared_prefix):
+    """Mixed plans (decode rows + prompt chunks) in the asynchronous pipeline: chunked prompts
+    over several ticks, prefix-cache hits, PP stages: the tokens of the synchronous
+    single-process engine."""
+    ref, ref_kinds, _, _ = _chunked_generate(0, 1, preset, {}, False, shared_prefix)
+    assert "mixed" in ref_kinds
+    outs = (run_world(_chunked_generate, world, preset, mesh_kw, True, shared_prefix) if world > 1
+            else [_chunked_generate(0, 1, preset, {}, True, shared_prefix)])
+    for o, kinds, hits, _ in outs:
+        assert o == ref
+        assert "mixed" in kinds
+        if shared_prefix:
+            assert hits > 0
+
+
+def test_async_mixed_preemption_recompute_matches_sync():
+    """A KV cache too small for every running sequence: preempted sequences are re-prefilled
+    (prompt + tokens generated so far) in later chunks, including the token sampled by the
+    plan right before (its value read from the pinned copy, not yet applied)."""
+    prompts = [[(3 * i + j) % 90 + 1 for i in range(30)] for j in range(4)]
+    ref, _, _, pre = _chunked_generate(0, 1, "llama-tiny", {}, False, kv_tokens=160, prompts=prompts, max_new=12)
+    got, _, _, pre_async = _chunked_generate(0, 1, "llama-tiny", {}, True, kv_tokens=160, prompts=prompts, max_new=12)
+    assert pre > 0 and pre_async > 0, "the configuration must preempt"
+    assert got == ref
+
+
 def test_data_parallel_replicas():
     halves = [PROMPTS[:2], PROMPTS[2:]]
     outs = run_world(_dist_generate, 2, "llama-tiny", dict(dp=2), halves, 6)

@@ -121,4 +121,6 @@ def test_nan_fault_fails_the_step(monkeypatch):
     eng.step()
     eng.step()
     with pytest.raises(RuntimeError, match="non-finite"):
-        eng.step()
+        # the overlapped engine reads a step's token values two steps later
+        for _ in range(3 if eng.async_pp else 1):
+            eng.step()
