@@ -933,6 +933,14 @@ struct MidCfg {
   static_assert(ST * SLOT <= 160 * 1024, "mid ring exceeds the LDS");
 };
 
+// One 1-KiB LDS-DMA block through a buffer descriptor (a __device__ helper: the builtin's LDS
+// address-space cast inside the kernel template's lambda left the template uninstantiable on
+// the host side, i.e. no launch stub was emitted)
+template <int AUX>
+__device__ __forceinline__ void mid_dma1(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, soff, 0, AUX);
+}
+
 template <int BM, int BN, int ST>
 __global__ void __launch_bounds__(kMidThreads)
 gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
@@ -975,12 +983,9 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     for (int j = 0; j < H; ++j) {
       const int i = half * H + j;
       const int blk = wid + 8 * i;
-      if (i < BM / 64)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr_t)(s + blk * 1024), 16, voff[i], soff, 0, 0);
-      else if (wpol)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr_t)(s + blk * 1024), 16, voff[i], soff, 0, 2);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr_t)(s + blk * 1024), 16, voff[i], soff, 0, 0);
+      if (i < BM / 64) mid_dma1<0>(rsa, s + blk * 1024, voff[i], soff);
+      else if (wpol) mid_dma1<2>(rsb, s + blk * 1024, voff[i], soff);
+      else mid_dma1<0>(rsb, s + blk * 1024, voff[i], soff);
     }
   };
   // retire this wave's DMA of the K-tiles before `k + 1` (k + 1 .. k + ST - 1 may fly)
