@@ -141,7 +141,9 @@ class LLMEngine:
         # (engine/pipeline.py); EP layouts keep the synchronous path (EP collectives span DP ranks)
         # (pp == 1 with EngineConfig.async_decode: the same machinery with one group overlaps
         # the host's scheduling of step k+1 with the device's step k)
-        self.async_pp = mesh.ep == 1 and flags.get("BFLY_PP_ASYNC") and (
+        # (EP layouts, pp == 1, too: the EP ranks agree on padding / step mode over the gloo
+        # control plane, which never waits for the device)
+        self.async_pp = flags.get("BFLY_PP_ASYNC") and (mesh.ep == 1 or mesh.pp == 1) and (
             mesh.pp > 1 or (bool(engine_cfg.async_decode) and not (engine_cfg.cp_prefill_min_tokens and mesh.dp > 1)))
         # mixed steps (chunked prefill riding along decode rows, prefix caching): every
         # non-EP layout; in the asynchronous pipeline each group's plans are mixed
@@ -614,6 +616,20 @@ class LLMEngine:
         # schedule the group entering stage 0 (every rank: replicated deterministic state)
         g = k % pp
         plan = self.scheduler.groups[g].schedule()
+        ep_pad = any_prefill = 0
+        if self.mesh.ep > 1:
+            # every EP rank runs a step whenever one of them has work (the MoE exchange meets
+            # every peer), padded to the same rows; a prefill anywhere switches the step to the
+            # variable exchange. Host integers over the gloo control plane: no device sync.
+            t_local = 0 if plan.kind == 0 else (sum(plan.prefill_lens) if plan.kind == 1 else len(plan.seq_ids))
+            ep_pad, any_prefill, anyw = self.comm.all_reduce_max_int(
+                [t_local, int(plan.kind == 1), int(plan.kind != 0)], "ep")
+            if plan.kind == 0 and anyw:
+                eb = empty_batch(self.device, ep_pad)
+                eb.ep_alltoall = bool(any_prefill)
+                self.runner.run(eb)
+                if not out.new_tokens:
+                    out.kind = "ep-idle"
         if plan.kind != 0:
             seqs = list(plan.seq_ids)
             nd = plan.num_decode if plan.kind != 1 else 0
@@ -625,7 +641,8 @@ class LLMEngine:
                 T = nd + int(sum(plan.prefill_lens))
             if plan.preempted:
                 self.metrics.inc("preempted_sequences", len(plan.preempted))
-            self._inflight.append(PipePlan(k, g, plan, rids, T, list(plan.cow), seqs=seqs))
+            self._inflight.append(PipePlan(k, g, plan, rids, T, list(plan.cow), seqs=seqs, ep_pad=ep_pad,
+                                           ep_prefill=bool(any_prefill)))
             if s == 0:
                 with trace.range("pp.stage_work", tick=k, stage=0):
                     self._pp_stage_work(self._inflight[-1])
@@ -808,10 +825,14 @@ class LLMEngine:
                         fb.input_ids[:nd].copy_(ids)
                 out = self.runner.run(fb, h)
             elif p.plan.kind == 1:
-                out = self.runner.run(self.runner.prefill_batch(p.plan, self._chunk_tokens(p)), h)
+                fb = self.runner.prefill_batch(p.plan, self._chunk_tokens(p))
+                fb.ep_tokens = p.ep_pad
+                fb.ep_alltoall = self.mesh.ep > 1
+                out = self.runner.run(fb, h)
             else:
                 ids = self._first_stage_ids(p) if self.pp_first else np.zeros(len(p.rids), dtype=np.int32)
-                out = self.runner.run_decode(self.runner.decode_inputs(p.plan, ids), h)
+                out = self.runner.run_decode(self.runner.decode_inputs(p.plan, ids), h, ep_tokens=p.ep_pad,
+                                             graphs_ok=not p.ep_prefill, ep_alltoall=p.ep_prefill)
             posted = state.get("posted")
             if posted is not None and self._comm_stream is not None:
                 ev = torch.cuda.Event()

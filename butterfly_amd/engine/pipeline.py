@@ -87,6 +87,8 @@ class PipePlan:
     tokens: int               # rows of the residual stream between stages
     cow: list = field(default_factory=list)
     seqs: list = field(default_factory=list)   # every sequence with a row in the plan
+    ep_pad: int = 0           # expert parallelism: rows every EP rank pads this step to
+    ep_prefill: bool = False  # some EP rank prefills this step (variable exchange, no graphs)
     ids: Optional[object] = None   # sampled ids tensor (last stage / after broadcast)
     host: Optional[object] = None  # pinned host copy of `ids` (async D2H at broadcast time)
     event: Optional[object] = None # marks that copy complete

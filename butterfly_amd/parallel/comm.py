@@ -55,6 +55,7 @@ class GroupHandle:
     pg: Optional[object]          # torch ProcessGroup, None when size == 1
     rank_in_group: int
     native: Optional[object] = None   # parallel/rccl.RcclComm (BFLY_NATIVE_RCCL) for the data path
+    ctrl: Optional[object] = None     # gloo ProcessGroup for host integers when `pg` is RCCL
 
     @property
     def size(self) -> int:
@@ -99,6 +100,15 @@ class Communicator:
                 if rank in ranks:
                     mine = GroupHandle(ranks, pg, ranks.index(rank))
             groups[axis] = mine
+        if dist.get_backend() == "nccl" and mesh.dp > 1:
+            # control plane of the data-parallel / expert-parallel axis: host integers (EP
+            # padding and step-mode agreement, lockstep liveness) over gloo on CPU tensors, so
+            # agreeing never waits for the device (an RCCL all-reduce read back with .tolist()
+            # would drain the compute stream every step)
+            for ranks in mesh.all_groups("dp"):
+                cpg = dist.new_group(ranks, backend="gloo")
+                if rank in ranks:
+                    groups["dp"].ctrl = cpg
         groups["ep"] = groups["dp"] if mesh.ep > 1 else GroupHandle([rank], None, 0)
         groups["world"] = GroupHandle(list(range(mesh.world_size)), dist.group.WORLD, rank)
         comm = cls(mesh, rank, groups)
@@ -480,6 +490,10 @@ class Communicator:
         g = self.groups[group]
         if g.size == 1:
             return list(values)
+        if g.ctrl is not None:        # gloo control plane: no device work, no stream sync
+            t = torch.tensor(values, dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.ctrl)
+            return [int(v) for v in t.tolist()]
         dev = "cuda" if dist.get_backend(g.pg) == "nccl" else "cpu"
         t = torch.tensor(values, dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.pg)

@@ -208,6 +208,48 @@ def test_expert_parallel_mixtral():
     assert outs[1] == _single("mixtral-tiny", halves[1])
 
 
+def _ep_async_generate(rank, world, mesh_kw, async_pp):
+    """Expert-parallel replicas with uneven loads (replica r gets r + 1 requests, one more added
+    mid-run on replica 0 only): idle ranks must keep joining their peers' MoE exchanges."""
+    import os
+
+    from butterfly_amd.parallel.comm import Communicator
+
+    saved = os.environ.get("BFLY_PP_ASYNC")
+    os.environ["BFLY_PP_ASYNC"] = "1" if async_pp else "0"
+    mesh = Mesh(**mesh_kw)
+    comm = Communicator.from_mesh(mesh)
+    cfg = ModelConfig.from_preset("mixtral-tiny")
+    ecfg = EngineConfig(max_batch=4, max_seq_len=96, kv_cache_tokens=1024, use_graphs=False, seed=5)
+    try:
+        eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")
+        assert eng.async_pp == async_pp
+    finally:
+        if saved is None:
+            os.environ.pop("BFLY_PP_ASYNC", None)
+        else:
+            os.environ["BFLY_PP_ASYNC"] = saved
+    dp = mesh.coord(rank).dp
+    mine = [PROMPTS[(dp + i) % len(PROMPTS)] for i in range(dp + 1)]
+    rids = [eng.add_request(p, SamplingParams(max_tokens=3 + i + dp, ignore_eos=True)) for i, p in enumerate(mine)]
+    for _ in range(3):
+        eng.step()
+    if dp == 0:
+        rids.append(eng.add_request([9, 8, 7], SamplingParams(max_tokens=5, ignore_eos=True)))
+    while eng.has_unfinished_global():
+        eng.step()
+    return [eng.requests[r].output for r in rids]
+
+
+@pytest.mark.parametrize("mesh_kw,world", [(dict(dp=2, ep=2), 2), (dict(dp=4, ep=4), 4)])
+def test_expert_parallel_async_matches_sync(mesh_kw, world):
+    """EP layouts on the asynchronous engine (host agreement over the control plane, token
+    values one step late) give every replica the tokens of the synchronous EP engine."""
+    ref = run_world(_ep_async_generate, world, mesh_kw, False)
+    got = run_world(_ep_async_generate, world, mesh_kw, True)
+    assert got == ref
+
+
 def _probe_worker(rank, world):
     import torch
 
