@@ -186,7 +186,8 @@ class LLMEngine:
             ops.reserve_workspace(self.device, max_tokens=max(engine_cfg.max_prefill_tokens, engine_cfg.max_batch),
                                   max_n=self._max_gemm_n(), max_k=self._max_gemm_k(),
                                   max_batch=max(engine_cfg.graph_batch_sizes + [engine_cfg.max_batch]),
-                                  max_ctx=engine_cfg.max_seq_len, num_kv_heads=d.hkv, head_dim=cfg.head_dim)
+                                  max_ctx=engine_cfg.max_seq_len, num_kv_heads=d.hkv, head_dim=cfg.head_dim,
+                                  shapes=self.model.gemm_shapes())
         buckets = [b for b in engine_cfg.graph_batch_sizes if b <= engine_cfg.max_batch] or [engine_cfg.max_batch]
         if self.async_pp and self.scheduler.group_batch not in buckets:
             buckets.append(self.scheduler.group_batch)    # a full group replays one graph

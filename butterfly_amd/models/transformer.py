@@ -619,6 +619,10 @@ class TransformerLM:
         bits = torch.finfo(dtype or self.dtype).bits
         return 2 * len(self.layer_ids) * self.dims.hkv * self.cfg.head_dim * bits // 8
 
+    def gemm_shapes(self) -> list:
+        """(N, K) of every weight this stage multiplies by (workspace sizing)."""
+        return sorted({tuple(w.shape) for k, w in self.p.items() if w.dim() == 2 and k != "embed"})
+
     def allocate_kv_cache(self, num_blocks: int, block_size: int, dtype: Optional[torch.dtype] = None) -> list:
         D, hk = self.cfg.head_dim, self.dims.hkv
         dt = dtype or self.dtype

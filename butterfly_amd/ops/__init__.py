@@ -102,6 +102,9 @@ class _Arena:
     def __init__(self):
         self.bufs: dict[tuple, torch.Tensor] = {}
         self.frozen = False
+        # buffers replaced by a larger one stay allocated: a hipGraph captured earlier still
+        # reads / writes the old address (freeing it would hand that memory to someone else)
+        self.retired: list = []
 
     def get(self, device, name: str, numel: int, dtype, zero: bool = False) -> torch.Tensor:
         key = (str(device), name, dtype, getattr(_scope, "name", None))
@@ -111,6 +114,8 @@ class _Arena:
                 raise RuntimeError(
                     f"workspace '{name}' needs {numel} elements but is frozen/capturing; "
                     "call ops.reserve_workspace() before capture")
+            if buf is not None:
+                self.retired.append(buf)
             buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
             if zero:
                 zero_(buf)
@@ -165,15 +170,20 @@ def arena_scope(name) -> None:
 
 
 def reserve_workspace(device, max_tokens: int, max_n: int, max_k: int, max_batch: int = 0,
-                      max_ctx: int = 0, num_kv_heads: int = 0, head_dim: int = 128) -> None:
-    """Pre-size every workspace for problems up to the given bounds (call before capture)."""
+                      max_ctx: int = 0, num_kv_heads: int = 0, head_dim: int = 128, shapes=()) -> None:
+    """Pre-size every workspace for problems up to the given bounds (call before capture).
+    `shapes`: the model's GEMM weight shapes (N, K); the split-K slab need is the max over them
+    and every token-count bucket of the plan table (a tuned plan may split a small projection
+    more than the largest one is split)."""
     if not load_library():
         return
     ws = 0
-    for m in sorted({1, 16, 32, 48, 64, 128, 256, max_tokens}):
+    nk = {(int(max_n), int(max_k))} | {(int(n), int(k)) for n, k in shapes}
+    for m in sorted({1, 16, 32, 48, 64, 128, 256, 512, max_tokens}):
         if m > max_tokens:
             continue
-        ws = max(ws, torch.ops.bfly.gemm_workspace_size(m, max_n, max_k))
+        for n, k in nk:
+            ws = max(ws, torch.ops.bfly.gemm_workspace_size(m, n, k))
     _arena.get(device, "gemm", ws // 4 + 1, torch.float32, zero=True)
     if max_batch and max_ctx:
         ns = max(torch.ops.bfly.attn_decode_splits(max_ctx, torch.ops.bfly.attn_decode_part_tokens(b, num_kv_heads, max_ctx))

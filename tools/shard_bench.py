@@ -68,7 +68,7 @@ def main():
                       ctx_lens=torch.full((B,), ctx, dtype=torch.int32, device=dev), max_ctx=ctx + 1)
     ops.reserve_workspace(dev, B, max(cfg.vocab_size // tp, 4 * cfg.intermediate_size // tp, 16384),
                           max(cfg.hidden_size, cfg.intermediate_size // tp), B, ctx + 1,
-                          max(1, cfg.num_kv_heads // tp), cfg.head_dim)
+                          max(1, cfg.num_kv_heads // tp), cfg.head_dim, shapes=model.gemm_shapes())
     print(f"[shard_bench] {cfg.name} tp{tp} rank-0 shard, batch {B}, ctx {ctx}: "
           f"{model.local_bytes() / 1e9:.1f} GB weights, built in {time.perf_counter() - t0:.1f}s", flush=True)
     s = torch.cuda.Stream()
