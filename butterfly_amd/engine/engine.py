@@ -193,6 +193,12 @@ class LLMEngine:
             buckets.append(self.scheduler.group_batch)    # a full group replays one graph
         self.runner = ModelRunner(self.model, self.kv, engine_cfg.max_seq_len, engine_cfg.use_graphs,
                                   buckets, max_batch=engine_cfg.max_batch)
+        if flags.get("BFLY_GRAPH_SAMPLING"):
+            # the last stage's decode graphs end with the sampler on per-request temperatures /
+            # seeds staged with the other inputs: one replay per step yields the tokens
+            # (top-k / top-p rows and poisoned steps sample eagerly from the graph's logits)
+            check = bool(flags.get("BFLY_NAN_CHECK"))
+            self.runner.sample_fn = lambda lg, t, sd: self.sampler.sample(lg, t, sd, None, check_finite=check)
         # byte-minimal EP dispatch for the decode MoE layer (collective over the EP group, so
         # every EP rank sets it up here, eagerly, before any graph capture)
         self.ep_ipc = self.ep_ipc_prefill = False
@@ -334,7 +340,21 @@ class LLMEngine:
             t.fill_(float("nan"))
         return t
 
-    def _sample(self, logits: torch.Tensor, rids: list) -> torch.Tensor:
+    def _decode_sampling(self, rids: list) -> tuple:
+        """Per-row temperatures / seeds of a decode plan for the graph's sampler (the values
+        _sample_params gives the eager sampler), and whether some row needs the top-k / top-p
+        filter (sampled eagerly instead)."""
+        reqs = [self.requests[r] for r in rids]
+        temps = np.asarray([max(0.0, q.params.temperature) for q in reqs], dtype=np.float32)
+        seeds = np.asarray([(q.params.seed or r) * 1000003 + q.n_gen for q, r in zip(reqs, rids)], dtype=np.int64)
+        return temps, seeds, any(q.params.needs_filter for q in reqs)
+
+    def _sample(self, logits: torch.Tensor, rids: list, graph_ids=None) -> torch.Tensor:
+        if graph_ids is not None and not self._poison:
+            return graph_ids
+        return self._sample_eager(logits, rids)
+
+    def _sample_eager(self, logits: torch.Tensor, rids: list) -> torch.Tensor:
         """Sample one token per row. With BFLY_NAN_CHECK the sampling kernel also flags rows
         with non-finite logits (id -1, no extra kernel, no host sync); a poisoned or corrupted
         step then raises in _apply_tokens instead of emitting garbage tokens."""
@@ -832,7 +852,12 @@ class LLMEngine:
                 out = self.runner.run(fb, h)
             else:
                 ids = self._first_stage_ids(p) if self.pp_first else np.zeros(len(p.rids), dtype=np.int32)
-                out = self.runner.run_decode(self.runner.decode_inputs(p.plan, ids), h, ep_tokens=p.ep_pad,
+                inp = self.runner.decode_inputs(p.plan, ids)
+                filtered = False
+                if self.pp_last and self.runner.sample_fn is not None:
+                    inp["temps"], inp["seeds"], filtered = self._decode_sampling(p.rids)
+                state["filtered"] = filtered
+                out = self.runner.run_decode(inp, h, ep_tokens=p.ep_pad,
                                              graphs_ok=not p.ep_prefill, ep_alltoall=p.ep_prefill)
             posted = state.get("posted")
             if posted is not None and self._comm_stream is not None:
@@ -856,7 +881,9 @@ class LLMEngine:
                     self._sends.append(w)
 
         def sample(mb, out):
-            p.ids = self._sample(out, p.rids) if p.rids else torch.empty(0, dtype=torch.int32, device=self.device)
+            graph_ids = self.runner.last_ids if (p.plan.kind == 2 and not state.get("filtered")) else None
+            p.ids = self._sample(out, p.rids, graph_ids) if p.rids else \
+                torch.empty(0, dtype=torch.int32, device=self.device)
 
         self._execute(self._ops(1, native_dec), recv, run, send, sample)
 

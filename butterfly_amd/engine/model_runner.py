@@ -49,18 +49,22 @@ def _recover_from_capture(device) -> None:
 
 
 class _DecodeGraph:
-    """Static inputs / output of one decode graph (bucket). The int32 inputs are views of ONE
-    device buffer [ids | positions | slots | ctx_lens | block tables], so a step stages them
-    with a single host-to-device copy from a pinned buffer (two, alternating, each reused only
-    after the event of its previous copy)."""
+    """Static inputs / output of one decode graph (bucket). The inputs are views of ONE int32
+    device buffer [ids | positions | slots | ctx_lens | block tables | temperatures (f32 bits)
+    | seeds (int64)], so a step stages them with a single host-to-device copy from a pinned
+    buffer (two, alternating, each reused only after the event of its previous copy). A last
+    stage's graph ends with the sampling kernel (and the TP merge) on those per-request
+    temperatures / seeds: `ids` are the step's tokens, one replay per step."""
 
     def __init__(self, bucket: int, max_blocks: int, device, hidden: int, first: bool):
         b = bucket
         self.bucket = bucket
         self.max_blocks = max_blocks
+        self.off_t = b * (4 + max_blocks)                 # temperatures
+        self.off_s = (self.off_t + b + 1) // 2 * 2        # seeds: 8-byte aligned int32 offset
         # initial state built on the host and copied once: padding rows have no cache slot (-1)
         # and context 1 (no torch fill kernels on the device)
-        init = torch.zeros(b * (4 + max_blocks), dtype=torch.int32)
+        init = torch.zeros(self.off_s + 2 * b, dtype=torch.int32)
         init[2 * b:3 * b] = -1
         init[3 * b:4 * b] = 1
         self.inbuf = init.to(device)
@@ -68,7 +72,10 @@ class _DecodeGraph:
         self.positions = self.inbuf[b:2 * b]
         self.slots = self.inbuf[2 * b:3 * b]
         self.ctx_lens = self.inbuf[3 * b:4 * b]
-        self.block_tables = self.inbuf[4 * b:].view(b, max_blocks)
+        self.block_tables = self.inbuf[4 * b:self.off_t].view(b, max_blocks)
+        self.temps = self.inbuf[self.off_t:self.off_t + b].view(torch.float32)
+        self.seeds = self.inbuf[self.off_s:self.off_s + 2 * b].view(torch.int64)
+        self.ids: Optional[torch.Tensor] = None     # sampled in the graph (last stage)
         pin = torch.cuda.is_available() and torch.device(device).type == "cuda"
         self.host = [torch.zeros(self.inbuf.numel(), dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self.host_np = [h.numpy() for h in self.host]
@@ -105,6 +112,10 @@ class ModelRunner:
         # native pipeline I/O (set_pipeline_io)
         self.recv_fn = None
         self.instances = 1
+        # sample_fn(logits, temps, seeds) -> ids, captured at the end of a last stage's decode
+        # graphs (set by the engine); last_ids: the ids of the latest graph replay, else None
+        self.sample_fn = None
+        self.last_ids: Optional[torch.Tensor] = None
         self._flip: dict = {}          # bucket -> index of the instance replayed next
         self.last_instance: Optional[_DecodeGraph] = None
 
@@ -217,6 +228,7 @@ class ModelRunner:
         shape; steps where some EP rank is prefilling run eagerly (graphs_ok=False)."""
         B = len(inp["ids"])
         need = max(B, ep_tokens)
+        self.last_ids = None
         if self.recv_fn is not None or self.instances > 1:
             if need > self.buckets[-1]:
                 raise RuntimeError(f"pipeline decode of {need} rows exceeds the largest bucket {self.buckets[-1]}")
@@ -241,6 +253,8 @@ class ModelRunner:
                 return self.run(self.decode_batch(inp, ep_tokens), hidden_in)
         self._stage(g, inp, hidden_in)
         g.graph.replay()
+        if g.ids is not None:
+            self.last_ids = g.ids[:B]
         return g.output[:B]
 
     def _run_pipeline_decode(self, bucket: int, inp: dict, hidden_in):
@@ -278,6 +292,8 @@ class ModelRunner:
         self._stage(g, inp, None if self.recv_fn is not None else hidden_in)
         if g.graph is not None:
             g.graph.replay()
+            if g.ids is not None:
+                self.last_ids = g.ids[:B]
         else:
             if self.recv_fn is not None:
                 self.recv_fn(g.hidden_in)
@@ -307,9 +323,16 @@ class ModelRunner:
         h[2 * b + B:3 * b] = -1
         h[3 * b:3 * b + B] = inp["ctx"]
         h[3 * b + B:4 * b] = 1
-        tab = h[4 * b:].reshape(b, g.max_blocks)
+        tab = h[4 * b:g.off_t].reshape(b, g.max_blocks)
         tab[:B] = inp["tables"]
         tab[B:] = 0
+        ht = h[g.off_t:g.off_t + b].view(np.float32)
+        hs = h[g.off_s:g.off_s + 2 * b].view(np.int64)
+        t, sd = inp.get("temps"), inp.get("seeds")
+        ht[:B] = 0.0 if t is None else t
+        ht[B:] = 0.0
+        hs[:B] = 0 if sd is None else sd
+        hs[B:] = 0
         start = b if ids_dev else 0
         g.inbuf[start:].copy_(g.host[k][start:], non_blocking=True)
         if self.device.type == "cuda":
@@ -334,9 +357,12 @@ class ModelRunner:
         fb = self._graph_batch(g)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
+        sample = self.sample_fn if (self.sample_fn is not None and self.model.last) else None
         with torch.cuda.stream(s):
             for _ in range(2):   # warm up allocator / workspaces outside capture (no receive:
-                self.run(fb, g.hidden_in)   # a transfer would consume a real message)
+                out = self.run(fb, g.hidden_in)   # a transfer would consume a real message)
+                if sample is not None:
+                    sample(out, g.temps, g.seeds)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         if self.pool is None:
@@ -346,6 +372,8 @@ class ModelRunner:
             if self.recv_fn is not None and g.hidden_in is not None:
                 self.recv_fn(g.hidden_in)       # the boundary receive is the graph's first node
             g.output = self.run(fb, g.hidden_in)
+            if sample is not None:
+                g.ids = sample(g.output, g.temps, g.seeds)
         g.graph = graph
         if register:
             self.graphs[bucket] = g

@@ -907,30 +907,38 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 //     global segment:  4k     4k+1   4k+2   4k+3   (k = K-tile)
 //     group 0:         R0(k)  M0(k)  R1(k)  M1(k)
 //     group 1:         M1(k-1) R0(k) M0(k)  R1(k)
-// LDS: an ST-stage ring of whole K-tiles (A | B images, 128-B rows, XOR-swizzled like
-// lds_frag). The DMA of K-tile k + ST - 1 is issued during K-tile k into the slot of K-tile
-// k - 1, whose last reader (group 1's R1(k-1), global segment 4k-1) retired its reads
-// (lgkmcnt(0)) before the barrier opening segment 4k. RAW: K-tile k+1 is first read in global
-// segment 4k+4 (group 0's R0(k+1)), so every wave retires its own DMA of K-tile k+1 before the
-// barrier that closes segment 4k+3: group 0 at the end of M1(k), group 1 at the end of R1(k).
+// LDS: two rings of K-tile images (128-B rows, XOR-swizzled like lds_frag): SX slots of the
+// activation rows X (BM x 64, mostly L2 hits: short latency) and SW >= SX slots of the weight
+// rows W (BN x 64, streamed from HBM: the deep one). Iteration k issues X(k + SX - 1) in its
+// first read segment and W(k + SW - 1) in its second, each into the slot of K-tile k - 1,
+// whose last reader (group 1's R1(k-1), global segment 4k-1) retired its reads (lgkmcnt(0))
+// before the barrier opening segment 4k. RAW: K-tile k+1 is first read in global segment 4k+4
+// (group 0's R0(k+1)), so every wave retires its own DMA of K-tile k+1 before the barrier that
+// closes segment 4k+3: group 0 at the end of M1(k), group 1 at the end of R1(k); the counted
+// wait leaves exactly the loads issued after the later of X(k+1) / W(k+1) in flight (counted
+// at run time near the tail, where the load stream thins out).
 // DMA through buffer descriptors based at the tile's first row (A rows past M read zeros);
 // weights streamed non-temporally when one row tile covers M (each byte read by one workgroup).
 // Grid: 1-D, split-major then N-tile then M-tile, XCD-remapped, so an XCD's consecutive
 // workgroups share a weight panel (and K range) across the M tiles in its L2.
+// Measured (profiles/r5_gemm): one ring of whole K-tiles (SX = SW = 3) kept the matrix pipe
+// 29 % busy on the tp8 down projection at M = 512, the waves parked on the DMA wait (SQ_WAIT_ANY
+// 35 %) with 75 % L2 hits: the weight stream's latency, not the MFMA or LDS issue, bounds it.
 // ---------------------------------------------------------------------------------------
 constexpr int kMidThreads = 512;
 
-template <int BM, int BN, int ST>
+template <int BM, int BN, int SX, int SW>
 struct MidCfg {
   static constexpr int WM = 64;                          // wave rows
   static constexpr int WN = (BM * BN) / (8 * WM);        // wave columns: 8 waves cover the tile
   static constexpr int WGN = BN / WN, WGM = BM / WM;     // wave grid
   static constexpr int TI = WM / 16, TJ = WN / 16;
-  static constexpr int ROWS = BM + BN;                   // LDS image rows per K-tile
-  static constexpr int SLOT = ROWS * 128;                // bytes per K-tile slot
-  static constexpr int L = ROWS / 64;                    // DMA instructions per wave per K-tile
-  static_assert(WGM * WGN == 8 && WN % 16 == 0 && L % 2 == 0, "mid tile shape");
-  static_assert(ST * SLOT <= 160 * 1024, "mid ring exceeds the LDS");
+  static constexpr int XB = BM * 128, WB = BN * 128;     // bytes per X / W slot
+  static constexpr int LX = BM / 64, LW = BN / 64;       // DMA instructions per wave per K-tile
+  static constexpr int LDS = SX * XB + SW * WB;
+  static_assert(WGM * WGN == 8 && WN % 16 == 0, "mid tile shape");
+  static_assert(SX >= 2 && SW >= SX, "mid rings");
+  static_assert(LDS <= 160 * 1024, "mid rings exceed the LDS");
 };
 
 // One 1-KiB LDS-DMA block through a buffer descriptor (a __device__ helper: the builtin's LDS
@@ -941,15 +949,33 @@ __device__ __forceinline__ void mid_dma1(__amdgpu_buffer_rsrc_t r, char* lds, in
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, soff, 0, AUX);
 }
 
-template <int BM, int BN, int ST>
+// s_waitcnt vmcnt(n) for a run-time n (the count is an immediate): a jump over constants;
+// n above the largest case waits for less than allowed, i.e. is clamped to a safe (longer) wait
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+  switch (n) {
+    case 0: vm_wait<0>(); break;   case 1: vm_wait<1>(); break;   case 2: vm_wait<2>(); break;
+    case 3: vm_wait<3>(); break;   case 4: vm_wait<4>(); break;   case 5: vm_wait<5>(); break;
+    case 6: vm_wait<6>(); break;   case 7: vm_wait<7>(); break;   case 8: vm_wait<8>(); break;
+    case 9: vm_wait<9>(); break;   case 10: vm_wait<10>(); break; case 11: vm_wait<11>(); break;
+    case 12: vm_wait<12>(); break; case 13: vm_wait<13>(); break; case 14: vm_wait<14>(); break;
+    case 15: vm_wait<15>(); break; case 16: vm_wait<16>(); break; case 17: vm_wait<17>(); break;
+    case 18: vm_wait<18>(); break; case 19: vm_wait<19>(); break; case 20: vm_wait<20>(); break;
+    case 21: vm_wait<21>(); break; case 22: vm_wait<22>(); break; case 23: vm_wait<23>(); break;
+    default: vm_wait<24>(); break;
+  }
+}
+
+template <int BM, int BN, int SX, int SW>
 __global__ void __launch_bounds__(kMidThreads)
 gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
                  bf16* __restrict__ out, long ldo, float* __restrict__ part, int nsplit,
                  RowScale rsc) {
-  using C = MidCfg<BM, BN, ST>;
-  constexpr int TI = C::TI, TJ = C::TJ, L = C::L, H = L / 2;
+  using C = MidCfg<BM, BN, SX, SW>;
+  constexpr int TI = C::TI, TJ = C::TJ, LX = C::LX, LW = C::LW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const xs = smem;
+  char* const wsm = smem + SX * C::XB;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int grp = wid >> 2;
   const int wm = wid / C::WGN, wn = wid % C::WGN;
@@ -961,39 +987,55 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   const int kt0 = (int)(((long)ktiles * ksplit) / nsplit);
   const int nk = (int)(((long)ktiles * (ksplit + 1)) / nsplit) - kt0;
 
-  // DMA: wave w moves 1-KiB blocks w, w + 8, ... of the slot (blocks < BM / 8 are A rows)
+  // DMA: wave w moves the 1-KiB blocks w, w + 8, ... of an X / W slot (BM / 8, BN / 8 blocks)
   const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);
   const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
-  const int wpol = (mtiles == 1 && g_tile_w_nt) ? 2 : 0;   // runtime: the aux operand is an immediate
-  // (BM / 8 is a multiple of 8: instruction i of every wave is an A block iff i < BM / 64)
-  int voff[L];
+  const bool wnt = mtiles == 1 && g_tile_w_nt;
+  int vx[LX], vw[LW];
 #pragma unroll
-  for (int i = 0; i < L; ++i) {
-    const int blk = wid + 8 * i;
-    const bool isA = i < BM / 64;
-    const int row = (isA ? blk : blk - BM / 8) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    voff[i] = (int)((row * (isA ? ldx : ldw) + chunk * 8) * 2);
+  for (int i = 0; i < LX; ++i) {
+    const int row = (wid + 8 * i) * 8 + (lane >> 3);
+    vx[i] = (int)((row * ldx + (((lane & 7) ^ ((row >> 1) & 7)) * 8)) * 2);
   }
-  auto slot_of = [&](int k) -> char* { return smem + (k % ST) * C::SLOT; };
-  auto dma = [&](int k, int half) {   // half 0 / 1: instructions [0, H) / [H, L) of K-tile k
-    char* s = slot_of(k);
+#pragma unroll
+  for (int i = 0; i < LW; ++i) {
+    const int row = (wid + 8 * i) * 8 + (lane >> 3);
+    vw[i] = (int)((row * ldw + (((lane & 7) ^ ((row >> 1) & 7)) * 8)) * 2);
+  }
+  auto dma_x = [&](int k) {
+    char* s = xs + (k % SX) * C::XB;
     const int soff = (kt0 + k) * kBK * 2;
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
-      const int i = half * H + j;
-      const int blk = wid + 8 * i;
-      if (i < BM / 64) mid_dma1<0>(rsa, s + blk * 1024, voff[i], soff);
-      else if (wpol) mid_dma1<2>(rsb, s + blk * 1024, voff[i], soff);
-      else mid_dma1<0>(rsb, s + blk * 1024, voff[i], soff);
+    for (int i = 0; i < LX; ++i) mid_dma1<0>(rsa, s + (wid + 8 * i) * 1024, vx[i], soff);
+  };
+  auto dma_w = [&](int k) {
+    char* s = wsm + (k % SW) * C::WB;
+    const int soff = (kt0 + k) * kBK * 2;
+    if (wnt) {
+#pragma unroll
+      for (int i = 0; i < LW; ++i) mid_dma1<2>(rsb, s + (wid + 8 * i) * 1024, vw[i], soff);
+    } else {
+#pragma unroll
+      for (int i = 0; i < LW; ++i) mid_dma1<0>(rsb, s + (wid + 8 * i) * 1024, vw[i], soff);
     }
   };
-  // retire this wave's DMA of the K-tiles before `k + 1` (k + 1 .. k + ST - 1 may fly)
-  auto wait_through = [&](int k) {
-    const int after = min(ST - 2, nk - 2 - k);   // K-tiles issued after k + 1
-    if (ST >= 4 && after >= 2) vm_wait<(ST >= 4 ? 2 : 0) * L>();
-    else if (after >= 1) vm_wait<L>();
-    else vm_wait<0>();
+  // Loads issued (in order X(j + SX - 1), W(j + SW - 1) per iteration j; the prologue is the
+  // virtual iterations 1 - SW .. -1) after the later of X(k+1) / W(k+1): what may stay in
+  // flight once K-tile k+1 must have landed (k = -1: the prologue's wait for K-tile 0).
+  auto after = [&](int k) {
+    const int kt = k + 1;
+    const int jx = kt - SX + 1, jw = kt - SW + 1;   // iterations that issued X(kt), W(kt)
+    int n = 0;
+    if (jw == jx) {   // SW == SX: W(kt) is the later one
+      // nothing else of iteration jx after it
+    } else if (kt + SW - SX < nk) {
+      n += LW;        // W(jx + SW - 1) of the same iteration, behind X(kt)
+    }
+    for (int j = jx + 1; j <= k; ++j) {
+      if (j + SX - 1 < nk) n += LX;
+      if (j + SW - 1 < nk) n += LW;
+    }
+    return n;
   };
 
   f32x4 acc[TI][TJ];
@@ -1002,29 +1044,34 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: K-tiles 0 .. ST-2 in flight, K-tile 0 landed everywhere
+  // prologue = virtual iterations 1-SW .. -1: W(0 .. SW-2), X(0 .. SX-2) in issue order
 #pragma unroll
-  for (int s = 0; s < ST - 1; ++s)
-    if (s < nk) { dma(s, 0); dma(s, 1); }
-  wait_through(-1);
+  for (int v = 1 - SW; v <= -1; ++v) {
+    if (v + SX - 1 >= 0 && v + SX - 1 < nk) dma_x(v + SX - 1);
+    if (v + SW - 1 < nk) dma_w(v + SW - 1);
+  }
+  vm_wait_dyn(after(-1));
   __builtin_amdgcn_s_barrier();
   if (grp == 1) __builtin_amdgcn_s_barrier();
 
   const int ar = wm * C::WM + (lane & 15), bc = wn * C::WN + (lane & 15);
   bf16x8 af[TI], bfr[TJ];
   for (int k = 0; k < nk; ++k) {
-    const char* As = slot_of(k);
-    const char* Bs = As + BM * 128;
-    const bool pre = k + ST - 1 < nk;
+    const char* As = xs + (k % SX) * C::XB;
+    const char* Bs = wsm + (k % SW) * C::WB;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      // ---- read segment: this k-step's fragments, half of the DMA of K-tile k + ST - 1
+      // ---- read segment: this k-step's fragments; X(k + SX - 1) / W(k + SW - 1) DMA
 #pragma unroll
       for (int i = 0; i < TI; ++i) af[i] = lds_frag(As, ar + 16 * i, ks * 4 + (lane >> 4));
 #pragma unroll
       for (int j = 0; j < TJ; ++j) bfr[j] = lds_frag(Bs, bc + 16 * j, ks * 4 + (lane >> 4));
-      if (pre) dma(k + ST - 1, ks);
-      if (ks == 1 && grp == 1) wait_through(k);
+      if (ks == 0) {
+        if (k + SX - 1 < nk) dma_x(k + SX - 1);
+      } else {
+        if (k + SW - 1 < nk) dma_w(k + SW - 1);
+        if (grp == 1) vm_wait_dyn(after(k));
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       // ---- MFMA segment
@@ -1034,7 +1081,7 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);   // C^T tile
       __builtin_amdgcn_s_setprio(0);
-      if (ks == 1 && grp == 0) wait_through(k);
+      if (ks == 1 && grp == 0) vm_wait_dyn(after(k));
       __builtin_amdgcn_s_barrier();
     }
   }
@@ -1136,20 +1183,20 @@ static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   gemm_big8_kernel<<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
-template <int BM, int BN, int ST>
+template <int BM, int BN, int SX, int SW>
 static void run_mid8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                      const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream,
                      const RowScale& rsc) {
   init_nt_policy();
-  constexpr size_t lds = (size_t)ST * MidCfg<BM, BN, ST>::SLOT;
+  constexpr size_t lds = (size_t)MidCfg<BM, BN, SX, SW>::LDS;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid8_kernel<BM, BN, ST>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid8_kernel<BM, BN, SX, SW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  gemm_mid8_kernel<BM, BN, ST><<<tiles * sk, kMidThreads, lds, stream>>>(
+  gemm_mid8_kernel<BM, BN, SX, SW><<<tiles * sk, kMidThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, sk, rsc);
 }
 
@@ -1294,16 +1341,21 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
     if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
   } else if (p.kind == 5) {
-    // mid-M 8-wave staggered GEMM: plan {5, ST (ring depth), 0, 0, BM, BN, sk}
+    // mid-M 8-wave staggered GEMM: plan {5, SW (weight ring), SX (activation ring; 0 = SW), 0,
+    // BM, BN, sk}
     if (N % p.bn != 0 || K % kBK != 0 || K / kBK < p.sk) return -1;
     if (epi == EPI_SILU && p.bn * p.bm / 512 % 32 != 0) return -1;
+    const int sx = p.nt > 0 ? p.nt : p.mt;
     bool done = false;
-#define MID_CASE(BM_, BN_, ST_)                                                                   \
-  if (!done && p.bm == BM_ && p.bn == BN_ && p.mt == ST_) {                                        \
-    if (!dry) run_mid8<BM_, BN_, ST_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+#define MID_CASE(BM_, BN_, SX_, SW_)                                                              \
+  if (!done && p.bm == BM_ && p.bn == BN_ && sx == SX_ && p.mt == SW_) {                           \
+    if (!dry) run_mid8<BM_, BN_, SX_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                   \
   }
-    MID_CASE(256, 128, 3) MID_CASE(128, 256, 3) MID_CASE(128, 128, 4) MID_CASE(128, 128, 3)
+    MID_CASE(256, 128, 3, 3) MID_CASE(256, 128, 2, 6) MID_CASE(256, 128, 3, 4)
+    MID_CASE(128, 256, 3, 3) MID_CASE(128, 256, 2, 4)
+    MID_CASE(128, 128, 4, 4) MID_CASE(128, 128, 3, 3) MID_CASE(128, 128, 3, 6) MID_CASE(128, 128, 2, 8)
+    MID_CASE(128, 128, 2, 2)   // 64 KiB: two workgroups per CU
 #undef MID_CASE
     if (!done) return -2;
   } else if (p.kind == 3) {

@@ -67,6 +67,47 @@ def test_engine_graph_replay_matches_eager():
     assert outs[0] == outs[1]
 
 
+@pytest.mark.parametrize("params", [dict(temperature=0.0), dict(temperature=0.9, seed=5),
+                                    dict(temperature=0.7, top_k=20, seed=2)])
+def test_graph_sampling_matches_eager(params, monkeypatch):
+    """Decode steps whose tokens come from the sampler captured at the end of the hipGraph
+    (per-request temperatures / seeds in the graph's static inputs) give the tokens of eager
+    steps with the eager sampler; top-k rows fall back to eager sampling of the graph's
+    logits. The engine replays exactly one graph per decode step."""
+    cfg = ModelConfig.from_preset("llama-small")
+    prompts = [[i + 1, 2 * i + 3, 5] * 7 for i in range(6)]
+    outs, replays = [], []
+    for graphs in (False, True):
+        ecfg = EngineConfig(max_batch=8, max_seq_len=256, kv_cache_tokens=4096, use_graphs=graphs,
+                            graph_batch_sizes=[8], seed=11)
+        eng = LLMEngine(cfg, engine_cfg=ecfg, device="cuda")
+        assert eng.async_pp and (eng.runner.sample_fn is not None)
+        n = {"replay": 0, "eager_sample": 0}
+        orig = torch.cuda.CUDAGraph.replay
+        orig_sample = eng._sample_eager
+
+        def count_replay(self, _o=orig):
+            n["replay"] += 1
+            return _o(self)
+
+        def count_sample(*a, _o=orig_sample):
+            n["eager_sample"] += 1
+            return _o(*a)
+
+        monkeypatch.setattr(torch.cuda.CUDAGraph, "replay", count_replay)
+        monkeypatch.setattr(eng, "_sample_eager", count_sample)
+        outs.append(eng.generate(prompts, SamplingParams(max_tokens=12, ignore_eos=True, **params)))
+        monkeypatch.setattr(torch.cuda.CUDAGraph, "replay", orig)
+        replays.append(dict(n))
+    assert outs[0] == outs[1]
+    g = replays[1]
+    assert g["replay"] > 0
+    if params.get("top_k"):
+        assert g["eager_sample"] >= g["replay"]     # filtered rows: eager sampling of the logits
+    else:
+        assert g["eager_sample"] <= 2                # only the prefill steps sample eagerly
+
+
 def test_engine_temperature_sampling_runs():
     cfg = ModelConfig.from_preset("llama-tiny")
     eng = LLMEngine(cfg, engine_cfg=EngineConfig(max_batch=4, max_seq_len=128, kv_cache_tokens=2048), device="cuda")

@@ -416,16 +416,18 @@ def test_gemm_tile_plans(bm, bn, wmw, epi):
                 _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
 
 
-MID_CFGS = [(256, 128, 3), (128, 256, 3), (128, 128, 4), (128, 128, 3)]
+MID_CFGS = [(256, 128, 3, 3), (256, 128, 2, 6), (256, 128, 3, 4), (128, 256, 3, 3), (128, 256, 2, 4),
+            (128, 128, 4, 4), (128, 128, 3, 3), (128, 128, 3, 6), (128, 128, 2, 8), (128, 128, 2, 2)]
 
 
-@pytest.mark.parametrize("bm,bn,st", MID_CFGS)
-def test_gemm_mid8_plans(bm, bn, st):
-    """Mid-M 8-wave staggered GEMM (plan kind 5): ragged M below and above one row tile (rows
-    past M read as zeros through the descriptor), K-tile counts of 1 .. 2 x the ring depth per
-    split (prologue / tail waits), uneven split-K, all epilogues, asymmetric operands."""
+@pytest.mark.parametrize("bm,bn,sx,st", MID_CFGS)
+def test_gemm_mid8_plans(bm, bn, sx, st):
+    """Mid-M 8-wave staggered GEMM (plan kind 5, activation ring sx / weight ring st): ragged M
+    below and above one row tile (rows past M read as zeros through the descriptor), K-tile
+    counts of 1 .. 2 x the ring depth per split (prologue / tail waits), uneven split-K, all
+    epilogues, asymmetric operands."""
     N = 3 * bn
-    for M, K in ((bm - 5, 1024), (bm + 9, 192), (3 * bm + 1, 4096), (7, 64 * st)):
+    for M, K in ((bm - 5, 1024), (bm + 9, 192), (3 * bm + 1, 4096), (7, 64 * st), (bm, 64 * (st + 1))):
         x = _bf(M, K, seed=47)
         w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=48)
         b = _bf(N, seed=49)
@@ -437,15 +439,15 @@ def test_gemm_mid8_plans(bm, bn, st):
                     continue
                 out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
                 ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
-                torch.ops.bfly.gemm_with_plan(x, w, out, [5, st, 0, 0, bm, bn, sk], ops.EPILOGUES[epi], ws,
+                torch.ops.bfly.gemm_with_plan(x, w, out, [5, st, sx, 0, bm, bn, sk], ops.EPILOGUES[epi], ws,
                                               b if epi == "bias" else None)
                 _close(out, want, 2e-2, 2e-2)
 
 
 @pytest.mark.parametrize("M,N,K,plan", [(512, 1280, 8192, [5, 3, 0, 0, 128, 256, 12]),    # tp8 QKV
                                         (512, 8192, 3584, [5, 3, 0, 0, 128, 256, 2]),     # tp8 down
-                                        (256, 14336, 8192, [5, 3, 0, 0, 256, 128, 2]),    # tp4 gate_up
-                                        (256, 2560, 8192, [5, 4, 0, 0, 128, 128, 6])])    # tp4 QKV
+                                        (256, 14336, 8192, [5, 6, 2, 0, 256, 128, 2]),    # tp4 gate_up
+                                        (256, 2560, 8192, [5, 6, 3, 0, 128, 128, 6])])    # tp4 QKV
 def test_gemm_mid8_production(M, N, K, plan):
     """The mid-M kernel at the TP shard shapes it is tuned for (K up to 8192, >= 240
     workgroups), against the fp32 reference."""

@@ -37,6 +37,9 @@ DEC_CFGS = [(128, 224, 8, 1, 4), (128, 224, 8, 1, 3), (128, 256, 8, 1, 3), (128,
             (128, 128, 4, 2, 5), (128, 160, 8, 1, 4), (128, 80, 8, 1, 6), (128, 64, 8, 1, 8), (128, 64, 4, 2, 8),
             (64, 128, 4, 2, 6), (64, 256, 4, 2, 4), (64, 224, 4, 1, 4), (64, 160, 4, 2, 5), (64, 64, 4, 2, 8)]
 
+MID_CFGS = [(256, 128, 3, 3), (256, 128, 2, 6), (256, 128, 3, 4), (128, 256, 3, 3), (128, 256, 2, 4),
+            (128, 128, 4, 4), (128, 128, 3, 6), (128, 128, 2, 8), (128, 128, 2, 2)]
+
 SERIAL = False
 LOG = None
 
@@ -131,14 +134,14 @@ def main():
                         for sk in (1, 2, 4, 8):
                             if K // 64 >= sk * 8:
                                 cands.append([3, sw, nwm * nwn, nwm, bm, bn, sk])
-                    # mid-M 8-wave kernel (kind 5): {5, ST, 0, 0, BM, BN, sk}
+                    # mid-M 8-wave kernel (kind 5): {5, SW, SX, 0, BM, BN, sk}
                     if M >= 64:
-                        for bm, bn, st in ((256, 128, 3), (128, 256, 3), (128, 128, 4)):
+                        for bm, bn, sx, sw in MID_CFGS:
                             if N % bn or (bm == 256 and M <= 128):
                                 continue
                             for sk in (1, 2, 3, 4, 6, 8, 12, 16):
                                 if K // 64 >= sk * 2:
-                                    cands.append([5, st, 0, 0, bm, bn, sk])
+                                    cands.append([5, sw, sx, 0, bm, bn, sk])
                     if M >= 128 and N % 256 == 0:
                         for sk in (1, 2, 4, 8, 16):
                             if K // 64 >= sk * 4:
