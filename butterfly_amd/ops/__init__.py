@@ -136,6 +136,8 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
 # (floating point) or a negative sentinel (integers) instead of left uninitialised, so an
 # element a kernel forgot to write shows up in the comparison against the unpoisoned run.
 _POISON = os.environ.get("BFLY_POISON_OUTPUTS", "0").strip().lower() in ("1", "true", "yes", "on")
+# MoE prefill expert GEMMs on the 256x256 8-phase tile (BFLY_MOE_BIG_TILE=0: the 64/128-row tile)
+_BIG_MOE = os.environ.get("BFLY_MOE_BIG_TILE", "1").strip().lower() not in ("0", "false", "no", "off")
 # Host-side index checks of ops whose kernels cannot raise (BFLY_DEBUG_CHECKS; each costs a sync)
 _DEBUG_CHECKS = os.environ.get("BFLY_DEBUG_CHECKS", "0").strip().lower() in ("1", "true", "yes", "on")
 
@@ -587,7 +589,10 @@ def moe_sparse_ffn(x, topk_ids, topk_w, gu_w, down_w, e0: int, num_local: int, f
     # `expected_slots`: (token, k) pairs expected to be local (the EP dispatch pads with
     # non-local / empty slots; they cost nothing but must not size the launch)
     exp = TK if expected_slots is None else max(1, min(TK, expected_slots))
-    bm = 128 if exp >= 96 * num_local else 64
+    # prefill-scale expert batches (>= 256 rows per local expert on average): the 8-phase
+    # 256x256 tile over the tile list (gemm.hip gemm_big8_kernel<GROUPED>)
+    bm = 256 if (exp >= 256 * num_local and H % 256 == 0 and (2 * ffn) % 256 == 0 and _BIG_MOE) else \
+        (128 if exp >= 96 * num_local else 64)
     rows = _arena.get(dev, "moe_rows", TK, torch.int32)[:TK]
     slot_of = _arena.get(dev, "moe_slot", TK, torch.int32)[:TK]
     nt = L.moe_max_tiles(TK, num_local, bm)
@@ -637,7 +642,9 @@ def ep_combine(back, slot):
 
 def moe_down_splits(TK: int, num_local: int, H: int, ffn: int, bm: int, cus: int = 256) -> int:
     """Split-K factor of the grouped down projection: enough workgroups for ~2 per CU, with
-    at least 16 K-tiles (1024 columns) per split."""
+    at least 16 K-tiles (1024 columns) per split (none for the 256-row big tile)."""
+    if bm == 256:
+        return 1
     tiles = -(-TK // bm) + (num_local if TK >= num_local else 0)
     wgs = max(1, tiles) * (H // 128)
     sk = 1

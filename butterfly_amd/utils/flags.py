@@ -37,6 +37,8 @@ define("BFLY_POISON_OUTPUTS", False, _bool, "allocate every op output filled wit
        "a kernel leaves unwritten show up (debug; read at import, ops.set_poison at run time)")
 define("BFLY_DEBUG_CHECKS", False, _bool, "host-side index checks (one sync each) in ops whose kernels cannot raise, "
        "e.g. gather_rows (read at import)")
+define("BFLY_MOE_BIG_TILE", True, _bool, "prefill-scale MoE expert GEMMs (>= 256 routed rows per local expert) on "
+       "the 256x256 8-phase tile over the device tile list (read at import)")
 define("BFLY_GRAPH_SAMPLING", True, _bool, "a last stage's decode hipGraphs end with the token sampler (per-request "
        "temperatures / seeds staged with the inputs: one replay per step); top-k / top-p rows sample eagerly")
 define("BFLY_DISABLE_GRAPHS", False, _bool, "run decode steps eagerly instead of replaying hipGraphs")

@@ -701,7 +701,7 @@ static const int* block_counts(const c10::optional<Tensor>& bcnt, int64_t bcap, 
 
 void moe_align(const Tensor& topk_ids, int64_t e0, int64_t num_local, Tensor& rows, Tensor& slot_of,
                Tensor& tiles, Tensor& count, int64_t bm, const c10::optional<Tensor>& bcnt, int64_t bcap) {
-  TORCH_CHECK(bm == 64 || bm == 128, "moe_align: tile rows 64 or 128");
+  TORCH_CHECK(bm == 64 || bm == 128 || bm == 256, "moe_align: tile rows 64, 128 or 256");
   CHECK_GPU(topk_ids); CHECK_I32(topk_ids); CHECK_I32(rows); CHECK_I32(slot_of); CHECK_I32(tiles); CHECK_I32(count);
   TORCH_CHECK(topk_ids.dim() == 2 && topk_ids.is_contiguous(), "moe_align: topk_ids [T, k]");
   const int T = topk_ids.size(0), K = topk_ids.size(1);

@@ -753,21 +753,59 @@ __device__ __forceinline__ void b8_stage_buf(__amdgpu_buffer_rsrc_t ra, __amdgpu
   }
 }
 
+// GROUPED (MoE expert GEMM at prefill scale, K13): the M tiles are the entries of a device-built
+// tile list gtiles[i] = {expert, first row slot, end row slot, -} (count in *gcount, up to
+// `M` = the list's capacity; excess workgroups exit): the expert selects W + expert *
+// w_estride, and the A rows of slot s are the token rows grows[s] (nullptr: slot s itself),
+// gathered by per-lane LDS-DMA addresses (rows past the tile's end re-read its last row; their
+// outputs are not stored). Output rows are slots. Consecutive list entries are mostly tiles of
+// one expert, so the GROUP_M walk shares the expert's weight panels in an XCD's L2.
+__device__ __forceinline__ void b8_stage_gather(const bf16* const (&arow)[4], int k0, char* buf, int half, int wid) {
+  const int base = half == 3 ? 2 : 0;   // A-lo: pointers 0, 1; A-hi: 2, 3
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = b8_block(half, 2 * wid + i);
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(arow[base + i] + k0), (lds_ptr_t)(buf + blk * 1024), 16, 0, 0);
+  }
+}
+
+template <bool GROUPED = false>
 __global__ void __launch_bounds__(kB8Threads)
 gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                 bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+                 bf16* __restrict__ out, long ldo, float* __restrict__ part,
+                 const int* __restrict__ grows = nullptr, const int4* __restrict__ gtiles = nullptr,
+                 const int* __restrict__ gcount = nullptr, long w_estride = 0) {
   constexpr int BM = 256, BN = 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wr = wid >> 2, wc = wid & 3;
-  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;   // GROUPED: M = tile-list capacity x BM
   const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
   const int per_group = kBigGroupM * ntiles;
   const int grp = t / per_group, first_m = grp * kBigGroupM;
   const int gsize = min(mtiles - first_m, kBigGroupM);
-  const int m0 = (first_m + (t % per_group) % gsize) * BM;
+  int m0 = (first_m + (t % per_group) % gsize) * BM;
   const int n0 = ((t % per_group) / gsize) * BN;
+  const bf16* arow[4] = {};
+  if constexpr (GROUPED) {
+    const int ti = m0 / BM;
+    if (ti >= *gcount) return;
+    const int4 info = gtiles[ti];
+    W += (long)info.x * w_estride;
+    m0 = info.y;
+    M = info.z;                    // rows [m0, M) of the slot space
+    // this lane's A rows: the 4 row blocks it DMAs (A-lo: b8_block(0, 2 wid + i), A-hi: (3, ...))
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = b8_block(i < 2 ? 0 : 3, 2 * wid + (i & 1)) * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      int slot = m0 + row;
+      slot = slot < M ? slot : M - 1;
+      const long src = grows != nullptr ? grows[slot] : slot;
+      arow[i] = X + src * ldx + chunk * 8;
+    }
+  }
   const int ktiles = K / 64;
   const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
   const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
@@ -784,7 +822,12 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);
   const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
   const B8Dma dma = b8_dma_offsets(ldx, ldw, wid, lane);
-  auto stage = [&](int k, int half) { b8_stage_buf(rsa, rsb, ldx, ldw, (kt0 + k) * 64, bufp(k), half, wid, dma); };
+  auto stage = [&](int k, int half) {
+    if (GROUPED && (half == 0 || half == 3))
+      b8_stage_gather(arow, (kt0 + k) * 64, bufp(k), half, wid);
+    else
+      b8_stage_buf(rsa, rsb, ldx, ldw, (kt0 + k) * 64, bufp(k), half, wid, dma);
+  };
   // prologue: all of K-tile 0, then A-lo, B-lo, B-hi of K-tile 1 (the load stream's order)
   stage(0, 0); stage(0, 1); stage(0, 2); stage(0, 3);
   stage(1, 0); stage(1, 1); stage(1, 2);
@@ -1173,14 +1216,14 @@ static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        kB8LdsBytes);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
     attr = true;
   }
   const int tiles = ((M + 255) / 256) * (N / 256);
   dim3 grid(tiles, sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  gemm_big8_kernel<<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  gemm_big8_kernel<false><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
 template <int BM, int BN, int SX, int SW>
@@ -1483,6 +1526,20 @@ int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w
   if (N % 128 != 0 || K % kBK != 0 || max_tiles <= 0) return -1;
   if (epi != EPI_NONE && epi != EPI_SILU) return -1;
   if (sk < 1 || sk > K / kBK || (sk > 1 && (part == nullptr || epi != EPI_NONE || slots <= 0))) return -2;
+  if (bm == 256) {
+    // prefill-scale expert batches: the 8-phase 256x256 tile over the tile list, no split
+    if (N % 256 != 0 || K / 64 < 2 || sk != 1) return -2;
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+      attr = true;
+    }
+    dim3 grid(max_tiles * (N / 256), 1);
+    gemm_big8_kernel<true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(
+        X, ldx, W, ldw, max_tiles * 256, N, K, epi, nullptr, out, ldo, nullptr, rows, tiles, count, w_estride);
+    return 0;
+  }
   if (bm == 128)
     return launch_grouped_bm<128>(X, ldx, W, ldw, w_estride, N, K, epi, rows, tiles, count, max_tiles,
                                   slots, sk, part, out, ldo, stream);

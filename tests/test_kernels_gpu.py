@@ -4,6 +4,7 @@ Random normal (asymmetric) operands throughout: a symmetric or identity operand 
 transposed C-write (cdna_hip_programming.md §3, "Always A=I-check with ASYMMETRIC B").
 """
 import math
+import os
 
 import pytest
 import torch
@@ -615,6 +616,39 @@ def test_moe_sparse_ffn(T, E, El, e0, k, H, F):
     ops.moe_gate_scale_(h, gates, e0, El)
     dense = ops.linear(h, dn)
     _close(got, dense, 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("T,El,e0,H,F,skew", [(4096, 8, 0, 512, 256, False), (3000, 8, 0, 256, 512, True),
+                                                (4096, 2, 2, 512, 256, True), (2600, 4, 4, 1024, 256, False)])
+def test_moe_sparse_ffn_big_tile(T, El, e0, H, F, skew):
+    """Prefill-scale routing (>= 256 rows per local expert): the expert GEMMs run the 8-phase
+    256x256 tile over the device tile list (gathered token rows, expert weight slices, ragged
+    last tiles), with skewed loads and an expert that gets no rows, against the fp32 reference
+    and the dense gate-scaled path."""
+    E, k = 8, 2
+    g = torch.Generator().manual_seed(90 + T)
+    if skew:   # experts 0-2 take most pairs, expert 5 none
+        p = torch.tensor([0.3, 0.25, 0.2, 0.08, 0.08, 0.0, 0.05, 0.04])
+    else:
+        p = torch.full((E,), 1.0 / E)
+    ids = torch.stack([torch.multinomial(p, k, replacement=False, generator=g) for _ in range(T)]).to(torch.int32)
+    w = torch.rand(T, k, generator=g)
+    w = (w / w.sum(1, keepdim=True)).float()
+    x = _bf(T, H, seed=84)
+    gu = _bf(El * 2 * F, H, scale=1.0 / math.sqrt(H), seed=85)
+    dn = _bf(H, El * F, scale=1.0 / math.sqrt(F), seed=86)
+    ids_d, w_d = ids.to(DEV), w.to(DEV)
+    got = ops.moe_sparse_ffn(x, ids_d, w_d, gu, dn, e0, El, F)
+    want = ref.moe_sparse_ffn(x.cpu().float(), ids, w, gu.cpu().float(), dn.cpu().float(), e0, El, F)
+    _close(got, want, 3e-2, 3e-2)
+    os.environ["BFLY_MOE_BIG_TILE"] = "0"
+    try:
+        ops._BIG_MOE = False
+        base = ops.moe_sparse_ffn(x, ids_d, w_d, gu, dn, e0, El, F)
+    finally:
+        ops._BIG_MOE = True
+        os.environ.pop("BFLY_MOE_BIG_TILE")
+    _close(got, base, 2e-2, 2e-2)
 
 
 @pytest.mark.parametrize("cap,counts,El", [(96, [0, 37, 96, 5], 1), (256, [200, 3, 0, 17, 250, 1, 90, 64], 2)])
