@@ -56,7 +56,6 @@ define("BFLY_PROBE_BUTTERFLY", False, _bool, "the start-up comm probe also times
 define("BFLY_CUSTOM_AR_2SHOT_BYTES", 512 << 10, int, "IPC all-reduces of at least this many bytes over 4 or 8 "
        "ranks run as reduce-scatter + all-gather (2S/W bytes per link instead of S; 0 = always one-shot)")
 define("BFLY_GEMM_TUNED", True, _bool, "consult the measured GEMM plan table (0: heuristic plans only; read by the kernel library)")
-define("BFLY_GEMM_SPLITK_FIXUP", False, _bool, "reduce split-K partials inside the GEMM (last-arriver) instead of a reduce kernel")
 define("BFLY_GEMM_NT_WEIGHTS", True, _bool, "stream decode GEMM weights with the non-temporal policy (read by the kernel library)")
 define("BFLY_GEMM_PLAN", "", str, "force GEMM plans for whole-model A/B runs: \"N,K,Mbucket:kind,mt,nt,wk,bm,bn,sk;...\" "
        "(read by the kernel library)")

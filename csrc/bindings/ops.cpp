@@ -1080,7 +1080,6 @@ TORCH_LIBRARY(bfly, m) {
         "Tensor? bias=None) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
   m.def("gemm_plan(int M, int N, int K) -> int[]", &gemm_plan);
-  m.def("gemm_set_splitk_fixup(bool on) -> ()", [](bool on) { bfly::gemm_set_splitk_fixup(on); });
   m.def("gemm_check(int M, int N, int K, int epilogue) -> int",
         [](int64_t M, int64_t N, int64_t K, int64_t e) -> int64_t { return bfly::gemm_check(M, N, K, e); });
   m.def("attn_decode_splits(int max_ctx, int part_tokens) -> int", &attn_decode_splits);

@@ -107,7 +107,6 @@ int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M
 size_t gemm_slab_offset_floats();
 void launch_splitk_reduce(const float* part, int sk, int M, int N, bf16* out, long ldo,
                           hipStream_t stream);
-void gemm_set_splitk_fixup(bool on);   // in-kernel split-K reduction (default: env / off)   // 0 if the auto plan can run this shape
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
                 hipStream_t stream, const RowScale* rs = nullptr);

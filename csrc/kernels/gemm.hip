@@ -107,76 +107,12 @@ __global__ void gemm_splitk_reduce_kernel(const float* __restrict__ part, int SK
   }
 }
 
-// In-kernel split-K fixup ("last workgroup reduces"): every split writes its f32 partial,
-// publishes it (device-scope release) and bumps the tile's arrival counter; the split that
-// arrives last sums all partials in split order 0..SK-1 (deterministic, independent of which
-// split finished last), applies the epilogue, writes bf16 and re-arms the counter to 0 for the
-// next GEMM. Removes the separate reduce launch and its kernel boundary, and the reduction of
-// early tiles overlaps the MFMA work of late ones. Counters live at a fixed place (the start
-// of the workspace), so every GEMM on the stream shares them and always leaves them zeroed.
+// Workspace head: kCounterBytes reserved ahead of the split-K slabs (the slab offset every
+// consumer of deferred slabs uses, gemm_slab_offset_floats). Measured and removed: an in-kernel
+// "last arriver reduces" fixup on these words; it only paid when sk x slab bytes per tile were
+// a few tens of KB, and the decode plans write 256 KB per tile.
 constexpr int kSplitCounters = 16384;
 constexpr size_t kCounterBytes = kSplitCounters * sizeof(int);
-
-// Hand-off recipe of cdna_hip_programming.md §5 (split-K item 2): plain slab stores, every
-// wave drains its stores, barrier, ONE agent-scope release + relaxed ticket by lane 0; the
-// last arriver does ONE agent-scope acquire. `flag` is a word of the kernel's existing LDS
-// array (a second __shared__ object would perturb the k-loop's waits: item 4a).
-__device__ __forceinline__ bool splitk_arrive(int* counter, int sk, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == sk - 1;
-    if (last) {
-      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-__device__ __forceinline__ void splitk_fixup(const float* __restrict__ part, int SK, int M, int N,
-                                             int m0, int m1, int n0, int n1, int epi,
-                                             const bf16* __restrict__ bias, bf16* __restrict__ out,
-                                             long ldo) {
-  const long slab = (long)M * N;
-  if (m1 > M) m1 = M;
-  if (epi == EPI_SILU) {
-    const int f0 = n0 / 2, nf = (n1 - n0) / 2;   // output columns of this tile
-    const int total = (m1 - m0) * (nf / 4);
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
-      const int m = m0 + e / (nf / 4), f = f0 + (e % (nf / 4)) * 4;
-      const long gi = (long)m * N + (f >> 4) * 32 + (f & 15), ui = gi + 16;
-      f32x4 g = {0.f, 0.f, 0.f, 0.f}, u = g;
-      for (int sp = 0; sp < SK; ++sp) {
-        g += *reinterpret_cast<const f32x4*>(part + sp * slab + gi);
-        u += *reinterpret_cast<const f32x4*>(part + sp * slab + ui);
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = f2bf(silu(g[j]) * u[j]);
-      *reinterpret_cast<bf16x4*>(out + (long)m * ldo + f) = o;
-    }
-  } else {
-    const int nc = (n1 - n0) / 4;
-    const int total = (m1 - m0) * nc;
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
-      const int m = m0 + e / nc, n = n0 + (e % nc) * 4;
-      const long i = (long)m * N + n;
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
-      for (int sp = 0; sp < SK; ++sp) a += *reinterpret_cast<const f32x4*>(part + sp * slab + i);
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = f2bf(epi == EPI_BIAS ? a[j] + bf2f(bias[n + j]) : a[j]);
-      *reinterpret_cast<bf16x4*>(out + (long)m * ldo + n) = o;
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // Skinny (decode) GEMM
@@ -224,8 +160,7 @@ template <int MT, int NT, int WK>
 __global__ void __launch_bounds__(kSkThreads)
 gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                    int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                   bf16* __restrict__ out, long ldo, float* __restrict__ part,
-                   int* __restrict__ counters) {
+                   bf16* __restrict__ out, long ldo, float* __restrict__ part) {
   constexpr int WN = 4 / WK;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wk = wid % WK, wn = wid / WK;
@@ -293,8 +228,6 @@ gemm_skinny_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict_
       store_out(out, ldo, m, n, epi == EPI_BIAS ? v + bf2f(bias[n]) : v);
     }
   }
-  if (part && counters && splitk_arrive(counters + blockIdx.x, gridDim.y, reinterpret_cast<int*>(red)))
-    splitk_fixup(part, gridDim.y, M, N, 0, M, nb0, nb0 + 16 * NT * WN, epi, bias, out, ldo);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -435,7 +368,7 @@ __global__ void __launch_bounds__(kTileThreads)
 gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
                  bf16* __restrict__ out, long ldo, float* __restrict__ part,
-                 int* __restrict__ counters, const int* __restrict__ grows = nullptr,
+                 const int* __restrict__ grows = nullptr,
                  const int4* __restrict__ gtiles = nullptr, const int* __restrict__ gcount = nullptr,
                  long w_estride = 0, RowScale rsc = RowScale{nullptr, 0, 0.f, 0.f}) {
   constexpr int WNW = 4 / WMW;                // waves along M x waves along N
@@ -524,8 +457,6 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   }
   tile_epilogue<TI, TJ>(acc, m0 + wm * WM, n0 + wn * WN, lane, M, N, epi, bias, out, ldo,
                         part ? part + (long)ksplit * m_slab * N + (long)m0 * N : nullptr, m0, rsc);
-  if (part && counters && splitk_arrive(counters + tile, nsplit, reinterpret_cast<int*>(smem)))
-    splitk_fixup(part, nsplit, M, N, m0, m0 + BM, n0, n0 + BN, epi, bias, out, ldo);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1138,21 +1069,10 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 // ---------------------------------------------------------------------------------------
 static int num_cus() { return 256; }
 
-// Workspace layout: [kCounterBytes of zeroed split counters | SK x M x N f32 partials].
+// Workspace layout: [kCounterBytes reserved head | SK x M x N f32 partials].
 static float* splitk_part(float* ws) { return ws + kCounterBytes / sizeof(float); }
 
-// BFLY_GEMM_SPLITK_FIXUP=1 reduces split-K partials inside the GEMM (last-arriver fixup)
-// instead of a separate reduce kernel. Off by default: it only pays when SK x slab bytes per
-// tile is a few tens of KB (the decode plans use SK=8 on 64x128 tiles = 256 KB per tile).
-static int g_fixup = -1;   // -1: not yet read from the environment
-static bool fixup_enabled() {
-  if (g_fixup < 0) {
-    const char* e = getenv("BFLY_GEMM_SPLITK_FIXUP");
-    g_fixup = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_fixup == 1;
-}
-void gemm_set_splitk_fixup(bool on) { g_fixup = on ? 1 : 0; }
+
 
 template <int MT, int NT, int WK>
 static void run_skinny(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
@@ -1160,8 +1080,7 @@ static void run_skinny(const bf16* X, long ldx, const bf16* W, long ldw, int M, 
                        hipStream_t stream) {
   dim3 grid(N / (16 * NT * (4 / WK)), sk);
   gemm_skinny_kernel<MT, NT, WK><<<grid, kSkThreads, 0, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
-      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr);
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr);
 }
 
 static void init_nt_policy() {
@@ -1188,8 +1107,7 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
     attr_set = true;
   }
   gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
-      sk > 1 && fixup_enabled() ? reinterpret_cast<int*>(ws) : nullptr, nullptr, nullptr,
+      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, nullptr, nullptr,
       nullptr, 0, rsc);
 }
 
@@ -1457,7 +1375,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef TL_CASE
     if (!done) return -2;
   }
-  if (p.sk > 1 && !dry && !defer && (!fixup_enabled() || p.kind >= 4)) {   // big / mid kernels: no fixup path
+  if (p.sk > 1 && !dry && !defer) {
     const int nout = epi == EPI_SILU ? N / 2 : N;
     long total = (long)M * nout;
     int grid = (int)((total + 255) / 256);
@@ -1514,7 +1432,7 @@ static int launch_grouped_bm(const bf16* X, long ldx, const bf16* W, long ldw, l
   }
   dim3 grid(max_tiles, sk, N / BN);
   gemm_tile_kernel<BM, BN, WMW, ST, true><<<grid, kTileThreads, lds, stream>>>(
-      X, ldx, W, ldw, slots, N, K, epi, nullptr, out, ldo, sk > 1 ? part : nullptr, nullptr, rows,
+      X, ldx, W, ldw, slots, N, K, epi, nullptr, out, ldo, sk > 1 ? part : nullptr, rows,
       tiles, count, w_estride);
   return 0;
 }
@@ -1562,7 +1480,7 @@ int launch_gemm_deferred(const bf16* X, long ldx, const bf16* W, long ldw, int M
   GemmPlan p = select_plan(M, N, K, EPI_NONE);
   if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
     p.sk = 1;
-  const bool defer = p.sk > 1 && !(fixup_enabled() && p.kind < 2);
+  const bool defer = p.sk > 1;
   const int rc = run_plan(p, X, ldx, W, ldw, M, N, K, EPI_NONE, nullptr, out, ldo, ws, stream,
                           false, defer, rs);
   if (rc != 0) return rc;

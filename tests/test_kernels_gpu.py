@@ -405,16 +405,45 @@ def test_gemm_tile_plans(bm, bn, wmw, epi):
         if st * (bm + bn) * 128 > 160 * 1024:
             continue
         for sk in (1, 3, 5):   # uneven K splits: 16 k-tiles over 3 / 5 workgroups (1..4 deep)
-            for fixup in (False, True) if sk > 1 else (False,):
-                torch.ops.bfly.gemm_set_splitk_fixup(fixup)
-                out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-                ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)  # [split counters | partials]
-                try:
-                    for _ in range(2):   # second call checks the counters were re-armed
-                        torch.ops.bfly.gemm_with_plan(x, w, out, [1, st, 0, wmw, bm, bn, sk], ops.EPILOGUES[epi], ws)
-                finally:
-                    torch.ops.bfly.gemm_set_splitk_fixup(False)
-                _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+            ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)  # [reserved head | partials]
+            torch.ops.bfly.gemm_with_plan(x, w, out, [1, st, 0, wmw, bm, bn, sk], ops.EPILOGUES[epi], ws)
+            _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+
+
+def _tuned_entries():
+    import re
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "kernels", "gemm_tuned.inc")
+    out = []
+    for line in open(path):
+        m = re.match(r"\{(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+)\}", line)
+        if m:
+            out.append(tuple(int(v) for v in m.groups()))
+    return out
+
+
+@pytest.mark.parametrize("NK", sorted({(e[0], e[1]) for e in _tuned_entries()}))
+def test_every_tuned_plan_matches_fp32(NK):
+    """Every entry of the measured plan table (gemm_tuned.inc: the plan the 70B / 8B / Mixtral
+    projections run at each token-count bucket) through ops.linear at that bucket's M, against
+    the fp32 reference; deferred (split-K slab) outputs reduced by the consumer-side reduce."""
+    N, K = NK
+    g = torch.Generator(device=DEV).manual_seed(N % 97)   # device-side: LM-head weights are 2 GB
+    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    for e in _tuned_entries():
+        if (e[0], e[1]) != NK:
+            continue
+        M = e[2]
+        x = _bf(M, K, seed=M + 3)
+        plan = ops.gemm_plan(M, N, K)
+        assert [("skinny", "tile", "big", "dec", "big8", "mid8").index(plan["kind"]), plan["splitk"]] == \
+            [e[3], e[9]], (e, plan)
+        want = x.float() @ w.float().t()
+        _close(ops.linear(x, w), want, 2e-2, 2e-2)
+        _close(ops.materialize(ops.linear(x, w, defer=True)), want, 2e-2, 2e-2)
+        if N % 32 == 0 and N <= 65536:
+            _close(ops.linear(x, w, epilogue="silu"), ref.linear(x, w, None, "silu"), 2e-2, 2e-2)
 
 
 MID_CFGS = [(256, 128, 3, 3), (256, 128, 2, 6), (256, 128, 3, 4), (128, 256, 3, 3), (128, 256, 2, 4),
@@ -496,16 +525,10 @@ def test_gemm_skinny_plans(mt, nt, wk):
     for epi in ("none", "silu") if nt % 2 == 0 else ("none",):
         nout = N // 2 if epi == "silu" else N
         for sk in (1, 2):
-            for fixup in (False, True) if sk > 1 else (False,):
-                torch.ops.bfly.gemm_set_splitk_fixup(fixup)
-                out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-                ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)  # [split counters | partials]
-                try:
-                    for _ in range(2):
-                        torch.ops.bfly.gemm_with_plan(x, w, out, [0, mt, nt, wk, 0, 0, sk], ops.EPILOGUES[epi], ws)
-                finally:
-                    torch.ops.bfly.gemm_set_splitk_fixup(False)
-                _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
+            out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+            ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)  # [reserved head | partials]
+            torch.ops.bfly.gemm_with_plan(x, w, out, [0, mt, nt, wk, 0, 0, sk], ops.EPILOGUES[epi], ws)
+            _close(out, ref.linear(x, w, epilogue=epi), 2e-2, 2e-2)
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 8192, 8192), (7, 1280, 8192), (64, 10240, 8192)])
