@@ -193,7 +193,7 @@ class LLMEngine:
             buckets.append(self.scheduler.group_batch)    # a full group replays one graph
         self.runner = ModelRunner(self.model, self.kv, engine_cfg.max_seq_len, engine_cfg.use_graphs,
                                   buckets, max_batch=engine_cfg.max_batch)
-        if flags.get("BFLY_GRAPH_SAMPLING"):
+        if flags.get("BFLY_GRAPH_SAMPLING") and self.comm.capturable("tp"):   # (TP merge: an all-gather)
             # the last stage's decode graphs end with the sampler on per-request temperatures /
             # seeds staged with the other inputs: one replay per step yields the tokens
             # (top-k / top-p rows and poisoned steps sample eagerly from the graph's logits)

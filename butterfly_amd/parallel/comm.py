@@ -341,6 +341,12 @@ class Communicator:
             return False
         return True
 
+    def capturable(self, group: str) -> bool:
+        """A collective over `group` can be captured into a hipGraph (single rank, native RCCL or
+        an RCCL ProcessGroup; not gloo, whose host staging invalidates a capture)."""
+        g = self.groups.get(group)
+        return g is None or g.size == 1 or g.native is not None or self._nccl(g)
+
     def close(self) -> dict:
         """Tear down this rank's native resources, bounded: the IPC buffers, then the native
         RCCL communicators (edges, axes, world) through their finalize-or-abort close. Graphs

@@ -46,12 +46,12 @@ def record(engine, store, forced=None):
     by (request, output position); with `forced`, return those tokens (teacher forcing)."""
     orig = engine._sample
 
-    def _sample(logits, rids):
+    def _sample(logits, rids, graph_ids=None):
         full = logits
         if engine.mesh.tp > 1:
             full = engine.comm.all_gather(logits.t().contiguous(), "tp").t()
         full = full[:, : cfg.vocab_size].float().cpu()
-        ids = orig(logits, rids)
+        ids = orig(logits, rids, graph_ids)
         # n_gen: tokens generated so far (the asynchronous pipeline applies VALUES a tick late,
         # so len(output) lags; n_gen is the position being sampled)
         for i, r in enumerate(rids):
