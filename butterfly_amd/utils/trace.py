@@ -28,7 +28,9 @@ def _lib():
     _roctx_tried = True
     if not flags.get("BFLY_ROCTX"):
         return None
-    for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so", "librocprofiler-sdk-roctx.so"):
+    # rocprofv3 (rocprofiler-sdk) records the SDK's roctx; the legacy libroctx64 is for rocprof v1/v2
+    for name in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so", "libroctx64.so",
+                 "/opt/rocm/lib/libroctx64.so"):
         try:
             lib = ctypes.CDLL(name)
             lib.roctxRangePushA.argtypes = [ctypes.c_char_p]

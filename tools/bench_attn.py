@@ -42,9 +42,13 @@ def main():
     ap.add_argument("--noncausal", action="store_true", help="time the prefill cases without the causal mask")
     ap.add_argument("--parts", default="0", help="decode split sizes to try (0 = auto)")
     ap.add_argument("--kv-dtype", default="bf16,fp8", help="decode cache element types to time")
+    ap.add_argument("--seq-tables", action="store_true", help="decode: each sequence's pages consecutive "
+                    "(as the block manager hands them out to a fresh batch) instead of a random permutation")
+    ap.add_argument("--rotate", type=int, default=1, help="decode: cycle through this many distinct caches "
+                    "(>= 4 for a 1k-context B=64 cache: each call streams cold from HBM, as one layer of a step)")
     a = ap.parse_args()
     ops.load_library()
-    for case in filter(None, a.prefill.split(",")):
+    for case in filter(None, "" if a.prefill == "none" else a.prefill.split(",")):
         n, Ls, Hq, Hkv = map(int, case.split(":"))
         D, T = 128, n * Ls
         q = torch.randn(T, Hq, D, device="cuda", dtype=torch.bfloat16)
@@ -63,19 +67,24 @@ def main():
         cdt = torch.float8_e4m3fn if kvd == "fp8" else torch.bfloat16
         D, BS = 128, 32
         nb = (ctx + BS - 1) // BS
-        kc = torch.randn(B * nb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16).to(cdt)
-        vc = torch.randn(B * nb, Hkv, D, BS, device="cuda", dtype=torch.bfloat16).to(cdt)
-        bt = torch.randperm(B * nb, device="cuda").to(torch.int32).view(B, nb)
+        kcs = [torch.randn(B * nb, Hkv, BS, D, device="cuda", dtype=torch.bfloat16).to(cdt) for _ in range(a.rotate)]
+        vcs = [torch.randn(B * nb, Hkv, D, BS, device="cuda", dtype=torch.bfloat16).to(cdt) for _ in range(a.rotate)]
+        kc = kcs[0]
+        turn = [0]
+        bt = (torch.arange(B * nb, device="cuda") if a.seq_tables else torch.randperm(B * nb, device="cuda"))
+        bt = bt.to(torch.int32).view(B, nb)
         cl = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
         q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
         out = torch.empty_like(q)
         for pt in [int(x) for x in a.parts.split(",")]:
-            f = lambda: ops.attn_decode(q, kc, vc, bt, cl, 0.088, ctx, part_tokens=pt, out=out)  # noqa: E731
+            def f(pt=pt):
+                i = turn[0] = (turn[0] + 1) % a.rotate
+                ops.attn_decode(q, kcs[i], vcs[i], bt, cl, 0.088, ctx, part_tokens=pt, out=out)
             us = timed(f)
             byts = 2 * B * ctx * Hkv * D * kc.element_size()
             used = pt if pt > 0 else torch.ops.bfly.attn_decode_part_tokens(B, Hkv, ctx)
             print(json.dumps({"B": B, "ctx": ctx, "Hq": Hq, "Hkv": Hkv, "kv": kvd, "us": round(us, 2),
-                              "TBps": round(byts / us / 1e6, 3), "part_tokens": used}), flush=True)
+                              "TBps": round(byts / us / 1e6, 3), "part_tokens": used, "rotate": a.rotate}), flush=True)
 
 if __name__ == "__main__":
     main()

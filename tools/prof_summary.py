@@ -73,7 +73,7 @@ def main():
         pre_lines += ["", ""]
     attn = [sum(1 for j in range(a + 1, b) if "attn_decode" in rows[j]["Kernel_Name"])
             for a, b in zip(samples, samples[1:])]
-    per_step = a.layers or max(set(attn), key=attn.count)
+    per_step = a.layers if a.layers in attn else max(set(attn), key=attn.count)
     first = next(i for i, n in enumerate(attn) if n == per_step)     # segment samples[i] -> samples[i+1]
     dec = rows[samples[first] + 1:samples[-1] + 1]
     steps = len(samples) - 1 - first
@@ -93,6 +93,11 @@ def main():
     lines.append(f"decode steps in the window: {steps} (sampling dispatches); per step: kernel time "
                  f"{tot / steps / 1e3:.3f} ms, wall span {span / steps / 1e3:.3f} ms, "
                  f"{len(dec) / steps:.1f} dispatches")
+    full = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in dec
+            if "attn_decode_kernel" in r["Kernel_Name"]]
+    if full:
+        lines.append(f"decode attention per call over the window: mean {sum(full) / len(full):.1f} us, "
+                     f"median {sorted(full)[len(full) // 2]:.1f} us")
     if a.layers:
         n_attn = sum(c for k, (c, _) in agg.items() if "attn_decode" in k)
         lines.append(f"cross-check: {n_attn} decode-attention dispatches / {a.layers} layers = {n_attn / a.layers:.2f} steps")
