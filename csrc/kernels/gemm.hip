@@ -867,6 +867,149 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
+// One wave per SIMD, 256x256 tile (plan kind 6, "big4"): 4 waves in 2 x 2, each owning a 128 x
+// 128 output block (8 x 8 mfma_16x16x32 accumulators, 256 registers: the AGPR half of the
+// 512-register file a lone wave gets). Per K-tile (BK = 64) a wave reads 32 fragments (16 KiB
+// of A and B rows) for 128 MFMAs: a third fewer LDS bytes per FLOP than big8's 128 x 64 wave
+// tile, whose fragment reads plus DMA writes fill the LDS port.
+// LDS (160 KiB, all of it): LDS-DMA rings of whole K-tile halves, 2 slots of A (activation
+// rows) and 3 of B (weight rows), 32 KiB each, so the weight stream has two K-tiles of lead and
+// no staging registers (those pushed the allocator into moving accumulators every K-tile).
+// One barrier per K-tile, between its two k-steps (ks):
+//   ks 0 of K-tile t: MFMAs on the ks-0 fragments; read the ks-1 fragments of t;
+//   own DMA of A(t+1), B(t+1) retired (vmcnt), lgkmcnt(0), s_barrier;
+//   ks 1: MFMAs on the ks-1 fragments; read the ks-0 fragments of t+1; DMA A(t+2) into A slot
+//     t % 2 and B(t+3) into B slot t % 3 — K-tile t's last reads (its ks-1 fragments) are
+//     before this barrier in every wave.
+// Source order is the schedule: each k-step is 16 slots of {4 MFMAs, 1 fragment read, 1 DMA}
+// fenced by sched_barrier(0) (cdna_hip_programming.md T19: the scheduler clusters memory
+// operations, and a lone wave has nothing to hide the stall behind). Branch-free: past the last
+// K-tile the DMA re-reads it into a slot nobody reads any more.
+// ---------------------------------------------------------------------------------------
+constexpr int kB4Threads = 256;
+constexpr int kB4Slot = 256 * 128;                 // one operand half of a K-tile: 32 KiB
+constexpr int kB4LdsBytes = 5 * kB4Slot;           // A slots 0-1, B slots 2-4: 160 KiB
+
+__device__ __forceinline__ void b4_dma(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, soff, 0, 0);
+}
+
+__global__ void __launch_bounds__(kB4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
+                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
+                 bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+  constexpr int BM = 256, BN = 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // wave index in an SGPR: the DMA's LDS destinations (M0) and the fragment row bases are then
+  // scalar (a VGPR wave index cost a readfirstlane + s_nop per DMA instruction)
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int per_group = kBigGroupM * ntiles;
+  const int grp = t / per_group, first_m = grp * kBigGroupM;
+  const int gsize = min(mtiles - first_m, kBigGroupM);
+  const int m0 = (first_m + (t % per_group) % gsize) * BM;
+  const int n0 = ((t % per_group) / gsize) * BN;
+  const int ktiles = K / 64;
+  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
+  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
+  const int nk = kt1 - kt0;   // >= 2 (host check)
+
+  // DMA: instruction s (0..7) of wave w fills LDS row block 8 w + s (8 rows x 128 B, lane-
+  // linear); lane L supplies row 8 (8 w + s) + (L >> 3) at the chunk lds_frag expects in
+  // position L & 7: chunk = (L & 7) ^ ((row >> 1) & 7) = (L & 7) ^ ((L >> 4) + 4 (s & 1)) & 7
+  const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);   // A rows past M read zeros
+  const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
+  const int drow = 64 * wid + (lane >> 3);
+  int va[2], vb[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int ch = (lane & 7) ^ (((lane >> 4) + 4 * e) & 7);
+    va[e] = (int)((drow * ldx + ch * 8) * 2);
+    vb[e] = (int)((drow * ldw + ch * 8) * 2);
+  }
+  auto dma_a = [&](int k, int slot, int s) {
+    b4_dma(rsa, smem + slot * kB4Slot + (8 * wid + s) * 1024, va[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldx * 2));
+  };
+  auto dma_b = [&](int k, int slot, int s) {
+    b4_dma(rsb, smem + (2 + slot) * kB4Slot + (8 * wid + s) * 1024, vb[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldw * 2));
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  // fragment idx 0-7: B rows (output columns) 16 idx, 8-15: A rows 16 (idx - 8), of k-step ks
+  auto rd1 = [&](int sa_, int sb_, int ks, int idx, bf16x8 (&f)[16]) {
+    f[idx] = idx < 8 ? lds_frag(smem + (2 + sb_) * kB4Slot, wc * 128 + 16 * idx + fr, ks * 4 + fq)
+                     : lds_frag(smem + sa_ * kB4Slot, wr * 128 + 16 * (idx - 8) + fr, ks * 4 + fq);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // MFMA group n (0..15): output row block i = n / 2, column blocks 4 (n & 1) .. + 3
+  auto mf4 = [&](int n, const bf16x8 (&f)[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = n >> 1, j = 4 * (n & 1) + q;
+      acc[i][j] = mfma16(f[j], f[8 + i], acc[i][j]);
+    }
+  };
+  bf16x8 f0[16], f1[16];   // all fragments of k-step 0 / k-step 1
+
+  // prologue: A(0), B(0), A(1), B(1), B(2) (the ring's load order: A(t+1) then B(t+2))
+#pragma unroll
+  for (int s = 0; s < 8; ++s) dma_a(0, 0, s);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) dma_b(0, 0, s);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) dma_a(1, 1, s);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) dma_b(1, 1, s);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) dma_b(min(2, nk - 1), 2, s);
+  vm_wait<24>();                      // K-tile 0 landed (own part)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int idx = 0; idx < 16; ++idx) rd1(0, 0, 0, idx, f0);
+
+  int sb = 0;   // B slot of K-tile k (k % 3)
+  for (int k = 0; k < nk; ++k) {
+    const int sa = k & 1, sb1 = sb == 2 ? 0 : sb + 1;
+    // fragment reads front-loaded (two per slot in the first half) so they have retired when
+    // the k-step ends: ks 0 closes on lgkmcnt(0) + barrier, ks 1 feeds the next ks 0 at once
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      mf4(n, f0);
+      if (n < 8) {
+        rd1(sa, sb, 1, 2 * n, f1);
+        rd1(sa, sb, 1, 2 * n + 1, f1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    vm_wait<8>();                     // A(k+1), B(k+1) landed; B(k+2) may fly
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int ka = min(k + 2, nk - 1), kb = min(k + 3, nk - 1);
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      mf4(n, f1);
+      if (n < 8) {
+        rd1(sa ^ 1, sb1, 0, 2 * n, f0);
+        rd1(sa ^ 1, sb1, 0, 2 * n + 1, f0);
+      }
+      if (n < 8) dma_a(ka, sa, n);
+      else dma_b(kb, sb, n - 8);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    sb = sb1;
+  }
+  vm_wait<0>();                       // no LDS-DMA may outlive the workgroup
+  tile_epilogue<8, 8>(acc, m0 + wr * 128, n0 + wc * 128, lane, M, N, epi, bias, out, ldo,
+                      part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0,
+                      RowScale{nullptr, 0, 0.f, 0.f});
+}
+
+// ---------------------------------------------------------------------------------------
 // Mid-M GEMM (plan kind 5): the tensor-parallel shard projections at M = 128-512 rows (tp2-tp8
 // decode at 64 sequences per GPU, large single-GPU batches), where a 256x256 tile grid leaves
 // most of the 256 CUs idle (tp8 QKV at M = 512: 10 tiles) and the 4-wave tile kernel keeps the
@@ -1144,6 +1287,19 @@ static void run_big8(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   gemm_big8_kernel<false><<<grid, kB8Threads, kB8LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
+static void run_big4(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                     int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big4_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kB4LdsBytes);
+    attr_set = true;
+  }
+  dim3 grid(((M + 255) / 256) * (N / 256), sk);
+  float* part = sk > 1 ? splitk_part(ws) : nullptr;
+  gemm_big4_kernel<<<grid, kB4Threads, kB4LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+}
+
 template <int BM, int BN, int SX, int SW>
 static void run_mid8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                      const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream,
@@ -1301,6 +1457,10 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
     if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+  } else if (p.kind == 6) {
+    // one-wave-per-SIMD 256x256 tile: every split needs >= 2 K-tiles of 64
+    if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
+    if (!dry) run_big4(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
   } else if (p.kind == 5) {
     // mid-M 8-wave staggered GEMM: plan {5, SW (weight ring), SX (activation ring; 0 = SW), 0,
     // BM, BN, sk}

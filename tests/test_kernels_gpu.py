@@ -354,10 +354,12 @@ def test_moe_route_and_gate_scale():
 
 @pytest.mark.parametrize("M,N,K", [(600, 512, 1024), (256, 768, 192), (77, 256, 128), (1000, 1280, 4096),
                                    (300, 512, 256), (520, 512, 128)])
+@pytest.mark.parametrize("kind", [4, 6])
 @pytest.mark.parametrize("epi", ["none", "bias", "silu"])
-def test_gemm_big_tile(M, N, K, epi):
-    """256x256 8-phase prefill kernel (plan kind 4): ragged M, the minimum of two 64-deep
-    K-tiles per split, uneven split-K, all epilogues, asymmetric operands."""
+def test_gemm_big_tile(M, N, K, epi, kind):
+    """256x256 prefill kernels (plan kind 4: 8-phase, 8 waves; kind 6: one wave per SIMD):
+    ragged M, the minimum of two 64-deep K-tiles per split, uneven split-K, all epilogues,
+    asymmetric operands."""
     x = _bf(M, K, seed=60)
     w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=61)
     b = _bf(N, seed=62) if epi == "bias" else None
@@ -368,15 +370,16 @@ def test_gemm_big_tile(M, N, K, epi):
             continue
         out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
         ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
-        torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
         _close(out, want, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("kind", [4, 6])
 @pytest.mark.parametrize("M,N,K,epi,sk", [(4096, 4096, 8192, "none", 1),      # 256-tile grid, K 8192
                                           (8192, 2560, 8192, "silu", 1),      # 70B prefill shapes
                                           (520, 7168, 8192, "silu", 4),       # tp8 gate_up at M 512+
                                           (512, 1280, 8192, "none", 8)])      # tp8 QKV, deep split
-def test_gemm_big_tile_production(M, N, K, epi, sk):
+def test_gemm_big_tile_production(M, N, K, epi, sk, kind):
     """The prefill kernel at production scale: K = 8192 (128 K-tiles per split down to 16),
     grids of >= 256 tiles (every CU busy, XCD remap and GROUP_M walk over many super-rows),
     the SwiGLU epilogue, against the fp32 reference."""
@@ -386,7 +389,7 @@ def test_gemm_big_tile_production(M, N, K, epi, sk):
     want = ref.linear(x, w, None, epi)
     out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
     ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
-    torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws)
+    torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws)
     _close(out, want, 2e-2, 2e-2)
 
 
@@ -437,7 +440,7 @@ def test_every_tuned_plan_matches_fp32(NK):
         M = e[2]
         x = _bf(M, K, seed=M + 3)
         plan = ops.gemm_plan(M, N, K)
-        assert [("skinny", "tile", "big", "dec", "big8", "mid8").index(plan["kind"]), plan["splitk"]] == \
+        assert [("skinny", "tile", "big", "dec", "big8", "mid8", "big4").index(plan["kind"]), plan["splitk"]] == \
             [e[3], e[9]], (e, plan)
         want = x.float() @ w.float().t()
         _close(ops.linear(x, w), want, 2e-2, 2e-2)

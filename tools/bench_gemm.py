@@ -96,7 +96,7 @@ def main():
                 nout = N // 2 if epi == "silu" else N
                 out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
                 plan = ops.gemm_plan(M, N, K)
-                auto = [("skinny", "tile", "big", "dec", "big8", "mid8").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
+                auto = [("skinny", "tile", "big", "dec", "big8", "mid8", "big4").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
                         plan["bn"], plan["splitk"]]
                 t = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, Ws[i % copies], out, auto, ops.EPILOGUES[epi], ws),
                            tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": auto, "auto": True})

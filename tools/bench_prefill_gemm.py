@@ -24,6 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from butterfly_amd import ops  # noqa: E402
 from butterfly_amd.ops import reference as ref  # noqa: E402
 
+KINDS = (4, 6)   # 4: gemm_big8_kernel (8 waves, the default); 6: gemm_big4_kernel (one wave per SIMD)
 SHAPES = [("qkv", 10240, 8192, "none"), ("o", 8192, 8192, "none"), ("gate_up", 57344, 8192, "silu"),
           ("down", 8192, 28672, "none")]
 
@@ -35,21 +36,20 @@ def uni(*shape):
 def check(ws):
     """kind 4 vs the fp32 reference: M tails, split-K, bias and SiLU epilogues."""
     bad = []
-    for mt, M, N, K, epi, sk in [(m,) + c for m in (1, 2, 3, 5) for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
+    for kind, M, N, K, epi, sk in [(m,) + c for m in KINDS for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
                              (1024, 1024, 2048, "silu", 1), (512, 1280, 4096, "none", 4), (777, 512, 1024, "bias", 1),
                              (2048, 2560, 8192, "none", 2)]]:
-        kind = 4
         x = uni(M, K) * 0.5
         w = uni(N, K) * 0.05
         b = uni(N) if epi == "bias" else None
         nout = N // 2 if epi == "silu" else N
         out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
-        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, mt, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
         want = ref.linear(x.float(), w.float(), b.float() if b is not None else None,
                           "silu" if epi == "silu" else "none")
         err = ((out.float() - want).abs() / (want.abs() + 2e-2)).max().item()
         rel = ((out.float() - want).norm() / want.norm()).item()
-        row = {"kind": kind, "mt": mt, "M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
+        row = {"kind": kind, "M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
         print(json.dumps({"check": row}), flush=True)
         if rel > 1e-2:
             bad.append(row)
@@ -82,13 +82,8 @@ def main():
                 if (K // 64) < 2 * sk:
                     continue
                 sfx = "" if a.sks == "1" else f"/sk{sk}"
-                variants["big8e" + sfx] = lambda sk=sk: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 1, 0, 0, 256, 256, sk], e, ws)
-            variants.update({
-                "big8": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, 1], e, ws),
-                "big8la": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 2, 0, 0, 256, 256, 1], e, ws),
-                "big8buf": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 3, 0, 0, 256, 256, 1], e, ws),
-                "big8lb": lambda: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 5, 0, 0, 256, 256, 1], e, ws),
-            })
+                variants["big8" + sfx] = lambda sk=sk: torch.ops.bfly.gemm_with_plan(x, w, out, [4, 0, 0, 0, 256, 256, sk], e, ws)
+                variants["big4" + sfx] = lambda sk=sk: torch.ops.bfly.gemm_with_plan(x, w, out, [6, 0, 0, 0, 256, 256, sk], e, ws)
             if a.variants:
                 keep = a.variants.split(",")
                 variants = {k: v for k, v in variants.items() if k.split("/")[0] in keep}

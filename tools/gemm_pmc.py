@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Prefill GEMM variants on one Llama-3-70B shape (QKV, 8192 tokens), a few serialized calls
-each, for rocprofv3 PMC passes (counters per kernel name: gemm_big8_kernel, plan kind 4) and
+each, for rocprofv3 PMC passes (counters per kernel name: gemm_big8_kernel, plan kind 4;
+gemm_big4_kernel, plan kind 6) and
 hipBLASLt as the yardstick."""
 import os
 import sys
@@ -16,7 +17,7 @@ x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
 w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.02).to(torch.bfloat16)
 out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 ws = torch.zeros(1 << 20, dtype=torch.float32, device="cuda")
-for plan in ([4, 0, 0, 0, 256, 256, 1],):
+for plan in ([4, 0, 0, 0, 256, 256, 1], [6, 0, 0, 0, 256, 256, 1]):
     for _ in range(4):
         torch.ops.bfly.gemm_with_plan(x, w, out, plan, 0, ws)
         torch.cuda.synchronize()
