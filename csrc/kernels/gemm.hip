@@ -872,23 +872,31 @@ gemm_big8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 // 512-register file a lone wave gets). Per K-tile (BK = 64) a wave reads 32 fragments (16 KiB
 // of A and B rows) for 128 MFMAs: a third fewer LDS bytes per FLOP than big8's 128 x 64 wave
 // tile, whose fragment reads plus DMA writes fill the LDS port.
-// LDS (160 KiB, all of it): LDS-DMA rings of whole K-tile halves, 2 slots of A (activation
-// rows) and 3 of B (weight rows), 32 KiB each, so the weight stream has two K-tiles of lead and
-// no staging registers (those pushed the allocator into moving accumulators every K-tile).
+// LDS (160 KiB, all of it): LDS-DMA rings of whole K-tile halves, 3 slots of A (activation
+// rows) and 2 of B (weight rows), 32 KiB each: no staging registers (those pushed the allocator
+// into moving accumulators every K-tile). A gets the deeper ring: an XCD's 32 resident tiles
+// are 8 row tiles x 4 column tiles (GROUP_M walk), so A misses its L2 twice as often as B.
 // One barrier per K-tile, between its two k-steps (ks):
-//   ks 0 of K-tile t: MFMAs on the ks-0 fragments; read the ks-1 fragments of t;
-//   own DMA of A(t+1), B(t+1) retired (vmcnt), lgkmcnt(0), s_barrier;
-//   ks 1: MFMAs on the ks-1 fragments; read the ks-0 fragments of t+1; DMA A(t+2) into A slot
-//     t % 2 and B(t+3) into B slot t % 3 — K-tile t's last reads (its ks-1 fragments) are
-//     before this barrier in every wave.
-// Source order is the schedule: each k-step is 16 slots of {4 MFMAs, 1 fragment read, 1 DMA}
-// fenced by sched_barrier(0) (cdna_hip_programming.md T19: the scheduler clusters memory
-// operations, and a lone wave has nothing to hide the stall behind). Branch-free: past the last
-// K-tile the DMA re-reads it into a slot nobody reads any more.
+//   ks 0 of K-tile t: MFMAs on the ks-0 fragments; read the ks-1 fragments of t; DMA A(t+2)
+//     into A slot (t+2) % 3, which K-tile t-1 left before the previous barrier;
+//   own DMA of A(t+1), B(t+1) retired (vmcnt 8: A(t+2) flies), lgkmcnt(0), s_barrier;
+//   ks 1: MFMAs on the ks-1 fragments; read the ks-0 fragments of t+1; DMA B(t+2) into B slot
+//     t % 2 — K-tile t's last reads (its ks-1 fragments) are before this barrier in every wave.
+// Source order is the schedule: each k-step is 16 slots of {4 MFMAs, 1 fragment read, a DMA
+// every other slot} fenced by sched_barrier(0) (cdna_hip_programming.md T19: left alone, the
+// scheduler clusters the memory operations, and a lone wave has nothing to hide the stall
+// behind). A lane's fragments of one (slot, ks) share one address VGPR (immediate offsets: 4
+// VALU per K-tile). Branch-free: past the last K-tile the DMA re-reads it into a slot nobody
+// reads any more (a guard made hipcc wait vmcnt(0) per slot: 3.5x slower).
+// Measured (profiles/r5_gemm_big4/): 1.52-1.55 PF at M = 8192 on the Llama-3-70B projections
+// against 1.39-1.47 for gemm_big8_kernel and 1.53-1.64 for hipBLASLt on the same box. Steps that
+// got it there from 1.0 PF: LDS-DMA rings instead of register staging (no accumulator moves),
+// one loop with no peeled iterations, one fragment read per slot (not two), the loop rotated to
+// end on the barrier, A's DMA moved into ks 0, immediate-offset fragment addresses.
 // ---------------------------------------------------------------------------------------
 constexpr int kB4Threads = 256;
 constexpr int kB4Slot = 256 * 128;                 // one operand half of a K-tile: 32 KiB
-constexpr int kB4LdsBytes = 5 * kB4Slot;           // A slots 0-1, B slots 2-4: 160 KiB
+constexpr int kB4LdsBytes = 5 * kB4Slot;           // A slots 0-2, B slots 3-4: 160 KiB
 
 __device__ __forceinline__ void b4_dma(__amdgpu_buffer_rsrc_t r, char* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, soff, 0, 0);
@@ -933,13 +941,23 @@ gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     b4_dma(rsa, smem + slot * kB4Slot + (8 * wid + s) * 1024, va[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldx * 2));
   };
   auto dma_b = [&](int k, int slot, int s) {
-    b4_dma(rsb, smem + (2 + slot) * kB4Slot + (8 * wid + s) * 1024, vb[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldw * 2));
+    b4_dma(rsb, smem + (3 + slot) * kB4Slot + (8 * wid + s) * 1024, vb[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldw * 2));
   };
   const int fr = lane & 15, fq = lane >> 4;
-  // fragment idx 0-7: B rows (output columns) 16 idx, 8-15: A rows 16 (idx - 8), of k-step ks
+  // fragment idx 0-7: B rows (output columns) 16 idx, 8-15: A rows 16 (idx - 8), of k-step ks.
+  // lds_frag's swizzle depends on row bits 1-3 = fr bits 1-3 only, so a lane's fragments of one
+  // (slot, ks) share one VGPR address and differ by immediates of 2048 B (16 rows)
+  int lo[2][2];   // [operand A / B][ks] lane byte offset inside a slot
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int ch = ((ks * 4 + fq) ^ ((fr >> 1) & 7)) * 16;
+    lo[0][ks] = (wr * 128 + fr) * 128 + ch;
+    lo[1][ks] = (wc * 128 + fr) * 128 + ch;
+  }
   auto rd1 = [&](int sa_, int sb_, int ks, int idx, bf16x8 (&f)[16]) {
-    f[idx] = idx < 8 ? lds_frag(smem + (2 + sb_) * kB4Slot, wc * 128 + 16 * idx + fr, ks * 4 + fq)
-                     : lds_frag(smem + sa_ * kB4Slot, wr * 128 + 16 * (idx - 8) + fr, ks * 4 + fq);
+    const char* p = idx < 8 ? smem + (3 + sb_) * kB4Slot + lo[1][ks] + 2048 * idx
+                            : smem + sa_ * kB4Slot + lo[0][ks] + 2048 * (idx - 8);
+    f[idx] = *reinterpret_cast<const bf16x8*>(p);
   };
   f32x4 acc[8][8];
 #pragma unroll
@@ -956,7 +974,7 @@ gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   };
   bf16x8 f0[16], f1[16];   // all fragments of k-step 0 / k-step 1
 
-  // prologue: A(0), B(0), A(1), B(1), B(2) (the ring's load order: A(t+1) then B(t+2))
+  // prologue: A(0), B(0), A(1), B(1), A(2) (the ring's load order: B(t+2) then A(t+3))
 #pragma unroll
   for (int s = 0; s < 8; ++s) dma_a(0, 0, s);
 #pragma unroll
@@ -965,44 +983,46 @@ gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   for (int s = 0; s < 8; ++s) dma_a(1, 1, s);
 #pragma unroll
   for (int s = 0; s < 8; ++s) dma_b(1, 1, s);
-#pragma unroll
-  for (int s = 0; s < 8; ++s) dma_b(min(2, nk - 1), 2, s);
-  vm_wait<24>();                      // K-tile 0 landed (own part)
+  vm_wait<16>();                      // K-tile 0 landed (own part); A(1), B(1) fly
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int idx = 0; idx < 16; ++idx) rd1(0, 0, 0, idx, f0);
 
-  int sb = 0;   // B slot of K-tile k (k % 3)
-  for (int k = 0; k < nk; ++k) {
-    const int sa = k & 1, sb1 = sb == 2 ? 0 : sb + 1;
-    // fragment reads front-loaded (two per slot in the first half) so they have retired when
-    // the k-step ends: ks 0 closes on lgkmcnt(0) + barrier, ks 1 feeds the next ks 0 at once
+  // The loop is rotated so its back edge sits right after the barrier (the compiler puts a
+  // conservative lgkmcnt(0) at a loop header: there it finds nothing outstanding): iteration k =
+  // ks 1 of K-tile k, then ks 0 of K-tile k + 1, then the barrier; the last ks 1 is peeled.
+  auto ks0 = [&](int k, int sa_, int sb_) {   // ks 0 of K-tile k: its ks-1 fragments read
 #pragma unroll
     for (int n = 0; n < 16; ++n) {
       mf4(n, f0);
-      if (n < 8) {
-        rd1(sa, sb, 1, 2 * n, f1);
-        rd1(sa, sb, 1, 2 * n + 1, f1);
-      }
+      // A(k+2) into the slot K-tile k-1 left (its last reads precede the previous barrier)
+      if (n & 1) dma_a(min(k + 2, nk - 1), sa_ == 0 ? 2 : sa_ - 1, n >> 1);
+      rd1(sa_, sb_, 1, n, f1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    vm_wait<8>();                     // A(k+1), B(k+1) landed; B(k+2) may fly
+    vm_wait<8>();                     // A(k+1), B(k+1) landed; A(k+2) may fly
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const int ka = min(k + 2, nk - 1), kb = min(k + 3, nk - 1);
+  };
+  auto ks1 = [&](int k, int sa_, int sb_, int sa1_) {   // ks 1 of K-tile k: next ks-0 read, DMA
+    const int kb = min(k + 2, nk - 1);
 #pragma unroll
     for (int n = 0; n < 16; ++n) {
       mf4(n, f1);
-      if (n < 8) {
-        rd1(sa ^ 1, sb1, 0, 2 * n, f0);
-        rd1(sa ^ 1, sb1, 0, 2 * n + 1, f0);
-      }
-      if (n < 8) dma_a(ka, sa, n);
-      else dma_b(kb, sb, n - 8);
+      rd1(sa1_, sb_ ^ 1, 0, n, f0);
+      if (n & 1) dma_b(kb, sb_, n >> 1);   // B(k+2) into the slot K-tile k just left
       __builtin_amdgcn_sched_barrier(0);
     }
-    sb = sb1;
+  };
+  int sa = 0;   // A slot of K-tile k (k % 3)
+  ks0(0, 0, 0);
+  for (int k = 0; k + 1 < nk; ++k) {
+    const int sb = k & 1, sa1 = sa == 2 ? 0 : sa + 1;
+    ks1(k, sa, sb, sa1);
+    ks0(k + 1, sa1, sb ^ 1);
+    sa = sa1;
   }
+  ks1(nk - 1, sa, (nk - 1) & 1, sa == 2 ? 0 : sa + 1);
   vm_wait<0>();                       // no LDS-DMA may outlive the workgroup
   tile_epilogue<8, 8>(acc, m0 + wr * 128, n0 + wc * 128, lane, M, N, epi, bias, out, ldo,
                       part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0,
@@ -1383,8 +1403,9 @@ GemmPlan plan_gemm(int M, int N, int K) {
     if (b >= M) { bucket = b; break; }
   if (bucket == 0) return plan_gemm_heuristic(M, N, K);
   for (const TunedPlan& t : kTuned)
-    if (t.N == N && t.K == K && t.M == bucket)
-      return GemmPlan{t.kind, t.kind == 4 ? 0 : t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
+    if (t.N == N && t.K == K && t.M == bucket)   // 256x256 entries (swept on big8) run big4:
+      return t.kind == 4 ? GemmPlan{6, 0, 0, 0, 256, 256, t.sk}   // >= big8 at every swept M / sk
+                         : GemmPlan{t.kind, t.mt, t.nt, t.wk, t.bm, t.bn, t.sk};
   return plan_gemm_heuristic(M, N, K);
 }
 
@@ -1408,10 +1429,11 @@ static GemmPlan plan_gemm_heuristic(int M, int N, int K) {
     return p;
   }
   if (M > 256 && N % 256 == 0 && K % 64 == 0) {
-    // prefill / large batch: the 256x256 8-phase tile (gemm_big8_kernel: 1.39-1.40 PF at
-    // M = 8192 on the 70B projections, profiles/r4_gemm_prefill_lb.log); split K only when the
-    // tile grid cannot fill the 256 CUs
-    p.kind = 4;
+    // prefill / large batch: the 256x256 one-wave-per-SIMD tile (gemm_big4_kernel: 1.52-1.55
+    // PF at M = 8192 on the 70B projections, 6-10 % over the 8-phase gemm_big8_kernel and ahead
+    // of it at M = 256-2048 too, profiles/r5_gemm_big4/); split K only when the tile grid cannot
+    // fill the 256 CUs
+    p.kind = 6;
     p.mt = 0;
     p.bm = p.bn = 256;
     const int tiles = ((M + 255) / 256) * (N / 256);

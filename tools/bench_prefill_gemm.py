@@ -1,14 +1,12 @@
 #!/usr/bin/env python3
-"""Prefill GEMM A/B on the Llama-3-70B projections: gemm_big8_kernel (plan kind 4, 8-phase
-BK 64; big8e = its early-release variant, plan mt = 1, the default; big8buf = big8e with
-buffer-descriptor staging, mt = 3; big8la = big8buf with the A-lo fragments read one phase ahead,
-mt = 2; big8lb = big8la with the B-lo fragments read early too, mt = 5, the default) vs torch.matmul (hipBLASLt,
-yardstick only; not used by the framework). The round-3 variants that lost (the BK-32 ring
-kernel, three one-wave-per-SIMD kernels) are recorded in profiles/r3_gemm_prefill_pmc.md.
+"""Prefill GEMM A/B on the Llama-3-70B projections: gemm_big8_kernel (plan kind 4: 8 waves,
+8-phase BK 64) and gemm_big4_kernel (plan kind 6: one wave per SIMD, 128 x 128 wave tiles,
+slot-fenced schedule) vs torch.matmul (hipBLASLt, yardstick only; not used by the framework).
+The round-3 variants that lost are recorded in profiles/r3_gemm_prefill_pmc.md.
 
 Random uniform [-1, 1) operands (cdna_hip_programming.md §5.4 rule 25: zero-filled data clocks
 higher), interleaved rounds in one process (rule 24), median and min per variant. First checks
-kind 4 against the fp32 reference (M tail, split-K, bias and SiLU epilogues).
+kinds 4 and 6 against the fp32 reference (M tail, split-K, bias and SiLU epilogues).
 
 usage: python tools/bench_prefill_gemm.py [--ms 8192] [--rounds 5] [--check-only]
 """
@@ -36,20 +34,21 @@ def uni(*shape):
 def check(ws):
     """kind 4 vs the fp32 reference: M tails, split-K, bias and SiLU epilogues."""
     bad = []
-    for kind, M, N, K, epi, sk in [(m,) + c for m in KINDS for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
+    for kv, M, N, K, epi, sk in [(m,) + c for m in KINDS for c in [(256, 256, 128, "none", 1), (300, 512, 1024, "none", 1), (4097, 768, 640, "none", 1),
                              (1024, 1024, 2048, "silu", 1), (512, 1280, 4096, "none", 4), (777, 512, 1024, "bias", 1),
                              (2048, 2560, 8192, "none", 2)]]:
+        kind, var = kv if isinstance(kv, tuple) else (kv, 0)
         x = uni(M, K) * 0.5
         w = uni(N, K) * 0.05
         b = uni(N) if epi == "bias" else None
         nout = N // 2 if epi == "silu" else N
         out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
-        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, 0, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
+        torch.ops.bfly.gemm_with_plan(x, w, out, [kind, var, 0, 0, 256, 256, sk], ops.EPILOGUES[epi], ws, b)
         want = ref.linear(x.float(), w.float(), b.float() if b is not None else None,
                           "silu" if epi == "silu" else "none")
         err = ((out.float() - want).abs() / (want.abs() + 2e-2)).max().item()
         rel = ((out.float() - want).norm() / want.norm()).item()
-        row = {"kind": kind, "M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
+        row = {"kind": kind, "variant": var, "M": M, "N": N, "K": K, "epi": epi, "sk": sk, "max_rel_err": round(err, 4), "rel_l2": round(rel, 5)}
         print(json.dumps({"check": row}), flush=True)
         if rel > 1e-2:
             bad.append(row)
