@@ -49,6 +49,11 @@ MODEL_NAMES = {"llama3-70b": "Llama-3-70B", "llama3-8b": "Llama-3-8B", "mixtral-
                "gpt2-small": "GPT-2-small"}
 
 
+def groups_of(eng, mesh) -> int:
+    """Request groups in flight (the asynchronous pipeline keeps pp of them)."""
+    return mesh.pp if eng.async_pp else 1
+
+
 def parse_plan(s: str):
     """"auto" or an axis product such as tp2xpp4, dp2xtp4, pp8, ep8 (Mixtral: dp = ep)."""
     if s == "auto":
@@ -243,12 +248,16 @@ def run(a) -> int:
     for i in range(replica_batch):
         prompt = torch.randint(0, cfg.vocab_size, (a.prompt_len,), generator=g).tolist()
         eng.add_request(prompt, params)
+    # the decode graph is captured before the prefill clock starts (a server captures at
+    # start-up); one rank only here: a multi-rank capture's warm-up runs issue collectives
+    if world == 1 and not a.no_graphs:
+        eng.precapture_decode(replica_batch // groups_of(eng, mesh))
     # prefill (untimed; reported separately)
     tp0 = time.perf_counter()
     prefill_tokens = 0
     # with the asynchronous pipeline (pp > 1) one step advances every stage by one request
     # group (replica_batch / pp sequences) and each sequence gets a token every pp steps
-    groups = mesh.pp if eng.async_pp else 1
+    groups = groups_of(eng, mesh)
     decode_streak = 0
     while eng.scheduler.num_waiting > 0 or decode_streak < groups:
         out = eng.step()

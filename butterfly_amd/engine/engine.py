@@ -267,6 +267,11 @@ class LLMEngine:
         return max(c.hidden_size, d.ffn * max(1, d.experts), d.hq * c.head_dim)
 
     # ------------------------------------------------------------------------------------
+    def precapture_decode(self, rows: int) -> bool:
+        """Capture the decode graph for `rows` concurrent sequences now (ModelRunner.precapture)
+        instead of inside the first decode step; every rank of the model group calls it."""
+        return self.device.type == "cuda" and self.runner.precapture(rows)
+
     def add_request(self, prompt: list, params: Optional[SamplingParams] = None, rid: Optional[int] = None) -> int:
         rid = next(self._ids) if rid is None else rid
         params = params or SamplingParams()

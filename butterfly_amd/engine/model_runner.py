@@ -257,6 +257,27 @@ class ModelRunner:
             self.last_ids = g.ids[:B]
         return g.output[:B]
 
+    def precapture(self, rows: int) -> bool:
+        """Capture the decode graph of the bucket `rows` rows use now rather than inside the
+        first decode step (as a server does at start-up). Single-stage runners only: a pipeline
+        stage's graphs hold their receives. The capture's warm-up runs issue the step's
+        collectives, so every rank of a TP / EP group must call it together."""
+        if self.recv_fn is not None or self.instances > 1 or not self.use_graphs or rows > self.buckets[-1]:
+            return False
+        bucket = self.buckets[bisect.bisect_left(self.buckets, rows)]
+        if bucket in self.graphs or bucket in self.eager_buckets:
+            return bucket in self.graphs
+        try:
+            self._capture(bucket)
+        except Exception as e:  # noqa: BLE001 — the first decode step then runs eagerly too
+            import warnings
+
+            warnings.warn(f"hipGraph capture of decode bucket {bucket} failed ({e!r}); running eagerly")
+            self.eager_buckets.add(bucket)
+            _recover_from_capture(self.device)
+            return False
+        return True
+
     def _run_pipeline_decode(self, bucket: int, inp: dict, hidden_in):
         """Decode of a pipeline stage with native I/O: alternate the bucket's instances, wait
         for the instance's previous send, receive (inside the graph, or eagerly into the same

@@ -132,7 +132,12 @@ class Communicator:
     def _nccl(g: GroupHandle) -> bool:
         # tensor-form collectives on RCCL; list forms on gloo (also used with GPU tensors
         # when several ranks share one device, which RCCL refuses)
-        return g.pg is not None and dist.get_backend(g.pg) == "nccl"
+        if g.pg is None:
+            return False
+        try:
+            return dist.get_backend(g.pg) == "nccl"
+        except (ValueError, RuntimeError):   # not a torch ProcessGroup (the loopback backend)
+            return False
 
     # -- queries ----------------------------------------------------------------------------
     def size(self, group: str = "tp") -> int:
