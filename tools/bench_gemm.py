@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--ms", default="1,16,32,64,128,256")
     ap.add_argument("--shapes", default="tp1,tp8")
     ap.add_argument("--sweep", action="store_true", help="also try alternative skinny plans")
+    ap.add_argument("--kinds", default="", help="sweep only these plan kinds (e.g. 6; the current plan is always timed)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--serial", default=None, help="serialised mode for rocprofv3: write the candidate log here")
     a = ap.parse_args()
@@ -143,9 +144,14 @@ def main():
                                 if K // 64 >= sk * 2:
                                     cands.append([5, sw, sx, 0, bm, bn, sk])
                     if M >= 128 and N % 256 == 0:
-                        for sk in (1, 2, 4, 8, 16):
-                            if K // 64 >= sk * 4:
-                                cands.append([4, 5, 0, 0, 256, 256, sk])
+                        # 256x256 one-wave-per-SIMD tile (kind 6; the 8-wave kind 4 is not swept
+                        # any more: kind 6 is ahead of it at every M / split measured)
+                        for sk in (1, 2, 3, 4, 6, 8, 12, 16):
+                            if K // 64 >= sk * 2:
+                                cands.append([6, 0, 0, 0, 256, 256, sk])
+                    if a.kinds:
+                        keep = {int(k) for k in a.kinds.split(",")}
+                        cands = [c for c in cands if c[0] in keep]
                     for pl in cands:
                         try:
                             tv = timeit(lambda i: torch.ops.bfly.gemm_with_plan(
