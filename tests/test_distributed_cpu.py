@@ -121,7 +121,7 @@ LONG = [[(7 * i + 3) % 97 + 1 for i in range(40)], [(5 * i + 1) % 89 + 1 for i i
 
 
 def _chunked_generate(rank, world, preset, mesh_kw, async_pp, shared_prefix=False, kv_tokens=2048, prompts=None,
-                      max_new=4):
+                      max_new=4, max_batch=4):
     """Prompts longer than the step's token budget (prefilled in chunks over several steps /
     ticks, decode rows riding along), more requests than the batch holds, a request added
     mid-run; with `shared_prefix` every prompt starts with the same 64 tokens (prefix cache);
@@ -135,7 +135,7 @@ def _chunked_generate(rank, world, preset, mesh_kw, async_pp, shared_prefix=Fals
     mesh = Mesh(**mesh_kw)
     comm = Communicator.from_mesh(mesh) if world > 1 else None
     cfg = ModelConfig.from_preset(preset)
-    ecfg = EngineConfig(max_batch=4, max_seq_len=160, kv_cache_tokens=kv_tokens, max_prefill_tokens=24,
+    ecfg = EngineConfig(max_batch=max_batch, max_seq_len=160, kv_cache_tokens=kv_tokens, max_prefill_tokens=24,
                         use_graphs=False, seed=5, async_decode=async_pp, mixed_prefill=True, prefix_caching=True)
     try:
         eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")
@@ -159,21 +159,22 @@ def _chunked_generate(rank, world, preset, mesh_kw, async_pp, shared_prefix=Fals
     return [eng.requests[r].output for r in rids], sorted(kinds), hits, pre
 
 
-@pytest.mark.parametrize("preset,mesh_kw,world", [
-    ("llama-tiny", {}, 1),
-    ("llama-tiny", dict(pp=2), 2),
-    ("llama-tiny", dict(tp=2), 2),
-    ("llama-tiny", dict(tp=2, pp=2), 4),
+@pytest.mark.parametrize("preset,mesh_kw,world,mb", [
+    ("llama-tiny", {}, 1, 4),
+    ("llama-tiny", dict(pp=2), 2, 4),
+    ("llama-tiny", dict(tp=2), 2, 4),
+    ("llama-tiny", dict(tp=2, pp=2), 4, 4),
+    ("llama-small", dict(pp=4), 4, 8),      # 4 groups of 2: a decode row beside each chunk
 ])
 @pytest.mark.parametrize("shared_prefix", [False, True])
-def test_async_mixed_chunked_prefill_matches_sync(preset, mesh_kw, world, shared_prefix):
+def test_async_mixed_chunked_prefill_matches_sync(preset, mesh_kw, world, mb, shared_prefix):
     """Mixed plans (decode rows + prompt chunks) in the asynchronous pipeline: chunked prompts
     over several ticks, prefix-cache hits, PP stages: the tokens of the synchronous
     single-process engine."""
-    ref, ref_kinds, _, _ = _chunked_generate(0, 1, preset, {}, False, shared_prefix)
+    ref, ref_kinds, _, _ = _chunked_generate(0, 1, preset, {}, False, shared_prefix, max_batch=mb)
     assert "mixed" in ref_kinds
-    outs = (run_world(_chunked_generate, world, preset, mesh_kw, True, shared_prefix) if world > 1
-            else [_chunked_generate(0, 1, preset, {}, True, shared_prefix)])
+    outs = (run_world(_chunked_generate, world, preset, mesh_kw, True, shared_prefix, 2048, None, 4, mb) if world > 1
+            else [_chunked_generate(0, 1, preset, {}, True, shared_prefix, max_batch=mb)])
     for o, kinds, hits, _ in outs:
         assert o == ref
         assert "mixed" in kinds
