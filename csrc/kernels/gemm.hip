@@ -1230,6 +1230,171 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 // ---------------------------------------------------------------------------------------
 // Host dispatch
 // ---------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
+// Mid-M one-wave-per-SIMD GEMM (plan kind 7, "mid4"): big4's structure on 128x128 / 256x128 /
+// 128x256 tiles for the TP-shard and large-batch decode projections (M = 128-512), where
+// split-K fills the chip and each workgroup walks only 8-30 K-tiles. 4 waves in 2 x 2, each
+// owning a (BM/2) x (BN/2) block; per K-tile a wave runs TI x TJ MFMAs per k-step in slots of 4
+// (sched_barrier-fenced, fragment reads and LDS-DMA spread over the slots); LDS-DMA rings of SA
+// activation and SB weight K-tiles (the whole 160 KiB: up to 5 weight K-tiles of lead for the
+// HBM stream); one barrier per K-tile; the loop rotated to end on it (see gemm_big4_kernel).
+// The DMA wait count at the barrier follows the fixed issue order
+//   prologue A(0), B(0), A(1 .. SA-2), B(1 .. SB-1); iteration t: A(t+SA-1) in k-step 0,
+//   B(t+SB) in k-step 1
+// and is computed per iteration (scalar), exact in the first iterations as in the steady state.
+// ---------------------------------------------------------------------------------------
+constexpr int kMid4Threads = 256;
+
+template <int BM, int BN, int SA, int SB>
+struct Mid4Cfg {
+  static constexpr int WM = BM / 2, WN = BN / 2, TI = WM / 16, TJ = WN / 16;
+  static constexpr int NS = TI * TJ / 4;            // MFMA slots per k-step
+  static constexpr int NF = TI + TJ;                // fragments per k-step
+  static constexpr int NA = BM / 32, NB = BN / 32;  // DMA instructions per thread per K-tile
+  static constexpr int ASLOT = BM * 128, BSLOT = BN * 128;
+  static constexpr int LDS = SA * ASLOT + SB * BSLOT;
+  static_assert(TJ % 4 == 0 && NA % 2 == 0 && NB % 2 == 0, "mid4 tile shape");
+  static_assert(SA >= 2 && SB >= 2 && LDS <= 160 * 1024, "mid4 rings");
+};
+
+template <int BM, int BN, int SA, int SB>
+__global__ void __launch_bounds__(kMid4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_mid4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
+                 int M, int N, int K, int epi, const bf16* __restrict__ bias,
+                 bf16* __restrict__ out, long ldo, float* __restrict__ part, RowScale rsc) {
+  using C = Mid4Cfg<BM, BN, SA, SB>;
+  constexpr int TI = C::TI, TJ = C::TJ, NS = C::NS, NF = C::NF, NA = C::NA, NB = C::NB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int per_group = kBigGroupM * ntiles;
+  const int grp = t / per_group, first_m = grp * kBigGroupM;
+  const int gsize = min(mtiles - first_m, kBigGroupM);
+  const int m0 = (first_m + (t % per_group) % gsize) * BM;
+  const int n0 = ((t % per_group) / gsize) * BN;
+  const int ktiles = K / 64;
+  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
+  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
+  const int nk = kt1 - kt0;   // >= 1 (host check)
+
+  // DMA: instruction s of wave w fills LDS row block NA w + s (A; NB w + s for B), 8 rows x
+  // 128 B lane-linear, lane L supplying row 8 (block) + (L >> 3) at lds_frag's swizzled chunk
+  // (L & 7) ^ ((L >> 4) + 4 (s & 1)) & 7 (NA, NB even)
+  const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);   // A rows past M read zeros
+  const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
+  int va[2], vb[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int ch = (lane & 7) ^ (((lane >> 4) + 4 * e) & 7);
+    va[e] = (int)(((8 * NA * wid + (lane >> 3)) * ldx + ch * 8) * 2);
+    vb[e] = (int)(((8 * NB * wid + (lane >> 3)) * ldw + ch * 8) * 2);
+  }
+  char* const bbase = smem + SA * C::ASLOT;
+  auto dma_a = [&](int k, int slot, int s) {
+    b4_dma(rsa, smem + slot * C::ASLOT + (NA * wid + s) * 1024, va[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldx * 2));
+  };
+  auto dma_b = [&](int k, int slot, int s) {
+    b4_dma(rsb, bbase + slot * C::BSLOT + (NB * wid + s) * 1024, vb[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldw * 2));
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  int lo[2][2];   // [A / B][ks] lane byte offset inside a slot (fragments differ by 2048 B)
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int ch = ((ks * 4 + fq) ^ ((fr >> 1) & 7)) * 16;
+    lo[0][ks] = (wr * C::WM + fr) * 128 + ch;
+    lo[1][ks] = (wc * C::WN + fr) * 128 + ch;
+  }
+  // fragment idx 0 .. TJ-1: B (output columns 16 idx), TJ .. NF-1: A (rows 16 (idx - TJ))
+  auto rd1 = [&](int sa_, int sb_, int ks, int idx, bf16x8 (&f)[NF]) {
+    const char* p = idx < TJ ? bbase + sb_ * C::BSLOT + lo[1][ks] + 2048 * idx
+                             : smem + sa_ * C::ASLOT + lo[0][ks] + 2048 * (idx - TJ);
+    f[idx] = *reinterpret_cast<const bf16x8*>(p);
+  };
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mf4 = [&](int n, const bf16x8 (&f)[NF]) {   // slot n: row block i, 4 column blocks
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = n / (TJ / 4), j = 4 * (n % (TJ / 4)) + q;
+      acc[i][j] = mfma16(f[j], f[TJ + i], acc[i][j]);
+    }
+  };
+  bf16x8 f0[NF], f1[NF];
+
+  // issue-order bookkeeping (per-thread load counts, see the header)
+  constexpr int P = (SA - 1) * NA + SB * NB;
+  auto idx_a = [&](int j) {
+    return j == 0 ? NA : j <= SA - 2 ? NA + NB + j * NA : P + (j - SA + 1) * (NA + NB) + NA;
+  };
+  auto idx_b = [&](int j) {
+    return j == 0 ? NA + NB : j <= SB - 1 ? NA + NB + (SA - 2) * NA + j * NB : P + (j - SB) * (NA + NB) + NA + NB;
+  };
+#pragma unroll
+  for (int s = 0; s < NA; ++s) dma_a(0, 0, s);
+#pragma unroll
+  for (int s = 0; s < NB; ++s) dma_b(0, 0, s);
+#pragma unroll
+  for (int j = 1; j <= SA - 2; ++j)
+#pragma unroll
+    for (int s = 0; s < NA; ++s) dma_a(min(j, nk - 1), j, s);
+#pragma unroll
+  for (int j = 1; j <= SB - 1; ++j)
+#pragma unroll
+    for (int s = 0; s < NB; ++s) dma_b(min(j, nk - 1), j, s);
+  vm_wait<P - NA - NB>();            // K-tile 0 landed (own part)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int idx = 0; idx < NF; ++idx) rd1(0, 0, 0, idx, f0);
+
+  auto ks0 = [&](int k, int sa_, int sb_) {   // k-step 0 of K-tile k; DMA A(k+SA-1); barrier
+    const int ka = min(k + SA - 1, nk - 1), slot = sa_ == 0 ? SA - 1 : sa_ - 1;
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      mf4(n, f0);
+#pragma unroll
+      for (int q = n * NA / NS; q < (n + 1) * NA / NS; ++q) dma_a(ka, slot, q);
+#pragma unroll
+      for (int idx = n * NF / NS; idx < (n + 1) * NF / NS; ++idx) rd1(sa_, sb_, 1, idx, f1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // A(k+1), B(k+1) landed (own part): the loads issued after the later of them may fly
+    const int total = P + k * (NA + NB) + NA;
+    vm_wait_dyn(total - max(idx_a(k + 1), idx_b(k + 1)));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  auto ks1 = [&](int k, int sa_, int sb_, int sa1_, int sb1_) {   // k-step 1; DMA B(k+SB)
+    const int kb = min(k + SB, nk - 1);
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      mf4(n, f1);
+#pragma unroll
+      for (int idx = n * NF / NS; idx < (n + 1) * NF / NS; ++idx) rd1(sa1_, sb1_, 0, idx, f0);
+#pragma unroll
+      for (int q = n * NB / NS; q < (n + 1) * NB / NS; ++q) dma_b(kb, sb_, q);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  int sa = 0, sb = 0;
+  ks0(0, 0, 0);
+  for (int k = 0; k + 1 < nk; ++k) {
+    const int sa1 = sa == SA - 1 ? 0 : sa + 1, sb1 = sb == SB - 1 ? 0 : sb + 1;
+    ks1(k, sa, sb, sa1, sb1);
+    ks0(k + 1, sa1, sb1);
+    sa = sa1;
+    sb = sb1;
+  }
+  ks1(nk - 1, sa, sb, sa == SA - 1 ? 0 : sa + 1, sb == SB - 1 ? 0 : sb + 1);
+  vm_wait<0>();                       // no LDS-DMA may outlive the workgroup
+  tile_epilogue<TI, TJ>(acc, m0 + wr * C::WM, n0 + wc * C::WN, lane, M, N, epi, bias, out, ldo,
+                        part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0, rsc);
+}
+
 static int num_cus() { return 256; }
 
 // Workspace layout: [kCounterBytes reserved head | SK x M x N f32 partials].
@@ -1318,6 +1483,23 @@ static void run_big4(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   dim3 grid(((M + 255) / 256) * (N / 256), sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
   gemm_big4_kernel<<<grid, kB4Threads, kB4LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+}
+
+template <int BM, int BN, int SA, int SB>
+static void run_mid4(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
+                     const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream,
+                     const RowScale& rsc) {
+  using C = Mid4Cfg<BM, BN, SA, SB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid4_kernel<BM, BN, SA, SB>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr_set = true;
+  }
+  dim3 grid(((M + BM - 1) / BM) * (N / BN), sk);
+  float* part = sk > 1 ? splitk_part(ws) : nullptr;
+  gemm_mid4_kernel<BM, BN, SA, SB><<<grid, kMid4Threads, C::LDS, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias,
+                                                                         out, ldo, part, rsc);
 }
 
 template <int BM, int BN, int SX, int SW>
@@ -1474,11 +1656,24 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
                     hipStream_t stream, bool dry = false, bool defer = false,
                     const RowScale* rs = nullptr) {
   const RowScale rsc = rs ? *rs : RowScale{nullptr, 0, 0.f, 0.f};
-  if (rs != nullptr && p.kind != 1 && p.kind != 3 && p.kind != 5) return -4;   // row scale: tile / ring / mid epilogues
+  if (rs != nullptr && p.kind != 1 && p.kind != 3 && p.kind != 5 && p.kind != 7) return -4;   // row scale: tile / ring / mid epilogues
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
     if (!dry) run_big8(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+  } else if (p.kind == 7) {
+    // mid-M one-wave-per-SIMD tile: plan {7, SA (activation ring), SB (weight ring), 0, BM, BN, sk}
+    if (N % p.bn != 0 || K % 64 != 0 || K / 64 < p.sk) return -1;
+    bool done = false;
+#define MID4_CASE(BM_, BN_, SA_, SB_)                                                               \
+  if (!done && p.bm == BM_ && p.bn == BN_ && p.mt == SA_ && p.nt == SB_) {                          \
+    if (!dry) run_mid4<BM_, BN_, SA_, SB_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    done = true;                                                                                   \
+  }
+    MID4_CASE(128, 128, 4, 6) MID4_CASE(128, 128, 3, 7) MID4_CASE(128, 128, 2, 8)
+    MID4_CASE(256, 128, 3, 4) MID4_CASE(256, 128, 2, 6) MID4_CASE(128, 256, 4, 3) MID4_CASE(128, 256, 2, 4)
+#undef MID4_CASE
+    if (!done) return -2;
   } else if (p.kind == 6) {
     // one-wave-per-SIMD 256x256 tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;

@@ -441,7 +441,7 @@ def test_every_tuned_plan_matches_fp32(NK):
         x = _bf(M, K, seed=M + 3)
         plan = ops.gemm_plan(M, N, K)
         # 256x256 entries (swept on big8, kind 4) run the one-wave-per-SIMD big4 (kind 6)
-        assert [("skinny", "tile", "big", "dec", "big8", "mid8", "big4").index(plan["kind"]), plan["splitk"]] == \
+        assert [("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4").index(plan["kind"]), plan["splitk"]] == \
             [6 if e[3] == 4 else e[3], e[9]], (e, plan)
         want = x.float() @ w.float().t()
         _close(ops.linear(x, w), want, 2e-2, 2e-2)
@@ -491,6 +491,34 @@ def test_gemm_mid8_production(M, N, K, plan):
     ws = torch.zeros(plan[6] * M * N + 16384, dtype=torch.float32, device=DEV)
     torch.ops.bfly.gemm_with_plan(x, w, out, plan, 0, ws)
     _close(out, ref.linear(x, w), 2e-2, 2e-2)
+
+
+MID4_CFGS = [(128, 128, 4, 6), (128, 128, 3, 7), (128, 128, 2, 8), (256, 128, 3, 4), (256, 128, 2, 6),
+             (128, 256, 4, 3), (128, 256, 2, 4)]
+
+
+@pytest.mark.parametrize("bm,bn,sa,sb", MID4_CFGS)
+def test_gemm_mid4_plans(bm, bn, sa, sb):
+    """Mid-M one-wave-per-SIMD GEMM (plan kind 7, activation ring sa / weight ring sb): ragged M
+    below and above one row tile, K-tile counts from 1 to past both rings per split (the
+    per-iteration DMA wait counts of the first iterations and the clamped tail loads), uneven
+    split-K, all epilogues, asymmetric operands."""
+    N = 3 * bn
+    for M, K in ((bm - 5, 1024), (bm + 9, 192), (3 * bm + 1, 4096), (7, 64), (bm, 64 * (sb + 2))):
+        x = _bf(M, K, seed=147)
+        w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=148)
+        b = _bf(N, seed=149)
+        for epi in ("none", "bias", "silu"):
+            nout = N // 2 if epi == "silu" else N
+            want = ref.linear(x, w, b if epi == "bias" else None, "silu" if epi == "silu" else "none")
+            for sk in (1, 2, 3, 7):
+                if K // 64 < sk:
+                    continue
+                out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
+                ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
+                torch.ops.bfly.gemm_with_plan(x, w, out, [7, sa, sb, 0, bm, bn, sk], ops.EPILOGUES[epi], ws,
+                                              b if epi == "bias" else None)
+                _close(out, want, 2e-2, 2e-2)
 
 
 DEC_CFGS = [(128, 224, 8, 1, 4), (128, 224, 8, 1, 3), (128, 256, 8, 1, 3), (128, 256, 4, 2, 3), (128, 128, 8, 1, 5),

@@ -37,6 +37,9 @@ DEC_CFGS = [(128, 224, 8, 1, 4), (128, 224, 8, 1, 3), (128, 256, 8, 1, 3), (128,
             (128, 128, 4, 2, 5), (128, 160, 8, 1, 4), (128, 80, 8, 1, 6), (128, 64, 8, 1, 8), (128, 64, 4, 2, 8),
             (64, 128, 4, 2, 6), (64, 256, 4, 2, 4), (64, 224, 4, 1, 4), (64, 160, 4, 2, 5), (64, 64, 4, 2, 8)]
 
+MID4_CFGS = [(128, 128, 4, 6), (128, 128, 3, 7), (128, 128, 2, 8), (256, 128, 3, 4), (256, 128, 2, 6),
+             (128, 256, 4, 3), (128, 256, 2, 4)]
+
 MID_CFGS = [(256, 128, 3, 3), (256, 128, 2, 6), (256, 128, 3, 4), (128, 256, 3, 3), (128, 256, 2, 4),
             (128, 128, 4, 4), (128, 128, 3, 6), (128, 128, 2, 8), (128, 128, 2, 2)]
 
@@ -97,7 +100,7 @@ def main():
                 nout = N // 2 if epi == "silu" else N
                 out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
                 plan = ops.gemm_plan(M, N, K)
-                auto = [("skinny", "tile", "big", "dec", "big8", "mid8", "big4").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
+                auto = [("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
                         plan["bn"], plan["splitk"]]
                 t = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, Ws[i % copies], out, auto, ops.EPILOGUES[epi], ws),
                            tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": auto, "auto": True})
@@ -143,6 +146,14 @@ def main():
                             for sk in (1, 2, 3, 4, 6, 8, 12, 16):
                                 if K // 64 >= sk * 2:
                                     cands.append([5, sw, sx, 0, bm, bn, sk])
+                    # mid-M one-wave-per-SIMD tile (kind 7): {7, SA, SB, 0, BM, BN, sk}
+                    if M >= 64:
+                        for bm, bn, sa, sb in MID4_CFGS:
+                            if N % bn or (bm == 256 and M <= 128):
+                                continue
+                            for sk in (1, 2, 3, 4, 6, 8, 12, 16):
+                                if K // 64 >= sk * 2:
+                                    cands.append([7, sa, sb, 0, bm, bn, sk])
                     if M >= 128 and N % 256 == 0:
                         # 256x256 one-wave-per-SIMD tile (kind 6; the 8-wave kind 4 is not swept
                         # any more: kind 6 is ahead of it at every M / split measured)
