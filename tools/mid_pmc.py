@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Mid-M GEMM plans on two TP-shard shapes, a few serialized calls each, for rocprofv3 PMC
 passes (counters per dispatch; rows grouped by plan in call order by tools/mid_pmc_md.py):
-tp8 down at M = 512 (N 8192, K 3584) and tp4 gate_up at M = 256 (N 14336, K 8192), each with
-the mid8 kernel (kind 5), the 4-wave tile kernel (kind 1) and the 8-phase big tile (kind 4)."""
+tp8 down / QKV at M = 512 and tp4 gate_up at M = 256, each with the 8-wave mid kernel (kind 5)
+and the one-wave-per-SIMD mid kernel (kind 7) at the plans the table gives them."""
 import json
 import os
 import sys
@@ -14,10 +14,9 @@ from butterfly_amd import ops  # noqa: E402
 
 assert ops.load_library(), ops._load_error
 CASES = [
-    ("tp8.down", 512, 8192, 3584, [[5, 3, 0, 0, 256, 128, 2], [5, 4, 0, 0, 128, 128, 1], [1, 4, 0, 2, 128, 128, 1],
-                                   [4, 0, 0, 0, 256, 256, 4]]),
-    ("tp4.gate_up", 256, 14336, 8192, [[5, 3, 0, 0, 256, 128, 2], [5, 3, 0, 0, 256, 128, 1], [1, 2, 0, 2, 128, 128, 2],
-                                       [4, 0, 0, 0, 256, 256, 4]]),
+    ("tp8.down", 512, 8192, 3584, [[5, 4, 4, 0, 128, 128, 1], [7, 4, 6, 0, 128, 128, 1]]),
+    ("tp8.qkv", 512, 1280, 8192, [[5, 4, 4, 0, 128, 128, 6], [7, 3, 7, 0, 128, 128, 6]]),
+    ("tp4.gate_up", 256, 14336, 8192, [[5, 4, 3, 0, 256, 128, 2], [7, 3, 4, 0, 256, 128, 2]]),
 ]
 ws = torch.zeros(64 << 20, dtype=torch.float32, device="cuda")
 log = []
