@@ -32,6 +32,13 @@ class ForwardBatch:
     prefix_lens: Optional[list] = None
     prefix_cu: Optional[torch.Tensor] = None
     prefix_tables: Optional[torch.Tensor] = None
+    # when the chunks with a cached prefix are the leading `split_seqs` chunks (split_rows rows)
+    # and the rest are fresh prompts: the fresh ones take the flash kernel (cu_fresh over them)
+    split_seqs: int = 0
+    split_rows: int = 0
+    cu_fresh: Optional[torch.Tensor] = None
+    max_fresh: int = 0
+    max_paged: int = 0
 
     @property
     def num_tokens(self) -> int:
@@ -49,7 +56,8 @@ class ForwardBatch:
                             mv(self.cu_seqlens), self.max_seqlen, mv(self.block_tables),
                             mv(self.ctx_lens), self.max_ctx, mv(self.logits_idx), self.ep_tokens,
                             self.ep_alltoall, self.cp, self.num_decode, self.prefix_lens,
-                            mv(self.prefix_cu), mv(self.prefix_tables))
+                            mv(self.prefix_cu), mv(self.prefix_tables), self.split_seqs, self.split_rows,
+                            mv(self.cu_fresh), self.max_fresh, self.max_paged)
 
 
 def make_prefill_batch(prompts: list[list[int]], slots: list[list[int]], device="cpu",

@@ -192,12 +192,20 @@ class ModelRunner:
                 b = self.kv.manager.block_table(sid)
                 tab[j, : len(b)] = b
             pre_tab = torch.from_numpy(tab).to(dev, non_blocking=True)
+        lens = [cu[i + 1] - cu[i] for i in range(len(cu) - 1)]
         fb = ForwardBatch(input_ids=t32(ids), positions=t32(pos), slots=t32(slots), is_prefill=True,
-                          cu_seqlens=t32(cu), max_seqlen=max((cu[i + 1] - cu[i] for i in range(len(cu) - 1)), default=0),
+                          cu_seqlens=t32(cu), max_seqlen=max(lens, default=0),
                           block_tables=bt, ctx_lens=ctx, max_ctx=self.max_seq_len,
                           logits_idx=torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True),
                           num_decode=nd, prefix_lens=prefix if any(prefix) else None, prefix_cu=pre_cu,
                           prefix_tables=pre_tab)
+        # continuation chunks first, fresh prompts after them (the scheduler's order when it
+        # resumes a partly prefilled prompt): only the continuations need the paged pass
+        s1 = next((j for j, p in enumerate(prefix) if p == 0), len(prefix))
+        if 0 < s1 < len(prefix) and not any(prefix[s1:]):
+            fb.split_seqs, fb.split_rows = s1, cu[s1]
+            fb.cu_fresh = t32([c - cu[s1] for c in cu[s1:]])
+            fb.max_paged, fb.max_fresh = max(lens[:s1]), max(lens[s1:])
         return fb, sample
 
     def decode_inputs(self, plan, last_tokens: list) -> dict:

@@ -465,7 +465,16 @@ class TransformerLM:
             ops.attn_decode(q[:nd], kc, vc, fb.block_tables, fb.ctx_lens, self.scale, fb.max_ctx, out=out[:nd])
         if q.shape[0] > nd:
             qp = q[nd:]
-            if fb.prefix_lens is not None and any(fb.prefix_lens):
+            if fb.split_seqs:
+                # continuation chunks (leading): one paged pass over prefix + chunk; the fresh
+                # prompts after them: flash attention over their own rows (2x the paged
+                # kernel's rate on fresh prompts, profiles/r5_prof/)
+                s1, r1 = fb.split_seqs, fb.split_rows
+                ops.attn_prefill_paged(qp[:r1], kc, vc, fb.prefix_tables[:s1], fb.cu_seqlens[:s1 + 1],
+                                       fb.positions[nd:nd + r1], fb.max_paged, self.scale, out=out[nd:nd + r1])
+                ops.attn_prefill(qp[r1:], k[nd + r1:], v[nd + r1:], fb.cu_fresh, fb.max_fresh, self.scale, True,
+                                 out=out[nd + r1:])
+            elif fb.prefix_lens is not None and any(fb.prefix_lens):
                 ops.attn_prefill_paged(qp, kc, vc, fb.prefix_tables, fb.cu_seqlens, fb.positions[nd:], fb.max_seqlen,
                                        self.scale, out=out[nd:])
             else:

@@ -349,3 +349,31 @@ def test_sequence_parallel_prefill_matches_single(preset, mesh_kw, world):
     for toks, n_rs in outs:
         assert toks == ref
         assert n_rs > 0          # the SP path really ran
+
+
+def test_mixed_step_splits_continuations_from_fresh_prompts(monkeypatch):
+    """A mixed step whose leading chunks continue cached prompts and whose remaining chunks are
+    fresh runs the paged pass on the continuations only and flash attention on the fresh
+    prompts (ForwardBatch.split_seqs); the tokens equal the all-paged path's."""
+    from butterfly_amd.engine.model_runner import ModelRunner
+
+    orig = ModelRunner.mixed_batch
+    seen = []
+
+    def counting(self, plan, tokens_of):
+        fb, sample = orig(self, plan, tokens_of)
+        seen.append(fb.split_seqs)
+        return fb, sample
+
+    monkeypatch.setattr(ModelRunner, "mixed_batch", counting)
+    split, _, _, _ = _chunked_generate(0, 1, "llama-tiny", {}, False)
+    assert any(s > 0 for s in seen), "the workload never mixed a continuation with fresh prompts"
+
+    def unsplit(self, plan, tokens_of):
+        fb, sample = orig(self, plan, tokens_of)
+        fb.split_seqs = 0
+        return fb, sample
+
+    monkeypatch.setattr(ModelRunner, "mixed_batch", unsplit)
+    whole, _, _, _ = _chunked_generate(0, 1, "llama-tiny", {}, False)
+    assert split == whole
