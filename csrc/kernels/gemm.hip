@@ -902,10 +902,17 @@ __device__ __forceinline__ void b4_dma(__amdgpu_buffer_rsrc_t r, char* lds, int 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, voff, soff, 0, 0);
 }
 
+// GROUPED (MoE expert GEMM at prefill scale): as gemm_big8_kernel<true> — M tiles are the
+// entries of the device tile list {expert, first row slot, end slot}, W is offset by the expert,
+// A rows are gathered through grows[slot] by per-lane LDS-DMA offsets from X (rows past the
+// tile's end re-read its last row; their outputs are not stored).
+template <bool GROUPED = false>
 __global__ void __launch_bounds__(kB4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                 bf16* __restrict__ out, long ldo, float* __restrict__ part) {
+                 bf16* __restrict__ out, long ldo, float* __restrict__ part,
+                 const int* __restrict__ grows = nullptr, const int4* __restrict__ gtiles = nullptr,
+                 const int* __restrict__ gcount = nullptr, long w_estride = 0) {
   constexpr int BM = 256, BN = 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // wave index in an SGPR: the DMA's LDS destinations (M0) and the fragment row bases are then
@@ -917,8 +924,16 @@ gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   const int per_group = kBigGroupM * ntiles;
   const int grp = t / per_group, first_m = grp * kBigGroupM;
   const int gsize = min(mtiles - first_m, kBigGroupM);
-  const int m0 = (first_m + (t % per_group) % gsize) * BM;
+  int m0 = (first_m + (t % per_group) % gsize) * BM;
   const int n0 = ((t % per_group) / gsize) * BN;
+  if constexpr (GROUPED) {
+    const int ti = m0 / BM;
+    if (ti >= *gcount) return;
+    const int4 info = gtiles[ti];
+    W += (long)info.x * w_estride;
+    m0 = info.y;
+    M = info.z;                    // rows [m0, M) of the slot space
+  }
   const int ktiles = K / 64;
   const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
   const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
@@ -937,8 +952,21 @@ gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     va[e] = (int)((drow * ldx + ch * 8) * 2);
     vb[e] = (int)((drow * ldw + ch * 8) * 2);
   }
+  int ga[8] = {};   // GROUPED: byte offsets from X of this lane's gathered rows (at its chunk)
+  const auto rsx = b8_rsrc(X, 1L << 30, 1);
+  if constexpr (GROUPED) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int slot = min(m0 + drow + 8 * q, M - 1);
+      const long src = grows != nullptr ? grows[slot] : slot;
+      ga[q] = (int)((src * ldx + (((lane & 7) ^ (((lane >> 4) + 4 * (q & 1)) & 7)) * 8)) * 2);
+    }
+  }
   auto dma_a = [&](int k, int slot, int s) {
-    b4_dma(rsa, smem + slot * kB4Slot + (8 * wid + s) * 1024, va[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldx * 2));
+    if constexpr (GROUPED)
+      b4_dma(rsx, smem + slot * kB4Slot + (8 * wid + s) * 1024, ga[s], (kt0 + k) * 128);
+    else
+      b4_dma(rsa, smem + slot * kB4Slot + (8 * wid + s) * 1024, va[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldx * 2));
   };
   auto dma_b = [&](int k, int slot, int s) {
     b4_dma(rsb, smem + (3 + slot) * kB4Slot + (8 * wid + s) * 1024, vb[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldw * 2));
@@ -1476,13 +1504,13 @@ static void run_big4(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big4_kernel),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big4_kernel<false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kB4LdsBytes);
     attr_set = true;
   }
   dim3 grid(((M + 255) / 256) * (N / 256), sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  gemm_big4_kernel<<<grid, kB4Threads, kB4LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
+  gemm_big4_kernel<false><<<grid, kB4Threads, kB4LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
 template <int BM, int BN, int SA, int SB>
@@ -1822,17 +1850,26 @@ int launch_gemm_grouped(const bf16* X, long ldx, const bf16* W, long ldw, long w
   if (epi != EPI_NONE && epi != EPI_SILU) return -1;
   if (sk < 1 || sk > K / kBK || (sk > 1 && (part == nullptr || epi != EPI_NONE || slots <= 0))) return -2;
   if (bm == 256) {
-    // prefill-scale expert batches: the 8-phase 256x256 tile over the tile list, no split
+    // prefill-scale expert batches: a 256x256 tile over the tile list, no split
     if (N % 256 != 0 || K / 64 < 2 || sk != 1) return -2;
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big8_kernel<true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kB8LdsBytes);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big4_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kB4LdsBytes);
       attr = true;
     }
     dim3 grid(max_tiles * (N / 256), 1);
-    gemm_big8_kernel<true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(
-        X, ldx, W, ldw, max_tiles * 256, N, K, epi, nullptr, out, ldo, nullptr, rows, tiles, count, w_estride);
+    // the SwiGLU gate/up GEMM on big4, the down projection on big8: Mixtral 8x7B at 32k routed
+    // rows, gate/up 6.02-6.04 vs 6.35-6.40 ms, down 3.64-3.66 vs 3.19-3.20 ms
+    // (profiles/r5_gemm_big4/grouped_moe_per_gemm.log)
+    if (epi == EPI_SILU)
+      gemm_big4_kernel<true><<<grid, kB4Threads, kB4LdsBytes, stream>>>(
+          X, ldx, W, ldw, max_tiles * 256, N, K, epi, nullptr, out, ldo, nullptr, rows, tiles, count, w_estride);
+    else
+      gemm_big8_kernel<true><<<grid, kB8Threads, kB8LdsBytes, stream>>>(
+          X, ldx, W, ldw, max_tiles * 256, N, K, epi, nullptr, out, ldo, nullptr, rows, tiles, count, w_estride);
     return 0;
   }
   if (bm == 128)
