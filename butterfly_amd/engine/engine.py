@@ -214,6 +214,8 @@ class LLMEngine:
         if self._native_pp:
             self.runner.set_pipeline_io(recv_fn=None if coord.pp == 0 else self.comm.recv_native,
                                         sends=coord.pp < mesh.pp - 1)
+        if flags.get("BFLY_PROGRAM_CHECK") and mesh.world_size > 1:
+            self.runner.conform = self._program_check()
         if self.runner.use_graphs and not self.comm.graph_safe():
             # a data-path collective on gloo (ranks sharing one GPU) cannot be captured: decode
             # eagerly instead of attempting (and invalidating) a capture
@@ -506,6 +508,27 @@ class LLMEngine:
         dt = time.perf_counter() - t0
         self.metrics.observe_step(kind, len(rids), dt)
         return StepOutput(kind, rids, new, finished, dt)
+
+    def _program_check(self):
+        """rows -> the collectives this rank's decode-step program (schedule.rank_program for
+        one microbatch of `rows` sequences) has the stage's model code issue, in order: what
+        ModelRunner.run enforces through comm.expect under BFLY_PROGRAM_CHECK. Engine-level
+        transfers (boundary send / recv, id broadcast) are program-driven already (_execute);
+        the EP agreement and the sampling all-gather run outside the stage's forward."""
+        from ..partition.schedule import rank_program
+
+        elt = torch.empty((), dtype=self.model.dtype).element_size()
+        checked = ("all_reduce", "all_to_all", "ep_dispatch", "ep_return")
+        cache: dict = {}
+
+        def instrs(rows: int) -> list:
+            v = cache.get(rows)
+            if v is None:
+                prog = rank_program(self.plan, self.rank, rows, 1, dtype_bytes=elt, native_pp=self._native_pp,
+                                    ep_ipc=bool(self.ep_ipc))
+                v = cache[rows] = [i for i in prog.comm() if not i.exec and i.op in checked]
+            return v
+        return instrs
 
     def _ops(self, microbatches: int, native_pp: bool = False) -> list:
         """Engine-level instructions of this rank's step program (schedule.exec_program)."""

@@ -105,6 +105,9 @@ class ModelRunner:
         self.eager_buckets: set = set()
         self.pool = None
         self.post_fn = post_fn
+        # BFLY_PROGRAM_CHECK: rows -> the in-stage collectives of this rank's decode-step
+        # program (engine._program_check); decode forwards run under comm.expect(...)
+        self.conform = None
         # host staging buffers (pinned) for per-step inputs
         hb = max(self.buckets + [max_batch])
         self._tables_host = np.zeros((hb, self.max_blocks), dtype=np.int32)
@@ -226,7 +229,11 @@ class ModelRunner:
 
     # ------------------------------------------------------------------------------------
     def run(self, fb: ForwardBatch, hidden_in=None):
-        out = self.model.forward(fb, self.kv.layers, hidden_in)
+        if self.conform is not None and not fb.is_prefill:
+            with self.model.comm.expect(self.conform(fb.num_tokens)):
+                out = self.model.forward(fb, self.kv.layers, hidden_in)
+        else:
+            out = self.model.forward(fb, self.kv.layers, hidden_in)
         return self.post_fn(out) if (self.post_fn is not None and self.model.last) else out
 
     def run_decode(self, inp: dict, hidden_in=None, ep_tokens: int = 0, graphs_ok: bool = True,

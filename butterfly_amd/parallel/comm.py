@@ -23,6 +23,7 @@ in a hipGraph together with the compute kernels.
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 from dataclasses import dataclass, field
@@ -32,6 +33,10 @@ import torch
 import torch.distributed as dist
 
 from .mesh import Mesh
+
+
+class ProgramMismatch(RuntimeError):
+    """A collective this rank was about to issue is not the next one of its step program."""
 
 
 class NativeWork:
@@ -76,6 +81,7 @@ class Communicator:
         self.pp_native_send = None
         self.pp_native_recv = None
         self._send_stream = None
+        self._expect = None              # [instructions, cursor] while a step program is enforced
 
     # -- construction ---------------------------------------------------------------------
     @classmethod
@@ -146,6 +152,39 @@ class Communicator:
     def rank_in(self, group: str = "tp") -> int:
         return self.groups[group].rank_in_group
 
+    # -- rank-program conformance ----------------------------------------------------------
+    @contextlib.contextmanager
+    def expect(self, instrs):
+        """Enforce a step program on the collectives issued inside the block:
+        every one is checked against the program's next instruction BEFORE it is issued (op,
+        group, payload), so a rank whose model code diverged from the program raises here,
+        naming both, instead of entering a collective its peers never issue (a hang on RCCL).
+        At the end of the block every listed instruction must have been issued."""
+        prev, self._expect = self._expect, [list(instrs), 0]
+        try:
+            yield
+            todo = self._expect[0][self._expect[1]:]
+            if todo:
+                raise ProgramMismatch(f"rank {self.rank}: the step ended with {len(todo)} program instruction(s) "
+                                      f"not issued, the first: {todo[0].op} {todo[0].group} ({todo[0].note})")
+        finally:
+            self._expect = prev
+
+    def _conform(self, op: str, group: str, nbytes: Optional[int] = None) -> None:
+        e = self._expect
+        if e is None:
+            return
+        instrs, i = e
+        ranks = tuple(self.groups[group].ranks)
+        if i >= len(instrs):
+            raise ProgramMismatch(f"rank {self.rank}: {op} on {ranks} ({nbytes} B) issued after the step program's "
+                                  f"last instruction")
+        ins = instrs[i]
+        if ins.op != op or tuple(ins.group) != ranks or (nbytes is not None and ins.nbytes != nbytes):
+            raise ProgramMismatch(f"rank {self.rank}: about to issue {op} on {ranks} ({nbytes} B) where the step "
+                                  f"program's instruction {i} is {ins.op} on {ins.group} ({ins.nbytes} B, {ins.note})")
+        e[1] = i + 1
+
     # -- collectives --------------------------------------------------------------------------
     def all_reduce_(self, t, group: str = "tp") -> torch.Tensor:
         """In-place sum over the group; returns the reduced tensor. `t` may be a deferred
@@ -156,9 +195,10 @@ class Communicator:
         g = self.groups[group]
         if g.size == 1:
             return ops.materialize(t)
+        nb = t.shape[0] * t.shape[1] * 2 if isinstance(t, ops.Partial) else t.numel() * t.element_size()
+        self._conform("all_reduce", group, nb)
         self.stats["calls"] += 1
-        self.stats["all_reduce_bytes"] += t.shape[0] * t.shape[1] * 2 if isinstance(t, ops.Partial) \
-            else t.numel() * t.element_size()
+        self.stats["all_reduce_bytes"] += nb
         if group == "tp" and self.custom_ar is not None and self.custom_ar.should_use(t):
             return self.custom_ar.all_reduce_(t)
         t = ops.materialize(t)
@@ -208,6 +248,7 @@ class Communicator:
         g = self.groups[group]
         car = self.custom_ar
         if g.size > 1 and group == "tp" and car is not None and car.should_use(t):
+            self._conform("all_reduce", group, t.shape[0] * t.shape[1] * 2)
             self.stats["calls"] += 1
             self.stats["all_reduce_bytes"] += t.shape[0] * t.shape[1] * 2
             return car.all_reduce_rms_norm_(t, w, eps, residual)
@@ -292,6 +333,7 @@ class Communicator:
 
         ipc = self.ep_ipc
         if ipc is not None and ipc.fits(x, ids, cap):
+            self._conform("ep_dispatch", "ep")   # routed bytes depend on the routing: op and group only
             return ipc.dispatch(x, ids, w, slots, experts_per_rank, cap)
         k = ids.shape[1]
         send, meta, slot = ops.ep_pack(x, ids, w, slots, experts_per_rank, self.size("ep"), cap)
@@ -306,6 +348,7 @@ class Communicator:
         from .. import ops
 
         if route.path != "a2a":
+            self._conform("ep_return", "ep")
             return self.ep_ipc.combine(y, route)
         return ops.ep_combine(self.all_to_all(y, "ep"), route.slot)
 
@@ -481,6 +524,7 @@ class Communicator:
                 out.copy_(t)
                 return out
             return t
+        self._conform("all_to_all", group, t.numel() * t.element_size())
         if out is None:
             out = torch.empty_like(t)
         self.stats["calls"] += 1

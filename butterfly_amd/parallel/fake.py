@@ -148,6 +148,7 @@ class FakeComm(Communicator):
     def all_reduce_(self, t, group="tp"):
         if self.groups[group].size == 1:
             return t
+        self._conform("all_reduce", group, t.numel() * t.element_size())
         self.stats["calls"] += 1
         self.stats["all_reduce_bytes"] += t.numel() * t.element_size()
         t.copy_(self._coll(group, "all_reduce", t, lambda xs: torch.stack([x.float() for x in xs]).sum(0).to(xs[0].dtype)))
@@ -219,6 +220,7 @@ class FakeComm(Communicator):
                 out.copy_(t)
                 return out
             return t
+        self._conform("all_to_all", group, t.numel() * t.element_size())
         me, n = g.rank_in_group, g.size
         self.stats["calls"] += 1
         allx = self._coll(group, "all_to_all", t.contiguous(), lambda xs: torch.stack(xs))

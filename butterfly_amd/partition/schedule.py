@@ -26,7 +26,11 @@ routed rows) — written down ahead of time so that it can be
   * EXECUTED: the engine-level instructions (`exec`: recv / stage / send / sample / broadcast,
     per microbatch; `exec_program`) are what engine._execute interprets for every pipelined or
     single-stage step — the peers, streams and order of the boundary transfers come from here,
-    not from code in the engine.
+    not from code in the engine;
+  * ENFORCED on the in-stage collectives (BFLY_PROGRAM_CHECK): every all-reduce / all-to-all /
+    EP dispatch / return the model code issues in a decode step is checked against the next
+    instruction of this program before it is issued (parallel/comm.Communicator.expect,
+    engine._program_check), so a divergent rank raises instead of deadlocking its group.
 
 Stream assignment follows the engine: TP all-reduces run on the compute stream (one-shot IPC
 kernel when BFLY_CUSTOM_AR is active, else RCCL, both stream-ordered), PP sends are `isend` on

@@ -218,3 +218,66 @@ def test_engine_executes_rank_program(kw, pp_async, monkeypatch):
                 assert ins.group == (r, mesh.next_stage(r))
             if ins.exec == "recv":
                 assert ins.group == (mesh.prev_stage(r), r)
+
+
+def _generate_checked(rank, comm, preset, mesh, stages):
+    cfg = ModelConfig.from_preset(preset)
+    ecfg = EngineConfig(max_batch=8, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu", stage_layers=stages)
+    assert eng.runner.conform is not None
+    rids = [eng.add_request(p, SamplingParams(max_tokens=3 + 2 * i, ignore_eos=True)) for i, p in enumerate(PROMPTS)]
+    while eng.has_unfinished():
+        eng.step()
+    return [eng.requests[r].output for r in rids]
+
+
+@pytest.mark.parametrize("pp_async", ["1", "0"])
+@pytest.mark.parametrize("preset,kw", [("llama-tiny", dict(tp=2)), ("llama-tiny", dict(tp=2, pp=2)),
+                                       ("mixtral-tiny", dict(dp=2, ep=2)), ("mixtral-tiny", dict(tp=2))])
+def test_program_enforced_on_every_decode_step(preset, kw, pp_async, monkeypatch):
+    """BFLY_PROGRAM_CHECK: every collective the model code issues in a decode step is checked
+    against the rank program's next instruction before it is issued (op, group, payload) and
+    the step must issue all of them. A whole generation passes on every layout, with the tokens
+    of the single-process engine."""
+    monkeypatch.setenv("BFLY_PP_ASYNC", pp_async)
+    monkeypatch.setenv("BFLY_PROGRAM_CHECK", "1")
+    torch.set_num_threads(1)
+    cfg = ModelConfig.from_preset(preset)
+    ecfg = EngineConfig(max_batch=8, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    single = LLMEngine(cfg, Mesh(), ecfg, device="cpu")
+    rids = [single.add_request(p, SamplingParams(max_tokens=3 + 2 * i, ignore_eos=True)) for i, p in enumerate(PROMPTS)]
+    while single.has_unfinished():
+        single.step()
+    want = [single.requests[r].output for r in rids]
+    n = kw.get("dp", 1) * kw.get("tp", 1) * kw.get("pp", 1)
+    plan = partition(cfg, n, kw, batch_per_gpu=4 * n // kw.get("dp", 1))
+    world = FakeWorld(plan.mesh, timeout_s=60)
+    outs = world.run(lambda r, c: _generate_checked(r, c, preset, plan.mesh, plan.stages))
+    assert all(o == want for o in outs)
+
+
+def test_program_check_raises_before_a_divergent_collective():
+    from butterfly_amd.parallel.comm import Communicator, GroupHandle, ProgramMismatch
+
+    g = GroupHandle([0, 1], None, 0)
+    c = Communicator(Mesh(), 0, {"tp": g, "ep": g, "pp": g, "dp": g, "world": g})
+    prog = [Instr("all_reduce", (0, 1), 64, note="layer 0 attention output"),
+            Instr("all_reduce", (0, 1), 64, note="layer 0 FFN output")]
+    with c.expect(prog):
+        c._conform("all_reduce", "tp", 64)
+        c._conform("all_reduce", "tp", 64)
+    with pytest.raises(ProgramMismatch, match="about to issue all_to_all"):
+        with c.expect(prog):
+            c._conform("all_to_all", "tp", 64)
+    with pytest.raises(ProgramMismatch, match="instruction 1 is all_reduce"):
+        with c.expect(prog):
+            c._conform("all_reduce", "tp", 64)
+            c._conform("all_reduce", "tp", 128)      # wrong payload
+    with pytest.raises(ProgramMismatch, match="not issued"):
+        with c.expect(prog):
+            c._conform("all_reduce", "tp", 64)
+    with pytest.raises(ProgramMismatch, match="after the step program's last"):
+        with c.expect(prog[:1]):
+            c._conform("all_reduce", "tp", 64)
+            c._conform("all_reduce", "tp", 64)
+    assert c._expect is None
