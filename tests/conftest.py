@@ -9,6 +9,9 @@ if ROOT not in sys.path:
 # the multi-rank GPU tests run their ranks on ONE device: let the IPC all-reduce / EP exchange
 # run there (production refuses shared-GPU IPC groups: parallel/custom_allreduce.py)
 os.environ.setdefault("BFLY_IPC_SHARED_DEVICE", "1")
+# every multi-rank engine in the suites runs its decode steps with the rank program enforced
+# on the in-stage collectives (comm.Communicator.expect): a divergence fails the test by name
+os.environ.setdefault("BFLY_PROGRAM_CHECK", "1")
 
 
 def pytest_configure(config):
