@@ -281,3 +281,28 @@ def test_program_check_raises_before_a_divergent_collective():
             c._conform("all_reduce", "tp", 64)
             c._conform("all_reduce", "tp", 64)
     assert c._expect is None
+
+
+def _diverging_rank(rank, comm, preset, mesh, stages):
+    """Rank 1's program has an extra EP all-to-all in front of the first all-reduce: its model
+    code no longer matches the program, and the check must stop it before the collective."""
+    cfg = ModelConfig.from_preset(preset)
+    ecfg = EngineConfig(max_batch=8, max_seq_len=128, kv_cache_tokens=2048, use_graphs=False, seed=5)
+    eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu", stage_layers=stages)
+    if rank == 1:
+        real = eng.runner.conform
+        eng.runner.conform = lambda rows: [Instr("all_to_all", (0, 1), 64, note="injected")] + real(rows)
+    for p in PROMPTS:
+        eng.add_request(p, SamplingParams(max_tokens=4, ignore_eos=True))
+    while eng.has_unfinished():
+        eng.step()
+
+
+def test_program_check_stops_a_diverging_rank(monkeypatch):
+    monkeypatch.setenv("BFLY_PROGRAM_CHECK", "1")
+    torch.set_num_threads(1)
+    cfg = ModelConfig.from_preset("llama-tiny")
+    plan = partition(cfg, 2, dict(tp=2), batch_per_gpu=8)
+    world = FakeWorld(plan.mesh, timeout_s=5)
+    with pytest.raises(RuntimeError, match="rank 1 failed: ProgramMismatch.*about to issue all_reduce"):
+        world.run(lambda r, c: _diverging_rank(r, c, "llama-tiny", plan.mesh, plan.stages))
