@@ -230,8 +230,9 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------
     def run(self, fb: ForwardBatch, hidden_in=None):
         if self.conform is not None and not fb.is_prefill and not getattr(fb, "ep_alltoall", False):
-            # (a decode step beside an EP peer's prefill mirrors the prefill exchange instead);
-            # EP ranks pad their exchange to the agreed row count (fb.ep_tokens)
+            # decode programs only: a decode step beside an EP peer's prefill (ep_alltoall) runs
+            # the prefill exchange instead. EP ranks pad their exchange to the agreed row count
+            # (fb.ep_tokens), which is the program's row count
             with self.model.comm.expect(self.conform(max(fb.num_tokens, fb.ep_tokens or 0))):
                 out = self.model.forward(fb, self.kv.layers, hidden_in)
         else:
