@@ -10,6 +10,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 
 import torch
 
@@ -23,10 +24,13 @@ def main():
     ap.add_argument("--tiled", default="6144x4096,4096x4096,4096x14336,10240x8192,8192x8192",
                     help="GEMM-shaped walks over these [N x K] weights ('' = skip)")
     a = ap.parse_args()
+    co = os.path.join(HERE, "probes", "read_floor.hsaco")
+    if not os.path.exists(co):   # git-ignored build product: compile it (gfx950, no GPU needed)
+        subprocess.run(["hipcc", "--genco", "--offload-arch=gfx950", "-O3", co[:-6] + ".hip", "-o", co], check=True)
     torch.cuda.init()
     hip = ctypes.CDLL("libamdhip64.so")
     mod, fns = ctypes.c_void_p(), {}
-    assert hip.hipModuleLoad(ctypes.byref(mod), os.path.join(HERE, "probes", "read_floor.hsaco").encode()) == 0
+    assert hip.hipModuleLoad(ctypes.byref(mod), co.encode()) == 0
     for name in ("read4", "read8", "read16", "tiled128", "tiled64", "tiled32", "frag1", "frag2", "frag4"):
         f = ctypes.c_void_p()
         assert hip.hipModuleGetFunction(ctypes.byref(f), mod, name.encode()) == 0
