@@ -337,7 +337,8 @@ def run(a) -> int:
                    "hipgraph": bool(runner.captured_buckets) and not runner.eager_buckets,
                    "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""),
                    "pp_async_groups": groups if groups > 1 else None,
-                   "async_decode": bool(eng.async_pp and mesh.pp == 1)},
+                   "async_decode": bool(eng.async_pp and mesh.pp == 1),
+                   "mixed": bool(eng.mixed), "prefix_caching": bool(eng.prefix_cache)},
     }
     if rank == 0:
         line = json.dumps(res)

@@ -143,11 +143,15 @@ class LLMEngine:
         # the host's scheduling of step k+1 with the device's step k)
         # (EP layouts, pp == 1, too: the EP ranks agree on padding / step mode over the gloo
         # control plane, which never waits for the device)
+        # (context-parallel prefill over the DP replicas, pp == 1, runs inside the asynchronous
+        # engine too: a tick that runs one is a CP tick, _pp_tick)
         self.async_pp = flags.get("BFLY_PP_ASYNC") and (mesh.ep == 1 or mesh.pp == 1) and (
-            mesh.pp > 1 or (bool(engine_cfg.async_decode) and not (engine_cfg.cp_prefill_min_tokens and mesh.dp > 1)))
-        # mixed steps (chunked prefill riding along decode rows, prefix caching): every
-        # non-EP layout; in the asynchronous pipeline each group's plans are mixed
-        self.mixed = bool(engine_cfg.mixed_prefill) and mesh.ep == 1 and (mesh.pp == 1 or self.async_pp)
+            mesh.pp > 1 or bool(engine_cfg.async_decode))
+        # mixed steps (chunked prefill riding along decode rows, prefix caching): every layout;
+        # in the asynchronous pipeline each group's plans are mixed. Expert-parallel replicas
+        # agree per step on the padded row count and on whether any of them runs prompt rows
+        # (which switches every peer's MoE layer to the variable exchange): _ep_agree
+        self.mixed = bool(engine_cfg.mixed_prefill) and (mesh.pp == 1 or self.async_pp)
         self.prefix_cache = self.mixed and bool(engine_cfg.prefix_caching)
         if self.async_pp:
             self.scheduler = GroupedScheduler(native, self.kv.manager, mesh.pp, engine_cfg.max_batch,
@@ -193,10 +197,13 @@ class LLMEngine:
             buckets.append(self.scheduler.group_batch)    # a full group replays one graph
         self.runner = ModelRunner(self.model, self.kv, engine_cfg.max_seq_len, engine_cfg.use_graphs,
                                   buckets, max_batch=engine_cfg.max_batch)
-        if flags.get("BFLY_GRAPH_SAMPLING") and self.comm.capturable("tp"):   # (TP merge: an all-gather)
+        if self.async_pp and flags.get("BFLY_GRAPH_SAMPLING") and self.comm.capturable("tp"):
             # the last stage's decode graphs end with the sampler on per-request temperatures /
             # seeds staged with the other inputs: one replay per step yields the tokens
-            # (top-k / top-p rows and poisoned steps sample eagerly from the graph's logits)
+            # (top-k / top-p rows and poisoned steps sample eagerly from the graph's logits).
+            # Only the asynchronous engine reads the graph's ids (_pp_stage_work); the
+            # synchronous paths sample eagerly, so their graphs carry no sampler (TP merge:
+            # an all-gather, capturable only on a capturable TP group)
             check = bool(flags.get("BFLY_NAN_CHECK"))
             self.runner.sample_fn = lambda lg, t, sd: self.sampler.sample(lg, t, sd, None, check_finite=check)
         # byte-minimal EP dispatch for the decode MoE layer (collective over the EP group, so
@@ -235,7 +242,7 @@ class LLMEngine:
         self.steps_done = 0
         # context-parallel prefill of long prompts over the DP replicas (parallel/context_parallel.py)
         self.cp_min = engine_cfg.cp_prefill_min_tokens if (
-            mesh.dp > 1 and mesh.pp == 1 and mesh.ep == 1 and not self.async_pp) else 0
+            mesh.dp > 1 and mesh.pp == 1 and mesh.ep == 1) else 0
         self._cp_queue: deque = deque()
 
     @property
@@ -380,13 +387,11 @@ class LLMEngine:
             if out is not None:
                 return out
         plan = self.scheduler.schedule()
-        ep_pad, any_prefill = 0, plan.kind == 1
+        ep_pad, any_prefill = 0, plan.kind in (1, 3)
         if self.mesh.ep > 1:
             # expert-parallel ranks must run the same number of MoE collectives with the same
             # row count: agree on the padded token count; idle ranks run an empty step.
-            t_local = 0 if plan.kind == 0 else (sum(plan.prefill_lens) if plan.kind == 1 else len(plan.seq_ids))
-            ep_pad, anyp, anyw = self.comm.all_reduce_max_int([t_local, int(plan.kind == 1), int(plan.kind != 0)], "ep")
-            any_prefill = bool(anyp)
+            ep_pad, any_prefill, anyw = self._ep_agree(plan)
             if not anyw:
                 return StepOutput("idle", [], [], [], 0.0)
             if plan.kind == 0:
@@ -410,6 +415,8 @@ class LLMEngine:
         if self.mixed and plan.kind in (1, 3):
             # chunked prefill (+ decode rows): sample the decode rows and completed prompts
             fb, sample = self.runner.mixed_batch(plan, lambda r: self.requests[r].tokens)
+            fb.ep_tokens = ep_pad
+            fb.ep_alltoall = self.mesh.ep > 1
             logits = self.runner.run(fb)
             new = []
             if sample:
@@ -508,6 +515,21 @@ class LLMEngine:
         dt = time.perf_counter() - t0
         self.metrics.observe_step(kind, len(rids), dt)
         return StepOutput(kind, rids, new, finished, dt)
+
+    def _ep_agree(self, plan) -> tuple:
+        """Expert-parallel step agreement (host integers over the control plane, no device
+        sync): (padded rows every EP rank runs, whether any rank's plan has prompt rows —
+        then every peer's MoE layer takes the variable exchange —, whether any rank has work).
+        A plan's rows: its decode rows plus its prompt chunks (mixed plans hold both)."""
+        k = plan.kind
+        if k == 0:
+            rows = 0
+        elif k == 2:
+            rows = len(plan.seq_ids)
+        else:
+            rows = int(sum(plan.prefill_lens)) + (plan.num_decode if k == 3 else 0)
+        pad, anyp, anyw = self.comm.all_reduce_max_int([rows, int(k in (1, 3)), int(k != 0)], "ep")
+        return pad, bool(anyp), bool(anyw)
 
     def _program_check(self):
         """rows -> the collectives this rank's decode-step program (schedule.rank_program for
@@ -646,6 +668,15 @@ class LLMEngine:
         for w in self._sends:
             w.wait()
         self._sends = []
+        if self.cp_min:
+            # context-parallel prefill of a long prompt over the DP replicas (pp == 1): when one
+            # is due it is this tick's work on every replica (the agreement is collective, so
+            # all replicas take the same branch); the group in flight is advanced next tick.
+            # Its first token is sampled and applied synchronously: the sequence is new, in no
+            # plan in flight, and joins the least-loaded group as a running sequence
+            out = self._cp_step(t0)
+            if out is not None:
+                return out
         # this rank's stage works on the plan that entered s ticks ago; stages >= 1 enqueue
         # their device work before blocking on the previous tick's ids (keeps the GPU fed)
         mine = next((p for p in self._inflight if p.tick == k - s), None)
@@ -670,9 +701,7 @@ class LLMEngine:
             # every EP rank runs a step whenever one of them has work (the MoE exchange meets
             # every peer), padded to the same rows; a prefill anywhere switches the step to the
             # variable exchange. Host integers over the gloo control plane: no device sync.
-            t_local = 0 if plan.kind == 0 else (sum(plan.prefill_lens) if plan.kind == 1 else len(plan.seq_ids))
-            ep_pad, any_prefill, anyw = self.comm.all_reduce_max_int(
-                [t_local, int(plan.kind == 1), int(plan.kind != 0)], "ep")
+            ep_pad, any_prefill, anyw = self._ep_agree(plan)
             if plan.kind == 0 and anyw:
                 eb = empty_batch(self.device, ep_pad)
                 eb.ep_alltoall = bool(any_prefill)
@@ -867,6 +896,8 @@ class LLMEngine:
                 self.kv.copy_blocks(p.cow)
             if self.mixed and p.plan.kind in (1, 3):
                 fb, _ = self.runner.mixed_batch(p.plan, self._chunk_tokens(p))
+                fb.ep_tokens = p.ep_pad
+                fb.ep_alltoall = self.mesh.ep > 1
                 nd = p.plan.num_decode
                 if self.pp_first and nd:
                     ids = self._first_stage_ids(p, list(p.plan.seq_ids)[:nd])

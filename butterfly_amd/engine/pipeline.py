@@ -43,13 +43,30 @@ class GroupedScheduler:
         self.owner: dict[int, int] = {}
 
     def add(self, rid: int, prompt_len: int, max_new: int, tokens: Optional[list] = None) -> None:
-        g = min(range(len(self.groups)),
-                key=lambda i: (self.groups[i].num_running + self.groups[i].num_waiting, i))
+        g = self._least_loaded()
         if self.prefix_cache and tokens is not None:
             self.groups[g].add(rid, prompt_len, max_new, tokens)
         else:
             self.groups[g].add(rid, prompt_len, max_new)
         self.owner[rid] = g
+
+    def _least_loaded(self) -> int:
+        return min(range(len(self.groups)),
+                   key=lambda i: (self.groups[i].num_running + self.groups[i].num_waiting, i))
+
+    def can_admit_prefilled(self, prompt_len: int) -> bool:
+        """A context-parallel prefill (engine._cp_step) can hand its sequence to the group that
+        would take it now (the least-loaded one)."""
+        return bool(self.groups[self._least_loaded()].can_admit_prefilled(prompt_len))
+
+    def admit_prefilled(self, rid: int, prompt_len: int, max_new: int) -> list:
+        """Admit a sequence whose prompt K/V is already cached (context-parallel prefill):
+        it joins the least-loaded group as a running sequence; returns its cache slots."""
+        g = self._least_loaded()
+        slots = self.groups[g].admit_prefilled(rid, prompt_len, max_new)
+        if slots:
+            self.owner[rid] = g
+        return slots
 
     @property
     def prefix_hit_tokens(self) -> int:

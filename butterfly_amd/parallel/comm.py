@@ -170,6 +170,16 @@ class Communicator:
         finally:
             self._expect = prev
 
+    @contextlib.contextmanager
+    def _unchecked(self):
+        """Collectives issued inside are one program instruction already conformed by the
+        caller (e.g. the all-to-all pair standing in for an IPC EP dispatch)."""
+        prev, self._expect = self._expect, None
+        try:
+            yield
+        finally:
+            self._expect = prev
+
     def _conform(self, op: str, group: str, nbytes: Optional[int] = None) -> None:
         e = self._expect
         if e is None:
@@ -337,8 +347,17 @@ class Communicator:
             return ipc.dispatch(x, ids, w, slots, experts_per_rank, cap)
         k = ids.shape[1]
         send, meta, slot = ops.ep_pack(x, ids, w, slots, experts_per_rank, self.size("ep"), cap)
-        xr = self.all_to_all(send, "ep")
-        mr = self.all_to_all(meta, "ep")
+        if ipc is not None:
+            # the IPC path is set up (the program lists ep_dispatch) but this call does not fit
+            # it (rows beyond its capacity): every EP rank takes this fallback together, and the
+            # all-to-all pair IS the program's dispatch step
+            self._conform("ep_dispatch", "ep")
+            with self._unchecked():
+                xr = self.all_to_all(send, "ep")
+                mr = self.all_to_all(meta, "ep")
+        else:
+            xr = self.all_to_all(send, "ep")
+            mr = self.all_to_all(meta, "ep")
         return EpRoute(xr, mr[:, :k].contiguous().view(torch.int32), mr[:, k:].contiguous(), slot,
                        x.shape[0], "a2a")
 
@@ -350,6 +369,11 @@ class Communicator:
         if route.path != "a2a":
             self._conform("ep_return", "ep")
             return self.ep_ipc.combine(y, route)
+        if self.ep_ipc is not None:             # the fallback of a listed ep_dispatch (above)
+            self._conform("ep_return", "ep")
+            with self._unchecked():
+                back = self.all_to_all(y, "ep")
+            return ops.ep_combine(back, route.slot)
         return ops.ep_combine(self.all_to_all(y, "ep"), route.slot)
 
     def enable_native_rccl(self) -> dict:

@@ -141,7 +141,7 @@ class CustomAllReduce:
         if self._vote(local_ok, pg):
             from .rccl import health_arm, health_quiet
 
-            with health_quiet() as q:       # a timeout here is a fallback vote, not a failure
+            with health_quiet(word="car") as q:   # a timeout here is a fallback vote, not a failure
                 self.ok = self._self_test(pg)
                 q.failed(not self.ok)
             if self.ok:
@@ -194,7 +194,7 @@ class CustomAllReduce:
         (`choose_routing`). Collective: every rank of the group calls it, in the same order."""
         from .rccl import health_quiet
 
-        with health_quiet() as q:
+        with health_quiet(word="car") as q:
             tuning = self._autotune(pg, rccl_all_reduce, sizes, iters)
             q.failed(self.route_bytes == 0)
         return tuning

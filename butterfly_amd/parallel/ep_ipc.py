@@ -114,7 +114,7 @@ class EpIpc:
             self.countsv = L.ep_ipc_view(self._ptr, L.ep_ipc_counts_offset(), 1, self.ep, 1, dev).view(self.ep)
             from .rccl import health_arm, health_quiet
 
-            with health_quiet() as q:       # a timeout here is a fallback vote, not a failure
+            with health_quiet(word="ep") as q:   # a timeout here is a fallback vote, not a failure
                 self.ok = self._self_test(pg)
                 q.failed(not self.ok)
             if self.ok:

@@ -185,41 +185,55 @@ HEALTHY_STATES = (NCCL_SUCCESS, NCCL_IN_PROGRESS)
 # Host-mapped IPC health words (custom all-reduce, EP IPC) are acted on only for IPC paths
 # that went LIVE (passed their self-test and route traffic): a flag-wait timeout inside a
 # self-test, autotune or preflight check is a vote to fall back, not a failure of the job.
+# Quiet and clear are scoped to the word under test ("car" or "ep"), so an EP self-test never
+# hides or wipes a custom all-reduce timeout and vice versa; a word that was already set for a
+# live path when a test on it began is kept (sticky) and still reported.
 _health_lock = threading.Lock()
 _health_live = {"car": 0, "ep": 0}     # live IPC objects per word
-_health_quiet = 0                      # self-tests / autotunes in progress: words not read
+_health_quiet = {"car": 0, "ep": 0}    # self-tests / autotunes in progress, per word
+_health_sticky = {"car": False, "ep": False}   # live timeouts seen at a test's start
+_WORD_INDEX = {"car": 0, "ep": 1}      # bfly::kHealthCar / kHealthEp
 
 
 def health_arm(word: str, on: bool = True) -> None:
     """An IPC object of `word` ("car" / "ep") went live (on) or was closed (off)."""
     with _health_lock:
         _health_live[word] = max(0, _health_live[word] + (1 if on else -1))
+        if _health_live[word] == 0:
+            _health_sticky[word] = False
 
 
 class health_quiet:
-    """Context of a collective self-test / autotune: the poller ignores the health words while
-    it runs, and a test that ends in a fallback (`failed(True)` or an exception) clears them."""
+    """Context of a collective self-test / autotune of the `word` IPC path ("car" or "ep"):
+    the poller ignores that word while it runs, and a test that ends in a fallback
+    (`failed(True)` or an exception) clears that word only."""
 
-    def __init__(self, lib=None):
-        self.lib, self.fallback = lib, False
+    def __init__(self, lib=None, word: str = "car"):
+        if word not in _WORD_INDEX:
+            raise ValueError(f"unknown health word {word!r}")
+        self.lib, self.word, self.fallback = lib, word, False
 
     def failed(self, fallback: bool = True) -> None:
         self.fallback = fallback
 
     def __enter__(self):
-        global _health_quiet
+        lib = self.lib or _lib()
+        w = self.word
         with _health_lock:
-            _health_quiet += 1
+            # a timeout of a live path of this word that happened before the test began is a
+            # real failure: keep it reportable whatever the test does with the word
+            if _health_live[w] and int(lib.health_words()[_WORD_INDEX[w]]):
+                _health_sticky[w] = True
+            _health_quiet[w] += 1
         return self
 
     def __exit__(self, et, ev, tb):
-        global _health_quiet
         try:
             if self.fallback or et is not None:
-                (self.lib or _lib()).health_clear()
+                (self.lib or _lib()).health_clear(_WORD_INDEX[self.word])
         finally:
             with _health_lock:
-                _health_quiet -= 1
+                _health_quiet[self.word] -= 1
         return False
 
 
@@ -230,14 +244,15 @@ def async_errors(lib=None) -> Optional[str]:
     `lib`: the op namespace to query (tests pass a stub)."""
     lib = _lib() if lib is None else lib
     with _health_lock:
-        watch = _health_quiet == 0
+        quiet = dict(_health_quiet)
         live = dict(_health_live)
-    if watch:
-        car, ep = (int(v) for v in lib.health_words())
-        if car and live["car"]:
-            return "custom all-reduce peer wait timed out (health word)"
-        if ep and live["ep"]:
-            return "EP IPC dispatch peer wait timed out (health word)"
+        sticky = dict(_health_sticky)
+    words = dict(zip(("car", "ep"), (int(v) for v in lib.health_words())))
+    what = {"car": "custom all-reduce peer wait timed out (health word)",
+            "ep": "EP IPC dispatch peer wait timed out (health word)"}
+    for w in ("car", "ep"):
+        if live[w] and (sticky[w] or (words[w] and quiet[w] == 0)):
+            return what[w]
     for h in lib.rccl_live():
         try:
             err = int(lib.rccl_async_error(h))

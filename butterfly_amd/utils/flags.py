@@ -72,9 +72,11 @@ define("BFLY_NORM_ROWSCALE", True, _bool, "decode add+RMSNorm split over (row, 1
        "and partial sums of squares; the consuming QKV / gate-up GEMM applies the 1/rms row scale in its epilogue "
        "(tp == 1, batches <= BFLY_NORM_ROWSCALE_MAX_ROWS; 0: one-workgroup-per-row add+RMSNorm)")
 define("BFLY_NORM_ROWSCALE_MAX_ROWS", 256, int, "largest batch that takes the row-split add+RMSNorm")
-define("BFLY_PROGRAM_CHECK", False, _bool, "enforce the rank's step program on every decode step: each "
-       "collective the model issues is checked against the program's next instruction before it is issued "
-       "(comm.Communicator.expect); a divergence raises ProgramMismatch instead of hanging the group")
+define("BFLY_PROGRAM_CHECK", True, _bool, "enforce the rank's step program on every decode step of a multi-rank "
+       "engine (world_size > 1): each collective the model issues is checked against the program's next "
+       "instruction before it is issued (comm.Communicator.expect); a divergence raises ProgramMismatch instead "
+       "of hanging the group. Host-side only, on eager steps and graph warm-up / capture passes: a graph "
+       "replay issues nothing from the host, so replayed steps cost nothing")
 define("BFLY_PP_PREPOST", True, _bool, "asynchronous pipeline on RCCL: post each stage's boundary receive one tick "
        "early on a dedicated comm stream into one of two persistent buffers (event-guarded reuse)")
 define("BFLY_NATIVE_RCCL", True, _bool, "data-path collectives (all-reduce / all-gather / reduce-scatter / "

@@ -948,7 +948,7 @@ std::vector<int64_t> health_words() {
   return {(int64_t)bfly::health_word(bfly::kHealthCar), (int64_t)bfly::health_word(bfly::kHealthEp)};
 }
 
-void health_clear() { bfly::health_clear(); }
+void health_clear(int64_t word) { bfly::health_clear((int)word); }
 
 std::vector<int64_t> ep_ipc_layout(int64_t ep, int64_t capmax, int64_t H, int64_t K) {
   const bfly::EpLayout L = bfly::ep_ipc_layout((int)ep, (int)capmax, (int)H, (int)K);
@@ -1123,7 +1123,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("health_init() -> bool", &health_init);
   m.def("hip_clear_error() -> int", &hip_clear_error);
   m.def("health_words() -> int[]", &health_words);
-  m.def("health_clear() -> ()", &health_clear);
+  m.def("health_clear(int word=-1) -> ()", &health_clear);
   m.def("ep_ipc_combine(Tensor slot, int k, int capmax, int[] bases, int rank, Tensor(a!) out) -> ()");
   m.def("ep_ipc_stats(int ptr) -> int[]", &ep_ipc_stats);
   m.def("ep_ipc_error(int ptr) -> int", [](int64_t p) -> int64_t { return bfly::ep_ipc_error(reinterpret_cast<const void*>(p)); });

@@ -146,7 +146,7 @@ struct ArPeers { char* base[kArMaxWorld]; uint32_t* herr; };
 constexpr int kHealthCar = 0, kHealthEp = 1, kHealthWords = 16;
 uint32_t* health_words_device();        // lazily allocated pinned, mapped, coherent host memory
 uint32_t health_word(int i);            // host read (no HIP call once allocated)
-void health_clear();
+void health_clear(int word = -1);   // one word (kHealthCar / kHealthEp) or, -1, all of them
 // flags/counters, two input buffers and two reduced-chunk buffers (two-shot), all double-buffered
 inline long car_buffer_bytes(long cap) { return kArDataOff + 4 * cap; }
 // `slabs` (optional): the input is split-K partials [sk][rows][dim] f32, reduced in the publish.

@@ -446,10 +446,11 @@ uint32_t health_word(int i) {
   return reinterpret_cast<volatile uint32_t*>(g_health_host)[i];
 }
 
-void health_clear() {
+void health_clear(int word) {
   std::lock_guard<std::mutex> lk(g_health_mu);
-  if (g_health_host != nullptr)
-    for (int i = 0; i < kHealthWords; ++i) reinterpret_cast<volatile uint32_t*>(g_health_host)[i] = 0;
+  if (g_health_host == nullptr) return;
+  for (int i = 0; i < kHealthWords; ++i)
+    if (word < 0 || i == word) reinterpret_cast<volatile uint32_t*>(g_health_host)[i] = 0;
 }
 
 int car_error(const void* base) {

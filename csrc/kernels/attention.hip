@@ -238,35 +238,63 @@ attn_decode_kernel(const bf16* __restrict__ q, long q_stride, const CT* __restri
 }
 
 // One workgroup per (query row, kv head, sequence); thread = head dim element. The split
-// maxima are reduced once per workgroup through LDS, then every thread streams its column.
+// (max, sum) pairs are loaded by all threads at once into LDS and reduced by one wave; every
+// thread then streams its column of the split outputs with 4 loads in flight. (The first
+// version reduced the pairs in thread 0 with dependent global loads: 2 x nsplit load latencies,
+// 4.8 us for 5 splits at B = 1 — profiles/r6_latency.md.)
 template <int D>
 __global__ void __launch_bounds__(D)
 attn_decode_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
                            int nsplit, int Hq, int Hkv, bf16* __restrict__ out) {
-  __shared__ float s_w[256];
+  static_assert(D >= 64, "one full wave reduces the split pairs");
+  __shared__ float s_m[256], s_l[256], s_w[256];
   __shared__ float s_inv;
   const int qr = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int G = Hq / Hkv;
   const long base = (long)(b * Hkv + h) * nsplit;
   const int d = threadIdx.x;
-  if (threadIdx.x == 0) {
-    float M = kNegInf;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[((base + s) * 16 + qr) * 2]);
-    const float Mb = M == kNegInf ? 0.f : M;
-    float L = 0.f;
-    for (int s = 0; s < nsplit && s < 256; ++s) {
-      const float ms = part_ml[((base + s) * 16 + qr) * 2];
-      const float w = ms == kNegInf ? 0.f : exp2f(ms - Mb);
-      s_w[s] = w;
-      L += w * part_ml[((base + s) * 16 + qr) * 2 + 1];
-    }
-    s_inv = L > 0.f ? 1.f / L : 0.f;
+  const int ns = nsplit < 256 ? nsplit : 256;
+  for (int s = d; s < ns; s += D) {
+    const float2 ml = *reinterpret_cast<const float2*>(part_ml + ((base + s) * 16 + qr) * 2);
+    s_m[s] = ml.x;
+    s_l[s] = ml.y;
   }
   __syncthreads();
+  if (d < 64) {
+    float M = kNegInf;
+    for (int s = d; s < ns; s += 64) M = fmaxf(M, s_m[s]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    const float Mb = M == kNegInf ? 0.f : M;
+    float L = 0.f;
+    for (int s = d; s < ns; s += 64) {
+      const float ms = s_m[s];
+      const float w = ms == kNegInf ? 0.f : exp2f(ms - Mb);
+      s_w[s] = w;
+      L += w * s_l[s];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) L += __shfl_xor(L, o, 64);
+    if (d == 0) s_inv = L > 0.f ? 1.f / L : 0.f;
+  }
+  __syncthreads();
+  const float* po = part_o + (base * 16 + qr) * D + d;
+  const long sstride = 16L * D;
   float O = 0.f;
-  for (int s = 0; s < nsplit && s < 256; ++s) {
+  int s = 0;
+  for (; s + 4 <= ns; s += 4) {
+    float x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = po[(s + j) * sstride];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float w = s_w[s + j];
+      O += w != 0.f ? w * x[j] : 0.f;   // empty splits wrote no output (it may be poison)
+    }
+  }
+  for (; s < ns; ++s) {
     const float w = s_w[s];
-    if (w != 0.f) O += w * part_o[((base + s) * 16 + qr) * D + d];
+    if (w != 0.f) O += w * po[s * sstride];
   }
   out[((long)b * Hq + h * G + qr) * D + d] = f2bf(O * s_inv);
 }

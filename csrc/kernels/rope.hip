@@ -27,9 +27,23 @@ __device__ __forceinline__ bf16x8 rope_load(const bf16* __restrict__ row, const 
                                             int sk, long slab, int col) {
   if (!prow) return *reinterpret_cast<const bf16x8*>(row + col);
   f32x4 lo = *reinterpret_cast<const f32x4*>(prow + col), hi = *reinterpret_cast<const f32x4*>(prow + col + 4);
-  for (int k = 1; k < sk; ++k) {
-    lo += *reinterpret_cast<const f32x4*>(prow + k * slab + col);
-    hi += *reinterpret_cast<const f32x4*>(prow + k * slab + col + 4);
+  // slabs in batches of 4 with all 8 loads issued before the adds: one dependent add chain
+  // over 16 slabs (the tp8 B = 1 QKV plan) waited ~0.8 us per slab, 14 us per launch
+  // (profiles/r6_latency.md); the adds keep the slab order, i.e. the reduce kernel's sum
+  for (int k0 = 1; k0 < sk; k0 += 4) {
+    f32x4 l[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + j < sk ? k0 + j : k0;
+      l[j] = *reinterpret_cast<const f32x4*>(prow + k * slab + col);
+      h[j] = *reinterpret_cast<const f32x4*>(prow + k * slab + col + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k0 + j < sk) {
+        lo += l[j];
+        hi += h[j];
+      }
   }
   bf16x8 a;
 #pragma unroll

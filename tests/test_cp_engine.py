@@ -21,9 +21,10 @@ SHORT = [[3, 14, 15, 92, 65], [35, 89, 79, 32, 38, 46, 26], [43]]
 PER_DP = [[LONG_A, SHORT[0]], [SHORT[1], LONG_B, LONG_C, SHORT[2]]]
 
 
-def _ecfg(cp_min=0, attn="ring", mixed=True):
+def _ecfg(cp_min=0, attn="ring", mixed=True, async_decode=True):
     return EngineConfig(max_batch=8, max_seq_len=160, kv_cache_tokens=2048, use_graphs=False, seed=5,
-                        cp_prefill_min_tokens=cp_min, cp_attention=attn, mixed_prefill=mixed)
+                        cp_prefill_min_tokens=cp_min, cp_attention=attn, mixed_prefill=mixed,
+                        async_decode=async_decode)
 
 
 def _single(prompts, max_tokens, mixed=True):
@@ -32,27 +33,31 @@ def _single(prompts, max_tokens, mixed=True):
     return eng.generate(prompts, SamplingParams(max_tokens=max_tokens, ignore_eos=True))
 
 
-def _cp_generate(rank, world, mesh_kw, attn, max_tokens, mixed):
+def _cp_generate(rank, world, mesh_kw, attn, max_tokens, mixed, async_decode=True):
     from butterfly_amd.parallel.comm import Communicator
 
     mesh = Mesh(**mesh_kw)
     comm = Communicator.from_mesh(mesh)
     cfg = ModelConfig.from_preset("llama-tiny")
-    eng = LLMEngine(cfg, mesh, _ecfg(cp_min=20, attn=attn, mixed=mixed), comm=comm, device="cpu")
+    eng = LLMEngine(cfg, mesh, _ecfg(cp_min=20, attn=attn, mixed=mixed, async_decode=async_decode), comm=comm,
+                    device="cpu")
+    # CP prefill no longer switches the serving engine to the synchronous one
+    assert eng.cp_min == 20 and eng.async_pp == async_decode
     outs = eng.generate(PER_DP[mesh.coord(rank).dp], SamplingParams(max_tokens=max_tokens, ignore_eos=True))
     m = eng.kv.manager
     return outs, eng.metrics.counters.get("cp_prefill_tokens", 0), m.num_free == m.num_blocks
 
 
-@pytest.mark.parametrize("mesh_kw,world,attn,mixed", [
-    (dict(dp=2), 2, "ring", True),
-    (dict(dp=2), 2, "ulysses", False),
-    (dict(dp=2, tp=2), 4, "ring", True),
+@pytest.mark.parametrize("mesh_kw,world,attn,mixed,async_decode", [
+    (dict(dp=2), 2, "ring", True, True),
+    (dict(dp=2), 2, "ring", True, False),
+    (dict(dp=2), 2, "ulysses", False, True),
+    (dict(dp=2, tp=2), 4, "ring", True, True),
 ])
-def test_cp_prefill_engine_matches_single(mesh_kw, world, attn, mixed):
+def test_cp_prefill_engine_matches_single(mesh_kw, world, attn, mixed, async_decode):
     n = 5
     want = [_single(p, n, mixed) for p in PER_DP]
-    outs = run_world(_cp_generate, world, mesh_kw, attn, n, mixed)
+    outs = run_world(_cp_generate, world, mesh_kw, attn, n, mixed, async_decode)
     mesh = Mesh(**mesh_kw)
     long_tokens = len(LONG_A) + len(LONG_B) + len(LONG_C)
     for rank, (got, cp_tokens, all_free) in enumerate(outs):

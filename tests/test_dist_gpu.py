@@ -52,3 +52,19 @@ def test_context_parallel_prefill_on_one_gpu(n, attn, mode):
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert r.stdout.count("PASS") == n, r.stdout[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4])
+def test_tp_production_dims_on_one_gpu(n):
+    """the real TP decode path at production dimensions (Llama-3-70B layers at
+    full width, 64 sequences per GPU: 128 / 256 rows, the mid-M shard plans, split-K slabs
+    deferred into the IPC all-reduce with fused add + RMSNorm), ranks sharing cuda:0: logits
+    against an fp32 reference model, graph replay bitwise against eager
+    (tools/gpu_tp_fullsize.py)."""
+    r = subprocess.run([sys.executable, "-m", "butterfly_amd", "launch", "-n", str(n), "--",
+                        sys.executable, os.path.join(ROOT, "tools", "gpu_tp_fullsize.py")],
+                       cwd=ROOT, env=dict(os.environ, BFLY_IPC_SHARED_DEVICE="1"), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
+    assert r.stdout.count("PASS") == n, r.stdout[-4000:]

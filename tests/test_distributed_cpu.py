@@ -251,6 +251,66 @@ def test_expert_parallel_async_matches_sync(mesh_kw, world):
     assert got == ref
 
 
+def _ep_mixed_generate(rank, world, mesh_kw, async_pp, shared_prefix, long_len=0):
+    """Expert-parallel replicas on the mixed scheduler: long prompts prefilled in chunks
+    beside decode rows (token budget 24), uneven loads per replica (one replica gets the long
+    prompt, the other only short ones), prefix caching; `mesh_kw` {} = the single-process
+    reference serving replica `rank`'s requests."""
+    import os
+
+    from butterfly_amd.parallel.comm import Communicator
+
+    saved = os.environ.get("BFLY_PP_ASYNC")
+    os.environ["BFLY_PP_ASYNC"] = "1" if async_pp else "0"
+    mesh = Mesh(**mesh_kw)
+    comm = Communicator.from_mesh(mesh) if mesh.world_size > 1 else None
+    cfg = ModelConfig.from_preset("mixtral-tiny")
+    ecfg = EngineConfig(max_batch=4, max_seq_len=max(160, long_len + 96), kv_cache_tokens=4096,
+                        max_prefill_tokens=24, use_graphs=False, seed=5, async_decode=async_pp,
+                        mixed_prefill=True, prefix_caching=True)
+    try:
+        eng = LLMEngine(cfg, mesh, ecfg, comm=comm, device="cpu")
+        assert eng.mixed and eng.async_pp == async_pp
+    finally:
+        if saved is None:
+            os.environ.pop("BFLY_PP_ASYNC", None)
+        else:
+            os.environ["BFLY_PP_ASYNC"] = saved
+    dp = rank if mesh.world_size == 1 else mesh.coord(rank).dp
+    head = [(11 * i) % 83 + 2 for i in range(64)] if shared_prefix else []
+    longp = [[(13 * i + 5) % 91 + 1 for i in range(long_len)]] if long_len else []
+    mine = (longp + LONG) if dp == 0 else PROMPTS[: 1 + dp]
+    rids = [eng.add_request(head + p, SamplingParams(max_tokens=3 + i, ignore_eos=True)) for i, p in enumerate(mine)]
+    kinds = set()
+    for _ in range(3):
+        kinds.add(eng.step().kind)
+    if dp == 0:
+        rids.append(eng.add_request(head + LONG[1][:20], SamplingParams(max_tokens=4, ignore_eos=True)))
+    step = eng.has_unfinished_global if mesh.world_size > 1 else eng.has_unfinished
+    while step():
+        kinds.add(eng.step().kind)
+    return [eng.requests[r].output for r in rids], sorted(kinds), eng.scheduler.prefix_hit_tokens
+
+
+@pytest.mark.parametrize("mesh_kw,world", [(dict(dp=2, ep=2), 2), (dict(dp=4, ep=4), 4)])
+@pytest.mark.parametrize("async_pp", [True, False])
+@pytest.mark.parametrize("shared_prefix", [False, True])
+def test_expert_parallel_mixed_chunked_prefill(mesh_kw, world, async_pp, shared_prefix):
+    """expert-parallel layouts run mixed plans (prompt chunks beside decode
+    rows, prefix caching) on the asynchronous and the synchronous engine; every replica's
+    tokens equal the single-process engine's for the same requests."""
+    long_len = 300 if world == 2 else 0
+    got = run_world(_ep_mixed_generate, world, mesh_kw, async_pp, shared_prefix, long_len)
+    for r in range(world):
+        want, want_kinds, _ = _ep_mixed_generate(r, 1, {}, False, shared_prefix, long_len)
+        out, kinds, hits = got[r]
+        assert out == want, r
+        if r == 0:
+            assert "mixed" in want_kinds and "mixed" in kinds
+            if shared_prefix:
+                assert hits > 0
+
+
 def _probe_worker(rank, world):
     import torch
 

@@ -103,3 +103,29 @@ def test_prefill_ipc_moe_equals_all_to_all(ep):
         return torch.equal(a, b) and a.shape == (T, cfg.hidden_size)
 
     assert all(world.run(run))
+
+
+def test_ipc_fallback_conforms_to_the_program():
+    """with the IPC exchange set up, the step program lists ep_dispatch /
+    ep_return; a call beyond the IPC capacity takes the all-to-all fallback on every EP rank,
+    which must pass the program check (BFLY_PROGRAM_CHECK) as that same dispatch / return."""
+    from butterfly_amd.partition.schedule import Instr
+
+    torch.set_num_threads(1)
+    ep = 2
+    mesh = Mesh(dp=ep, ep=ep)
+    world = FakeWorld(mesh, timeout_s=60)
+
+    def run(r, comm):
+        me = comm.rank_in("ep")
+        assert comm.enable_ep_ipc(CAP, H, K)
+        grp = tuple(comm.groups["ep"].ranks)
+        prog = [Instr("ep_dispatch", grp), Instr("ep_return", grp)]
+        x, ids, w, slots = _inputs(me, 2 * CAP, ep)       # more rows than the IPC capacity
+        with comm.expect(prog):
+            rt = comm.ep_dispatch(x, ids, w, slots, EL, 2 * CAP)
+            out = comm.ep_combine(rt.x, rt)
+        return rt.path, out.shape
+
+    for path, shape in world.run(run):
+        assert path == "a2a" and shape == (2 * CAP, H)

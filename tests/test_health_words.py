@@ -17,8 +17,8 @@ class StubLib:
     def health_words(self):
         return list(self.words)
 
-    def health_clear(self):
-        self.words = [0, 0]
+    def health_clear(self, word=-1):
+        self.words = [0 if word in (-1, i) else v for i, v in enumerate(self.words)]
         self.cleared += 1
 
     def rccl_live(self):
@@ -49,8 +49,8 @@ def test_health_words_only_for_live_ipc_paths():
     rccl.health_arm("car")
     try:
         assert "all-reduce" in rccl.async_errors(lib)
-        with rccl.health_quiet(lib):               # another group's self-test in progress
-            assert rccl.async_errors(lib) is None
+        with rccl.health_quiet(lib, word="car"):   # a test of the same word: its vote
+            pass
     finally:
         rccl.health_arm("car", False)
     lib.words = [0, 1]
@@ -98,3 +98,32 @@ def test_butterfly_ranges_keyed_by_group(monkeypatch):
     assert r[2] == (0, 4096) and r[8] == (0, 4096)
     monkeypatch.setenv("BFLY_AR_BUTTERFLY", "")
     assert butterfly_ranges() == {}
+
+
+def test_quiet_is_scoped_to_its_word():
+    """an EP self-test neither hides nor wipes a live custom all-reduce timeout."""
+    lib = StubLib()
+    rccl.health_arm("car")
+    try:
+        with rccl.health_quiet(lib, word="ep") as q:
+            lib.words = [1, 1]                     # a real car timeout + the EP test's own
+            assert "all-reduce" in rccl.async_errors(lib)
+            q.failed(True)
+        assert lib.words == [1, 0]                 # only the EP word was cleared
+        assert "all-reduce" in rccl.async_errors(lib)
+    finally:
+        rccl.health_arm("car", False)
+
+
+def test_timeout_before_a_test_stays_reported():
+    """A live path's timeout already set when a test of the same word starts is sticky."""
+    lib = StubLib(words=(1, 0))
+    rccl.health_arm("car")
+    try:
+        with rccl.health_quiet(lib, word="car") as q:
+            q.failed(True)                         # the test clears the word...
+        assert lib.words == [0, 0]
+        assert "all-reduce" in rccl.async_errors(lib)   # ...the earlier failure is kept
+    finally:
+        rccl.health_arm("car", False)
+    assert rccl.async_errors(lib) is None          # path closed: nothing live to report

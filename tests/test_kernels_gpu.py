@@ -606,7 +606,14 @@ def test_gemm_deferred_reduce_fusions(M, N, K):
 # gate/up (tile, SiLU), Llama-3-8B QKV (decode-ring plan), a biased consumer, ragged row counts
 ROWSCALE_CASES = [(64, 8192, 10240, "none", True), (64, 8192, 57344, "silu", False),
                   (64, 4096, 6144, "none", True), (61, 4096, 28672, "silu", False),
-                  (200, 8192, 1024, "bias", False), (33, 8192, 10240, "none", False)]
+                  (200, 8192, 1024, "bias", False), (33, 8192, 10240, "none", False),
+                  # production decode batches 65-256: consumers on the mid-M plans
+                  # (kinds 5 / 7), whose epilogue applies the row scale
+                  (128, 8192, 10240, "none", True), (256, 4096, 6144, "none", True),
+                  (256, 4096, 28672, "silu", False), (128, 8192, 57344, "silu", False),
+                  (250, 8192, 10240, "none", False)]
+MID_ROWSCALE = {(128, 8192, 10240), (256, 4096, 6144), (256, 4096, 28672), (128, 8192, 57344),
+                (250, 8192, 10240)}
 
 
 @pytest.mark.parametrize("M,H,N,epi,defer", ROWSCALE_CASES)
@@ -615,6 +622,10 @@ def test_rms_norm_rows_with_rowscale_consumer(M, H, N, epi, defer, src):
     """Row-split add + RMSNorm (y = x * g, partial sums of squares) followed by a GEMM that
     applies the 1/rms row scale in its epilogue == fp32 add + RMSNorm + GEMM; the residual
     update is bit-identical to the one-workgroup-per-row kernel's."""
+    if (M, H, N) in MID_ROWSCALE:
+        # these must run the mid-M kernels with the row-scale epilogue, not skip
+        assert ops.gemm_plan(M, N, H)["kind"] in ("mid8", "mid4"), ops.gemm_plan(M, N, H)
+        assert ops.rowscale_ok(M, N, H, epi)
     if not ops.rowscale_ok(M, N, H, epi):
         pytest.skip(f"plan for {M}x{N}x{H} takes no row scale")
     K0 = 8192   # long enough that the producer GEMM splits K (slab input)

@@ -42,7 +42,7 @@ def checks(tag, fused=True):
     """Every correctness check in the current kernel mode (one-shot / two-shot)."""
     # 1. plain sums, many shapes (every rank computes the same expected value)
     for salt, (rows, dim) in enumerate([(1, 8192), (7, 8192), (64, 8192), (128, 8192), (129, 1024),
-                                        (256, 8192), (512, 4096), (1, 16384)]):
+                                        (256, 8192), (512, 4096), (1, 16384), (512, 8192)]):
         xs = [data(rows, dim, r, salt) for r in range(world)]
         want = torch.zeros(rows, dim, device=dev)
         for x in xs:
@@ -76,7 +76,9 @@ def checks(tag, fused=True):
 
     # 2b. split-K slab input (ops.Partial): the kernel reduces the f32 slabs while publishing;
     #     equal to splitk_reduce -> all-reduce (-> add + RMSNorm)
-    for salt, (sk, rows, dim) in enumerate([(4, 64, 8192), (3, 5, 4096), (8, 128, 8192)]):
+    # (the last two: the tp4 / tp8 weak-scaling messages, 256 / 512 rows x 8192 = 4 / 8 MiB)
+    for salt, (sk, rows, dim) in enumerate([(4, 64, 8192), (3, 5, 4096), (8, 128, 8192), (2, 256, 8192),
+                                            (4, 512, 8192)]):
         slabs = [(torch.randn(sk, rows, dim, generator=torch.Generator().manual_seed(300 + 10 * salt + r)) * 0.3)
                  .to(dev) for r in range(world)]
         parts = []
