@@ -96,9 +96,12 @@ class LLMEngine:
         self.device = torch.device(device)
         if stage_layers is None:
             stage_layers = balanced_stages(cfg.num_layers, mesh.pp)
-        if mesh.ep > 1 and mesh.pp > 1:
-            raise ValueError("expert parallelism with pipeline stages is not a supported layout "
-                             "(EP collectives span DP replicas of one stage)")
+        if mesh.ep > 1 and mesh.pp > 1 and not flags.get("BFLY_PP_ASYNC"):
+            # EP x PP: each stage's MoE layers exchange tokens with that stage's ranks of the
+            # other replicas; only the asynchronous pipeline keeps those EP groups in lockstep
+            # (every replica's plan of tick k reaches stage s at tick k + s, idle plans included)
+            raise ValueError("expert parallelism with pipeline stages needs the asynchronous pipeline "
+                             "(BFLY_PP_ASYNC=1)")
         # the rank's step program (partition/schedule.py) drives the stage execution below:
         # boundary receives / sends, stage runs, sampling and the id broadcast, with their peers
         self.plan = PartitionPlan(model=cfg, n_gpus=mesh.world_size, dp=mesh.dp, tp=mesh.tp, pp=mesh.pp,
@@ -111,7 +114,7 @@ class LLMEngine:
             # fails here, naming the ranks, instead of hanging the first step
             from ..partition.schedule import check_programs, programs
 
-            for mb in sorted({1, mesh.pp}):
+            for mb in sorted({1, mesh.pp} if mesh.ep == 1 else {1}):   # (EP x PP: async only)
                 check_programs(programs(self.plan, max(1, engine_cfg.max_batch), microbatches=mb))
         a, b = stage_layers[coord.pp]
         shard = Shard(tp_rank=coord.tp, tp_size=mesh.tp, layer_start=a, layer_end=b,
@@ -145,8 +148,7 @@ class LLMEngine:
         # control plane, which never waits for the device)
         # (context-parallel prefill over the DP replicas, pp == 1, runs inside the asynchronous
         # engine too: a tick that runs one is a CP tick, _pp_tick)
-        self.async_pp = flags.get("BFLY_PP_ASYNC") and (mesh.ep == 1 or mesh.pp == 1) and (
-            mesh.pp > 1 or bool(engine_cfg.async_decode))
+        self.async_pp = flags.get("BFLY_PP_ASYNC") and (mesh.pp > 1 or bool(engine_cfg.async_decode))
         # mixed steps (chunked prefill riding along decode rows, prefix caching): every layout;
         # in the asynchronous pipeline each group's plans are mixed. Expert-parallel replicas
         # agree per step on the padded row count and on whether any of them runs prompt rows
@@ -691,7 +693,8 @@ class LLMEngine:
         if self._pending is not None:         # left at tick k - 1: advance, values next tick
             p, self._pending = self._pending, None
             self._advance(p)
-            self._last_left[p.group] = p
+            if not p.idle:
+                self._last_left[p.group] = p
             self._valued = p
         # schedule the group entering stage 0 (every rank: replicated deterministic state)
         g = k % pp
@@ -703,9 +706,19 @@ class LLMEngine:
             # variable exchange. Host integers over the gloo control plane: no device sync.
             ep_pad, any_prefill, anyw = self._ep_agree(plan)
             if plan.kind == 0 and anyw:
-                eb = empty_batch(self.device, ep_pad)
-                eb.ep_alltoall = bool(any_prefill)
-                self.runner.run(eb)
+                if pp == 1:
+                    eb = empty_batch(self.device, ep_pad)
+                    eb.ep_alltoall = bool(any_prefill)
+                    self.runner.run(eb)
+                else:
+                    # EP x PP: this replica's idle plan travels the pipeline like any other, so
+                    # at tick k + s its stage s joins the MoE exchanges of the other replicas'
+                    # plans of tick k (no rows: nothing is sent between stages, nothing sampled)
+                    self._inflight.append(PipePlan(k, g, plan, [], 0, [], seqs=[], ep_pad=ep_pad,
+                                                   ep_prefill=bool(any_prefill), idle=True))
+                    if s == 0:
+                        with trace.range("pp.stage_work", tick=k, stage=0):
+                            self._pp_stage_work(self._inflight[-1])
                 if not out.new_tokens:
                     out.kind = "ep-idle"
         if plan.kind != 0:
@@ -750,7 +763,7 @@ class LLMEngine:
         """Post the receive of the plan that enters this stage next tick (it entered stage 0 at
         `tick` and is already in flight; its previous stage sent it this tick)."""
         p = next((q for q in self._inflight if q.tick == tick), None)
-        if p is None or tick in self._posted:
+        if p is None or p.idle or tick in self._posted:
             return
         H = self.cfg.hidden_size
         if not self._bbufs:
@@ -874,6 +887,16 @@ class LLMEngine:
         """recv the residual stream (stage > 0) -> run this stage -> isend (not last) or sample
         (last stage: ids kept on the plan for the broadcast, which the tick issues when the plan
         leaves the pipeline) — the step program's instructions of one microbatch."""
+        if p.idle:
+            # EP x PP idle plan: this stage's MoE layers join the EP exchanges with padded empty
+            # rows; no boundary transfer (every rank of the replica knows the plan is empty)
+            eb = empty_batch(self.device, p.ep_pad)
+            eb.ep_alltoall = p.ep_prefill
+            h = None if self.pp_first else torch.empty(0, self.cfg.hidden_size, dtype=self.model.dtype,
+                                                       device=self.device)
+            self.runner.run(eb, h)
+            p.ids = torch.empty(0, dtype=torch.int32, device=self.device)
+            return
         native_dec = self._native_pp and p.plan.kind == 2   # the decode graph receives itself
         state: dict = {}
 

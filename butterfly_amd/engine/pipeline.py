@@ -106,10 +106,13 @@ class PipePlan:
     seqs: list = field(default_factory=list)   # every sequence with a row in the plan
     ep_pad: int = 0           # expert parallelism: rows every EP rank pads this step to
     ep_prefill: bool = False  # some EP rank prefills this step (variable exchange, no graphs)
+    idle: bool = False        # EP x PP: an empty plan that only joins its peers' MoE exchanges
     ids: Optional[object] = None   # sampled ids tensor (last stage / after broadcast)
     host: Optional[object] = None  # pinned host copy of `ids` (async D2H at broadcast time)
     event: Optional[object] = None # marks that copy complete
 
     @property
     def kind(self) -> str:
+        if self.idle:
+            return "ep-idle"
         return {1: "prefill", 3: "mixed"}.get(self.plan.kind, "decode")

@@ -101,8 +101,10 @@ def rank_program(plan: PartitionPlan, rank: int, tokens: int, microbatches: int 
     (default) a step is one tick carrying one request group (`tokens` = the group's size, one
     microbatch); the synchronous pipeline (engine._pipeline_decode) cuts the step's batch into
     `microbatches` parts that flow through the stages back to back, then broadcasts all ids."""
-    if plan.mesh.ep > 1 and plan.mesh.pp > 1:
-        raise ValueError("expert parallelism with pipeline stages is not a supported layout")
+    # (EP x PP: each stage's MoE collectives run on that stage's EP group, the stage's ranks of
+    # every replica; the asynchronous pipeline keeps them in lockstep, one microbatch per tick)
+    if plan.mesh.ep > 1 and plan.mesh.pp > 1 and microbatches > 1:
+        raise ValueError("expert parallelism with pipeline stages runs one microbatch per tick")
     prog = RankProgram(rank, tokens)
     M = max(1, min(microbatches, tokens))
     bounds = [tokens * i // M for i in range(M + 1)]

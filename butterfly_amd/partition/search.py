@@ -144,9 +144,9 @@ def partition(cfg: Union[ModelConfig, str], n_gpus: int, strategy: Union[str, di
         if not _tp_ok(cfg, tp) or pp > cfg.num_layers:
             continue
         eps = [1]
-        # expert parallelism spans the DP replicas of a single-stage layout: with pp > 1 the
-        # EP collectives would have to line up across independently scheduled pipeline ticks
-        if cfg.is_moe and dp > 1 and cfg.num_experts % dp == 0 and tp == 1 and pp == 1:
+        # expert parallelism spans the DP replicas (per pipeline stage when pp > 1: the
+        # asynchronous pipeline keeps each stage's EP group in lockstep)
+        if cfg.is_moe and dp > 1 and cfg.num_experts % dp == 0 and tp == 1:
             eps.append(dp)
         if "ep" in fixed:
             eps = [e for e in eps if e == fixed["ep"]]

@@ -22,36 +22,52 @@ constexpr int kRopeThreads = 256;
 // 8 elements of one V head (so a token's work spreads over several workgroups: at decode T is
 // only the batch size). With `part` the row is first assembled from the f32 split-K slabs of
 // the QKV GEMM (its deferred reduce fused here) and written back to `qkv` in bf16.
-template <int D>
-__device__ __forceinline__ bf16x8 rope_load(const bf16* __restrict__ row, const float* __restrict__ prow,
-                                            int sk, long slab, int col) {
-  if (!prow) return *reinterpret_cast<const bf16x8*>(row + col);
-  f32x4 lo = *reinterpret_cast<const f32x4*>(prow + col), hi = *reinterpret_cast<const f32x4*>(prow + col + 4);
-  // slabs in batches of 4 with all 8 loads issued before the adds: one dependent add chain
-  // over 16 slabs (the tp8 B = 1 QKV plan) waited ~0.8 us per slab, 14 us per launch
-  // (profiles/r6_latency.md); the adds keep the slab order, i.e. the reduce kernel's sum
-  for (int k0 = 1; k0 < sk; k0 += 4) {
-    f32x4 l[4], h[4];
+// Deferred split-K reduce of NC 8-column pieces of one row (the rotation pair's two halves, or one
+// V piece): slabs in batches of 8 with every load of the batch issued before any add — one
+// dependent add chain over the 16 slabs of the tp8 B = 1 QKV plan waited a load latency per slab
+// (14 us per launch, profiles/r6_latency.md). The adds keep the slab order (the reduce kernel's
+// sum, bit for bit).
+template <int NC>
+__device__ __forceinline__ void slab_sum(const float* __restrict__ prow, int sk, long slab, const int (&col)[NC],
+                                         f32x4 (&lo)[NC], f32x4 (&hi)[NC]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + j < sk ? k0 + j : k0;
-      l[j] = *reinterpret_cast<const f32x4*>(prow + k * slab + col);
-      h[j] = *reinterpret_cast<const f32x4*>(prow + k * slab + col + 4);
+  for (int c = 0; c < NC; ++c) {
+    lo[c] = *reinterpret_cast<const f32x4*>(prow + col[c]);
+    hi[c] = *reinterpret_cast<const f32x4*>(prow + col[c] + 4);
+  }
+  for (int k0 = 1; k0 < sk; k0 += 8) {
+    f32x4 l[8][NC], h[8][NC];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long off = (long)(k0 + j < sk ? k0 + j : k0) * slab;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        l[j][c] = *reinterpret_cast<const f32x4*>(prow + off + col[c]);
+        h[j][c] = *reinterpret_cast<const f32x4*>(prow + off + col[c] + 4);
+      }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 8; ++j)
       if (k0 + j < sk) {
-        lo += l[j];
-        hi += h[j];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          lo[c] += l[j][c];
+          hi[c] += h[j][c];
+        }
       }
   }
+}
+
+__device__ __forceinline__ bf16x8 pack8(f32x4 lo, f32x4 hi) {
   bf16x8 a;
 #pragma unroll
   for (int j = 0; j < 4; ++j) { a[j] = f2bf(lo[j]); a[j + 4] = f2bf(hi[j]); }
   return a;
 }
 
-template <int D, typename CT>
+// SLABS: the row comes from the QKV GEMM's split-K slabs (a separate instantiation, so the
+// register-hungry batched slab loads do not cost the plain path occupancy at prefill sizes)
+template <int D, typename CT, bool SLABS>
 __global__ void __launch_bounds__(kRopeThreads)
 rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
                const float* __restrict__ cos_t, const float* __restrict__ sin_t,
@@ -67,7 +83,7 @@ rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
   if (i >= nrot + nv) return;
   const long row_stride = (long)(Hq + 2 * Hkv) * D;
   bf16* row = qkv + (long)t * row_stride;
-  const float* prow = part ? part + (long)t * row_stride : nullptr;
+  const float* prow = SLABS ? part + (long)t * row_stride : nullptr;
   const int slot = slots ? slots[t] : -1;
   const int blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
@@ -76,8 +92,17 @@ rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
     const float* cr = cos_t + (long)pos * H2;
     const float* sr = sin_t + (long)pos * H2;
     const int h = i / LPH, p0 = (i % LPH) * 8;
-    const bf16x8 a = rope_load<D>(row, prow, sk, slab, h * D + p0);
-    const bf16x8 b = rope_load<D>(row, prow, sk, slab, h * D + p0 + H2);
+    bf16x8 a, b;
+    if constexpr (SLABS) {
+      const int cols[2] = {h * D + p0, h * D + p0 + H2};
+      f32x4 lo[2], hi[2];
+      slab_sum<2>(prow, sk, slab, cols, lo, hi);
+      a = pack8(lo[0], hi[0]);
+      b = pack8(lo[1], hi[1]);
+    } else {
+      a = *reinterpret_cast<const bf16x8*>(row + h * D + p0);
+      b = *reinterpret_cast<const bf16x8*>(row + h * D + p0 + H2);
+    }
     const f32x4 c0 = *reinterpret_cast<const f32x4*>(cr + p0);
     const f32x4 c1 = *reinterpret_cast<const f32x4*>(cr + p0 + 4);
     const f32x4 s0 = *reinterpret_cast<const f32x4*>(sr + p0);
@@ -107,8 +132,16 @@ rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
   const int iv = i - nrot;
   const int kh = iv / LPV, d0 = (iv % LPV) * 8;
   const int col = (Hq + Hkv + kh) * D + d0;
-  const bf16x8 v = rope_load<D>(row, prow, sk, slab, col);
-  if (prow) *reinterpret_cast<bf16x8*>(row + col) = v;
+  bf16x8 v;
+  if constexpr (SLABS) {
+    const int cols[1] = {col};
+    f32x4 lo[1], hi[1];
+    slab_sum<1>(prow, sk, slab, cols, lo, hi);
+    v = pack8(lo[0], hi[0]);
+  } else {
+    v = *reinterpret_cast<const bf16x8*>(row + col);
+  }
+  if constexpr (SLABS) *reinterpret_cast<bf16x8*>(row + col) = v;
   if (slot < 0 || !v_cache) return;
   CT* vp = v_cache + ((long)blk * Hkv + kh) * D * BS + off;
 #pragma unroll
@@ -147,13 +180,17 @@ static void run_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* pos
   const dim3 grid(T, (items + kRopeThreads - 1) / kRopeThreads);
   CT* kc = static_cast<CT*>(k_cache);
   CT* vc = static_cast<CT*>(v_cache);
+#define ROPE_LAUNCH(D_, S_)                                                                             \
+  rope_kv_kernel<D_, CT, S_><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, kc, vc, \
+                                                                Hq, Hkv, block_size, part, sk, slab)
   if (D == 128) {
-    rope_kv_kernel<128, CT><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, kc, vc,
-                                                              Hq, Hkv, block_size, part, sk, slab);
+    if (part) ROPE_LAUNCH(128, true);
+    else ROPE_LAUNCH(128, false);
   } else if (D == 64) {
-    rope_kv_kernel<64, CT><<<grid, kRopeThreads, 0, stream>>>(qkv, positions, cos_t, sin_t, slots, kc, vc,
-                                                             Hq, Hkv, block_size, part, sk, slab);
+    if (part) ROPE_LAUNCH(64, true);
+    else ROPE_LAUNCH(64, false);
   }
+#undef ROPE_LAUNCH
 }
 
 void launch_rope_kv(bf16* qkv, int T, int Hq, int Hkv, int D, const int* positions,

@@ -242,6 +242,18 @@ def _ep_async_generate(rank, world, mesh_kw, async_pp):
     return [eng.requests[r].output for r in rids]
 
 
+def test_expert_parallel_with_pipeline_stages():
+    """EP x PP: Mixtral experts split over 2 replicas, each replica a 2-stage
+    pipeline (4 ranks); each stage's MoE layers exchange tokens with the other replica's same
+    stage. Uneven loads (idle plans travel the pipeline): every replica's tokens equal the
+    synchronous EP engine's (= single process)."""
+    ref = run_world(_ep_async_generate, 2, dict(dp=2, ep=2), False)
+    got = run_world(_ep_async_generate, 4, dict(dp=2, ep=2, pp=2), True)
+    mesh = Mesh(dp=2, ep=2, pp=2)
+    for r in range(4):
+        assert got[r] == ref[mesh.coord(r).dp], r
+
+
 @pytest.mark.parametrize("mesh_kw,world", [(dict(dp=2, ep=2), 2), (dict(dp=4, ep=4), 4)])
 def test_expert_parallel_async_matches_sync(mesh_kw, world):
     """EP layouts on the asynchronous engine (host agreement over the control plane, token
@@ -292,8 +304,9 @@ def _ep_mixed_generate(rank, world, mesh_kw, async_pp, shared_prefix, long_len=0
     return [eng.requests[r].output for r in rids], sorted(kinds), eng.scheduler.prefix_hit_tokens
 
 
-@pytest.mark.parametrize("mesh_kw,world", [(dict(dp=2, ep=2), 2), (dict(dp=4, ep=4), 4)])
-@pytest.mark.parametrize("async_pp", [True, False])
+@pytest.mark.parametrize("mesh_kw,world,async_pp", [(dict(dp=2, ep=2), 2, True), (dict(dp=2, ep=2), 2, False),
+                                                   (dict(dp=4, ep=4), 4, True), (dict(dp=4, ep=4), 4, False),
+                                                   (dict(dp=2, ep=2, pp=2), 4, True)])
 @pytest.mark.parametrize("shared_prefix", [False, True])
 def test_expert_parallel_mixed_chunked_prefill(mesh_kw, world, async_pp, shared_prefix):
     """expert-parallel layouts run mixed plans (prompt chunks beside decode
@@ -301,11 +314,13 @@ def test_expert_parallel_mixed_chunked_prefill(mesh_kw, world, async_pp, shared_
     tokens equal the single-process engine's for the same requests."""
     long_len = 300 if world == 2 else 0
     got = run_world(_ep_mixed_generate, world, mesh_kw, async_pp, shared_prefix, long_len)
+    mesh = Mesh(**mesh_kw)
     for r in range(world):
-        want, want_kinds, _ = _ep_mixed_generate(r, 1, {}, False, shared_prefix, long_len)
+        dp = mesh.coord(r).dp
+        want, want_kinds, _ = _ep_mixed_generate(dp, 1, {}, False, shared_prefix, long_len)
         out, kinds, hits = got[r]
         assert out == want, r
-        if r == 0:
+        if dp == 0 and mesh.coord(r).pp == mesh.pp - 1:
             assert "mixed" in want_kinds and "mixed" in kinds
             if shared_prefix:
                 assert hits > 0
