@@ -61,6 +61,7 @@ class GroupHandle:
     rank_in_group: int
     native: Optional[object] = None   # parallel/rccl.RcclComm (BFLY_NATIVE_RCCL) for the data path
     ctrl: Optional[object] = None     # gloo ProcessGroup for host integers when `pg` is RCCL
+    shm: Optional[object] = None      # parallel/shm_ctrl.ShmCtrl: node-local host-integer max
 
     @property
     def size(self) -> int:
@@ -115,10 +116,20 @@ class Communicator:
                 cpg = dist.new_group(ranks, backend="gloo")
                 if rank in ranks:
                     groups["dp"].ctrl = cpg
+        from ..utils import flags
+
+        if mesh.dp > 1 and flags.get("BFLY_SHM_CTRL"):
+            # the per-step host agreements of the data-parallel / expert-parallel axis through
+            # shared memory when the group's ranks share a host (parallel/shm_ctrl.py); each
+            # group sets its own up (group-local collectives on its host-side process group)
+            from .shm_ctrl import make
+
+            g = groups["dp"]
+            gi = next(i for i, rs in enumerate(mesh.all_groups("dp")) if rank in rs)
+            g.shm = make(g.ranks, g.rank_in_group, g.ctrl if g.ctrl is not None else g.pg, f"dp{gi}")
         groups["ep"] = groups["dp"] if mesh.ep > 1 else GroupHandle([rank], None, 0)
         groups["world"] = GroupHandle(list(range(mesh.world_size)), dist.group.WORLD, rank)
         comm = cls(mesh, rank, groups)
-        from ..utils import flags
 
         gpu_rccl = dist.get_backend() == "nccl" and torch.cuda.is_available()
         if gpu_rccl and flags.get("BFLY_PREFLIGHT"):
@@ -445,6 +456,10 @@ class Communicator:
         for g in self.groups.values():
             if g is not None:
                 g.native = None
+                if g.shm is not None:
+                    g.shm.close()
+                    g.shm = None
+                    out["shm_ctrl"] = "closed"
         return out
 
     @property
@@ -569,6 +584,8 @@ class Communicator:
         g = self.groups[group]
         if g.size == 1:
             return list(values)
+        if g.shm is not None:         # node-local shared memory: a few microseconds, no sockets
+            return g.shm.max(values)
         if g.ctrl is not None:        # gloo control plane: no device work, no stream sync
             t = torch.tensor(values, dtype=torch.int64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g.ctrl)

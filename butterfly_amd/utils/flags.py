@@ -114,6 +114,9 @@ define("BFLY_FORCE_CPU", False, _bool, "bench.py: run on the CPU reference path 
        "(BASELINE config 1, the gloo plumbing configuration)")
 define("BFLY_RCCL_POLL_S", 1.0, float, "period of the thread polling native RCCL communicators for async errors "
        "(on one: abort every communicator, exit 75); 0 = off")
+define("BFLY_SHM_CTRL", True, _bool, "data-parallel / expert-parallel per-step host agreements (EP padding, "
+       "lockstep liveness) through a shared-memory segment when the group's ranks share a host, instead of a "
+       "gloo all-reduce (parallel/shm_ctrl.py)")
 define("BFLY_COMM_TIMEOUT_S", 600.0, float, "collective / process-group timeout in seconds")
 define("BFLY_HEARTBEAT_S", 5.0, float, "health heartbeat period (0 disables the watchdog)")
 define("BFLY_STEP_TIMEOUT_S", 0.0, float, "engine step watchdog: terminate a rank whose step exceeds this (0 = off)")
