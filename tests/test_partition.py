@@ -53,16 +53,21 @@ def test_mixtral_expert_parallel_candidate():
     assert p.ep == 8 and p.shard(3).ep_rank == 3
 
 
-def test_no_expert_parallel_with_pipeline_stages():
-    """EP layouts are single-stage: the search never proposes ep > 1 with pp > 1, an explicit
-    request is infeasible, and the schedule refuses such a plan."""
+def test_expert_parallel_with_pipeline_stages():
+    """EP x PP (round 6): an explicit ep2 x pp2 request is a valid plan whose stage ranks share
+    their EP groups per stage; its rank programs (one microbatch per tick) are consistent, and
+    the synchronous multi-microbatch program is refused."""
     import pytest as _pt
 
-    for n in (2, 4, 8):
-        p = partition("mixtral-8x7b", n)
-        assert not (p.ep > 1 and p.pp > 1)
+    from butterfly_amd.partition.schedule import check_programs, programs, rank_program
+
+    p = partition("mixtral-8x7b", 4, {"dp": 2, "ep": 2, "pp": 2})
+    assert p.ep == 2 and p.pp == 2
+    mesh = p.mesh
+    assert mesh.dp_group(mesh.rank(0, 1, 0)) == [mesh.rank(0, 1, 0), mesh.rank(1, 1, 0)]
+    check_programs(programs(p, 8, microbatches=1, ep_ipc=True))
     with _pt.raises(ValueError):
-        partition("mixtral-8x7b", 4, {"dp": 2, "ep": 2, "pp": 2})
+        rank_program(p, 0, 8, microbatches=2)
 
 
 @settings(max_examples=25, deadline=None)
