@@ -474,7 +474,7 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
 def gemm_plan(M: int, N: int, K: int) -> dict:
     load_library()
     k, mt, nt, bm, bn, sk, wk = torch.ops.bfly.gemm_plan(M, N, K)
-    return {"kind": ("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4", "big4w")[k], "mt": mt, "nt": nt, "wk": wk, "bm": bm, "bn": bn,
+    return {"kind": ("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4")[k], "mt": mt, "nt": nt, "wk": wk, "bm": bm, "bn": bn,
             "splitk": sk}
 
 

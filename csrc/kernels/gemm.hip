@@ -1058,148 +1058,6 @@ gemm_big4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------
-// 256 x 224 tile, one wave per SIMD (plan kind 8, "big4w"): the fused gate/up projections'
-// N = 57344 / tp = 256 x 224 / tp columns, so a 224-wide tile makes whole waves of 256 tiles
-// where 256-wide tiles leave 32 CUs idle (tp1 at M = 256: 224 tiles; tp4 at M = 256 with split-K
-// 4: 224 workgroups; tp8 at M = 512: 64 tiles x split 4 = 256 instead of 224).
-// big4's pipeline (LDS-DMA rings of whole K-tiles, 3 A slots of 32 KiB and 2 B slots of 28 KiB =
-// 152 KiB, one barrier per K-tile, sched_barrier-fenced slots, immediate-offset fragment reads)
-// with the 4 waves stacked along M: wave w owns rows 64w .. 64w + 63 and all 224 columns (4 x 14
-// accumulator tiles), so the gate / up 16-row column groups pair up inside every wave (the SiLU
-// epilogue). Per k-step a wave reads 4 A + 14 B fragments for 56 MFMAs in 14 slots of one column
-// block each; A's 8 DMA instructions per K-tile ride in k-step 0, B's 7 in k-step 1.
-// ---------------------------------------------------------------------------------------
-constexpr int kB4wBn = 224;
-constexpr int kB4wBSlot = kB4wBn * 128;            // 28 KiB
-constexpr int kB4wLdsBytes = 3 * kB4Slot + 2 * kB4wBSlot;   // 152 KiB
-
-__global__ void __launch_bounds__(kB4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
-gemm_big4w_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
-                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
-                  bf16* __restrict__ out, long ldo, float* __restrict__ part) {
-  constexpr int BM = 256, BN = kB4wBn, TJ = BN / 16;   // 14 column blocks
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
-  const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
-  const int per_group = kBigGroupM * ntiles;
-  const int grp = t / per_group, first_m = grp * kBigGroupM;
-  const int gsize = min(mtiles - first_m, kBigGroupM);
-  const int m0 = (first_m + (t % per_group) % gsize) * BM;
-  const int n0 = ((t % per_group) / gsize) * BN;
-  const int ktiles = K / 64;
-  const int kt0 = (int)(((long)ktiles * blockIdx.y) / gridDim.y);
-  const int kt1 = (int)(((long)ktiles * (blockIdx.y + 1)) / gridDim.y);
-  const int nk = kt1 - kt0;   // >= 2 (host check)
-
-  // DMA: A instruction s (0..7) of wave w fills row block 8w + s; B instruction s (0..6) row
-  // block 7w + s (8 rows x 128 B each, lane-linear). Lane L supplies row 8 (block) + (L >> 3) at
-  // the chunk lds_frag expects in position L & 7: (L & 7) ^ (((L >> 4) + 4 (block & 1)) & 7)
-  const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);   // A rows past M read zeros
-  const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
-  int va[2], vbs[7];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int ch = (lane & 7) ^ (((lane >> 4) + 4 * e) & 7);
-    va[e] = (int)(((64 * wid + (lane >> 3)) * ldx + ch * 8) * 2);
-  }
-#pragma unroll
-  for (int s = 0; s < 7; ++s) {
-    const int e = (wid + s) & 1;     // parity of B row block 7w + s
-    const int ch = (lane & 7) ^ (((lane >> 4) + 4 * e) & 7);
-    vbs[s] = (int)(((56 * wid + (lane >> 3)) * ldw + ch * 8) * 2);
-  }
-  char* const bbase = smem + 3 * kB4Slot;
-  auto dma_a = [&](int k, int slot, int s) {
-    b4_dma(rsa, smem + slot * kB4Slot + (8 * wid + s) * 1024, va[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldx * 2));
-  };
-  auto dma_b = [&](int k, int slot, int s) {
-    b4_dma(rsb, bbase + slot * kB4wBSlot + (7 * wid + s) * 1024, vbs[s], (kt0 + k) * 128 + (int)(8 * s * ldw * 2));
-  };
-  const int fr = lane & 15, fq = lane >> 4;
-  int lo[2][2];   // [A / B][ks] lane byte offset inside a slot (fragments 16 rows = 2048 B apart)
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int ch = ((ks * 4 + fq) ^ ((fr >> 1) & 7)) * 16;
-    lo[0][ks] = (64 * wid + fr) * 128 + ch;
-    lo[1][ks] = fr * 128 + ch;
-  }
-  // fragment idx 0 .. 13: B column block idx; 14 .. 17: A row block idx - 14
-  auto rd1 = [&](int sa_, int sb_, int ks, int idx, bf16x8 (&f)[TJ + 4]) {
-    const char* p = idx < TJ ? bbase + sb_ * kB4wBSlot + lo[1][ks] + 2048 * idx
-                             : smem + sa_ * kB4Slot + lo[0][ks] + 2048 * (idx - TJ);
-    f[idx] = *reinterpret_cast<const bf16x8*>(p);
-  };
-  f32x4 acc[4][TJ];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mf4 = [&](int n, const bf16x8 (&f)[TJ + 4]) {   // slot n: column block n, row blocks 0-3
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i][n] = mfma16(f[n], f[TJ + i], acc[i][n]);
-  };
-  bf16x8 f0[TJ + 4], f1[TJ + 4];
-  // per slot n (0..13): read positions [rlo(n), rlo(n+1)) of 18 in the order A0-A3, B0-B13
-  // (every slot of the next k-step needs all four A fragments and its own B block), A DMA when
-  // (n+1)*8/14 > n*8/14 (8 of them), B DMA when n is odd (7)
-  auto rlo = [](int n) { return n < 4 ? 2 * n : n + 4; };
-  auto pos_idx = [](int p) { return p < 4 ? TJ + p : p - 4; };
-
-  // prologue: A(0), B(0), A(1), B(1); wait for K-tile 0 (A(1), B(1) = 15 loads may fly)
-#pragma unroll
-  for (int s = 0; s < 8; ++s) dma_a(0, 0, s);
-#pragma unroll
-  for (int s = 0; s < 7; ++s) dma_b(0, 0, s);
-#pragma unroll
-  for (int s = 0; s < 8; ++s) dma_a(1, 1, s);
-#pragma unroll
-  for (int s = 0; s < 7; ++s) dma_b(1, 1, s);
-  vm_wait<15>();
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int idx = 0; idx < TJ + 4; ++idx) rd1(0, 0, 0, idx, f0);
-
-  auto ks0 = [&](int k, int sa_, int sb_) {   // k-step 0 of K-tile k: read its ks-1 fragments
-#pragma unroll
-    for (int n = 0; n < TJ; ++n) {
-      mf4(n, f0);
-      if ((n + 1) * 8 / TJ > n * 8 / TJ) dma_a(min(k + 2, nk - 1), sa_ == 0 ? 2 : sa_ - 1, n * 8 / TJ);
-#pragma unroll
-      for (int q = rlo(n); q < rlo(n + 1); ++q) rd1(sa_, sb_, 1, pos_idx(q), f1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    vm_wait<8>();                     // A(k+1), B(k+1) landed; A(k+2) may fly
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  auto ks1 = [&](int k, int sa_, int sb_, int sa1_) {   // k-step 1: next ks-0 reads, DMA B(k+2)
-    const int kb = min(k + 2, nk - 1);
-#pragma unroll
-    for (int n = 0; n < TJ; ++n) {
-      mf4(n, f1);
-#pragma unroll
-      for (int q = rlo(n); q < rlo(n + 1); ++q) rd1(sa1_, sb_ ^ 1, 0, pos_idx(q), f0);
-      if (n & 1) dma_b(kb, sb_, n >> 1);   // B(k+2) into the slot K-tile k just left
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  int sa = 0;
-  ks0(0, 0, 0);
-  for (int k = 0; k + 1 < nk; ++k) {
-    const int sb = k & 1, sa1 = sa == 2 ? 0 : sa + 1;
-    ks1(k, sa, sb, sa1);
-    ks0(k + 1, sa1, sb ^ 1);
-    sa = sa1;
-  }
-  ks1(nk - 1, sa, (nk - 1) & 1, sa == 2 ? 0 : sa + 1);
-  vm_wait<0>();                       // no LDS-DMA may outlive the workgroup
-  tile_epilogue<4, TJ>(acc, m0 + 64 * wid, n0, lane, M, N, epi, bias, out, ldo,
-                       part ? part + (long)blockIdx.y * M * N + (long)m0 * N : nullptr, m0,
-                       RowScale{nullptr, 0, 0.f, 0.f});
-}
-
-// ---------------------------------------------------------------------------------------
 // Mid-M GEMM (plan kind 5): the tensor-parallel shard projections at M = 128-512 rows (tp2-tp8
 // decode at 64 sequences per GPU, large single-GPU batches), where a 256x256 tile grid leaves
 // most of the 256 CUs idle (tp8 QKV at M = 512: 10 tiles) and the 4-wave tile kernel keeps the
@@ -1655,19 +1513,6 @@ static void run_big4(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   gemm_big4_kernel<false><<<grid, kB4Threads, kB4LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
-static void run_big4w(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
-                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big4w_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kB4wLdsBytes);
-    attr_set = true;
-  }
-  dim3 grid(((M + 255) / 256) * (N / kB4wBn), sk);
-  float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  gemm_big4w_kernel<<<grid, kB4Threads, kB4wLdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
-}
-
 template <int BM, int BN, int SA, int SB>
 static void run_mid4(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                      const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream,
@@ -1861,10 +1706,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     // one-wave-per-SIMD 256x256 tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
     if (!dry) run_big4(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
-  } else if (p.kind == 8) {
-    // one-wave-per-SIMD 256x224 tile (waves stacked along M): every split >= 2 K-tiles
-    if (N % kB4wBn != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
-    if (!dry) run_big4w(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream);
+
   } else if (p.kind == 5) {
     // mid-M 8-wave staggered GEMM: plan {5, SW (weight ring), SX (activation ring; 0 = SW), 0,
     // BM, BN, sk}

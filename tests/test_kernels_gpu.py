@@ -393,40 +393,6 @@ def test_gemm_big_tile_production(M, N, K, epi, sk, kind):
     _close(out, want, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("M,N,K,sk", [(600, 448, 1024, 1), (77, 224, 128, 1), (300, 672, 256, 2),
-                                      (1000, 1344, 4096, 3), (256, 448, 192, 1), (520, 896, 640, 5)])
-@pytest.mark.parametrize("epi", ["none", "bias", "silu"])
-def test_gemm_big4w_tile(M, N, K, sk, epi):
-    """256x224 one-wave-per-SIMD tile (plan kind 8, waves stacked along M): ragged M, the
-    minimum two K-tiles per split, uneven split-K, all epilogues (SiLU pairs inside each
-    wave's 14 column blocks), asymmetric operands, against fp32."""
-    x = _bf(M, K, seed=70)
-    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=71)
-    b = _bf(N, seed=72) if epi == "bias" else None
-    nout = N // 2 if epi == "silu" else N
-    want = ref.linear(x, w, b, "silu" if epi == "silu" else "none")
-    out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-    ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
-    torch.ops.bfly.gemm_with_plan(x, w, out, [8, 0, 0, 0, 256, 224, sk], ops.EPILOGUES[epi], ws, b)
-    _close(out, want, 2e-2, 2e-2)
-
-
-@pytest.mark.parametrize("M,N,K,epi,sk", [(256, 57344, 8192, "silu", 1),    # tp1 gate_up, 256 tiles
-                                          (512, 7168, 8192, "silu", 4),     # tp8 gate_up, 256 workgroups
-                                          (256, 14336, 8192, "silu", 4),    # tp4 gate_up
-                                          (2048, 28672, 8192, "none", 1)])  # prefill scale, no epilogue
-def test_gemm_big4w_production(M, N, K, epi, sk):
-    """kind 8 at the gate/up shard shapes it is for (K = 8192, whole waves of 256 tiles)."""
-    x = _bf(M, K, seed=73)
-    w = _bf(N, K, scale=1.0 / math.sqrt(K), seed=74)
-    nout = N // 2 if epi == "silu" else N
-    want = ref.linear(x, w, None, epi)
-    out = torch.empty(M, nout, dtype=torch.bfloat16, device=DEV)
-    ws = torch.zeros(sk * M * N + 16384, dtype=torch.float32, device=DEV)
-    torch.ops.bfly.gemm_with_plan(x, w, out, [8, 0, 0, 0, 256, 224, sk], ops.EPILOGUES[epi], ws)
-    _close(out, want, 2e-2, 2e-2)
-
-
 TILE_CFGS = [(16, 128, 1), (16, 256, 1), (32, 128, 1), (32, 256, 1), (64, 128, 1), (64, 128, 2),
              (64, 256, 1), (64, 256, 2), (128, 128, 2), (128, 256, 2), (64, 224, 4), (64, 160, 4)]
 
@@ -475,7 +441,7 @@ def test_every_tuned_plan_matches_fp32(NK):
         x = _bf(M, K, seed=M + 3)
         plan = ops.gemm_plan(M, N, K)
         # 256x256 entries (swept on big8, kind 4) run the one-wave-per-SIMD big4 (kind 6)
-        assert [("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4", "big4w").index(plan["kind"]), plan["splitk"]] == \
+        assert [("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4").index(plan["kind"]), plan["splitk"]] == \
             [6 if e[3] == 4 else e[3], e[9]], (e, plan)
         want = x.float() @ w.float().t()
         _close(ops.linear(x, w), want, 2e-2, 2e-2)

@@ -100,7 +100,7 @@ def main():
                 nout = N // 2 if epi == "silu" else N
                 out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
                 plan = ops.gemm_plan(M, N, K)
-                auto = [("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4", "big4w").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
+                auto = [("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4").index(plan["kind"]), plan["mt"], plan["nt"], plan["wk"], plan["bm"],
                         plan["bn"], plan["splitk"]]
                 t = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, Ws[i % copies], out, auto, ops.EPILOGUES[epi], ws),
                            tag={"shape": f"{group}.{name}", "M": M, "N": N, "K": K, "plan": auto, "auto": True})
@@ -160,12 +160,6 @@ def main():
                         for sk in (1, 2, 3, 4, 6, 8, 12, 16):
                             if K // 64 >= sk * 2:
                                 cands.append([6, 0, 0, 0, 256, 256, sk])
-                    if M >= 128 and N % 224 == 0:
-                        # 256x224 one-wave-per-SIMD tile (kind 8): whole waves of 256 tiles for
-                        # the gate/up shapes (N = 57344 / tp)
-                        for sk in (1, 2, 3, 4, 6, 8):
-                            if K // 64 >= sk * 2:
-                                cands.append([8, 0, 0, 0, 256, 224, sk])
                     if a.kinds:
                         keep = {int(k) for k in a.kinds.split(",")}
                         cands = [c for c in cands if c[0] in keep]

@@ -47,7 +47,7 @@ def main():
         e = res.setdefault(key, {"shape": tag["shape"], "M": tag["M"], "N": tag["N"], "K": tag["K"]})
         if tag.get("auto"):
             p = tag["plan"]
-            e["plan"] = {"kind": ("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4", "big4w")[p[0]], "mt": p[1], "nt": p[2], "wk": p[3],
+            e["plan"] = {"kind": ("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4")[p[0]], "mt": p[1], "nt": p[2], "wk": p[3],
                          "bm": p[4], "bn": p[5], "splitk": p[6]}
             e["us"] = round(us, 2)
             e["TBps"] = round(tag["N"] * tag["K"] * 2 / us / 1e6, 3)
