@@ -29,7 +29,8 @@ SHAPES = {
             ("down", 8192, 7168, "none"), ("lm_head", 32256, 8192, "none")],
     "8b": [("qkv", 6144, 4096, "none"), ("o", 4096, 4096, "none"), ("gate_up", 28672, 4096, "silu"),
            ("down", 4096, 14336, "none"), ("lm_head", 128256, 4096, "none")],
-    "mixtral": [("lm_head", 32000, 4096, "none")],
+    "mixtral": [("lm_head", 32000, 4096, "none"), ("moe_gate_up", 229376, 4096, "silu"),
+                ("moe_down", 4096, 114688, "none")],
 }
 
 

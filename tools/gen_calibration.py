@@ -23,6 +23,12 @@ def main():
                 cands.append(r["us"])
             if cands:
                 best[key] = min(best.get(key, 1e30), min(cands))
+    # round-6 event-timed same-run sweeps (the plan table takes their winners): best candidate
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r6_gemm", "sweep_evt_*.json"))):
+        for r in json.load(open(f)):
+            if r.get("best_us"):
+                key = f"{r['N']}x{r['K']}x{r['M']}"
+                best[key] = min(best.get(key, 1e30), r["best_us"])
     gemm = dict(old.get("gemm", {}))
     n = 0
     for key, us in best.items():
@@ -31,7 +37,8 @@ def main():
         gemm[key] = round(us, 2)
         n += 1
     old["gemm"] = dict(sorted(gemm.items()))
-    old["source"] = "tools/gen_calibration.py: fastest plan per shape in profiles/gemm_tune_*.json (rocprofv3-serialised sweeps)"
+    old["source"] = ("tools/gen_calibration.py: fastest plan per shape in profiles/gemm_tune_*.json (rocprofv3-"
+                     "serialised sweeps) and profiles/r6_gemm/sweep_evt_*.json (event-timed same-run sweeps)")
     json.dump(old, open(CAL, "w"), indent=1)
     print(f"{n} entries updated, {len(gemm)} total")
 
