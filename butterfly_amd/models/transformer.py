@@ -353,9 +353,16 @@ class TransformerLM:
                 x = self._add_norm(delta, pre + "in", residual, partial,
                                    consumer=(pre + "qkv_w", "bias" if pre + "qkv_b" in self.p else "none"))
             o = self._attention_block(li, pre, x, fb, kv_caches)
-            x = self._add_norm(o, pre + "post", residual, self.tp > 1,
-                               consumer=(pre + "gu_w", "silu") if self.cfg.act == "silu" else None)
-            delta, partial = self._ffn(pre, x, fb)
+            route = None
+            if (self.cfg.is_moe and self.tp == 1 and self.cfg.norm == "rms" and isinstance(o, ops.Partial)
+                    and flags.get("BFLY_MOE_NORM_ROUTE")):
+                # the add+RMSNorm routes the rows it normalises (one launch fewer per MoE layer)
+                x, route = ops.rms_norm_route(o, self.p[pre + "post_w"], self.cfg.norm_eps, residual,
+                                              self.p[pre + "router_w"], self.cfg.experts_per_token)
+            else:
+                x = self._add_norm(o, pre + "post", residual, self.tp > 1,
+                                   consumer=(pre + "gu_w", "silu") if self.cfg.act == "silu" else None)
+            delta, partial = self._ffn(pre, x, fb, route)
         return delta, partial
 
     def _attention_block(self, li: int, pre: str, x: torch.Tensor, fb: ForwardBatch,
@@ -498,12 +505,14 @@ class TransformerLM:
             t = self.comm.all_reduce_(t, "tp")
         return self._norm(t, w, b, residual=residual)
 
-    def _ffn(self, pre: str, x: torch.Tensor, fb: ForwardBatch) -> tuple:
+    def _ffn(self, pre: str, x: torch.Tensor, fb: ForwardBatch, route: Optional[tuple] = None) -> tuple:
         """Returns (out, partial): `partial` means `out` still needs the TP all-reduce, which
-        the caller fuses with the next residual add + norm."""
+        the caller fuses with the next residual add + norm. `route`: (gates, topk_ids, topk_w)
+        of a MoE layer already computed by the norm (ops.rms_norm_route)."""
         c, d = self.cfg, self.dims
         if c.is_moe:
-            gates, topk_ids, topk_w = ops.moe_route(x, self.p[pre + "router_w"], c.experts_per_token)
+            gates, topk_ids, topk_w = (route if route is not None else
+                                       ops.moe_route(x, self.p[pre + "router_w"], c.experts_per_token))
             T = x.shape[0]
             # prefill: token-routed sparse experts (K12/K13: only routed rows are computed);
             # decode: dense fixed-shape path (weight-streaming bound either way, graph friendly)
@@ -538,8 +547,11 @@ class TransformerLM:
                 out = ops.moe_sparse_ffn(xs, ids_s, w_s, self.p[pre + "moe_gu_w"], self.p[pre + "moe_down_w"],
                                          d.expert0, d.experts, d.ffn)
             else:
-                hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
-                ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
+                if flags.get("BFLY_MOE_GATE_EPILOGUE"):   # routing weight in the GEMM epilogue
+                    hmid = ops.linear_silu_gate(xs, self.p[pre + "moe_gu_w"], gs, d.expert0, d.experts)
+                else:
+                    hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
+                    ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
                 # one rank: the split-K reduce goes into the next add+RMSNorm, as for dense FFNs
                 out = ops.linear(hmid, self.p[pre + "moe_down_w"], defer=self.defer_reduce and self.ep == 1)
             if self.ep > 1:

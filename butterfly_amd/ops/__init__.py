@@ -278,6 +278,25 @@ def rms_norm(x, w, eps: float, out=None, residual=None, rows: bool = False):
     return out
 
 
+def rms_norm_route(x, w, eps: float, residual, router_w, top_k: int):
+    """The fused add + RMSNorm of a MoE layer's FFN input that also routes the rows it
+    normalises (norm.hip rmsnorm_partial_kernel<NV, 8>): returns (y, (gates, topk_ids, topk_w))
+    as `rms_norm` then `moe_route(y, router_w, top_k)` would, in one launch. Needs a deferred
+    split-K input (`Partial`), a residual and 8 experts; otherwise returns (rms_norm(...), None)
+    and the caller routes separately."""
+    if (isinstance(x, Partial) and residual is not None and router_w.shape[0] == 8
+            and torch.ops.bfly.rms_norm_route_ok(router_w.shape[0], router_w.shape[1]) == 1):
+        T = x.out.shape[0]
+        E = router_w.shape[0]
+        out = _empty_like(x.out)
+        gates = _empty(T, E, dtype=torch.float32, device=out.device)
+        ids = _empty(T, top_k, dtype=torch.int32, device=out.device)
+        tw = _empty(T, top_k, dtype=torch.float32, device=out.device)
+        torch.ops.bfly.rms_norm_partial_route(x.slabs, w, eps, out, residual, router_w, top_k, gates, ids, tw)
+        return out, (gates, ids, tw)
+    return rms_norm(x, w, eps, residual=residual), None
+
+
 def layer_norm(x, w, b, eps: float, out=None, residual=None):
     if not _gpu(x):
         return ref.layer_norm(x, w, b, eps, out, residual)
@@ -468,6 +487,18 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
         torch.ops.bfly.gemm_rs(x, w, out, bias, epi, ws, rn.ssp, rn.eps)
     else:
         torch.ops.bfly.gemm(x, w, out, bias, epi, ws)
+    return out
+
+
+def linear_silu_gate(x, w, gates, e0: int, num_local: int):
+    """The dense MoE decode gate/up GEMM over the concatenated local experts: SwiGLU, then every
+    expert's column block scaled by its routing weight gates[:, e0 + e] — `linear(x, w, 'silu')`
+    followed by `moe_gate_scale_`, bit for bit, in one launch (the tile kernel's epilogue)."""
+    if isinstance(x, RowNormed) or not _gpu(x):
+        h = linear(x, w, epilogue="silu")
+        return moe_gate_scale_(h, gates, e0, num_local)
+    out = _empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
+    torch.ops.bfly.gemm_silu_gate(x, w, out, gates, e0, num_local)
     return out
 
 

@@ -98,6 +98,10 @@ define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism:
        "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
 define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")
 define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped expert GEMMs instead of the dense path")
+define("BFLY_MOE_NORM_ROUTE", True, _bool, "MoE layers at tp = 1: the add+RMSNorm over the O projection's split-K "
+       "slabs also routes the rows (0: separate moe_route launch)")
+define("BFLY_MOE_GATE_EPILOGUE", True, _bool, "dense MoE decode path: the routing weights applied in the gate/up "
+       "GEMM's epilogue (0: separate moe_gate_scale pass)")
 define("BFLY_EP_DECODE_A2A", True, _bool, "EP MoE on decode (and idle) steps: fixed-capacity all-to-all dispatch with "
        "routed-rows-only expert GEMMs, graph-capturable (0: all-gather + dense local experts + reduce-scatter)")
 define("BFLY_EP_IPC", True, _bool, "EP MoE on decode: byte-minimal dispatch / return over peer IPC buffers "

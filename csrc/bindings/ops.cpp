@@ -378,6 +378,30 @@ void gemm(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Ten
   TORCH_CHECK(rc == 0, "gemm: unsupported shape M=", M, " N=", N, " K=", K, " (rc=", rc, ")");
 }
 
+// out[M, N/2] = moe_gate_scale(silu(gate) * up): the dense MoE decode gate/up GEMM over the
+// concatenated local experts with the routing weights gates[M, E] applied in its epilogue.
+void gemm_silu_gate(const Tensor& x, const Tensor& w, Tensor& out, const Tensor& gates, int64_t e0,
+                    int64_t num_local) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_GPU(gates);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "gemm_silu_gate: 2-D operands");
+  CHECK_INNER(x); CHECK_INNER(w); CHECK_INNER(out);
+  CHECK_ALIGN16(x); CHECK_ALIGN16(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 128 == 0, "gemm_silu_gate: shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_silu_gate: row strides % 8");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N / 2, "gemm_silu_gate: out shape");
+  TORCH_CHECK(gates.scalar_type() == at::kFloat && gates.dim() == 2 && gates.is_contiguous() &&
+                  gates.size(0) == M, "gemm_silu_gate: gates [M, E] f32");
+  TORCH_CHECK(num_local > 0 && (N / 2) % num_local == 0 && e0 >= 0 && e0 + num_local <= gates.size(1),
+              "gemm_silu_gate: experts");
+  const int F = (N / 2) / num_local;
+  c10::DeviceGuard g(x.device());
+  const int rc = bfly::launch_gemm_silu_gate(bf(x), x.stride(0), bf(w), w.stride(0), M, N, K, bf(out),
+                                             out.stride(0), gates.data_ptr<float>(), (int)gates.size(1),
+                                             (int)e0, F, cur_stream());
+  TORCH_CHECK(rc == 0, "gemm_silu_gate: unsupported shape M=", M, " N=", N, " K=", K, " F=", F, " (rc=", rc, ")");
+}
+
 // Benchmark / tuning entry: run an explicit plan [kind, mt, nt, wk, bm, bn, sk].
 void gemm_with_plan(const Tensor& x, const Tensor& w, Tensor& out, std::vector<int64_t> plan,
                     int64_t epilogue, const c10::optional<Tensor>& workspace,
@@ -551,6 +575,32 @@ void rms_norm_partial(const Tensor& slabs, const Tensor& w, double eps, Tensor& 
   bfly::launch_rmsnorm(nullptr, dim, res, bf(w), bf(out), dim, rows, dim, (float)eps, res != nullptr,
                        cur_stream(), slabs.data_ptr<float>(), sk);
 }
+
+// rms_norm_partial + MoE routing of the normalised rows (router_w [E, dim], E = 8)
+void rms_norm_partial_route(const Tensor& slabs, const Tensor& w, double eps, Tensor& out, Tensor& residual,
+                            const Tensor& router_w, int64_t top_k, Tensor& gates, Tensor& topk_ids, Tensor& topk_w) {
+  CHECK_GPU(slabs);
+  TORCH_CHECK(slabs.scalar_type() == at::kFloat && slabs.dim() == 3 && slabs.is_contiguous(), "rms_norm_partial_route: slabs");
+  const int sk = slabs.size(0), rows = slabs.size(1), dim = slabs.size(2);
+  CHECK_BF16(w); CHECK_BF16(out); CHECK_BF16(residual); CHECK_BF16(router_w);
+  TORCH_CHECK(dim % 8 == 0 && w.numel() == dim, "rms_norm_partial_route: dim");
+  TORCH_CHECK(out.is_contiguous() && out.size(0) == rows && out.size(1) == dim, "rms_norm_partial_route: out");
+  TORCH_CHECK(residual.is_contiguous() && residual.size(0) == rows && residual.size(1) == dim, "rms_norm_partial_route: residual");
+  const int E = router_w.size(0);
+  TORCH_CHECK(router_w.dim() == 2 && router_w.is_contiguous() && router_w.size(1) == dim, "rms_norm_partial_route: router_w");
+  TORCH_CHECK(gates.scalar_type() == at::kFloat && gates.is_contiguous() && gates.size(0) == rows && gates.size(1) == E,
+              "rms_norm_partial_route: gates");
+  TORCH_CHECK(topk_ids.scalar_type() == at::kInt && topk_w.scalar_type() == at::kFloat && topk_ids.is_contiguous() &&
+                  topk_w.is_contiguous() && topk_ids.size(0) == rows && topk_ids.size(1) == top_k &&
+                  topk_w.size(0) == rows && topk_w.size(1) == top_k, "rms_norm_partial_route: topk");
+  c10::DeviceGuard g(out.device());
+  const int rc = bfly::launch_rmsnorm_route(slabs.data_ptr<float>(), sk, bf(residual), bf(w), bf(out), rows, dim,
+                                            (float)eps, true, bf(router_w), E, (int)top_k, gates.data_ptr<float>(),
+                                            topk_ids.data_ptr<int>(), topk_w.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc == 0, "rms_norm_partial_route: unsupported (E=", E, ", dim=", dim, ", rc=", rc, ")");
+}
+
+int64_t rms_norm_route_ok(int64_t E, int64_t dim) { return E == 8 && dim % 8 == 0 && dim <= 16384 ? 1 : 0; }
 
 int64_t attn_decode_splits(int64_t max_ctx, int64_t part_tokens) {
   return bfly::attn_decode_splits(max_ctx, part_tokens);
@@ -1050,6 +1100,9 @@ TORCH_LIBRARY(bfly, m) {
   m.def("gemm_deferred(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) workspace) -> int");
   m.def("splitk_reduce(Tensor slabs, Tensor(a!) out) -> ()");
   m.def("rms_norm_partial(Tensor slabs, Tensor w, float eps, Tensor(a!) out, Tensor(b!)? residual) -> ()");
+  m.def("rms_norm_partial_route(Tensor slabs, Tensor w, float eps, Tensor(a!) out, Tensor(b!) residual, Tensor router_w, "
+        "int top_k, Tensor(c!) gates, Tensor(d!) topk_ids, Tensor(e!) topk_w) -> ()");
+  m.def("rms_norm_route_ok(int E, int dim) -> int", &rms_norm_route_ok);
   m.def("gemm_slab_offset() -> int", []() -> int64_t { return (int64_t)bfly::gemm_slab_offset_floats(); });
   m.def("gemm_rs(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace, "
         "Tensor ssp, float eps) -> ()");
@@ -1076,6 +1129,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("tkp_select(Tensor top_p, Tensor(a!) ws, int rows, int pass_, int phase) -> ()");
   m.def("tkp_final(Tensor(a!) ws, int rows, Tensor(b!) thresh) -> ()");
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
+  m.def("gemm_silu_gate(Tensor x, Tensor w, Tensor(a!) out, Tensor gates, int e0, int num_local) -> ()");
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace, "
         "Tensor? bias=None) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
@@ -1155,10 +1209,12 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("tkp_select", &tkp_select);
   m.impl("tkp_final", &tkp_final);
   m.impl("gemm", &gemm);
+  m.impl("gemm_silu_gate", &gemm_silu_gate);
   m.impl("gemm_with_plan", &gemm_with_plan);
   m.impl("gemm_deferred", &gemm_deferred);
   m.impl("splitk_reduce", &splitk_reduce);
   m.impl("rms_norm_partial", &rms_norm_partial);
+  m.impl("rms_norm_partial_route", &rms_norm_partial_route);
   m.impl("gemm_rs", &gemm_rs);
   m.impl("gemm_deferred_rs", &gemm_deferred_rs);
   m.impl("rms_norm_rows", &rms_norm_rows);

@@ -68,6 +68,41 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// MoE routing of token t from one wave holding expert `lane`'s router logit (E <= 64 experts,
+// `live` = lane < E): softmax over all experts, top-K by probability (ties to the lowest
+// expert id), the selected weights renormalised to sum 1. Writes gates[t][E] (0 for unselected
+// experts), topk_ids[t][K] and topk_w[t][K]. Shared by moe_route_kernel and the add+RMSNorm
+// that routes the rows it normalises (norm.hip).
+__device__ __forceinline__ void moe_select_topk(float logit, bool live, int lane, int t, int E, int K,
+                                                float* __restrict__ gates, int* __restrict__ topk_ids,
+                                                float* __restrict__ topk_w) {
+  logit = live ? logit : -INFINITY;
+  const float mx = wave_max(logit);
+  float p = live ? __expf(logit - mx) : 0.f;
+  const float den = wave_sum(p);
+  float g = 0.f, sel_sum = 0.f;
+  int my_rank = -1;                     // this expert's position in the top-k (-1: not selected)
+  for (int k = 0; k < K; ++k) {
+    float bv = live ? p : -1.f;
+    int bi = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    sel_sum += bv / den;
+    if (lane == bi) { my_rank = k; g = p / den; p = -1.f; }
+  }
+  if (!live) return;
+  const float w = my_rank >= 0 ? g / sel_sum : 0.f;
+  gates[(long)t * E + lane] = w;
+  if (my_rank >= 0) {
+    topk_ids[(long)t * K + my_rank] = lane;
+    topk_w[(long)t * K + my_rank] = w;
+  }
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;

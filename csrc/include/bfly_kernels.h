@@ -9,14 +9,22 @@ namespace bfly {
 
 typedef __bf16 bf16;
 
-enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_SILU = 2 };
+// EPI_SILU_GATE: the SwiGLU epilogue followed by the MoE dense decode path's routing weight
+// (what moe_gate_scale did as a separate pass): see RowScale::gate.
+enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_SILU = 2, EPI_SILU_GATE = 3 };
 
-// Per-row output scale of a GEMM whose X rows are un-normalised RMSNorm inputs (x * g):
-// row m is multiplied by rsqrt(sum_c ss[m * chunks + c] * inv_dim + eps) before the epilogue.
+// Per-row output scales of the tile / decode-ring / mid-M epilogues.
+// RMSNorm: the X rows are un-normalised RMSNorm inputs (x * g); row m is multiplied by
+// rsqrt(sum_c ss[m * chunks + c] * inv_dim + eps) before the epilogue.
+// MoE gate (EPI_SILU_GATE, tile kernel only): SwiGLU output column f of row m is rounded to
+// bf16, multiplied by gate[m * gld + ge0 + f / gF] and rounded again, bit-identical to the
+// SiLU epilogue followed by moe_gate_scale.
 struct RowScale {
   const float* ss;   // nullptr: no scaling
   int chunks;
   float inv_dim, eps;
+  const float* gate = nullptr;
+  int gld = 0, ge0 = 0, gF = 0;
 };
 
 struct GemmPlan {
@@ -37,6 +45,12 @@ void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w,
 // Row-split add + RMSNorm whose consumer GEMM applies the row scale: writes y = x * w and the
 // partial sums of squares ssp[rows][rmsnorm_rows_chunks(dim)]; pass RowScale{ssp, chunks, 1/dim,
 // eps} to the GEMM that consumes y.
+// launch_rmsnorm over split-K slabs that also routes every normalised row for a MoE layer
+// (router_w [E][dim], E = 8): writes gates [rows][E], topk_ids / topk_w [rows][topk] as
+// launch_moe_route would from y. < 0: unsupported.
+int launch_rmsnorm_route(const float* part, int sk, bf16* residual, const bf16* w, bf16* y, int rows,
+                         int dim, float eps, bool add_residual, const bf16* router_w, int E, int topk,
+                         float* gates, int* topk_ids, float* topk_w, hipStream_t stream);
 int rmsnorm_rows_chunks(int dim);
 int launch_rmsnorm_rows(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y, float* ssp,
                         int rows, int dim, bool add_residual, hipStream_t stream,
@@ -110,6 +124,12 @@ void launch_splitk_reduce(const float* part, int sk, int M, int N, bf16* out, lo
 int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                 const bf16* bias, bf16* out, long ldo, float* ws, size_t ws_bytes,
                 hipStream_t stream, const RowScale* rs = nullptr);
+// out[M, N/2] = gate-scaled SwiGLU (EPI_SILU_GATE) on the tile kernel without split-K: the
+// gate/up GEMM of the dense MoE decode path with moe_gate_scale folded into its epilogue.
+// gates [M][gld] f32; output column f belongs to expert ge0 + f / gF.
+int launch_gemm_silu_gate(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                          bf16* out, long ldo, const float* gates, int gld, int ge0, int gF,
+                          hipStream_t stream);
 
 // attention.hip
 int attn_decode_splits(int max_ctx, int part_tokens);

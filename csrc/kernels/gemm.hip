@@ -333,13 +333,19 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw
       const int n = nw + 16 * j + lc;
       if (pslab) {
         store_slab4(rs, ((m - m0) * N + n) * 4, acc[i][j] * sc[i]);
-      } else if (epi == EPI_SILU) {
+      } else if (epi == EPI_SILU || epi == EPI_SILU_GATE) {
         if constexpr (TJ % 2 == 0) {   // gate/up 16-row groups pair up inside the wave
           if (j & 1) continue;
           f32x4 h;
 #pragma unroll
           for (int r = 0; r < 4; ++r) h[r] = silu(acc[i][j][r] * sc[i]) * (acc[i][j + 1][r] * sc[i]);
-          store_out4(out, ldo, m, nw / 2 + 16 * (j / 2) + lc, h, vec);
+          const int f = nw / 2 + 16 * (j / 2) + lc;
+          if (epi == EPI_SILU_GATE) {   // the 4 columns share an expert (gF % 16 == 0)
+            const float g = rsc.gate[(long)m * rsc.gld + rsc.ge0 + f / rsc.gF];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = bf2f(f2bf(h[r])) * g;
+          }
+          store_out4(out, ldo, m, f, h, vec);
         }
       } else {
         f32x4 v = acc[i][j] * sc[i];
@@ -1685,6 +1691,7 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
                     const RowScale* rs = nullptr) {
   const RowScale rsc = rs ? *rs : RowScale{nullptr, 0, 0.f, 0.f};
   if (rs != nullptr && p.kind != 1 && p.kind != 3 && p.kind != 5 && p.kind != 7) return -4;   // row scale: tile / ring / mid epilogues
+  if (epi == EPI_SILU_GATE && (p.kind != 1 || p.sk != 1)) return -4;   // gate: tile epilogue, no slabs
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
@@ -1920,6 +1927,28 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
   if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
     p.sk = 1;
   return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream, false, false, rs);
+}
+
+// The dense MoE decode path's gate/up GEMM with the routing weight in its epilogue: one launch
+// and one pass over the [M, E * ffn] activation fewer per MoE layer (Mixtral 8x7B B = 64:
+// moe_gate_scale was 6.5 us per layer, profiles/r5_moe/mixtral_prefill_decode_trace.md). The
+// expert GEMM is a weight stream over >= 1792 column tiles, so the tile plan never splits K.
+int launch_gemm_silu_gate(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
+                          bf16* out, long ldo, const float* gates, int gld, int ge0, int gF,
+                          hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (gates == nullptr || gF <= 0 || gF % 16 != 0 || (N / 2) % gF != 0) return -5;
+  GemmPlan p = plan_gemm(M, N, K);
+  if (run_plan(p, nullptr, 0, nullptr, 0, M, N, K, EPI_SILU_GATE, nullptr, nullptr, 0, nullptr, nullptr, true) != 0) {
+    const int bm = M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128;
+    p = GemmPlan{1, 3, 0, bm <= 32 ? 1 : 2, bm, 128, 1};
+  }
+  RowScale rs{nullptr, 0, 0.f, 0.f};
+  rs.gate = gates;
+  rs.gld = gld;
+  rs.ge0 = ge0;
+  rs.gF = gF;
+  return run_plan(p, X, ldx, W, ldw, M, N, K, EPI_SILU_GATE, nullptr, out, ldo, nullptr, stream, false, false, &rs);
 }
 
 }  // namespace bfly

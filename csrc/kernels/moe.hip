@@ -75,32 +75,8 @@ moe_route_kernel(const bf16* __restrict__ x, long x_stride, const bf16* __restri
   __syncthreads();
   if (wv != 0) return;
   const bool live = lane < E;
-  const float logit = live ? red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane] : -INFINITY;
-  const float mx = wave_max(logit);
-  float p = live ? __expf(logit - mx) : 0.f;
-  const float den = wave_sum(p);
-  float g = 0.f, sel_sum = 0.f;
-  int my_rank = -1;                     // this expert's position in the top-k (-1: not selected)
-  for (int k = 0; k < K; ++k) {
-    // arg-max over lanes, ties to the lowest expert id
-    float bv = live ? p : -1.f;
-    int bi = lane;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    sel_sum += bv / den;
-    if (lane == bi) { my_rank = k; g = p / den; p = -1.f; }
-  }
-  if (!live) return;
-  const float w = my_rank >= 0 ? g / sel_sum : 0.f;
-  gates[(long)t * E + lane] = w;
-  if (my_rank >= 0) {
-    topk_ids[(long)t * K + my_rank] = lane;
-    topk_w[(long)t * K + my_rank] = w;
-  }
+  const float logit = live ? red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane] : 0.f;
+  moe_select_topk(logit, live, lane, t, E, K, gates, topk_ids, topk_w);
 }
 
 __global__ void moe_gate_scale_kernel(bf16* __restrict__ h, const float* __restrict__ gates,

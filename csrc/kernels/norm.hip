@@ -73,11 +73,17 @@ rmsnorm_kernel(const bf16* __restrict__ x, long x_stride, bf16* __restrict__ res
 // workgroup's agent-scope release writes back its XCD's L2 and the hand-off crosses XCDs.
 constexpr int kNormPartThreads = 1024;
 
-template <int NV>
+// EC > 0 (MoE layers, EC = number of experts): the workgroup also routes the row it normalised
+// — router logits from the stored bf16 row, then softmax / top-k (moe_select_topk) — which
+// saves the separate moe_route launch per MoE layer (Mixtral 8x7B B = 64: 6.2 us per layer,
+// profiles/r5_moe/mixtral_prefill_decode_trace.md).
+template <int NV, int EC = 0>
 __global__ void __launch_bounds__(kNormPartThreads)
 rmsnorm_partial_kernel(const float* __restrict__ part, int sk, long slab, bf16* __restrict__ residual,
                        const bf16* __restrict__ w, bf16* __restrict__ y, int dim, float eps,
-                       int add_residual) {
+                       int add_residual, const bf16* __restrict__ rw = nullptr, int topk = 0,
+                       float* __restrict__ gates = nullptr, int* __restrict__ topk_ids = nullptr,
+                       float* __restrict__ topk_w = nullptr) {
   __shared__ float red[16];
   const long row = blockIdx.x;
   const int nvec = dim >> 3;
@@ -119,6 +125,9 @@ rmsnorm_partial_kernel(const float* __restrict__ part, int sk, long slab, bf16* 
   const float inv = rsqrtf(ss / (float)dim + eps);
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + row * (long)dim);
+  float racc[EC > 0 ? EC : 1];
+#pragma unroll
+  for (int e = 0; e < (EC > 0 ? EC : 1); ++e) racc[e] = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = threadIdx.x + i * kNormPartThreads;
@@ -128,7 +137,33 @@ rmsnorm_partial_kernel(const float* __restrict__ part, int sk, long slab, bf16* 
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
       yr[c] = o;
+      if constexpr (EC > 0) {
+        bf16x8 rv[EC];   // every expert's router chunk in flight together
+#pragma unroll
+        for (int e = 0; e < EC; ++e) rv[e] = reinterpret_cast<const bf16x8*>(rw + (long)e * dim)[c];
+#pragma unroll
+        for (int e = 0; e < EC; ++e)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) racc[e] += bf2f(o[j]) * bf2f(rv[e][j]);
+      }
     }
+  }
+  if constexpr (EC > 0) {
+    __shared__ float rred[kNormPartThreads / 64][EC];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < EC; ++e) {
+      const float s = wave_sum(racc[e]);
+      if (lane == 0) rred[wv][e] = s;
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    const bool live = lane < EC;
+    float logit = 0.f;
+    if (live)
+#pragma unroll
+      for (int q = 0; q < kNormPartThreads / 64; ++q) logit += rred[q][lane];
+    moe_select_topk(logit, live, lane, (int)row, EC, topk, gates, topk_ids, topk_w);
   }
 }
 
@@ -294,6 +329,25 @@ void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w,
     case 4: rmsnorm_kernel<4><<<grid, block, 0, stream>>>(x, x_stride, residual, w, y, y_stride, dim, eps, ar); break;
     default: rmsnorm_kernel<kNormMaxVec><<<grid, block, 0, stream>>>(x, x_stride, residual, w, y, y_stride, dim, eps, ar); break;
   }
+}
+
+int launch_rmsnorm_route(const float* part, int sk, bf16* residual, const bf16* w, bf16* y, int rows,
+                         int dim, float eps, bool add_residual, const bf16* router_w, int E, int topk,
+                         float* gates, int* topk_ids, float* topk_w, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (part == nullptr || E != 8 || topk < 1 || topk > E || dim % 8 != 0) return -1;
+  const long slab = (long)rows * dim;
+  const int nv = (dim / 8 + kNormPartThreads - 1) / kNormPartThreads;
+  const int ar = add_residual ? 1 : 0;
+  if (nv <= 1)
+    rmsnorm_partial_kernel<1, 8><<<rows, kNormPartThreads, 0, stream>>>(part, sk, slab, residual, w, y, dim, eps, ar,
+                                                                       router_w, topk, gates, topk_ids, topk_w);
+  else if (nv <= 2)
+    rmsnorm_partial_kernel<2, 8><<<rows, kNormPartThreads, 0, stream>>>(part, sk, slab, residual, w, y, dim, eps, ar,
+                                                                       router_w, topk, gates, topk_ids, topk_w);
+  else
+    return -2;
+  return 0;
 }
 
 void launch_layernorm(const bf16* x, bf16* residual, const bf16* w, const bf16* b, bf16* y,

@@ -352,6 +352,67 @@ def test_moe_route_and_gate_scale():
     _close(h, h2, 1e-2, 1e-2)
 
 
+@pytest.mark.parametrize("T,dim,sk,k", [(64, 4096, 4, 2), (37, 4096, 1, 2), (5, 8192, 3, 1), (130, 1024, 2, 3)])
+def test_rms_norm_route_equals_norm_then_route(T, dim, sk, k):
+    """ops.rms_norm_route (the add+RMSNorm over split-K slabs that also routes its rows for a
+    MoE layer): the normalised rows and the residual are bit-identical to rms_norm_partial, and
+    gates / top-k match moe_route on those rows (same softmax / top-k code; the router dot
+    products sum in a different order, so gates agree to f32 rounding and the chosen experts
+    are the same unless two probabilities tie to within it)."""
+    slabs = (torch.randn(sk, T, dim, generator=torch.Generator().manual_seed(80)) * 0.5).to(DEV)
+    res0 = _bf(T, dim, seed=81)
+    w = (1.0 + 0.1 * _bf(dim, seed=82).float()).to(torch.bfloat16)
+    wr = _bf(8, dim, scale=0.05, seed=83)
+    part = ops.Partial(slabs, torch.empty(T, dim, dtype=torch.bfloat16, device=DEV))
+    res_a = res0.clone()
+    y, route = ops.rms_norm_route(part, w, 1e-5, res_a, wr, k)
+    assert route is not None
+    gates, ids, tw = route
+    res_b = res0.clone()
+    y_ref = ops.rms_norm(part, w, 1e-5, residual=res_b)
+    assert torch.equal(y, y_ref) and torch.equal(res_a, res_b)
+    g2, ids2, tw2 = ops.moe_route(y_ref, wr, k)
+    _close(gates, g2, 1e-5, 1e-4)
+    _close(tw, tw2, 1e-5, 1e-4)
+    p = torch.softmax((y_ref.float() @ wr.float().t()), dim=-1).cpu()
+    srt = p.sort(dim=-1, descending=True).values
+    clear = (srt[:, k - 1] - srt[:, k]) > 1e-4          # no near-tie at the top-k boundary
+    assert clear.sum() >= T // 2
+    assert torch.equal(ids.cpu()[clear].sort(dim=-1).values, ids2.cpu()[clear].sort(dim=-1).values)
+
+
+@pytest.mark.parametrize("M,El,e0,E,H,F", [(64, 8, 0, 8, 512, 256), (37, 3, 2, 8, 256, 128), (130, 2, 0, 4, 1024, 512),
+                                           (16, 4, 4, 8, 512, 64), (64, 1, 3, 8, 4096, 14336)])
+def test_gate_scaled_silu_epilogue(M, El, e0, E, H, F):
+    """ops.linear_silu_gate (the routing weight applied in the tile kernel's SwiGLU epilogue,
+    EPI_SILU_GATE) is bit-identical to the same plan's SiLU GEMM followed by moe_gate_scale,
+    and matches the fp32 reference; zero gates (unselected experts) give exact zeros. The last
+    case is one Mixtral 8x7B expert at the decode batch."""
+    x, w = _bf(M, H, seed=70), _bf(2 * El * F, H, scale=0.05, seed=71)
+    g = torch.Generator(device="cpu").manual_seed(72)
+    gates = torch.rand(M, E, generator=g)
+    gates[torch.rand(M, E, generator=g) < 0.5] = 0.0
+    gates = gates.to(DEV)
+    N, K = w.shape[0], H
+    got = ops.linear_silu_gate(x, w, gates, e0, El)
+    p = ops.gemm_plan(M, N, K)
+    if p["kind"] == "tile" and p["splitk"] == 1:
+        plan = [1, p["mt"], p["nt"], p["wk"], p["bm"], p["bn"], 1]
+    else:
+        bm = 16 if M <= 16 else 32 if M <= 32 else 64 if M <= 64 else 128
+        plan = [1, 3, 0, 1 if bm <= 32 else 2, bm, 128, 1]
+    base = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+    torch.ops.bfly.gemm_with_plan(x, w, base, plan, ops.EPILOGUES["silu"], None)
+    ops.moe_gate_scale_(base, gates, e0, El)
+    assert torch.equal(got, base)
+    want = ref.linear(x.cpu(), w.cpu(), None, "silu")
+    ref.moe_gate_scale(want, gates.cpu(), e0, El)
+    _close(got, want, 2e-2, 2e-2)
+    cols = torch.arange(N // 2) // F + e0
+    off = (gates.cpu()[:, cols] == 0)
+    assert (got.cpu()[off] == 0).all()
+
+
 @pytest.mark.parametrize("M,N,K", [(600, 512, 1024), (256, 768, 192), (77, 256, 128), (1000, 1280, 4096),
                                    (300, 512, 256), (520, 512, 128)])
 @pytest.mark.parametrize("kind", [4, 6])
