@@ -280,11 +280,11 @@ def rms_norm(x, w, eps: float, out=None, residual=None, rows: bool = False):
 
 def rms_norm_route(x, w, eps: float, residual, router_w, top_k: int):
     """The fused add + RMSNorm of a MoE layer's FFN input that also routes the rows it
-    normalises (norm.hip rmsnorm_partial_kernel<NV, 8>): returns (y, (gates, topk_ids, topk_w))
+    normalises (norm.hip rmsnorm_partial_kernel<NV, E>): returns (y, (gates, topk_ids, topk_w))
     as `rms_norm` then `moe_route(y, router_w, top_k)` would, in one launch. Needs a deferred
-    split-K input (`Partial`), a residual and 8 experts; otherwise returns (rms_norm(...), None)
-    and the caller routes separately."""
-    if (isinstance(x, Partial) and residual is not None and router_w.shape[0] == 8
+    split-K input (`Partial`), a residual and 4 or 8 experts; otherwise returns (rms_norm(...),
+    None) and the caller routes separately."""
+    if (isinstance(x, Partial) and residual is not None
             and torch.ops.bfly.rms_norm_route_ok(router_w.shape[0], router_w.shape[1]) == 1):
         T = x.out.shape[0]
         E = router_w.shape[0]

@@ -576,7 +576,7 @@ void rms_norm_partial(const Tensor& slabs, const Tensor& w, double eps, Tensor& 
                        cur_stream(), slabs.data_ptr<float>(), sk);
 }
 
-// rms_norm_partial + MoE routing of the normalised rows (router_w [E, dim], E = 8)
+// rms_norm_partial + MoE routing of the normalised rows (router_w [E, dim], E = 4 or 8)
 void rms_norm_partial_route(const Tensor& slabs, const Tensor& w, double eps, Tensor& out, Tensor& residual,
                             const Tensor& router_w, int64_t top_k, Tensor& gates, Tensor& topk_ids, Tensor& topk_w) {
   CHECK_GPU(slabs);
@@ -600,7 +600,7 @@ void rms_norm_partial_route(const Tensor& slabs, const Tensor& w, double eps, Te
   TORCH_CHECK(rc == 0, "rms_norm_partial_route: unsupported (E=", E, ", dim=", dim, ", rc=", rc, ")");
 }
 
-int64_t rms_norm_route_ok(int64_t E, int64_t dim) { return E == 8 && dim % 8 == 0 && dim <= 16384 ? 1 : 0; }
+int64_t rms_norm_route_ok(int64_t E, int64_t dim) { return (E == 4 || E == 8) && dim % 8 == 0 && dim <= 16384 ? 1 : 0; }
 
 int64_t attn_decode_splits(int64_t max_ctx, int64_t part_tokens) {
   return bfly::attn_decode_splits(max_ctx, part_tokens);

@@ -42,15 +42,15 @@ struct GemmPlan {
 void launch_rmsnorm(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y,
                     long y_stride, int rows, int dim, float eps, bool add_residual,
                     hipStream_t stream, const float* part = nullptr, int sk = 0);
-// Row-split add + RMSNorm whose consumer GEMM applies the row scale: writes y = x * w and the
-// partial sums of squares ssp[rows][rmsnorm_rows_chunks(dim)]; pass RowScale{ssp, chunks, 1/dim,
-// eps} to the GEMM that consumes y.
 // launch_rmsnorm over split-K slabs that also routes every normalised row for a MoE layer
-// (router_w [E][dim], E = 8): writes gates [rows][E], topk_ids / topk_w [rows][topk] as
+// (router_w [E][dim], E = 4 or 8): writes gates [rows][E], topk_ids / topk_w [rows][topk] as
 // launch_moe_route would from y. < 0: unsupported.
 int launch_rmsnorm_route(const float* part, int sk, bf16* residual, const bf16* w, bf16* y, int rows,
                          int dim, float eps, bool add_residual, const bf16* router_w, int E, int topk,
                          float* gates, int* topk_ids, float* topk_w, hipStream_t stream);
+// Row-split add + RMSNorm whose consumer GEMM applies the row scale: writes y = x * w and the
+// partial sums of squares ssp[rows][rmsnorm_rows_chunks(dim)]; pass RowScale{ssp, chunks, 1/dim,
+// eps} to the GEMM that consumes y.
 int rmsnorm_rows_chunks(int dim);
 int launch_rmsnorm_rows(const bf16* x, long x_stride, bf16* residual, const bf16* w, bf16* y, float* ssp,
                         int rows, int dim, bool add_residual, hipStream_t stream,

@@ -335,18 +335,21 @@ int launch_rmsnorm_route(const float* part, int sk, bf16* residual, const bf16* 
                          int dim, float eps, bool add_residual, const bf16* router_w, int E, int topk,
                          float* gates, int* topk_ids, float* topk_w, hipStream_t stream) {
   if (rows <= 0) return 0;
-  if (part == nullptr || E != 8 || topk < 1 || topk > E || dim % 8 != 0) return -1;
+  if (part == nullptr || (E != 4 && E != 8) || topk < 1 || topk > E || dim % 8 != 0) return -1;
   const long slab = (long)rows * dim;
   const int nv = (dim / 8 + kNormPartThreads - 1) / kNormPartThreads;
+  if (nv > 2) return -2;
   const int ar = add_residual ? 1 : 0;
-  if (nv <= 1)
-    rmsnorm_partial_kernel<1, 8><<<rows, kNormPartThreads, 0, stream>>>(part, sk, slab, residual, w, y, dim, eps, ar,
-                                                                       router_w, topk, gates, topk_ids, topk_w);
-  else if (nv <= 2)
-    rmsnorm_partial_kernel<2, 8><<<rows, kNormPartThreads, 0, stream>>>(part, sk, slab, residual, w, y, dim, eps, ar,
-                                                                       router_w, topk, gates, topk_ids, topk_w);
-  else
-    return -2;
+#define NORM_ROUTE(NV_, EC_)                                                                          \
+  rmsnorm_partial_kernel<NV_, EC_><<<rows, kNormPartThreads, 0, stream>>>(part, sk, slab, residual, w, y, dim, \
+                                                                         eps, ar, router_w, topk, gates,   \
+                                                                         topk_ids, topk_w)
+  if (E == 8) {
+    if (nv <= 1) NORM_ROUTE(1, 8); else NORM_ROUTE(2, 8);
+  } else {
+    if (nv <= 1) NORM_ROUTE(1, 4); else NORM_ROUTE(2, 4);
+  }
+#undef NORM_ROUTE
   return 0;
 }
 

@@ -352,8 +352,9 @@ def test_moe_route_and_gate_scale():
     _close(h, h2, 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("T,dim,sk,k", [(64, 4096, 4, 2), (37, 4096, 1, 2), (5, 8192, 3, 1), (130, 1024, 2, 3)])
-def test_rms_norm_route_equals_norm_then_route(T, dim, sk, k):
+@pytest.mark.parametrize("T,dim,sk,k,E", [(64, 4096, 4, 2, 8), (37, 4096, 1, 2, 8), (5, 8192, 3, 1, 8), (130, 1024, 2, 3, 8),
+                                         (40, 256, 2, 2, 4)])
+def test_rms_norm_route_equals_norm_then_route(T, dim, sk, k, E):
     """ops.rms_norm_route (the add+RMSNorm over split-K slabs that also routes its rows for a
     MoE layer): the normalised rows and the residual are bit-identical to rms_norm_partial, and
     gates / top-k match moe_route on those rows (same softmax / top-k code; the router dot
@@ -362,7 +363,7 @@ def test_rms_norm_route_equals_norm_then_route(T, dim, sk, k):
     slabs = (torch.randn(sk, T, dim, generator=torch.Generator().manual_seed(80)) * 0.5).to(DEV)
     res0 = _bf(T, dim, seed=81)
     w = (1.0 + 0.1 * _bf(dim, seed=82).float()).to(torch.bfloat16)
-    wr = _bf(8, dim, scale=0.05, seed=83)
+    wr = _bf(E, dim, scale=0.05, seed=83)
     part = ops.Partial(slabs, torch.empty(T, dim, dtype=torch.bfloat16, device=DEV))
     res_a = res0.clone()
     y, route = ops.rms_norm_route(part, w, 1e-5, res_a, wr, k)
