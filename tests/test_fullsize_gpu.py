@@ -1,5 +1,5 @@
-"""End to end at the BENCH dimensions: the Llama-3-70B and Llama-3-8B
-presets cut to 2 layers (every projection, the 128k-vocab embedding and LM head at full size),
+"""End to end at the BENCH dimensions: the Llama-3-70B, Llama-3-8B and
+Mixtral 8x7B presets cut to 2 layers (every projection, the 128k-vocab embedding and LM head at full size),
 with the production kernels the benchmark runs:
 
 * prefill of 64 prompts x 128 tokens = 8192 rows through the 256x256 8-phase GEMMs and the
@@ -9,6 +9,12 @@ with the production kernels the benchmark runs:
 * a B = 64 decode step (the bench's batch) through the split-K decode GEMMs, the row-split
   add+RMSNorm and the paged decode attention, eager against the reference, and hipGraph replay
   bitwise against eager.
+
+Mixtral runs the token-routed grouped expert GEMMs in prefill and, in decode, the dense expert
+path with routing inside the add+RMSNorm and the routing weight in the gate/up GEMM epilogue.
+Routing is a discrete choice: a token whose top-2 experts nearly tie can pick another expert in
+bf16 than in fp32, so for MoE presets 90 % of the rows must match individually (a flip changes
+one token's row, not the others), each within 2.5x the dense bound.
 """
 import dataclasses
 
@@ -30,6 +36,20 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm()).item()
 
 
+def _check(a, b, tol, moe):
+    if not moe:
+        rel = _rel(a, b)
+        assert rel < tol, f"logits rel err {rel:.3e}"
+        return
+    # per-row bf16 noise through the expert GEMMs is ~2 % here (median row error 2.2e-2 in the
+    # prefill of the first run), so the per-row bound is 2.5x the dense presets' whole-matrix bound
+    a, b = a.float(), b.float()
+    rows = (a - b).norm(dim=-1) / b.norm(dim=-1)
+    ok = (rows < 2.5 * tol).float().mean().item()
+    print(f"moe logits: median row rel err {rows.median().item():.3e}, {ok:.0%} within {2.5 * tol}")
+    assert ok >= 0.9, f"only {ok:.0%} of rows within {2.5 * tol} (median {rows.median().item():.3e})"
+
+
 def _models(preset):
     cfg = dataclasses.replace(ModelConfig.from_preset(preset), num_layers=2)
     g = build_model(cfg, device="cuda", dtype=torch.bfloat16)
@@ -41,7 +61,7 @@ def _models(preset):
     return cfg, g, r
 
 
-@pytest.mark.parametrize("preset", ["llama3-8b", "llama3-70b"])
+@pytest.mark.parametrize("preset", ["llama3-8b", "llama3-70b", "mixtral-8x7b"])
 def test_bench_dims_prefill_decode_and_graph(preset):
     cfg, g, r = _models(preset)
     V = cfg.vocab_size
@@ -62,8 +82,7 @@ def test_bench_dims_prefill_decode_and_graph(preset):
         lr = r.forward(fb, kr)
     torch.cuda.synchronize()
     assert lg.shape[0] == B
-    rel = _rel(lg[:, :V], lr[:, :V])
-    assert rel < 2e-2, f"prefill logits rel err {rel:.3e}"
+    _check(lg[:, :V], lr[:, :V], 2e-2, cfg.is_moe)
 
     toks = [int(t) for t in lr[:, :V].argmax(-1)]
     pos = [P] * B
@@ -75,8 +94,7 @@ def test_bench_dims_prefill_decode_and_graph(preset):
     with ops.reference_mode():
         dr = r.forward(db, kr)
     torch.cuda.synchronize()
-    rel = _rel(dg[:, :V], dr[:, :V])
-    assert rel < 3e-2, f"decode logits rel err {rel:.3e}"
+    _check(dg[:, :V], dr[:, :V], 3e-2, cfg.is_moe)
 
     # hipGraph replay of the same decode step: bitwise the eager logits and cache writes
     for (k, v), (k0, v0) in zip(kg, kg_snapshot):
