@@ -25,6 +25,9 @@ INSITU = {
     (14336, 8192, 256): ([7, 3, 4, 0, 256, 128, 2],
                          "tp4 shard step in situ: 19.67 ms with this plan (profiles/r6_gemm/shard_after_table.jsonl) vs "
                          "20.32 ms with big4 sk4 (profiles/r6_gemm/shard_bias_aware_table.jsonl)"),
+    (4096, 114688, 64): ([1, 2, 0, 1, 64, 128, 16],
+                         "Mixtral dense expert down, in situ: 17.70-17.85 vs 18.30-18.38 ms/step "
+                         "(profiles/r6_moe/down_plan_insitu.log)"),
 }
 
 
@@ -134,6 +137,11 @@ def main():
         lines.append(f"{{{N}, {K}, {M}, {', '.join(str(int(v)) for v in best_pl)}}},  // {meas[key]['shape']}: "
                      f"{best_us:.1f} us vs {h_us if h_us is not None else float('nan'):.1f}")
         n += 1
+    # in-situ choices for shapes no serialised sweep covered (e.g. the Mixtral expert GEMMs)
+    for (N, K, M), (pl, note) in INSITU.items():
+        if (N, K, M) not in meas:
+            lines.append(f"{{{N}, {K}, {M}, {', '.join(str(v) for v in pl)}}},  // {note}")
+            n += 1
     n += apply_event_sweeps(lines, meas)
     out = os.path.join(ROOT, "csrc", "kernels", "gemm_tuned.inc")
     with open(out, "w") as fh:
