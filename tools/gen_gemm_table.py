@@ -17,8 +17,9 @@ MARGIN = 0.03
 # Plans chosen by in-situ whole-step A/B runs (BFLY_GEMM_PLAN overrides through tools/gpu_run.sh bench steps) over the isolated sweep's
 # winner: {(N, K, M): ([kind, mt, nt, wk, bm, bn, sk], note)}
 INSITU = {
-    (8192, 28672, 64): ([3, 6, 8, 4, 64, 128, 4],
-                        "in situ: 29.72-29.87 vs 29.90-30.02 ms/step, profiles/r2_decode_gemm_down_sk4_insitu.log"),
+    (8192, 28672, 64): ([1, 3, 0, 1, 64, 256, 8],
+                        "in situ (round 6, alternating runs): 28.92-29.13 vs 29.27-29.34 ms/step with the round-2 "
+                        "decode ring [3,6,8,4,64,128,4], profiles/r6_gemm/down_m64_insitu.log"),
     (10240, 8192, 64): ([1, 3, 0, 2, 64, 128, 3],
                         "in situ 29.22-29.37 vs 29.66 ms/step (240 workgroups, one per CU; smaller slabs for rope_kv), "
                         "profiles/r3_decode_qkv_sk3_insitu.log"),
