@@ -26,6 +26,9 @@ INSITU = {
     (14336, 8192, 256): ([7, 3, 4, 0, 256, 128, 2],
                          "tp4 shard step in situ: 19.67 ms with this plan (profiles/r6_gemm/shard_after_table.jsonl) vs "
                          "20.32 ms with big4 sk4 (profiles/r6_gemm/shard_bias_aware_table.jsonl)"),
+    (7168, 8192, 512): ([6, 0, 0, 0, 256, 256, 4],
+                        "tp8 shard step in situ, alternating runs: 17.45-17.62 vs 17.77-17.85 ms with the mid4 "
+                        "[7,4,3,0,128,256,2] (profiles/r6_gemm/tp8_gate_up_insitu.log)"),
     (4096, 114688, 64): ([1, 2, 0, 1, 64, 128, 16],
                          "Mixtral dense expert down, in situ: 17.70-17.85 vs 18.30-18.38 ms/step "
                          "(profiles/r6_moe/down_plan_insitu.log)"),
