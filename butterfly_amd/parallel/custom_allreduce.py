@@ -112,6 +112,12 @@ class CustomAllReduce:
         dist.all_gather_object(handles, (handle, me, device_identity(me)), group=pg)
         devs = [d for _, d, _ in handles]
         refusal = shared_device_refusal([i for _, _, i in handles], "custom all-reduce")
+        # ranks sharing one GPU (tests): a smaller grid per rank, so the spinning workgroups of the
+        # ranks that arrive first cannot hold every CU while a late rank still has to run a
+        # one-workgroup-per-CU GEMM before it reaches the rendezvous (seen as a 20 s flag-wait
+        # timeout in the 4-rank production-dims test); the same on every rank
+        shared = len({i for _, _, i in handles}) < len(handles)
+        self.blocks = max(1, 128 // self.world) if shared else 128
         handles = [h for h, _, _ in handles]
         local_ok = all(h is not None for h in handles)
         if refusal:
@@ -166,10 +172,11 @@ class CustomAllReduce:
         if isinstance(t, ops.Partial):
             two = self.use_two_shot(t.out) if two_shot is None else two_shot
             torch.ops.bfly.custom_all_reduce(t.out, t.out, None, None, 0.0, self.bases, self.rank, self.cap,
-                                             t.slabs, two)
+                                             t.slabs, two, self.blocks)
             return t.out
         two = self.use_two_shot(t) if two_shot is None else two_shot
-        torch.ops.bfly.custom_all_reduce(t, t, None, None, 0.0, self.bases, self.rank, self.cap, None, two)
+        torch.ops.bfly.custom_all_reduce(t, t, None, None, 0.0, self.bases, self.rank, self.cap, None, two,
+                                         self.blocks)
         return t
 
     def all_reduce_rms_norm_(self, t, w: torch.Tensor, eps: float,
@@ -182,7 +189,7 @@ class CustomAllReduce:
         if out is None:
             out = torch.empty_like(t)
         torch.ops.bfly.custom_all_reduce(t, out, residual, w, float(eps), self.bases, self.rank, self.cap, slabs,
-                                         self.use_two_shot(t))
+                                         self.use_two_shot(t), self.blocks)
         return out
 
     def autotune(self, pg, rccl_all_reduce, sizes=(32 << 10, 128 << 10, 512 << 10, 2 << 20, 8 << 20),

@@ -925,7 +925,7 @@ void car_clear_error(int64_t p) {
 void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tensor>& residual,
                        const c10::optional<Tensor>& w, double eps, at::IntArrayRef bases,
                        int64_t rank, int64_t cap, const c10::optional<Tensor>& slabs,
-                       bool two_shot) {
+                       bool two_shot, int64_t blocks) {
   CHECK_GPU(inp); CHECK_BF16(inp); CHECK_BF16(out);
   TORCH_CHECK(inp.dim() == 2 && inp.is_contiguous() && out.is_contiguous() &&
                   out.sizes() == inp.sizes(), "custom_all_reduce: 2-D contiguous, same shape");
@@ -968,7 +968,7 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, const c10::optional<Tenso
   c10::DeviceGuard g(inp.device());
   const int rc = bfly::launch_custom_allreduce(bf(inp), bf(out), res, wp, (float)eps, rows, dim,
                                                peers, world, (int)rank, cap, cur_stream(), sp, sk,
-                                               two_shot);
+                                               two_shot, (int)blocks);
   TORCH_CHECK(rc == 0, "custom_all_reduce: launch rejected (", rc, ")");
 }
 
@@ -1167,7 +1167,7 @@ TORCH_LIBRARY(bfly, m) {
   m.def("car_clear_error(int ptr) -> ()", &car_clear_error);
   m.def("car_buffer_bytes(int cap) -> int", [](int64_t cap) -> int64_t { return bfly::car_buffer_bytes(cap); });
   m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, Tensor(b!)? residual, Tensor? w, float eps, "
-        "int[] bases, int rank, int cap, Tensor? slabs=None, bool two_shot=False) -> ()");
+        "int[] bases, int rank, int cap, Tensor? slabs=None, bool two_shot=False, int blocks=128) -> ()");
   m.def("ep_ipc_layout(int ep, int capmax, int H, int K) -> int[]", &ep_ipc_layout);
   m.def("ep_ipc_view(int ptr, int offset, int rows, int cols, int dtype, int device) -> Tensor", &ep_ipc_view);
   m.def("ep_ipc_dispatch(Tensor x, Tensor ids, Tensor w, Tensor? slots, int experts_per_rank, int capmax, "

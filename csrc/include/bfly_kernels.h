@@ -170,10 +170,14 @@ void health_clear(int word = -1);   // one word (kHealthCar / kHealthEp) or, -1,
 // flags/counters, two input buffers and two reduced-chunk buffers (two-shot), all double-buffered
 inline long car_buffer_bytes(long cap) { return kArDataOff + 4 * cap; }
 // `slabs` (optional): the input is split-K partials [sk][rows][dim] f32, reduced in the publish.
+// `blocks`: the grid (<= kArBlocks), the same on every rank and for every call of a communicator:
+// kArBlocks on a node (one rank per GPU); kArBlocks / world for ranks that share one GPU (tests),
+// so the waves of ranks that arrived first and spin on their peers' flags can never occupy every
+// CU — a late rank's one-workgroup-per-CU GEMM must still find CUs to run on.
 int launch_custom_allreduce(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
                             int rows, int dim, const ArPeers& peers, int world, int rank,
                             long cap, hipStream_t stream, const float* slabs = nullptr, int sk = 0,
-                            bool two_shot = false);
+                            bool two_shot = false, int blocks = kArBlocks);
 void* car_alloc(size_t bytes);
 void car_free(void* p);
 int car_ipc_handle(void* p, unsigned char* out64);

@@ -17,8 +17,10 @@
 //   [64 KiB, +2*cap)  two data buffers; epoch parity selects one (double buffering)
 //   [+2*cap, +4*cap)  two reduced-chunk buffers (two-shot)
 //
-// Protocol for workgroup b (grid is ALWAYS kArBlocks, so row r is always owned by block
-// r % kArBlocks and its epoch advances by one per call on every rank):
+// Protocol for workgroup b of a grid of G <= kArBlocks workgroups (G is fixed for the life of a
+// communicator and equal on every rank, so row r is always owned by block r % G and its epoch
+// advances by one per call on every rank; G = kArBlocks, or kArBlocks / world when the ranks
+// share one GPU — see launch_custom_allreduce):
 //   e = cnt[b] + 1                       (device-resident, so graph replays stay in sync)
 //   stage own rows into data[e & 1]; fence(system); barrier
 //   thread p < W: store e into flags of peer p at [b][rank]  (release, system scope)
@@ -97,7 +99,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
                  int rank, long cap, const float* __restrict__ slabs, int sk) {
   __shared__ uint32_t s_epoch;
   __shared__ float red[16];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, nblk = gridDim.x;
   char* my = peers.base[rank];
   uint32_t* cnt = reinterpret_cast<uint32_t*>(my + kArCntOff);
   if (threadIdx.x == 0) s_epoch = cnt[b] + 1;
@@ -111,7 +113,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
   // have written) is fused into the publish, and the local operand is read back from `mine`.
   bf16* mine = reinterpret_cast<bf16*>(my + data_off);
   const long slab = (long)rows * dim;
-  for (int r = b; r < rows; r += kArBlocks) {
+  for (int r = b; r < rows; r += nblk) {
     bf16x8* dst = reinterpret_cast<bf16x8*>(mine + (long)r * dim);
     if (slabs != nullptr) {
       for (int c = threadIdx.x; c < nvec; c += kArThreads) {
@@ -150,7 +152,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
     const long red_off = kArDataOff + 2 * cap + (long)(e & 1) * cap;
     const int per = nvec / W, c0 = rank * per;
     bf16* red_mine = reinterpret_cast<bf16*>(my + red_off);
-    for (int r = b; r < rows; r += kArBlocks) {
+    for (int r = b; r < rows; r += nblk) {
       const long ro = (long)r * dim;
       for (int c = c0 + threadIdx.x; c < c0 + per; c += kArThreads) {
         bf16x8 v[W];
@@ -177,7 +179,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
     // 3b. all-gather: chunk q of every row comes from rank q's reduced buffer
 #pragma unroll
     for (int p = 0; p < W; ++p) src[p] = reinterpret_cast<const bf16*>(peers.base[p] + red_off);
-    for (int r = b; r < rows; r += kArBlocks) {
+    for (int r = b; r < rows; r += nblk) {
       const long ro = (long)r * dim;
       if constexpr (MODE == 0) {
         for (int c = threadIdx.x; c < nvec; c += kArThreads)
@@ -229,7 +231,7 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
     if (threadIdx.x == 0) cnt[b] = e;
     return;
   }
-  for (int r = b; r < rows; r += kArBlocks) {
+  for (int r = b; r < rows; r += nblk) {
     const long ro = (long)r * dim;
     if constexpr (MODE == 0) {
       // U vectors per thread per round, all peers' loads issued before the first store (the
@@ -331,8 +333,8 @@ allreduce_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, bf16* __re
 template <int W, bool TWO>
 int launch_w(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps, int rows,
              int dim, const ArPeers& peers, int rank, long cap, const float* slabs, int sk,
-             hipStream_t stream) {
-  const dim3 grid(kArBlocks), block(kArThreads);
+             int blocks, hipStream_t stream) {
+  const dim3 grid(blocks), block(kArThreads);
   if (residual == nullptr) {
     allreduce_kernel<W, 0, 1, TWO><<<grid, block, 0, stream>>>(in, out, nullptr, nullptr, 0.f, rows,
                                                                dim, peers, rank, cap, slabs, sk);
@@ -356,25 +358,27 @@ int launch_w(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps
 template <int W>
 int launch_mode(bool two, const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
                 int rows, int dim, const ArPeers& peers, int rank, long cap, const float* slabs,
-                int sk, hipStream_t stream) {
-  if (two) return launch_w<W, true>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
-  return launch_w<W, false>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+                int sk, int blocks, hipStream_t stream) {
+  if (two) return launch_w<W, true>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, blocks, stream);
+  return launch_w<W, false>(in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, blocks, stream);
 }
 
 }  // namespace
 
 int launch_custom_allreduce(const bf16* in, bf16* out, bf16* residual, const bf16* w, float eps,
                             int rows, int dim, const ArPeers& peers, int world, int rank,
-                            long cap, hipStream_t stream, const float* slabs, int sk, bool two_shot) {
+                            long cap, hipStream_t stream, const float* slabs, int sk, bool two_shot,
+                            int blocks) {
   if (dim % 8 != 0 || dim > 16384 || rows < 0) return -2;
+  if (blocks < 1 || blocks > kArBlocks) return -8;
   if (slabs != nullptr && sk < 1) return -6;
   if ((long)rows * dim * 2 > cap) return -3;
   if (rank < 0 || rank >= world) return -4;
   if (two_shot && (dim / 8) % world != 0) return -7;   // column chunks of whole 16-B vectors
   switch (world) {
-    case 2: return launch_mode<2>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
-    case 4: return launch_mode<4>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
-    case 8: return launch_mode<8>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, stream);
+    case 2: return launch_mode<2>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, blocks, stream);
+    case 4: return launch_mode<4>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, blocks, stream);
+    case 8: return launch_mode<8>(two_shot, in, out, residual, w, eps, rows, dim, peers, rank, cap, slabs, sk, blocks, stream);
     default: return -5;
   }
 }
