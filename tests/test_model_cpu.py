@@ -104,3 +104,29 @@ def test_paged_prefill_reference_equals_flash_over_the_whole_prompt():
                                  i32(list(range(st, L))), L - st, scale)
     want = ref.attn_prefill(q, k, v, i32([0, L]), L, scale, True)[st:]
     torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-5)
+
+
+def test_moe_decode_fusion_entry_points_fall_back_on_cpu():
+    """ops.linear_silu_gate and ops.rms_norm_route (the MoE decode fusions: routing weight in
+    the gate/up GEMM epilogue, routing inside the add+RMSNorm) equal their two-op forms on CPU
+    tensors, where no fused kernel exists; rms_norm_route without a deferred split-K input
+    routes nothing (the caller calls moe_route)."""
+    from butterfly_amd import ops
+    from butterfly_amd.ops import reference as ref
+
+    g = torch.Generator().manual_seed(7)
+    T, H, F, El, E, e0 = 5, 64, 32, 2, 4, 1
+    x = torch.randn(T, H, generator=g)
+    w = torch.randn(2 * El * F, H, generator=g) * 0.1
+    gates = torch.rand(T, E, generator=g)
+    got = ops.linear_silu_gate(x, w, gates, e0, El)
+    want = ref.linear(x, w, None, "silu")
+    ref.moe_gate_scale(want, gates, e0, El)
+    torch.testing.assert_close(got, want)
+    res = torch.randn(T, H, generator=g)
+    nw = torch.rand(H, generator=g) + 0.5
+    r1, r2 = res.clone(), res.clone()
+    y, route = ops.rms_norm_route(x, nw, 1e-5, r1, torch.randn(E, H, generator=g), 2)
+    assert route is None
+    torch.testing.assert_close(y, ops.rms_norm(x, nw, 1e-5, residual=r2))
+    torch.testing.assert_close(r1, r2)
