@@ -88,6 +88,19 @@ rmsnorm_partial_kernel(const float* __restrict__ part, int sk, long slab, bf16* 
   const long row = blockIdx.x;
   const int nvec = dim >> 3;
   bf16x8* rr = reinterpret_cast<bf16x8*>(residual + row * (long)dim);
+  // MoE: the router chunks do not depend on the row, so their loads go out first and their
+  // latency hides behind the slab loads
+  constexpr int RE = EC > 0 ? EC : 1, RN = EC > 0 ? NV : 1;
+  bf16x8 rv[RN][RE];
+  if constexpr (EC > 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = threadIdx.x + i * kNormPartThreads;
+      if (c < nvec)
+#pragma unroll
+        for (int e = 0; e < EC; ++e) rv[i][e] = reinterpret_cast<const bf16x8*>(rw + (long)e * dim)[c];
+    }
+  }
   float v[NV][8];
   float ss = 0.f;
 #pragma unroll
@@ -138,13 +151,10 @@ rmsnorm_partial_kernel(const float* __restrict__ part, int sk, long slab, bf16* 
       for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv * bf2f(g[j]));
       yr[c] = o;
       if constexpr (EC > 0) {
-        bf16x8 rv[EC];   // every expert's router chunk in flight together
-#pragma unroll
-        for (int e = 0; e < EC; ++e) rv[e] = reinterpret_cast<const bf16x8*>(rw + (long)e * dim)[c];
 #pragma unroll
         for (int e = 0; e < EC; ++e)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) racc[e] += bf2f(o[j]) * bf2f(rv[e][j]);
+          for (int j = 0; j < 8; ++j) racc[e] += bf2f(o[j]) * bf2f(rv[i][e][j]);
       }
     }
   }
