@@ -39,3 +39,30 @@ def test_every_plan_is_instantiated(preset, tp):
         for M in Ms:
             rc = torch.ops.bfly.gemm_check(M, N, K, epi)
             assert rc == 0, (preset, tp, M, N, K, epi, rc, torch.ops.bfly.gemm_plan(M, N, K))
+
+
+def test_in_situ_plan_choices_are_in_the_table():
+    """Every whole-step (in-situ) A/B choice pinned in tools/gen_gemm_table.py (INSITU) is an
+    entry of the generated gemm_tuned.inc with that plan, and plan_gemm returns it (a pinned
+    choice that the generator dropped would silently fall back to the sweep's or the heuristic
+    plan)."""
+    import importlib.util
+    import os
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gen_gemm_table", os.path.join(root, "tools", "gen_gemm_table.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    table = {}
+    for ln in open(os.path.join(root, "csrc", "kernels", "gemm_tuned.inc")):
+        m = re.match(r"\{(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+)\}", ln)
+        if m:
+            v = [int(x) for x in m.groups()]
+            table[tuple(v[:3])] = v[3:]
+    kinds = ("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4")
+    for (N, K, M), (pl, _) in mod.INSITU.items():
+        assert table.get((N, K, M)) == pl, ((N, K, M), table.get((N, K, M)), pl)
+        p = ops.gemm_plan(M, N, K)
+        got = [kinds.index(p["kind"]), p["mt"], p["nt"], p["wk"], p["bm"], p["bn"], p["splitk"]]
+        assert got == pl, ((N, K, M), got, pl)
