@@ -338,7 +338,9 @@ def run(a) -> int:
                    "kv_cache_dtype": str(eng.kv_dtype).replace("torch.", ""),
                    "pp_async_groups": groups if groups > 1 else None,
                    "async_decode": bool(eng.async_pp and mesh.pp == 1),
-                   "mixed": bool(eng.mixed), "prefix_caching": bool(eng.prefix_cache)},
+                   "mixed": bool(eng.mixed), "prefix_caching": bool(eng.prefix_cache),
+                   "packed_decode_weights_gb": round(sum(t.numel() * t.element_size()
+                                                         for t in eng.model.packed.values()) / 1e9, 1)},
     }
     if rank == 0:
         line = json.dumps(res)

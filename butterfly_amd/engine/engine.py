@@ -138,6 +138,13 @@ class LLMEngine:
             nblocks = min(nblocks, max(need, 1))
         if nblocks <= 0:
             raise RuntimeError("no HBM left for the KV cache")
+        if (self.device.type == "cuda" and flags.get("BFLY_PACKED_DECODE") and mesh.ep == 1
+                and engine_cfg.max_batch <= 64):
+            # decode-layout copies of the gate/up weights, only from HBM the KV cache leaves free
+            extra = self.model.packed_decode_bytes()
+            free = device_kv_budget(self.device, engine_cfg.hbm_utilization, self._activation_reserve())
+            if extra and free - nblocks * per_tok * bs >= extra + (2 << 30):
+                self.model.pack_decode_weights()
         self.kv = KVCache(self.model, nblocks, bs, self.kv_dtype)
         native = __import__("butterfly_amd._native_loader", fromlist=["native"]).native()
         # pipeline parallelism without per-step fill/drain: pp request groups in flight

@@ -96,6 +96,8 @@ class TransformerLM:
         if self.device.type == "cuda" and cfg.head_dim != 128:
             raise NotImplementedError(f"GPU attention kernels need head_dim 128 (got {cfg.head_dim})")
         self.p: dict[str, torch.Tensor] = {}
+        # K-tile-blocked copies of the gate/up weights for the decode GEMMs (pack_decode_weights)
+        self.packed: dict[str, torch.Tensor] = {}
         self._alloc()
         self.cos = self.sin = None
         if cfg.pos_emb == "rope":
@@ -152,6 +154,31 @@ class TransformerLM:
             elif not self.first:
                 # tied head on a last stage that does not hold the embedding: its own copy
                 self.p["head"] = z(d.vocab, h)
+
+    def _packable(self) -> list:
+        names = []
+        for i in self.layer_ids:
+            for k in (f"l{i}.gu_w", f"l{i}.moe_gu_w"):
+                w = self.p.get(k)
+                if w is not None and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0:
+                    names.append(k)
+        return names
+
+    def packed_decode_bytes(self) -> int:
+        """HBM a pack_decode_weights() call would add."""
+        return sum(self.p[k].numel() * self.p[k].element_size() for k in self._packable())
+
+    def pack_decode_weights(self) -> None:
+        """Keep a K-tile-blocked copy (ops.pack_w256) of every gate/up weight, read by the decode
+        GEMMs whose plan is a 64 x 128 tile (batches of 33-64 rows): each 128-row weight stage is
+        one 16 KiB run of memory instead of 128 row segments, 8 % faster on the Llama-3-70B
+        gate/up GEMM with bitwise the same result (tools/packed_probe.py). The engine calls it
+        once, after the weights are final and only when the HBM left after the KV cache holds the
+        copies; weights must not change afterwards."""
+        if self.device.type != "cuda":
+            return
+        for k in self._packable():
+            self.packed[k] = ops.pack_w256(self.p[k])
 
     @property
     def head_weight(self) -> torch.Tensor:
@@ -548,7 +575,8 @@ class TransformerLM:
                                          d.expert0, d.experts, d.ffn)
             else:
                 if flags.get("BFLY_MOE_GATE_EPILOGUE"):   # routing weight in the GEMM epilogue
-                    hmid = ops.linear_silu_gate(xs, self.p[pre + "moe_gu_w"], gs, d.expert0, d.experts)
+                    hmid = ops.linear_silu_gate(xs, self.p[pre + "moe_gu_w"], gs, d.expert0, d.experts,
+                                                packed=self.packed.get(pre + "moe_gu_w"))
                 else:
                     hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
                     ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
@@ -558,7 +586,7 @@ class TransformerLM:
                 return self.comm.reduce_scatter(out, "ep")[:T], False
             return out, self.tp > 1
         if c.act == "silu":
-            hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu")
+            hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu", packed=self.packed.get(pre + "gu_w"))
             out = ops.linear(hmid, self.p[pre + "down_w"], defer=self.defer_reduce)
         else:
             hmid = ops.linear(x, self.p[pre + "fc_w"], bias=self.p.get(pre + "fc_b"))

@@ -449,15 +449,31 @@ def topkp_threshold(logits, temps, top_k, top_p, reduce_sum=None, reduce_max=Non
     return thr
 
 
-def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = False):
+def pack_w256(w: torch.Tensor) -> torch.Tensor:
+    """A [N, K] weight in the K-tile-blocked layout [N/256][K/64][256][64] (returned viewed as
+    [N, K]) that the packed decode GEMM reads (gemm.hip launch_gemm_packed)."""
+    N, K = w.shape
+    return w.view(N // 256, 256, K // 64, 64).permute(0, 2, 1, 3).contiguous().view(N, K)
+
+
+def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = False, packed=None):
     """y = x @ w.T (+ bias) with optional fused SwiGLU epilogue ('silu': w rows gate/up
     interleaved in 16-row groups, output width w.shape[0] // 2). `defer=True` (no bias /
-    epilogue): when the plan splits K, return a `Partial` whose reduce the consumer fuses."""
+    epilogue): when the plan splits K, return a `Partial` whose reduce the consumer fuses.
+    `packed`: the weight's pack_w256 copy: used when the shape's plan has a packed form (decode
+    tile plans), else `w`."""
     rn = None
     if isinstance(x, RowNormed):   # consumer of a row-split RMSNorm: the GEMM applies 1/rms
         rn, x = x, x.y
     if not _gpu(x):
         return ref.linear(x, w, bias, epilogue, out)
+    if packed is not None and bias is None and not defer and epilogue in ("none", "silu"):
+        M, N = x.shape[0], w.shape[0]
+        if out is None:
+            out = _empty(M, N // 2 if epilogue == "silu" else N, dtype=x.dtype, device=x.device)
+        if torch.ops.bfly.gemm_packed(x, packed, out, EPILOGUES[epilogue], rn.ssp if rn is not None else None,
+                                      rn.eps if rn is not None else 0.0) == 0:
+            return out
     if defer and bias is None and epilogue == "none":
         M, N = x.shape[0], w.shape[0]
         if out is None:
@@ -490,14 +506,17 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
     return out
 
 
-def linear_silu_gate(x, w, gates, e0: int, num_local: int):
+def linear_silu_gate(x, w, gates, e0: int, num_local: int, packed=None):
     """The dense MoE decode gate/up GEMM over the concatenated local experts: SwiGLU, then every
     expert's column block scaled by its routing weight gates[:, e0 + e] — `linear(x, w, 'silu')`
-    followed by `moe_gate_scale_`, bit for bit, in one launch (the tile kernel's epilogue)."""
+    followed by `moe_gate_scale_`, bit for bit, in one launch (the tile kernel's epilogue).
+    `packed`: the weight's pack_w256 copy (used when the plan has a packed form)."""
     if isinstance(x, RowNormed) or not _gpu(x):
         h = linear(x, w, epilogue="silu")
         return moe_gate_scale_(h, gates, e0, num_local)
     out = _empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
+    if packed is not None and torch.ops.bfly.gemm_packed(x, packed, out, 3, None, 0.0, gates, e0, num_local) == 0:
+        return out
     torch.ops.bfly.gemm_silu_gate(x, w, out, gates, e0, num_local)
     return out
 

@@ -402,6 +402,40 @@ void gemm_silu_gate(const Tensor& x, const Tensor& w, Tensor& out, const Tensor&
   TORCH_CHECK(rc == 0, "gemm_silu_gate: unsupported shape M=", M, " N=", N, " K=", K, " F=", F, " (rc=", rc, ")");
 }
 
+static bfly::RowScale row_scale(const Tensor& ssp, double eps, int M, int K);
+
+// Decode GEMM over the K-tile-blocked copy `wp` ([N/256][K/64][256][64] viewed as [N, K]) of a
+// weight; optional RMSNorm row scale (ssp, eps) and MoE gate (gates, e0, num_local: epilogue 3).
+// Returns 0 when it ran, < 0 when the shape's plan has no packed form (nothing launched).
+int64_t gemm_packed(const Tensor& x, const Tensor& wp, Tensor& out, int64_t epilogue,
+                    const c10::optional<Tensor>& ssp, double eps, const c10::optional<Tensor>& gates,
+                    int64_t e0, int64_t num_local) {
+  CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out);
+  TORCH_CHECK(x.dim() == 2 && wp.dim() == 2 && out.dim() == 2 && wp.is_contiguous(), "gemm_packed: operands");
+  CHECK_INNER(x); CHECK_INNER(out); CHECK_ALIGN16(x); CHECK_ALIGN16(wp);
+  const int M = x.size(0), K = x.size(1), N = wp.size(0);
+  TORCH_CHECK(wp.size(1) == K && x.stride(0) % 8 == 0, "gemm_packed: shape");
+  const bool silu = epilogue == bfly::EPI_SILU || epilogue == bfly::EPI_SILU_GATE;
+  TORCH_CHECK(epilogue != bfly::EPI_BIAS, "gemm_packed: no bias epilogue");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (silu ? N / 2 : N), "gemm_packed: out shape");
+  bfly::RowScale rs{nullptr, 0, 0.f, 0.f};
+  if (ssp.has_value()) rs = row_scale(*ssp, eps, M, K);
+  if (epilogue == bfly::EPI_SILU_GATE) {
+    TORCH_CHECK(gates.has_value() && gates->scalar_type() == at::kFloat && gates->dim() == 2 &&
+                    gates->is_contiguous() && gates->size(0) == M, "gemm_packed: gates [M, E] f32");
+    TORCH_CHECK(num_local > 0 && (N / 2) % num_local == 0 && e0 + num_local <= gates->size(1), "gemm_packed: experts");
+    rs.gate = gates->data_ptr<float>();
+    rs.gld = (int)gates->size(1);
+    rs.ge0 = (int)e0;
+    rs.gF = (int)((N / 2) / num_local);
+    if (rs.gF % 16 != 0) return -5;
+  }
+  const bool any = ssp.has_value() || epilogue == bfly::EPI_SILU_GATE;
+  c10::DeviceGuard g(x.device());
+  return bfly::launch_gemm_packed(bf(x), x.stride(0), bf(wp), M, N, K, (int)epilogue, bf(out), out.stride(0),
+                                  cur_stream(), any ? &rs : nullptr);
+}
+
 // Benchmark / tuning entry: run an explicit plan [kind, mt, nt, wk, bm, bn, sk].
 void gemm_with_plan(const Tensor& x, const Tensor& w, Tensor& out, std::vector<int64_t> plan,
                     int64_t epilogue, const c10::optional<Tensor>& workspace,
@@ -1130,6 +1164,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("tkp_final(Tensor(a!) ws, int rows, Tensor(b!) thresh) -> ()");
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_silu_gate(Tensor x, Tensor w, Tensor(a!) out, Tensor gates, int e0, int num_local) -> ()");
+  m.def("gemm_packed(Tensor x, Tensor wp, Tensor(a!) out, int epilogue, Tensor? ssp=None, float eps=0.0, "
+        "Tensor? gates=None, int e0=0, int num_local=1) -> int");
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace, "
         "Tensor? bias=None) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);
@@ -1210,6 +1246,7 @@ TORCH_LIBRARY_IMPL(bfly, CUDA, m) {
   m.impl("tkp_final", &tkp_final);
   m.impl("gemm", &gemm);
   m.impl("gemm_silu_gate", &gemm_silu_gate);
+  m.impl("gemm_packed", &gemm_packed);
   m.impl("gemm_with_plan", &gemm_with_plan);
   m.impl("gemm_deferred", &gemm_deferred);
   m.impl("splitk_reduce", &splitk_reduce);

@@ -245,7 +245,10 @@ constexpr int stage_loads() { return (ROWS / 8 + 3) / 4; }
 // `nt`: stream the operand with the non-temporal policy (aux = 2) — for weights that exactly
 // one workgroup reads once (decode, a single M tile): issued->landed ~18 % shorter and 5-10 %
 // per decode layer on MI355X (MI355X_MICROARCH.md 'nt-weights'); never for re-read panels.
-template <int ROWS, bool GATHER = false>
+// PACKED: `src` is a weight in the K-tile-blocked layout [N/256][K/64][256][64] (pack_w256):
+// a 256-row x 64-column block is 32 KiB of contiguous memory, so a 128-row stage reads 16 KiB
+// in one run instead of 128 runs of 128 B one row pitch apart; `ld` then carries K.
+template <int ROWS, bool GATHER = false, bool PACKED = false>
 __device__ __forceinline__ void tile_stage(const bf16* __restrict__ src, long ld, int row0,
                                            int row_max, int k0, char* lds, int wid, int lane,
                                            const int* __restrict__ rows = nullptr, bool nt = false) {
@@ -264,7 +267,8 @@ __device__ __forceinline__ void tile_stage(const bf16* __restrict__ src, long ld
     if constexpr (GATHER) {
       if (rows) gr = rows[gr];   // grouped GEMM: row slot -> source token
     }
-    const bf16* g = src + (long)gr * ld + k0 + chunk * 8;
+    const bf16* g = PACKED ? src + (((long)(gr >> 8) * (ld >> 6) + (k0 >> 6)) << 14) + (gr & 255) * 64 + chunk * 8
+                           : src + (long)gr * ld + k0 + chunk * 8;
     if (nt)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)g, (lds_ptr_t)(lds + blk * 1024), 16, 0, 2);
     else
@@ -369,7 +373,7 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[TI][TJ], int mw
 // gtiles[i] = {expert, first row slot, end row slot} (count in *gcount; excess workgroups
 // exit), blockIdx.z the N tile; the expert selects W + expert * w_estride and A rows are
 // gathered through grows[slot] (nullptr: slots are rows). Output rows are row slots.
-template <int BM, int BN, int WMW, int STAGES, bool GROUPED = false>
+template <int BM, int BN, int WMW, int STAGES, bool GROUPED = false, bool PACKW = false>
 __global__ void __launch_bounds__(kTileThreads)
 gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -426,7 +430,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
     if (kt0 + s < kt1) {
       char* b = smem + s * STAGE_BYTES;
       tile_stage<BM, GROUPED>(X, ldx, m0, M, (kt0 + s) * kBK, b, wid, lane, grows);
-      tile_stage<BN>(W, ldw, n0, N, (kt0 + s) * kBK, b + A_BYTES, wid, lane, nullptr, w_nt);
+      tile_stage<BN, false, PACKW>(W, ldw, n0, N, (kt0 + s) * kBK, b + A_BYTES, wid, lane, nullptr, w_nt);
     }
   }
   int buf = 0;
@@ -443,7 +447,7 @@ gemm_tile_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
       if (nbuf >= STAGES) nbuf -= STAGES;
       char* nb = smem + nbuf * STAGE_BYTES;
       tile_stage<BM, GROUPED>(X, ldx, m0, M, (kt + STAGES - 1) * kBK, nb, wid, lane, grows);
-      tile_stage<BN>(W, ldw, n0, N, (kt + STAGES - 1) * kBK, nb + A_BYTES, wid, lane, nullptr, w_nt);
+      tile_stage<BN, false, PACKW>(W, ldw, n0, N, (kt + STAGES - 1) * kBK, nb + A_BYTES, wid, lane, nullptr, w_nt);
     }
     const char* As = smem + buf * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
@@ -1454,7 +1458,7 @@ static void init_nt_policy() {
   if (e && e[0] == '0') (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile_w_nt), &zero, sizeof(int));
 }
 
-template <int BM, int BN, int WMW, int STAGES>
+template <int BM, int BN, int WMW, int STAGES, bool PACKW = false>
 static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                      int epi, const bf16* bias, bf16* out, long ldo, float* ws, int sk,
                      hipStream_t stream, const RowScale& rsc) {
@@ -1464,13 +1468,13 @@ static void run_tile(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   const dim3 grid(tiles, sk);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
   if (!attr_set && lds > 65536) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW, STAGES>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tile_kernel<BM, BN, WMW, STAGES, false, PACKW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  gemm_tile_kernel<BM, BN, WMW, STAGES><<<grid, kTileThreads, lds, stream>>>(
-      X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, nullptr, nullptr,
-      nullptr, 0, rsc);
+  gemm_tile_kernel<BM, BN, WMW, STAGES, false, PACKW><<<grid, kTileThreads, lds, stream>>>(
+      X, ldx, W, PACKW ? (long)K : ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr,
+      nullptr, nullptr, nullptr, 0, rsc);
 }
 
 template <int BM, int BN, int NWM, int NWN, int SW>
@@ -1767,6 +1771,18 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef SK_WK
 #undef SK_CASE
     if (!done) return -2;
+  } else if (p.kind == 1 && p.nt == 1) {
+    // tile plan over a K-tile-blocked weight (pack_w256 layout): 64 x 128 tiles, no split-K
+    if (N % 256 != 0 || K % 64 != 0 || p.bm != 64 || p.bn != 128 || p.sk != 1) return -1;
+    bool done = false;
+#define TLP_CASE(WMW_, ST_)                                                                          \
+  if (!done && p.wk == WMW_ && p.mt == ST_) {                                                        \
+    if (!dry) run_tile<64, 128, WMW_, ST_, true>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, 1, stream, rsc); \
+    done = true;                                                                                     \
+  }
+    TLP_CASE(2, 3) TLP_CASE(1, 3) TLP_CASE(2, 4) TLP_CASE(1, 4)
+#undef TLP_CASE
+    if (!done) return -2;
   } else {
     if (N % p.bn != 0 || K % kBK != 0) return -1;
     if (p.sk > 1 && (long)((M + p.bm - 1) / p.bm) * (N / p.bn) > kSplitCounters) return -1;
@@ -1927,6 +1943,33 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
   if (p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
     p.sk = 1;
   return run_plan(p, X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, stream, false, false, rs);
+}
+
+// Decode GEMM over a K-tile-blocked copy of the weight (layout [N/256][K/64][256][64], made
+// once by the engine when HBM allows, models/transformer.pack_decode_weights): the plan the
+// row-major weight would run (tile 64 x 128, no split-K; EPI_SILU_GATE: the gate plan) on the
+// packed copy. Each 128-row weight stage is then one 16 KiB run of memory instead of 128
+// runs of 128 B a row pitch apart: the Llama-3-70B gate/up GEMM at M = 64 in 145 against
+// 158 us, bitwise the same result (tools/packed_probe.py). Returns < 0 (nothing launched)
+// when the plan for this shape is not such a tile plan: the caller then uses the row-major
+// weight. `dry`: only report whether it applies.
+int launch_gemm_packed(const bf16* X, long ldx, const bf16* Wp, int M, int N, int K, int epi, bf16* out,
+                       long ldo, hipStream_t stream, const RowScale* rs, bool dry) {
+  if (M <= 0) return dry ? 0 : 0;
+  if (N % 256 != 0 || K % 64 != 0) return -1;
+  GemmPlan p = plan_gemm(M, N, K);
+  if (epi != EPI_SILU_GATE &&
+      run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true) != 0)
+    p = plan_gemm_heuristic(M, N, K);
+  if (epi == EPI_SILU_GATE &&
+      run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true) != 0) {
+    const int bm = M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128;
+    p = GemmPlan{1, 3, 0, bm <= 32 ? 1 : 2, bm, 128, 1};
+  }
+  if (p.kind != 1 || p.bm != 64 || p.bn != 128 || p.sk != 1) return -2;
+  p.nt = 1;
+  if (dry) return run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true);
+  return run_plan(p, X, ldx, Wp, K, M, N, K, epi, nullptr, out, ldo, nullptr, stream, false, false, rs);
 }
 
 // The dense MoE decode path's gate/up GEMM with the routing weight in its epilogue: one launch

@@ -96,6 +96,20 @@ def test_bench_dims_prefill_decode_and_graph(preset):
     torch.cuda.synchronize()
     _check(dg[:, :V], dr[:, :V], 3e-2, cfg.is_moe)
 
+    # the decode step over the K-tile-blocked gate/up copies (what an engine with HBM to spare
+    # runs): bitwise the eager logits and cache writes
+    for (k, v), (k0, v0) in zip(kg, kg_snapshot):
+        k.copy_(k0)
+        v.copy_(v0)
+    dg_eager = dg.clone()
+    g.pack_decode_weights()
+    assert g.packed
+    dp = g.forward(db, kg)
+    torch.cuda.synchronize()
+    assert torch.equal(dp, dg_eager), "decode over the packed gate/up weights differs"
+    for (k, v), (k1, v1) in zip(kg, kv_eager):
+        assert torch.equal(k, k1) and torch.equal(v, v1)
+
     # hipGraph replay of the same decode step: bitwise the eager logits and cache writes
     for (k, v), (k0, v0) in zip(kg, kg_snapshot):
         k.copy_(k0)

@@ -382,6 +382,40 @@ def test_rms_norm_route_equals_norm_then_route(T, dim, sk, k, E):
     assert torch.equal(ids.cpu()[clear].sort(dim=-1).values, ids2.cpu()[clear].sort(dim=-1).values)
 
 
+@pytest.mark.parametrize("M,N,K,mode", [(64, 57344, 8192, "silu"), (64, 28672, 4096, "rowscale"),
+                                         (48, 28672, 4096, "silu"), (64, 2 * 2 * 14336, 4096, "gate"),
+                                         (16, 28672, 4096, "silu"), (200, 28672, 4096, "silu")])
+def test_packed_decode_gemm_is_bitwise_the_row_major_one(M, N, K, mode):
+    """The decode GEMM over the K-tile-blocked copy of a weight (ops.pack_w256, gemm.hip
+    launch_gemm_packed) runs the plan the row-major weight would run with the same arithmetic
+    order: bitwise the same output, for the SwiGLU epilogue, with a row-split RMSNorm row scale
+    and with the MoE gate; shapes whose plan has no packed form (M = 16, 200) report so and
+    ops.linear falls back to the row-major weight."""
+    x, w = _bf(M, K, seed=90), _bf(N, K, scale=0.02, seed=91)
+    wp = ops.pack_w256(w)
+    if mode == "gate":
+        E, El = 8, 2
+        gates = torch.rand(M, E, generator=torch.Generator().manual_seed(92)).to(DEV)
+        got = ops.linear_silu_gate(x, w, gates, 3, El, packed=wp)
+        want = ops.linear_silu_gate(x, w, gates, 3, El)
+        assert torch.equal(got, want)
+        out = torch.empty_like(got)
+        assert torch.ops.bfly.gemm_packed(x, wp, out, 3, None, 0.0, gates, 3, El) == 0
+        return
+    if mode == "rowscale":
+        res = _bf(M, K, seed=93)
+        nw = (1.0 + 0.1 * _bf(K, seed=94).float()).to(torch.bfloat16)
+        xin = ops.rms_norm(x, nw, 1e-5, residual=res.clone(), rows=True)
+    else:
+        xin = x
+    got = ops.linear(xin, w, epilogue="silu", packed=wp)
+    want = ops.linear(xin, w, epilogue="silu")
+    assert torch.equal(got, want)
+    out = torch.empty_like(got)
+    applies = torch.ops.bfly.gemm_packed(x, wp, out, ops.EPILOGUES["silu"]) == 0
+    assert applies == (32 < M <= 64), (M, applies)
+
+
 @pytest.mark.parametrize("M,El,e0,E,H,F", [(64, 8, 0, 8, 512, 256), (37, 3, 2, 8, 256, 128), (130, 2, 0, 4, 1024, 512),
                                            (16, 4, 4, 8, 512, 64), (64, 1, 3, 8, 4096, 14336)])
 def test_gate_scaled_silu_epilogue(M, El, e0, E, H, F):

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Decode gate/up GEMM (M = 64) over a K-tile-blocked weight layout [N/256][K/64][256][64]
+against the row-major weight: same tile plan, same arithmetic order (outputs bitwise equal),
+different DRAM access pattern (a 128-row stage reads one 16 KiB run instead of 128 runs of
+128 B one row pitch apart). Weight copies rotate over > 1 GiB so every call streams from HBM.
+
+usage: python tools/packed_probe.py [--n 57344] [--k 8192] [--m 64]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from butterfly_amd import ops  # noqa: E402
+
+
+def pack_w256(w: torch.Tensor) -> torch.Tensor:
+    N, K = w.shape
+    return w.view(N // 256, 256, K // 64, 64).permute(0, 2, 1, 3).contiguous().view(N, K)
+
+
+def timeit(fn, iters=30):
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for i in range(iters):
+        fn(i)
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=57344)
+    ap.add_argument("--k", type=int, default=8192)
+    ap.add_argument("--m", type=int, default=64)
+    a = ap.parse_args()
+    assert ops.load_library()
+    N, K, M = a.n, a.k, a.m
+    copies = max(2, (1 << 30) // (N * K * 2) + 1)
+    Ws = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
+    Ps = [pack_w256(w) for w in Ws]
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+    ref = torch.empty_like(out)
+    silu = ops.EPILOGUES["silu"]
+    torch.ops.bfly.gemm_with_plan(x, Ws[0], ref, [1, 3, 0, 2, 64, 128, 1], silu, None)
+    torch.ops.bfly.gemm_with_plan(x, Ps[0], out, [1, 3, 1, 2, 64, 128, 1], silu, None)
+    torch.cuda.synchronize()
+    print(json.dumps({"bitwise_equal": bool(torch.equal(out, ref))}), flush=True)
+    cases = [("rowmajor_wk2", Ws, [1, 3, 0, 2, 64, 128, 1]), ("packed_wk2", Ps, [1, 3, 1, 2, 64, 128, 1]),
+             ("rowmajor_wk1", Ws, [1, 3, 0, 1, 64, 128, 1]), ("packed_wk1", Ps, [1, 3, 1, 1, 64, 128, 1])]
+    for rep in range(3):
+        for name, W, pl in cases:
+            us = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, W[i % copies], out, pl, silu, None))
+            print(json.dumps({"rep": rep, "case": name, "M": M, "N": N, "K": K, "us": round(us, 2),
+                              "TBps": round(N * K * 2 / us / 1e6, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
