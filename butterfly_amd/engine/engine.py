@@ -140,11 +140,12 @@ class LLMEngine:
             raise RuntimeError("no HBM left for the KV cache")
         if (self.device.type == "cuda" and flags.get("BFLY_PACKED_DECODE") and mesh.ep == 1
                 and engine_cfg.max_batch <= 64):
-            # decode-layout copies of the gate/up weights, only from HBM the KV cache leaves free
-            extra = self.model.packed_decode_bytes()
+            # decode-layout copies of the projection weights, only from HBM the KV cache leaves free
             free = device_kv_budget(self.device, engine_cfg.hbm_utilization, self._activation_reserve())
-            if extra and free - nblocks * per_tok * bs >= extra + (2 << 30):
-                self.model.pack_decode_weights()
+            room = free - nblocks * per_tok * bs - (2 << 30)
+            if room > 0:
+                kinds = [k.strip() for k in flags.get("BFLY_PACKED_KINDS").split(",") if k.strip()]
+                self.model.pack_decode_weights(budget_bytes=room, kinds=kinds)
         self.kv = KVCache(self.model, nblocks, bs, self.kv_dtype)
         native = __import__("butterfly_amd._native_loader", fromlist=["native"]).native()
         # pipeline parallelism without per-step fill/drain: pp request groups in flight

@@ -155,30 +155,52 @@ class TransformerLM:
                 # tied head on a last stage that does not hold the embedding: its own copy
                 self.p["head"] = z(d.vocab, h)
 
+    # decode projections in the order their packed copies are made when HBM is short: gate/up
+    # first (the largest decode GEMM), then the others
+    _PACK_ORDER = ("gu_w", "moe_gu_w", "qkv_w", "o_w", "down_w", "moe_down_w")
+
+    _PACK_EPI = {"gu_w": 2, "moe_gu_w": 3}    # GEMM epilogue of each kind (others: none)
+
     def _packable(self) -> list:
+        """Weights whose decode GEMM at a 64-row batch has a packed-weight plan."""
+        if self.device.type != "cuda" or not ops.load_library():
+            return []
         names = []
-        for i in self.layer_ids:
-            for k in (f"l{i}.gu_w", f"l{i}.moe_gu_w"):
+        for kind in self._PACK_ORDER:
+            for i in self.layer_ids:
+                k = f"l{i}.{kind}"
                 w = self.p.get(k)
-                if w is not None and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0:
+                if (w is not None and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0
+                        and torch.ops.bfly.gemm_packed_check(64, w.shape[0], w.shape[1], self._PACK_EPI.get(kind, 0)) == 0):
                     names.append(k)
         return names
 
-    def packed_decode_bytes(self) -> int:
-        """HBM a pack_decode_weights() call would add."""
-        return sum(self.p[k].numel() * self.p[k].element_size() for k in self._packable())
+    def packed_decode_bytes(self, kinds=None) -> int:
+        """HBM a pack_decode_weights(kinds) call would add."""
+        return sum(self.p[k].numel() * self.p[k].element_size() for k in self._packable()
+                   if kinds is None or k.split(".", 1)[1] in kinds)
 
-    def pack_decode_weights(self) -> None:
-        """Keep a K-tile-blocked copy (ops.pack_w256) of every gate/up weight, read by the decode
-        GEMMs whose plan is a 64 x 128 tile (batches of 33-64 rows): each 128-row weight stage is
-        one 16 KiB run of memory instead of 128 row segments, 8 % faster on the Llama-3-70B
-        gate/up GEMM with bitwise the same result (tools/packed_probe.py). The engine calls it
-        once, after the weights are final and only when the HBM left after the KV cache holds the
-        copies; weights must not change afterwards."""
+    def pack_decode_weights(self, budget_bytes: Optional[int] = None, kinds=None) -> int:
+        """Keep K-tile-blocked copies (ops.pack_w256) of the decode projections' weights, read by
+        the decode GEMMs whose plan is a 64-row tile (batches of 33-64 rows): each weight stage is
+        one contiguous run of memory instead of a row segment per weight row, 8 % faster on the
+        Llama-3-70B gate/up GEMM with bitwise the same result (tools/packed_probe.py). Whole
+        projection kinds, in the order of `kinds` (None: _PACK_ORDER), while they fit
+        `budget_bytes` (None: all). The engine
+        calls it once, after the weights are final; weights must not change afterwards. Returns
+        the bytes added."""
         if self.device.type != "cuda":
-            return
-        for k in self._packable():
-            self.packed[k] = ops.pack_w256(self.p[k])
+            return 0
+        added = 0
+        for kind in (self._PACK_ORDER if kinds is None else kinds):
+            names = [k for k in self._packable() if k.split(".", 1)[1] == kind]
+            size = sum(self.p[k].numel() * self.p[k].element_size() for k in names)
+            if not names or (budget_bytes is not None and added + size > budget_bytes):
+                continue
+            for k in names:
+                self.packed[k] = ops.pack_w256(self.p[k])
+            added += size
+        return added
 
     @property
     def head_weight(self) -> torch.Tensor:
@@ -401,7 +423,8 @@ class TransformerLM:
         slots = fb.slots if kc is not None else None
         # split-K reduces are deferred into the consuming kernel (rope_kv / add+rmsnorm)
         # when no all-reduce sits in between (tp == 1)
-        qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv)
+        qkv = ops.linear(x, self.p[pre + "qkv_w"], bias=self.p.get(pre + "qkv_b"), defer=self.defer_qkv,
+                         packed=self.packed.get(pre + "qkv_w"))
         if c.pos_emb == "rope":
             qkv = ops.rope_kv(qkv, fb.positions, self.cos, self.sin, d.hq, d.hkv, slots, kc, vc)
         elif kc is not None:
@@ -432,7 +455,8 @@ class TransformerLM:
     def _o_proj(self, pre: str, attn: torch.Tensor, T: int):
         d, D = self.dims, self.cfg.head_dim
         o_b = self.p.get(pre + "o_b") if self.shard.tp_rank == 0 else None
-        return ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce)
+        return ops.linear(attn.view(T, d.hq * D), self.p[pre + "o_w"], bias=o_b, defer=self.defer_reduce,
+                          packed=self.packed.get(pre + "o_w"))
 
     # ------------------------------------------------------------------------------------
     # sequence parallelism (TP prefill)
@@ -581,13 +605,14 @@ class TransformerLM:
                     hmid = ops.linear(xs, self.p[pre + "moe_gu_w"], epilogue="silu")
                     ops.moe_gate_scale_(hmid, gs, d.expert0, d.experts)
                 # one rank: the split-K reduce goes into the next add+RMSNorm, as for dense FFNs
-                out = ops.linear(hmid, self.p[pre + "moe_down_w"], defer=self.defer_reduce and self.ep == 1)
+                out = ops.linear(hmid, self.p[pre + "moe_down_w"], defer=self.defer_reduce and self.ep == 1,
+                                 packed=self.packed.get(pre + "moe_down_w"))
             if self.ep > 1:
                 return self.comm.reduce_scatter(out, "ep")[:T], False
             return out, self.tp > 1
         if c.act == "silu":
             hmid = ops.linear(x, self.p[pre + "gu_w"], epilogue="silu", packed=self.packed.get(pre + "gu_w"))
-            out = ops.linear(hmid, self.p[pre + "down_w"], defer=self.defer_reduce)
+            out = ops.linear(hmid, self.p[pre + "down_w"], defer=self.defer_reduce, packed=self.packed.get(pre + "down_w"))
         else:
             hmid = ops.linear(x, self.p[pre + "fc_w"], bias=self.p.get(pre + "fc_b"))
             hmid = ops.gelu(hmid)

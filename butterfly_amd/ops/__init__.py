@@ -467,13 +467,19 @@ def linear(x, w, bias=None, epilogue: str = "none", out=None, defer: bool = Fals
         rn, x = x, x.y
     if not _gpu(x):
         return ref.linear(x, w, bias, epilogue, out)
-    if packed is not None and bias is None and not defer and epilogue in ("none", "silu"):
+    if packed is not None and bias is None and epilogue in ("none", "silu") and not (defer and epilogue != "none"):
         M, N = x.shape[0], w.shape[0]
         if out is None:
             out = _empty(M, N // 2 if epilogue == "silu" else N, dtype=x.dtype, device=x.device)
-        if torch.ops.bfly.gemm_packed(x, packed, out, EPILOGUES[epilogue], rn.ssp if rn is not None else None,
-                                      rn.eps if rn is not None else 0.0) == 0:
+        need = torch.ops.bfly.gemm_workspace_size(M, N, x.shape[1])
+        ws = _arena.get(x.device, "gemm", need // 4 + 1, torch.float32, zero=True) if need else None
+        sk = torch.ops.bfly.gemm_packed(x, packed, out, EPILOGUES[epilogue], rn.ssp if rn is not None else None,
+                                        rn.eps if rn is not None else 0.0, None, 0, 1, ws, bool(defer))
+        if sk == 1:
             return out
+        if sk > 1:     # deferred split-K slabs for the consumer
+            off = torch.ops.bfly.gemm_slab_offset()
+            return Partial(ws[off:off + sk * M * N].view(sk, M, N), out)
     if defer and bias is None and epilogue == "none":
         M, N = x.shape[0], w.shape[0]
         if out is None:
@@ -515,7 +521,7 @@ def linear_silu_gate(x, w, gates, e0: int, num_local: int, packed=None):
         h = linear(x, w, epilogue="silu")
         return moe_gate_scale_(h, gates, e0, num_local)
     out = _empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
-    if packed is not None and torch.ops.bfly.gemm_packed(x, packed, out, 3, None, 0.0, gates, e0, num_local) == 0:
+    if packed is not None and torch.ops.bfly.gemm_packed(x, packed, out, 3, None, 0.0, gates, e0, num_local) > 0:
         return out
     torch.ops.bfly.gemm_silu_gate(x, w, out, gates, e0, num_local)
     return out

@@ -409,7 +409,7 @@ static bfly::RowScale row_scale(const Tensor& ssp, double eps, int M, int K);
 // Returns 0 when it ran, < 0 when the shape's plan has no packed form (nothing launched).
 int64_t gemm_packed(const Tensor& x, const Tensor& wp, Tensor& out, int64_t epilogue,
                     const c10::optional<Tensor>& ssp, double eps, const c10::optional<Tensor>& gates,
-                    int64_t e0, int64_t num_local) {
+                    int64_t e0, int64_t num_local, const c10::optional<Tensor>& workspace, bool defer) {
   CHECK_GPU(x); CHECK_BF16(x); CHECK_BF16(wp); CHECK_BF16(out);
   TORCH_CHECK(x.dim() == 2 && wp.dim() == 2 && out.dim() == 2 && wp.is_contiguous(), "gemm_packed: operands");
   CHECK_INNER(x); CHECK_INNER(out); CHECK_ALIGN16(x); CHECK_ALIGN16(wp);
@@ -431,9 +431,22 @@ int64_t gemm_packed(const Tensor& x, const Tensor& wp, Tensor& out, int64_t epil
     if (rs.gF % 16 != 0) return -5;
   }
   const bool any = ssp.has_value() || epilogue == bfly::EPI_SILU_GATE;
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  if (workspace.has_value()) {
+    TORCH_CHECK(workspace->scalar_type() == at::kFloat && workspace->is_contiguous(), "gemm_packed: workspace");
+    ws = workspace->data_ptr<float>();
+    ws_bytes = workspace->numel() * 4;
+  }
   c10::DeviceGuard g(x.device());
   return bfly::launch_gemm_packed(bf(x), x.stride(0), bf(wp), M, N, K, (int)epilogue, bf(out), out.stride(0),
-                                  cur_stream(), any ? &rs : nullptr);
+                                  cur_stream(), any ? &rs : nullptr, false, ws, ws_bytes, defer);
+}
+
+// 0 when the plan for (M, N, K, epilogue) has a packed-weight form (launch_gemm_packed dry run)
+int64_t gemm_packed_check(int64_t M, int64_t N, int64_t K, int64_t epilogue) {
+  return bfly::launch_gemm_packed(nullptr, 0, nullptr, (int)M, (int)N, (int)K, (int)epilogue, nullptr, 0, nullptr,
+                                  nullptr, true);
 }
 
 // Benchmark / tuning entry: run an explicit plan [kind, mt, nt, wk, bm, bn, sk].
@@ -1165,7 +1178,8 @@ TORCH_LIBRARY(bfly, m) {
   m.def("gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor? bias, int epilogue, Tensor(b!)? workspace) -> ()");
   m.def("gemm_silu_gate(Tensor x, Tensor w, Tensor(a!) out, Tensor gates, int e0, int num_local) -> ()");
   m.def("gemm_packed(Tensor x, Tensor wp, Tensor(a!) out, int epilogue, Tensor? ssp=None, float eps=0.0, "
-        "Tensor? gates=None, int e0=0, int num_local=1) -> int");
+        "Tensor? gates=None, int e0=0, int num_local=1, Tensor(b!)? workspace=None, bool defer=False) -> int");
+  m.def("gemm_packed_check(int M, int N, int K, int epilogue) -> int", &gemm_packed_check);
   m.def("gemm_with_plan(Tensor x, Tensor w, Tensor(a!) out, int[] plan, int epilogue, Tensor(b!)? workspace, "
         "Tensor? bias=None) -> ()");
   m.def("gemm_workspace_size(int M, int N, int K) -> int", &gemm_workspace_size);

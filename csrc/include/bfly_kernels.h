@@ -127,11 +127,14 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 // out[M, N/2] = gate-scaled SwiGLU (EPI_SILU_GATE) on the tile kernel without split-K: the
 // gate/up GEMM of the dense MoE decode path with moe_gate_scale folded into its epilogue.
 // gates [M][gld] f32; output column f belongs to expert ge0 + f / gF.
-// Decode GEMM over the K-tile-blocked copy Wp ([N/256][K/64][256][64]) of a weight: < 0 (nothing
-// launched) when the shape's plan is not a 64 x 128 tile without split-K. `rs`: row scale and / or
-// MoE gate (EPI_SILU_GATE). `dry`: only report whether it applies.
+// Decode GEMM over the K-tile-blocked copy Wp ([N/256][K/64][256][64]) of a weight, with the plan
+// the row-major weight would run: < 0 (nothing launched) when that plan is not a 64-row tile plan.
+// `rs`: row scale and / or MoE gate (EPI_SILU_GATE). Split-K plans need `ws`; with `defer` their
+// slabs stay in it for the consumer (returns the split count), else they are reduced (returns 1).
+// `dry`: only report whether it applies (0).
 int launch_gemm_packed(const bf16* X, long ldx, const bf16* Wp, int M, int N, int K, int epi, bf16* out,
-                       long ldo, hipStream_t stream, const RowScale* rs = nullptr, bool dry = false);
+                       long ldo, hipStream_t stream, const RowScale* rs = nullptr, bool dry = false,
+                       float* ws = nullptr, size_t ws_bytes = 0, bool defer = false);
 int launch_gemm_silu_gate(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K,
                           bf16* out, long ldo, const float* gates, int gld, int ge0, int gF,
                           hipStream_t stream);

@@ -1772,15 +1772,17 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef SK_CASE
     if (!done) return -2;
   } else if (p.kind == 1 && p.nt == 1) {
-    // tile plan over a K-tile-blocked weight (pack_w256 layout): 64 x 128 tiles, no split-K
-    if (N % 256 != 0 || K % 64 != 0 || p.bm != 64 || p.bn != 128 || p.sk != 1) return -1;
+    // tile plan over a K-tile-blocked weight (pack_w256 layout): 64-row tiles of 128 / 256 columns
+    if (N % 256 != 0 || K % 64 != 0 || p.bm != 64 || (p.bn != 128 && p.bn != 256) || K / kBK < p.sk) return -1;
+    if (p.sk > 1 && (long)((M + 63) / 64) * (N / p.bn) > kSplitCounters) return -1;
     bool done = false;
-#define TLP_CASE(WMW_, ST_)                                                                          \
-  if (!done && p.wk == WMW_ && p.mt == ST_) {                                                        \
-    if (!dry) run_tile<64, 128, WMW_, ST_, true>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, 1, stream, rsc); \
-    done = true;                                                                                     \
+#define TLP_CASE(BN_, WMW_, ST_)                                                                      \
+  if (!done && p.bn == BN_ && p.wk == WMW_ && p.mt == ST_) {                                          \
+    if (!dry) run_tile<64, BN_, WMW_, ST_, true>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    done = true;                                                                                      \
   }
-    TLP_CASE(2, 3) TLP_CASE(1, 3) TLP_CASE(2, 4) TLP_CASE(1, 4)
+    TLP_CASE(128, 2, 3) TLP_CASE(128, 1, 3) TLP_CASE(128, 2, 4) TLP_CASE(128, 1, 4) TLP_CASE(128, 1, 2)
+    TLP_CASE(256, 1, 3) TLP_CASE(256, 2, 3)
 #undef TLP_CASE
     if (!done) return -2;
   } else {
@@ -1954,8 +1956,9 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 // when the plan for this shape is not such a tile plan: the caller then uses the row-major
 // weight. `dry`: only report whether it applies.
 int launch_gemm_packed(const bf16* X, long ldx, const bf16* Wp, int M, int N, int K, int epi, bf16* out,
-                       long ldo, hipStream_t stream, const RowScale* rs, bool dry) {
-  if (M <= 0) return dry ? 0 : 0;
+                       long ldo, hipStream_t stream, const RowScale* rs, bool dry, float* ws, size_t ws_bytes,
+                       bool defer) {
+  if (M <= 0) return dry ? 0 : 1;
   if (N % 256 != 0 || K % 64 != 0) return -1;
   GemmPlan p = plan_gemm(M, N, K);
   if (epi != EPI_SILU_GATE &&
@@ -1966,10 +1969,15 @@ int launch_gemm_packed(const bf16* X, long ldx, const bf16* Wp, int M, int N, in
     const int bm = M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128;
     p = GemmPlan{1, 3, 0, bm <= 32 ? 1 : 2, bm, 128, 1};
   }
-  if (p.kind != 1 || p.bm != 64 || p.bn != 128 || p.sk != 1) return -2;
+  if (p.kind != 1 || p.bm != 64 || (p.bn != 128 && p.bn != 256)) return -2;
+  if (!dry && p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
+    return -3;
   p.nt = 1;
   if (dry) return run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true);
-  return run_plan(p, X, ldx, Wp, K, M, N, K, epi, nullptr, out, ldo, nullptr, stream, false, false, rs);
+  const bool d = defer && p.sk > 1;
+  const int rc = run_plan(p, X, ldx, Wp, K, M, N, K, epi, nullptr, out, ldo, ws, stream, false, d, rs);
+  if (rc != 0) return rc;
+  return d ? p.sk : 1;     // split count of slabs left in the workspace (deferred), else 1
 }
 
 // The dense MoE decode path's gate/up GEMM with the routing weight in its epilogue: one launch

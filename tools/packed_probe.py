@@ -36,14 +36,48 @@ def timeit(fn, iters=30):
     return st.elapsed_time(en) / iters * 1e3
 
 
+def table_plan(M, N, K):
+    p = ops.gemm_plan(M, N, K)
+    kinds = ("skinny", "tile", "big", "dec", "big8", "mid8", "big4", "mid4")
+    return [kinds.index(p["kind"]), p["mt"], p["nt"], p["wk"], p["bm"], p["bn"], p["splitk"]]
+
+
+def split_k_shapes(M):
+    """The table plans of the other decode projections, row-major vs packed (split-K plans,
+    their reduce launch included)."""
+    ws = torch.zeros(256 << 20, dtype=torch.float32, device="cuda")
+    for name, N, K in (("70b.qkv", 10240, 8192), ("70b.o", 8192, 8192), ("70b.down", 8192, 28672),
+                       ("8b.down", 4096, 14336), ("mixtral.moe_down", 4096, 114688)):
+        pl = table_plan(M, N, K)
+        if pl[0] != 1 or pl[4] != 64:
+            continue
+        copies = max(2, (1 << 30) // (N * K * 2) + 1)
+        Ws = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
+        Ps = [pack_w256(w) for w in Ws]
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        pk = list(pl)
+        pk[2] = 1
+        for rep in range(2):
+            for case, W, p in (("rowmajor", Ws, pl), ("packed", Ps, pk)):
+                us = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, W[i % copies], out, p, 0, ws))
+                print(json.dumps({"rep": rep, "shape": name, "case": case, "plan": p, "us": round(us, 2),
+                                  "TBps": round(N * K * 2 / us / 1e6, 3)}), flush=True)
+        del Ws, Ps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=57344)
     ap.add_argument("--k", type=int, default=8192)
     ap.add_argument("--m", type=int, default=64)
+    ap.add_argument("--others", action="store_true", help="also the split-K decode projections")
     a = ap.parse_args()
     assert ops.load_library()
     N, K, M = a.n, a.k, a.m
+    if a.others:
+        split_k_shapes(M)
+        return
     copies = max(2, (1 << 30) // (N * K * 2) + 1)
     Ws = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
     Ps = [pack_w256(w) for w in Ws]
