@@ -1772,17 +1772,24 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
 #undef SK_CASE
     if (!done) return -2;
   } else if (p.kind == 1 && p.nt == 1) {
-    // tile plan over a K-tile-blocked weight (pack_w256 layout): 64-row tiles of 128 / 256 columns
-    if (N % 256 != 0 || K % 64 != 0 || p.bm != 64 || (p.bn != 128 && p.bn != 256) || K / kBK < p.sk) return -1;
-    if (p.sk > 1 && (long)((M + 63) / 64) * (N / p.bn) > kSplitCounters) return -1;
+    // tile plan over a K-tile-blocked weight (pack_w256 layout): 16 / 32 / 64-row tiles of 128 /
+    // 256 columns (the packed layout only changes the weight stage's addresses, so every decode
+    // tile the row-major table picks, down to the B = 1 bucket, has its packed twin)
+    if (N % 256 != 0 || K % 64 != 0 || (p.bm != 16 && p.bm != 32 && p.bm != 64) || (p.bn != 128 && p.bn != 256) ||
+        K / kBK < p.sk)
+      return -1;
+    if (p.sk > 1 && (long)((M + p.bm - 1) / p.bm) * (N / p.bn) > kSplitCounters) return -1;
     bool done = false;
-#define TLP_CASE(BN_, WMW_, ST_)                                                                      \
-  if (!done && p.bn == BN_ && p.wk == WMW_ && p.mt == ST_) {                                          \
-    if (!dry) run_tile<64, BN_, WMW_, ST_, true>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    const int st = p.mt > 0 ? p.mt : 2;
+#define TLP_CASE(BM_, BN_, WMW_, ST_)                                                                 \
+  if (!done && p.bm == BM_ && p.bn == BN_ && p.wk == WMW_ && st == ST_) {                             \
+    if (!dry) run_tile<BM_, BN_, WMW_, ST_, true>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                      \
   }
-    TLP_CASE(128, 2, 3) TLP_CASE(128, 1, 3) TLP_CASE(128, 2, 4) TLP_CASE(128, 1, 4) TLP_CASE(128, 1, 2)
-    TLP_CASE(256, 1, 3) TLP_CASE(256, 2, 3)
+#define TLP_ST(BM_, BN_, WMW_) TLP_CASE(BM_, BN_, WMW_, 2) TLP_CASE(BM_, BN_, WMW_, 3) TLP_CASE(BM_, BN_, WMW_, 4)
+    TLP_ST(16, 128, 1) TLP_ST(16, 256, 1) TLP_ST(32, 128, 1) TLP_ST(32, 256, 1)
+    TLP_ST(64, 128, 1) TLP_ST(64, 128, 2) TLP_ST(64, 256, 1) TLP_ST(64, 256, 2)
+#undef TLP_ST
 #undef TLP_CASE
     if (!done) return -2;
   } else {
@@ -1969,7 +1976,7 @@ int launch_gemm_packed(const bf16* X, long ldx, const bf16* Wp, int M, int N, in
     const int bm = M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128;
     p = GemmPlan{1, 3, 0, bm <= 32 ? 1 : 2, bm, 128, 1};
   }
-  if (p.kind != 1 || p.bm != 64 || (p.bn != 128 && p.bn != 256)) return -2;
+  if (p.kind != 1 || (p.bm != 16 && p.bm != 32 && p.bm != 64) || (p.bn != 128 && p.bn != 256)) return -2;
   if (!dry && p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
     return -3;
   p.nt = 1;
