@@ -28,6 +28,7 @@ from butterfly_amd.models.transformer import TransformerLM  # noqa: E402
 from butterfly_amd.parallel.comm import Communicator  # noqa: E402
 from butterfly_amd.partition.costmodel import CostModel  # noqa: E402
 from butterfly_amd.partition.hw import MI355X  # noqa: E402
+from butterfly_amd.utils import flags  # noqa: E402
 
 
 def compute_estimate(cfg, tp: int, batch: int, ctx: int) -> float:
@@ -56,6 +57,10 @@ def main():
     t0 = time.perf_counter()
     model = TransformerLM(cfg, Shard(tp_rank=0, tp_size=tp), device="cuda", comm=Communicator.single())
     model.init_random(seed=0)
+    packed_gb = 0.0
+    if flags.get("BFLY_PACKED_DECODE"):   # as the engine does when HBM allows (all of it fits a shard)
+        kinds = [k.strip() for k in flags.get("BFLY_PACKED_KINDS").split(",") if k.strip()]
+        packed_gb = model.pack_decode_weights(kinds=kinds) / 1e9
     BS = 32
     nb = -(-(ctx + 1) // BS)
     kv = model.allocate_kv_cache(B * nb, BS)
@@ -97,7 +102,8 @@ def main():
     est = compute_estimate(cfg, tp, B, ctx) * 1e3
     print(json.dumps({"model": cfg.name, "tp": tp, "batch": B, "ctx": ctx, "ms_per_step_p50": round(ms, 3),
                       "ms_min": round(times[0], 3), "tokens_per_s_per_replica": round(B / ms * 1e3, 1),
-                      "costmodel_compute_ms": round(est, 3), "ratio_measured_over_model": round(ms / est, 3)}),
+                      "costmodel_compute_ms": round(est, 3), "ratio_measured_over_model": round(ms / est, 3),
+                      "packed_decode_weights_gb": round(packed_gb, 1)}),
           flush=True)
 
 
