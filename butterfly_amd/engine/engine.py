@@ -139,7 +139,7 @@ class LLMEngine:
         if nblocks <= 0:
             raise RuntimeError("no HBM left for the KV cache")
         if (self.device.type == "cuda" and flags.get("BFLY_PACKED_DECODE") and mesh.ep == 1
-                and engine_cfg.max_batch <= 64):
+                and engine_cfg.max_batch <= 512):
             # decode-layout copies of the projection weights, only from HBM the KV cache leaves free
             free = device_kv_budget(self.device, engine_cfg.hbm_utilization, self._activation_reserve())
             room = free - nblocks * per_tok * bs - (2 << 30)

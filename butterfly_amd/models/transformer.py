@@ -162,7 +162,7 @@ class TransformerLM:
     _PACK_EPI = {"gu_w": 2, "moe_gu_w": 3}    # GEMM epilogue of each kind (others: none)
 
     def _packable(self) -> list:
-        """Weights whose decode GEMM at a 64-row batch has a packed-weight plan."""
+        """Weights whose decode GEMM has a packed-weight plan at some batch of 1-256 rows."""
         if self.device.type != "cuda" or not ops.load_library():
             return []
         names = []
@@ -171,7 +171,8 @@ class TransformerLM:
                 k = f"l{i}.{kind}"
                 w = self.p.get(k)
                 if (w is not None and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0
-                        and torch.ops.bfly.gemm_packed_check(64, w.shape[0], w.shape[1], self._PACK_EPI.get(kind, 0)) == 0):
+                        and any(torch.ops.bfly.gemm_packed_check(m, w.shape[0], w.shape[1], self._PACK_EPI.get(kind, 0)) == 0
+                                for m in (1, 16, 64, 128, 256, 512))):
                     names.append(k)
         return names
 
@@ -182,7 +183,8 @@ class TransformerLM:
 
     def pack_decode_weights(self, budget_bytes: Optional[int] = None, kinds=None) -> int:
         """Keep K-tile-blocked copies (ops.pack_w256) of the decode projections' weights, read by
-        the decode GEMMs whose plan is a 64-row tile (batches of 33-64 rows): each weight stage is
+        the decode GEMMs whose plan is a 16 / 32 / 64-row tile or a mid-M kernel (batches of 1-512
+        rows): each weight stage is
         one contiguous run of memory instead of a row segment per weight row, 8 % faster on the
         Llama-3-70B gate/up GEMM with bitwise the same result (tools/packed_probe.py). Whole
         projection kinds, in the order of `kinds` (None: _PACK_ORDER), while they fit

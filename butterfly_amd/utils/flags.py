@@ -98,7 +98,7 @@ define("BFLY_SEQ_PARALLEL", False, _bool, "TP prefill with sequence parallelism:
        "split by tokens over the TP group (reduce-scatter + all-gather replace each all-reduce)")
 define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on prefill steps with at least this many tokens")
 define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped expert GEMMs instead of the dense path")
-define("BFLY_PACKED_DECODE", True, _bool, "engines whose decode batch fits one 64-row tile keep K-tile-blocked copies of "
+define("BFLY_PACKED_DECODE", True, _bool, "engines whose decode batch is at most 512 rows keep K-tile-blocked copies of "
        "projection weights for the decode GEMMs in the HBM left after the KV cache (BFLY_PACKED_KINDS)")
 define("BFLY_PACKED_KINDS", "gu_w,moe_gu_w,qkv_w", str, "projection kinds packed by BFLY_PACKED_DECODE, in "
        "priority order: a kind is packed whole or not at all, while the HBM lasts (o_w / down_w / moe_down_w also "

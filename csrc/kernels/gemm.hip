@@ -1140,7 +1140,7 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
   }
 }
 
-template <int BM, int BN, int SX, int SW>
+template <int BM, int BN, int SX, int SW, bool PK = false>
 __global__ void __launch_bounds__(kMidThreads)
 gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -1164,7 +1164,11 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 
   // DMA: wave w moves the 1-KiB blocks w, w + 8, ... of an X / W slot (BM / 8, BN / 8 blocks)
   const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);
-  const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
+  // PK: W in the K-tile-blocked layout [N/256][K/64][256][64] (pack_w256): the tile's BN rows
+  // lie in one 256-row block (BN divides 256), a row is 128 B and a K-tile 32 KiB further on
+  const long wpitch = PK ? 64 : ldw;
+  const auto rsb = PK ? b8_rsrc(W + ((long)(n0 >> 8) * K << 8) + (n0 & 255) * 64, 1, (long)K * 256 - (n0 & 255) * 64)
+                      : b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
   const bool wnt = mtiles == 1 && g_tile_w_nt;
   int vx[LX], vw[LW];
 #pragma unroll
@@ -1175,7 +1179,7 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
 #pragma unroll
   for (int i = 0; i < LW; ++i) {
     const int row = (wid + 8 * i) * 8 + (lane >> 3);
-    vw[i] = (int)((row * ldw + (((lane & 7) ^ ((row >> 1) & 7)) * 8)) * 2);
+    vw[i] = (int)((row * wpitch + (((lane & 7) ^ ((row >> 1) & 7)) * 8)) * 2);
   }
   auto dma_x = [&](int k) {
     char* s = xs + (k % SX) * C::XB;
@@ -1185,7 +1189,7 @@ gemm_mid8_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   };
   auto dma_w = [&](int k) {
     char* s = wsm + (k % SW) * C::WB;
-    const int soff = (kt0 + k) * kBK * 2;
+    const int soff = (kt0 + k) * (PK ? 256 * kBK * 2 : kBK * 2);
     if (wnt) {
 #pragma unroll
       for (int i = 0; i < LW; ++i) mid_dma1<2>(rsb, s + (wid + 8 * i) * 1024, vw[i], soff);
@@ -1295,7 +1299,7 @@ struct Mid4Cfg {
   static_assert(SA >= 2 && SB >= 2 && LDS <= 160 * 1024, "mid4 rings");
 };
 
-template <int BM, int BN, int SA, int SB>
+template <int BM, int BN, int SA, int SB, bool PK = false>
 __global__ void __launch_bounds__(kMid4Threads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 gemm_mid4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ W, long ldw,
                  int M, int N, int K, int epi, const bf16* __restrict__ bias,
@@ -1321,20 +1325,24 @@ gemm_mid4_kernel(const bf16* __restrict__ X, long ldx, const bf16* __restrict__ 
   // 128 B lane-linear, lane L supplying row 8 (block) + (L >> 3) at lds_frag's swizzled chunk
   // (L & 7) ^ ((L >> 4) + 4 (s & 1)) & 7 (NA, NB even)
   const auto rsa = b8_rsrc(X + (long)m0 * ldx, M - m0, ldx);   // A rows past M read zeros
-  const auto rsb = b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
+  // PK: W in the pack_w256 layout (see gemm_mid8_kernel): 128-B rows, 32-KiB K-tiles
+  const long wpitch = PK ? 64 : ldw;
+  const int kstep = PK ? 256 * 128 : 128;
+  const auto rsb = PK ? b8_rsrc(W + ((long)(n0 >> 8) * K << 8) + (n0 & 255) * 64, 1, (long)K * 256 - (n0 & 255) * 64)
+                      : b8_rsrc(W + (long)n0 * ldw, N - n0, ldw);
   int va[2], vb[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int ch = (lane & 7) ^ (((lane >> 4) + 4 * e) & 7);
     va[e] = (int)(((8 * NA * wid + (lane >> 3)) * ldx + ch * 8) * 2);
-    vb[e] = (int)(((8 * NB * wid + (lane >> 3)) * ldw + ch * 8) * 2);
+    vb[e] = (int)(((8 * NB * wid + (lane >> 3)) * wpitch + ch * 8) * 2);
   }
   char* const bbase = smem + SA * C::ASLOT;
   auto dma_a = [&](int k, int slot, int s) {
     b4_dma(rsa, smem + slot * C::ASLOT + (NA * wid + s) * 1024, va[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldx * 2));
   };
   auto dma_b = [&](int k, int slot, int s) {
-    b4_dma(rsb, bbase + slot * C::BSLOT + (NB * wid + s) * 1024, vb[s & 1], (kt0 + k) * 128 + (int)(8 * s * ldw * 2));
+    b4_dma(rsb, bbase + slot * C::BSLOT + (NB * wid + s) * 1024, vb[s & 1], (kt0 + k) * kstep + (int)(8 * s * wpitch * 2));
   };
   const int fr = lane & 15, fq = lane >> 4;
   int lo[2][2];   // [A / B][ks] lane byte offset inside a slot (fragments differ by 2048 B)
@@ -1523,24 +1531,24 @@ static void run_big4(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   gemm_big4_kernel<false><<<grid, kB4Threads, kB4LdsBytes, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, part);
 }
 
-template <int BM, int BN, int SA, int SB>
+template <int BM, int BN, int SA, int SB, bool PK = false>
 static void run_mid4(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                      const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream,
                      const RowScale& rsc) {
   using C = Mid4Cfg<BM, BN, SA, SB>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid4_kernel<BM, BN, SA, SB>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid4_kernel<BM, BN, SA, SB, PK>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr_set = true;
   }
   dim3 grid(((M + BM - 1) / BM) * (N / BN), sk);
   float* part = sk > 1 ? splitk_part(ws) : nullptr;
-  gemm_mid4_kernel<BM, BN, SA, SB><<<grid, kMid4Threads, C::LDS, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias,
+  gemm_mid4_kernel<BM, BN, SA, SB, PK><<<grid, kMid4Threads, C::LDS, stream>>>(X, ldx, W, ldw, M, N, K, epi, bias,
                                                                          out, ldo, part, rsc);
 }
 
-template <int BM, int BN, int SX, int SW>
+template <int BM, int BN, int SX, int SW, bool PK = false>
 static void run_mid8(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, int K, int epi,
                      const bf16* bias, bf16* out, long ldo, float* ws, int sk, hipStream_t stream,
                      const RowScale& rsc) {
@@ -1548,12 +1556,12 @@ static void run_mid8(const bf16* X, long ldx, const bf16* W, long ldw, int M, in
   constexpr size_t lds = (size_t)MidCfg<BM, BN, SX, SW>::LDS;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid8_kernel<BM, BN, SX, SW>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid8_kernel<BM, BN, SX, SW, PK>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  gemm_mid8_kernel<BM, BN, SX, SW><<<tiles * sk, kMidThreads, lds, stream>>>(
+  gemm_mid8_kernel<BM, BN, SX, SW, PK><<<tiles * sk, kMidThreads, lds, stream>>>(
       X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, sk > 1 ? splitk_part(ws) : nullptr, sk, rsc);
 }
 
@@ -1692,10 +1700,12 @@ size_t gemm_workspace_bytes(int M, int N, int K) {
 static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, long ldw, int M,
                     int N, int K, int epi, const bf16* bias, bf16* out, long ldo, float* ws,
                     hipStream_t stream, bool dry = false, bool defer = false,
-                    const RowScale* rs = nullptr) {
+                    const RowScale* rs = nullptr, bool packed = false) {
   const RowScale rsc = rs ? *rs : RowScale{nullptr, 0, 0.f, 0.f};
   if (rs != nullptr && p.kind != 1 && p.kind != 3 && p.kind != 5 && p.kind != 7) return -4;   // row scale: tile / ring / mid epilogues
   if (epi == EPI_SILU_GATE && (p.kind != 1 || p.sk != 1)) return -4;   // gate: tile epilogue, no slabs
+  // packed (pack_w256) weights: the tile plans mark it with nt = 1, the mid-M kernels take it here
+  if (packed && p.kind != 5 && p.kind != 7) return -5;
   if (p.kind == 4) {
     // 8-phase big tile: every split needs >= 2 K-tiles of 64
     if (N % 256 != 0 || K % 64 != 0 || K / 64 < 2 * p.sk) return -1;
@@ -1706,7 +1716,8 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     bool done = false;
 #define MID4_CASE(BM_, BN_, SA_, SB_)                                                               \
   if (!done && p.bm == BM_ && p.bn == BN_ && p.mt == SA_ && p.nt == SB_) {                          \
-    if (!dry) run_mid4<BM_, BN_, SA_, SB_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    if (!dry && packed) run_mid4<BM_, BN_, SA_, SB_, true>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    else if (!dry) run_mid4<BM_, BN_, SA_, SB_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                   \
   }
     MID4_CASE(128, 128, 4, 6) MID4_CASE(128, 128, 3, 7) MID4_CASE(128, 128, 2, 8)
@@ -1727,7 +1738,8 @@ static int run_plan(const GemmPlan& p, const bf16* X, long ldx, const bf16* W, l
     bool done = false;
 #define MID_CASE(BM_, BN_, SX_, SW_)                                                              \
   if (!done && p.bm == BM_ && p.bn == BN_ && sx == SX_ && p.mt == SW_) {                           \
-    if (!dry) run_mid8<BM_, BN_, SX_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    if (!dry && packed) run_mid8<BM_, BN_, SX_, SW_, true>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
+    else if (!dry) run_mid8<BM_, BN_, SX_, SW_>(X, ldx, W, ldw, M, N, K, epi, bias, out, ldo, ws, p.sk, stream, rsc); \
     done = true;                                                                                   \
   }
     MID_CASE(256, 128, 3, 3) MID_CASE(256, 128, 2, 6) MID_CASE(256, 128, 3, 4)
@@ -1956,8 +1968,8 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 
 // Decode GEMM over a K-tile-blocked copy of the weight (layout [N/256][K/64][256][64], made
 // once by the engine when HBM allows, models/transformer.pack_decode_weights): the plan the
-// row-major weight would run (tile 64 x 128, no split-K; EPI_SILU_GATE: the gate plan) on the
-// packed copy. Each 128-row weight stage is then one 16 KiB run of memory instead of 128
+// row-major weight would run (16 / 32 / 64-row tiles and the mid-M kernels of kinds 5 / 7, with
+// their split-K; EPI_SILU_GATE: the gate plan) on the packed copy. Each 128-row weight stage is then one 16 KiB run of memory instead of 128
 // runs of 128 B a row pitch apart: the Llama-3-70B gate/up GEMM at M = 64 in 145 against
 // 158 us, bitwise the same result (tools/packed_probe.py). Returns < 0 (nothing launched)
 // when the plan for this shape is not such a tile plan: the caller then uses the row-major
@@ -1976,13 +1988,17 @@ int launch_gemm_packed(const bf16* X, long ldx, const bf16* Wp, int M, int N, in
     const int bm = M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128;
     p = GemmPlan{1, 3, 0, bm <= 32 ? 1 : 2, bm, 128, 1};
   }
-  if (p.kind != 1 || (p.bm != 16 && p.bm != 32 && p.bm != 64) || (p.bn != 128 && p.bn != 256)) return -2;
+  // mid-M kernels (kinds 5 / 7): their weight DMA takes the packed layout as a template flag
+  const bool mid = (p.kind == 5 || p.kind == 7) && (p.bn == 128 || p.bn == 256);
+  if (!mid && (p.kind != 1 || (p.bm != 16 && p.bm != 32 && p.bm != 64) || (p.bn != 128 && p.bn != 256))) return -2;
   if (!dry && p.sk > 1 && (ws == nullptr || ws_bytes < kCounterBytes + (size_t)p.sk * M * N * sizeof(float)))
     return -3;
-  p.nt = 1;
-  if (dry) return run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true);
+  if (!mid) p.nt = 1;
+  if (dry)
+    return run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true, false,
+                    nullptr, mid);
   const bool d = defer && p.sk > 1;
-  const int rc = run_plan(p, X, ldx, Wp, K, M, N, K, epi, nullptr, out, ldo, ws, stream, false, d, rs);
+  const int rc = run_plan(p, X, ldx, Wp, K, M, N, K, epi, nullptr, out, ldo, ws, stream, false, d, rs, mid);
   if (rc != 0) return rc;
   return d ? p.sk : 1;     // split count of slabs left in the workspace (deferred), else 1
 }

@@ -390,14 +390,18 @@ def test_rms_norm_route_equals_norm_then_route(T, dim, sk, k, E):
                                          (64, 4096, 14336, "none"), (1, 57344, 8192, "silu"),
                                          (3, 28672, 4096, "rowscale"), (1, 4096, 14336, "none"),
                                          (1, 10240, 8192, "defer"), (8, 8192, 28672, "defer"),
-                                         (24, 8192, 8192, "defer")])
+                                         (24, 8192, 8192, "defer"), (128, 8192, 8192, "defer"),
+                                         (256, 8192, 8192, "defer"), (128, 8192, 4096, "none"),
+                                         (256, 28672, 8192, "silu"), (256, 5120, 8192, "defer"),
+                                         (600, 28672, 4096, "silu")])
 def test_packed_decode_gemm_is_bitwise_the_row_major_one(M, N, K, mode):
     """The decode GEMM over the K-tile-blocked copy of a weight (ops.pack_w256, gemm.hip
     launch_gemm_packed) runs the plan the row-major weight would run with the same arithmetic
     order: bitwise the same output, for the SwiGLU epilogue, with a row-split RMSNorm row scale
-    and with the MoE gate, down to the 16 / 32-row tiles of the B = 1-32 latency buckets; shapes
-    whose plan has no packed form (M = 200) report so and ops.linear falls back to the
-    row-major weight."""
+    and with the MoE gate, down to the 16 / 32-row tiles of the B = 1-32 latency buckets and up
+    to the mid-M kernels (plan kinds 5 / 7, M = 128-256, split-K slabs included); shapes whose
+    plan has no packed form (M = 600: the 256 x 256 prefill tile) report so and ops.linear
+    falls back to the row-major weight."""
     x, w = _bf(M, K, seed=90), _bf(N, K, scale=0.02, seed=91)
     wp = ops.pack_w256(w)
     if mode == "gate":
@@ -437,7 +441,7 @@ def test_packed_decode_gemm_is_bitwise_the_row_major_one(M, N, K, mode):
     assert torch.equal(got, want)
     out = torch.empty_like(got)
     applies = torch.ops.bfly.gemm_packed(x, wp, out, ops.EPILOGUES["silu"]) > 0
-    assert applies == (M <= 64), (M, applies)
+    assert applies == (M <= 256), (M, applies)
 
 
 @pytest.mark.parametrize("M,El,e0,E,H,F", [(64, 8, 0, 8, 512, 256), (37, 3, 2, 8, 256, 128), (130, 2, 0, 4, 1024, 512),
