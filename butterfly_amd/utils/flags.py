@@ -101,8 +101,9 @@ define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped
 define("BFLY_PACKED_DECODE", True, _bool, "engines whose decode batch is at most 512 rows keep K-tile-blocked copies of "
        "projection weights for the decode GEMMs in the HBM left after the KV cache (BFLY_PACKED_KINDS)")
 define("BFLY_PACKED_KINDS", "gu_w,moe_gu_w,qkv_w", str, "projection kinds packed by BFLY_PACKED_DECODE, in "
-       "priority order: a kind is packed whole or not at all, while the HBM lasts (o_w / down_w / moe_down_w also "
-       "work; isolated they ran 1-3 percent slower packed, whole-step within noise: profiles/r6_packed/kinds_ab.log)")
+       "priority order: a kind is packed whole or not at all, while the HBM lasts (down_w / moe_down_w also "
+       "work: whole-step within noise, profiles/r6_packed/kinds_ab.log; o_w runs its own packed plan where one is "
+       "tuned, gemm.hip kPackedTuned)")
 define("BFLY_MOE_NORM_ROUTE", True, _bool, "MoE layers at tp = 1: the add+RMSNorm over the O projection's split-K "
        "slabs also routes the rows (0: separate moe_route launch)")
 define("BFLY_MOE_GATE_EPILOGUE", True, _bool, "dense MoE decode path: the routing weights applied in the gate/up "

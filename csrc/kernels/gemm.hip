@@ -1974,12 +1974,37 @@ int launch_gemm(const bf16* X, long ldx, const bf16* W, long ldw, int M, int N, 
 // 158 us, bitwise the same result (tools/packed_probe.py). Returns < 0 (nothing launched)
 // when the plan for this shape is not such a tile plan: the caller then uses the row-major
 // weight. `dry`: only report whether it applies.
+// Packed-weight plans that differ from the row-major table's (tools/packed_probe.py --sweep,
+// isolated, weights rotating through HBM; profiles/r6_packed/sweep_m64.jsonl): kind -1 = keep
+// this shape on the row-major weight (its row-major plan is faster than any packed one).
+struct PackedTuned { int N, K, M; GemmPlan p; };
+static const PackedTuned kPackedTuned[] = {
+    {8192, 8192, 64, {1, 3, 1, 2, 64, 128, 4}},   // 70B O: 29.3 us vs 32.7 (row-major table plan, split-K 8)
+    {4096, 4096, 1, {-1, 0, 0, 0, 0, 0, 0}},      // 8B O: row-major 13.7 us vs 14.2 packed at M = 64;
+    {4096, 4096, 16, {-1, 0, 0, 0, 0, 0, 0}},     // packing O / down measured 1-2 % slower per step
+    {4096, 4096, 32, {-1, 0, 0, 0, 0, 0, 0}},     // at B = 1 (kinds_b1_ab.log)
+    {4096, 4096, 64, {-1, 0, 0, 0, 0, 0, 0}},
+};
+
 int launch_gemm_packed(const bf16* X, long ldx, const bf16* Wp, int M, int N, int K, int epi, bf16* out,
                        long ldo, hipStream_t stream, const RowScale* rs, bool dry, float* ws, size_t ws_bytes,
                        bool defer) {
   if (M <= 0) return dry ? 0 : 1;
   if (N % 256 != 0 || K % 64 != 0) return -1;
   GemmPlan p = plan_gemm(M, N, K);
+  if (tuned_enabled() && plan_overrides().empty() && epi != EPI_SILU_GATE) {
+    static const int kB[] = {1, 16, 32, 64, 128, 256, 512};
+    int bucket = 0;
+    for (int b : kB)
+      if (b >= M) { bucket = b; break; }
+    for (const PackedTuned& t : kPackedTuned)
+      if (t.N == N && t.K == K && t.M == bucket) {
+        if (t.p.kind < 0) return -2;
+        if (run_plan(t.p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true) == 0)
+          p = t.p;
+        break;
+      }
+  }
   if (epi != EPI_SILU_GATE &&
       run_plan(p, nullptr, 0, nullptr, 0, M, N, K, epi, nullptr, nullptr, 0, nullptr, nullptr, true) != 0)
     p = plan_gemm_heuristic(M, N, K);

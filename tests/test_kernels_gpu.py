@@ -393,7 +393,7 @@ def test_rms_norm_route_equals_norm_then_route(T, dim, sk, k, E):
                                          (24, 8192, 8192, "defer"), (128, 8192, 8192, "defer"),
                                          (256, 8192, 8192, "defer"), (128, 8192, 4096, "none"),
                                          (256, 28672, 8192, "silu"), (256, 5120, 8192, "defer"),
-                                         (600, 28672, 4096, "silu")])
+                                         (600, 28672, 4096, "silu"), (64, 4096, 4096, "keep")])
 def test_packed_decode_gemm_is_bitwise_the_row_major_one(M, N, K, mode):
     """The decode GEMM over the K-tile-blocked copy of a weight (ops.pack_w256, gemm.hip
     launch_gemm_packed) runs the plan the row-major weight would run with the same arithmetic
@@ -413,10 +413,24 @@ def test_packed_decode_gemm_is_bitwise_the_row_major_one(M, N, K, mode):
         out = torch.empty_like(got)
         assert torch.ops.bfly.gemm_packed(x, wp, out, 3, None, 0.0, gates, 3, El) > 0
         return
+    if mode == "keep":
+        # a shape the packed table keeps on the row-major weight: no packed plan, same result
+        assert torch.ops.bfly.gemm_packed_check(M, N, K, 0) != 0
+        assert torch.equal(ops.linear(x, w, packed=wp), ops.linear(x, w))
+        return
     if mode in ("defer", "none"):
         # split-K plans over the packed copy: the slabs (deferred, as for the QKV / O / down
         # projections the consumer reduces) and the reduced output are bitwise the row-major ones
         d = mode == "defer"
+        own = {(64, 8192, 8192): [1, 3, 0, 2, 64, 128, 4]}.get((M, N, K))
+        if own is not None:
+            # a packed-table plan (gemm.hip kPackedTuned): bitwise the row-major weight on that plan
+            got = ops.linear(x, w, packed=wp).clone()   # both through the plan's own split-K reduce
+            want = torch.empty_like(got)
+            torch.ops.bfly.gemm_with_plan(x, w, want, own, 0, torch.zeros(16 << 20, dtype=torch.float32, device=DEV))
+            assert torch.equal(got, want)
+            _close(got, x.float() @ w.float().t(), 2e-2, 2e-2)
+            return
         got = ops.linear(x, w, defer=d, packed=wp)      # slabs live in the shared GEMM workspace:
         got_slabs = got.slabs.clone() if isinstance(got, ops.Partial) else None   # copy before the next GEMM
         got = ops.materialize(got).clone()

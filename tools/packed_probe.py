@@ -66,15 +66,63 @@ def split_k_shapes(M):
         del Ws, Ps
 
 
+SWEEP_SHAPES = {"70b.qkv": (10240, 8192, "none"), "70b.o": (8192, 8192, "none"), "70b.down": (8192, 28672, "none"),
+                "70b.gate_up": (57344, 8192, "silu"), "8b.qkv": (6144, 4096, "none"), "8b.o": (4096, 4096, "none"),
+                "8b.gate_up": (28672, 4096, "silu"), "8b.down": (4096, 14336, "none")}
+
+
+def sweep(M, names):
+    """Every packed tile plan (64-row tiles; 128 / 256 columns, 1 / 2 waves along M, 2-4 stages,
+    split-K 1-8) against the table plan on the row-major and the packed weight, event-timed with
+    the weights rotating through HBM; split-K plans include their reduce launch."""
+    ws = torch.zeros(256 << 20, dtype=torch.float32, device="cuda")
+    for name in names:
+        N, K, e = SWEEP_SHAPES[name]
+        epi = ops.EPILOGUES[e]
+        copies = max(2, (1 << 30) // (N * K * 2) + 1)
+        Ws = [torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
+        Ps = [pack_w256(w) for w in Ws]
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty(M, N // 2 if e == "silu" else N, device="cuda", dtype=torch.bfloat16)
+        tp = table_plan(M, N, K)
+        cands = [("table_rowmajor", Ws, tp)]
+        if tp[0] == 1 and tp[4] <= 64:
+            cands.append(("table_packed", Ps, tp[:2] + [1] + tp[3:]))
+        for bn in (128, 256):
+            for wk in (1, 2):
+                for st in (2, 3, 4):
+                    for sk in (1, 2, 3, 4, 6, 8):
+                        if (K // 64) < 4 * sk:
+                            continue
+                        cands.append((f"packed_{bn}_{wk}_{st}_{sk}", Ps, [1, st, 1, wk, 64, bn, sk]))
+        res = {}
+        for rep in range(2):
+            for tag, W, pl in cands:
+                try:
+                    us = timeit(lambda i: torch.ops.bfly.gemm_with_plan(x, W[i % copies], out, pl, epi, ws), iters=20)
+                except RuntimeError:
+                    continue
+                res.setdefault(tag, []).append(us)
+        best = sorted((min(v), k) for k, v in res.items())
+        for us, tag in best[:6] + [(min(res["table_rowmajor"]), "table_rowmajor")]:
+            print(json.dumps({"shape": name, "M": M, "case": tag, "us": round(us, 2),
+                              "TBps": round(N * K * 2 / us / 1e6, 3), "table_plan": tp}), flush=True)
+        del Ws, Ps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=57344)
     ap.add_argument("--k", type=int, default=8192)
     ap.add_argument("--m", type=int, default=64)
     ap.add_argument("--others", action="store_true", help="also the split-K decode projections")
+    ap.add_argument("--sweep", default="", help="comma-separated SWEEP_SHAPES names: sweep packed tile plans")
     a = ap.parse_args()
     assert ops.load_library()
     N, K, M = a.n, a.k, a.m
+    if a.sweep:
+        sweep(M, a.sweep.split(","))
+        return
     if a.others:
         split_k_shapes(M)
         return
