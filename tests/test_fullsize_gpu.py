@@ -96,13 +96,15 @@ def test_bench_dims_prefill_decode_and_graph(preset):
     torch.cuda.synchronize()
     _check(dg[:, :V], dr[:, :V], 3e-2, cfg.is_moe)
 
-    # the decode step over the K-tile-blocked gate/up copies (what an engine with HBM to spare
-    # runs): bitwise the eager logits and cache writes
+    # the decode step over the K-tile-blocked copies the engine makes by default
+    # (BFLY_PACKED_KINDS; what an engine with HBM to spare runs): they run the row-major plans,
+    # so bitwise the eager logits and cache writes (a kind with its own packed plan in
+    # gemm.hip kPackedTuned, e.g. the 70B O projection, sums its split-K in another order)
     for (k, v), (k0, v0) in zip(kg, kg_snapshot):
         k.copy_(k0)
         v.copy_(v0)
     dg_eager = dg.clone()
-    g.pack_decode_weights()
+    g.pack_decode_weights(kinds=["gu_w", "moe_gu_w", "qkv_w"])
     assert g.packed
     dp = g.forward(db, kg)
     torch.cuda.synchronize()
