@@ -100,7 +100,7 @@ define("BFLY_SEQ_PARALLEL_MIN_TOKENS", 256, int, "sequence parallelism only on p
 define("BFLY_MOE_SPARSE", True, _bool, "prefill MoE layers: token-routed grouped expert GEMMs instead of the dense path")
 define("BFLY_PACKED_DECODE", True, _bool, "engines whose decode batch is at most 512 rows keep K-tile-blocked copies of "
        "projection weights for the decode GEMMs in the HBM left after the KV cache (BFLY_PACKED_KINDS)")
-define("BFLY_PACKED_KINDS", "gu_w,moe_gu_w,qkv_w", str, "projection kinds packed by BFLY_PACKED_DECODE, in "
+define("BFLY_PACKED_KINDS", "gu_w,moe_gu_w,qkv_w,o_w", str, "projection kinds packed by BFLY_PACKED_DECODE, in "
        "priority order: a kind is packed whole or not at all, while the HBM lasts (down_w / moe_down_w also "
        "work: whole-step within noise, profiles/r6_packed/kinds_ab.log; o_w runs its own packed plan where one is "
        "tuned, gemm.hip kPackedTuned)")
